@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""Headline benchmark: rendered views/sec (forward + backward) of the MI355X
+Gaussian rasterizer at 1080p with 1M synthetic Gaussians (BASELINE.json
+config 2), N data-parallel ranks (config 5 at N = 8).
+
+One *step* = per rank: one forward + backward through the drop-in API
+(``diff_gaussian_rasterization.GaussianRasterizer``, autograd) of one
+1920x1080 view of the same 1M-Gaussian scene, with a fixed N(0,1) cotangent;
+for N > 1 the flattened parameter gradients (59 floats per Gaussian:
+means3D 3, SH 48, opacity 1, scales 3, rotations 4) are summed across ranks
+with one RCCL all-reduce.  Per-GPU work is fixed as N grows ("weak").
+
+Inputs are resident in HBM before the timed region.  The timed region is K
+steps bracketed by barrier + synchronize; the reported time is the max over
+ranks.  ``roofline`` is computed from the per-stage HIP events the library
+records on the launch stream during the timed region (gs_profile_*), for the
+stage that takes the most time, with the algorithmic bytes of DESIGN.md.
+``cpu_baseline`` times the CPU oracle (a scalar port of the reference path)
+on one full view on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+CONFIGS = {
+    # name: (P, W, H)
+    "cfg2_1080p_1M": (1_000_000, 1920, 1080),
+    "cfg4_bicycle_6M": (6_100_000, 1600, 1063),
+    "small": (100_000, 640, 360),
+}
+
+
+def algorithmic_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: int) -> float:
+    """Compulsory HBM bytes of one launch of `stage`."""
+    if stage == "preprocess":
+        return 20.0 * P + 289.0 * V + 4.0 * K
+    if stage == "render":
+        return 40.0 * K + 20.0 * N + 12.0 * T
+    if stage == "render_bwd":
+        return 76.0 * Kb + 20.0 * N + 12.0 * T
+    if stage == "bwd_gauss":
+        return 24.0 * P + 64.0 * V + 236.0 * P + 300.0 * P + 44.0 * V
+    if stage == "duplicate":
+        return 16.0 * V + 12.0 * K
+    if stage == "sort_tiles":
+        return 12.0 * K + 8.0 * T
+    if stage == "zero_accum":
+        return 64.0 * P
+    if stage == "tile_scan":
+        return 28.0 * T
+    return 0.0
+
+
+def load_traffic(stage: str):
+    """HBM bytes per launch of `stage` from a committed rocprofv3 PMC summary
+    (profiles/*pmc*.json written by tools/pmc_summary.py), or None."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+            if stage in d.get("per_launch_hbm_bytes", {}):
+                return float(d["per_launch_hbm_bytes"][stage])
+        except Exception:
+            continue
+    return None
+
+
+def cpu_baseline_views_per_s(P: int, W: int, H: int, seed: int = 0):
+    """The CPU oracle (scalar C port of the reference path) timed on one full
+    view, forward + backward, single thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    O.lib()
+    cam = S.make_camera(W, H)
+    sc = S.make_scene(P, cam, seed=seed)
+    s = O.settings_from_camera(cam)
+    dpix = S.make_cotangent(H, W, 1)
+    kw = dict(shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+    t0 = time.perf_counter()
+    r = O.forward(s, sc.means3D, sc.opacities, **kw)
+    O.backward(s, r, sc.means3D, dpix, **kw)
+    dt = time.perf_counter() - t0
+    return 1.0 / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2_1080p_1M", choices=sorted(CONFIGS))
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="disable the per-stage event timing")
+    ap.add_argument("--yaw-spread", type=float, default=0.0,
+                    help="rank r renders the camera yawed by (r-(N-1)/2)*spread degrees (config 5 uses 5)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+
+    P, W, H = CONFIGS[args.config]
+    cam0 = S.make_camera(W, H)
+    sc = S.make_scene(P, cam0, seed=args.seed)
+    yaw = (rank - (world - 1) / 2.0) * args.yaw_spread
+    cam = cam0 if yaw == 0.0 else S.make_orbit_camera(W, H, yaw)
+    settings = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+        bg=torch.zeros(3, device=dev), scale_modifier=1.0,
+        viewmatrix=torch.from_numpy(cam.world_view_transform).to(dev),
+        projmatrix=torch.from_numpy(cam.full_proj_transform).to(dev), sh_degree=3,
+        campos=torch.from_numpy(cam.camera_center).to(dev), prefiltered=False, debug=False)
+    params = {k: torch.from_numpy(np.ascontiguousarray(getattr(sc, k))).to(dev).requires_grad_(True)
+              for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+    means2D = torch.zeros_like(params["means3D"], requires_grad=True)
+    dpix = torch.from_numpy(S.make_cotangent(H, W, 100 + rank)).to(dev)
+    rasterizer = GaussianRasterizer(settings)
+    order = ("means3D", "shs", "opacities", "scales", "rotations")
+
+    def step():
+        for p in params.values():
+            p.grad = None
+        means2D.grad = None
+        color, radii = rasterizer(means3D=params["means3D"], means2D=means2D, opacities=params["opacities"],
+                                  shs=params["shs"], scales=params["scales"], rotations=params["rotations"])
+        torch.autograd.backward(color, dpix)
+        if distributed:
+            flat = torch.cat([params[k].grad.reshape(-1) for k in order])
+            dist.all_reduce(flat)
+        return color
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if not args.no_profile:
+        _C.profile_enable(True)
+        _C.profile_read(True)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    prof = {}
+    if not args.no_profile:
+        prof = _C.profile_read(True)
+        _C.profile_enable(False)
+    if distributed:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms_per_step = 1000.0 * elapsed / args.steps
+    views = world * args.steps
+    value = views / elapsed
+
+    result = None
+    if rank == 0:
+        # Workload statistics (K, V, ...) from one extra forward, outside the timed region.
+        with torch.no_grad():
+            K, color, radii, geom, binning, img = _C.rasterize_gaussians(
+                settings.bg, params["means3D"], torch.Tensor([]), params["opacities"], params["scales"],
+                params["rotations"], 1.0, torch.Tensor([]), settings.viewmatrix, settings.projmatrix,
+                settings.tanfovx, settings.tanfovy, H, W, params["shs"], 3, settings.campos, False, False)
+            bufs = _C.parse_buffers(geom, binning, img, P, K, W, H, 16)
+        V = int((radii > 0).sum().item())
+        rng = bufs["ranges"].cpu().numpy().astype(np.int64)
+        n_t = rng[:, 1] - rng[:, 0]
+        Kb = int(np.minimum(n_t, bufs["max_contrib"].cpu().numpy().astype(np.int64)).sum())
+        N = W * H
+        T = ((W + 15) // 16) * ((H + 15) // 16)
+        stages = {}
+        for name, (ms, cnt) in prof.items():
+            if cnt:
+                stages[name] = {"avg_ms": ms / cnt, "launches": cnt, "ms_per_step": ms / args.steps}
+        roofline = None
+        if stages:
+            dom = max(stages, key=lambda n: stages[n]["ms_per_step"])
+            by = algorithmic_bytes(dom, P, V, K, Kb, N, T)
+            ach = by / (stages[dom]["avg_ms"] * 1e-3) / 1e9
+            roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic(dom),
+                        "algorithmic_bytes": by, "avg_ms": round(stages[dom]["avg_ms"], 4)}
+            for n, st in stages.items():
+                b = algorithmic_bytes(n, P, V, K, Kb, N, T)
+                st["algorithmic_GBps"] = round(b / (st["avg_ms"] * 1e-3) / 1e9, 1) if b else None
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            v, dt = cpu_baseline_views_per_s(P, W, H, args.seed)
+            cpu = {"value": v, "unit": "views/s", "cores": 1, "kind": "port",
+                   "sample": f"one full {W}x{H} view, {P} Gaussians, fwd+bwd, CPU oracle (C, 1 thread): {dt:.1f} s"}
+        result = {
+            "metric": "rendered views/sec (fwd+bwd) at 1080p, 1M Gaussians; achieved HBM GB/s %",
+            "value": value, "unit": "views/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32", "data": "synthetic (SURVEY §8(d) generator, seed 0)",
+            "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, 16x16 tiles, forward+backward, "
+                                   f"1 view per GPU per step" + (" + RCCL all-reduce of 59 f32/Gaussian grads"
+                                                                 if world > 1 else ""),
+                       "P": P, "width": W, "height": H, "views_per_gpu_per_step": 1,
+                       "parallelism": f"dp{world}", "K_instances": K, "V_visible": V, "K_bwd_entries": Kb},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "stages": stages,
+        }
+        print(json.dumps(result), flush=True)
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,470 @@
+// backward.hip -- gradients on gfx950.
+//
+// render_bwd_kernel follows base/cr/backward.cu:399-557 (renderCUDA
+// backward): per pixel, back-to-front replay from n_contrib with the same
+// T/accum_rec recurrences and the same nine per-(pixel, Gaussian) gradient
+// terms.  What changes is where the sums go: the reference issues 9 global
+// float atomics per contributing (pixel, Gaussian) pair -- on MI355X those
+// are memory-side atomics at ~one 64-B request each, and 64 lanes hitting one
+// address serialise.  Here, per Gaussian j of the LDS batch:
+//   1. each wave sums its 64 lanes' 9 terms in registers (skipped when no lane
+//      of the wave contributes -- a wave-uniform ballot),
+//   2. one lane per wave adds the 9 sums into an LDS accumulator (ds_add_f32),
+//   3. at the end of the batch the block flushes each Gaussian's 9 sums as a
+//      single 64-B row of grad_accum[P][16] (16 lanes per row, 4 rows per
+//      wave instruction): one memory-side request per (tile, Gaussian).
+// The backward also starts each tile at max(n_contrib) of its pixels
+// (recorded by the forward) instead of the end of the range: entries past it
+// are skipped by every pixel in the reference too.
+//
+// backward_gaussians_kernel fuses computeCov2DCUDA (base/cr/backward.cu:
+// 144-274), preprocessCUDA (:346-396), computeColorFromSH (:20-139) and
+// computeCov3D (:278-341) into one per-Gaussian pass that also emits the
+// reference's dL_dmeans2D / dL_dconic / dL_dopacity / dL_dcolors layout from
+// grad_accum, and writes every output element (zeros included).
+#include "gs_device.cuh"
+#include "gs_kernels.h"
+
+namespace gsamd {
+
+constexpr int kBlk = 256;
+constexpr int kNG = 9;  // gradient terms per (pixel, Gaussian)
+
+__global__ void __launch_bounds__(kBlk) render_bwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
+                                                          const uint32_t* __restrict__ max_contrib,
+                                                          const uint32_t* __restrict__ point_list,
+                                                          const float2* __restrict__ means2D,
+                                                          const float4* __restrict__ conic_opacity,
+                                                          const float* __restrict__ colors,
+                                                          const float* __restrict__ final_Ts,
+                                                          const uint32_t* __restrict__ n_contrib,
+                                                          const float* __restrict__ dL_dpixels,
+                                                          const float* __restrict__ bg,
+                                                          float* __restrict__ grad_accum) {
+#pragma clang fp contract(fast)
+    __shared__ uint32_t s_id[kBlk];
+    __shared__ float2 s_xy[kBlk];
+    __shared__ float4 s_co[kBlk];
+    __shared__ float4 s_rgb[kBlk];
+    __shared__ float s_acc[kBlk * kNG];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const uint32_t px = blockIdx.x * 16 + (tid & 15);
+    const uint32_t py = blockIdx.y * 16 + (tid >> 4);
+    const bool inside = px < (uint32_t)W && py < (uint32_t)H;
+    const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
+    const int n = (int)(range.y - range.x);
+    const int m = min(n, (int)max_contrib[tile]);
+    if (m == 0) return;  // block-uniform
+
+    const size_t plane = (size_t)H * W;
+    const uint32_t pid = inside ? (uint32_t)W * py + px : 0u;
+    const float T_final = inside ? final_Ts[pid] : 0.f;
+    float T = T_final;
+    const uint32_t last_contributor = inside ? n_contrib[pid] : 0u;
+    float dpx[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) dpx[c] = inside ? dL_dpixels[c * plane + pid] : 0.f;
+    float accum_rec[3] = {0.f, 0.f, 0.f}, last_color[3] = {0.f, 0.f, 0.f};
+    float last_alpha = 0.f;
+    const float bg_dot_dpixel = bg[0] * dpx[0] + bg[1] * dpx[1] + bg[2] * dpx[2];
+    const float ddelx_dx = (float)(0.5 * W);
+    const float ddely_dy = (float)(0.5 * H);
+    const float pxf = (float)px, pyf = (float)py;
+
+    const int rounds = (m + kBlk - 1) / kBlk;
+    for (int b = 0; b < rounds; b++) {
+        const int top = m - b * kBlk;  // entries [top-cnt, top) in reverse
+        const int cnt = min(kBlk, top);
+        __syncthreads();
+        if (tid < cnt) {
+            const uint32_t id = point_list[range.x + top - 1 - tid];
+            s_id[tid] = id;
+            s_xy[tid] = means2D[id];
+            s_co[tid] = conic_opacity[id];
+            s_rgb[tid] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2], 0.f);
+        }
+#pragma unroll
+        for (int q = 0; q < kNG; q++) s_acc[q * kBlk + tid] = 0.f;
+        __syncthreads();
+
+        for (int k = 0; k < cnt; k++) {
+            const uint32_t contributor = (uint32_t)(top - 1 - k);
+            float g[kNG];
+#pragma unroll
+            for (int q = 0; q < kNG; q++) g[q] = 0.f;
+            bool contrib = contributor < last_contributor;
+            if (contrib) {
+                const float2 xy = s_xy[k];
+                const float4 co = s_co[k];
+                const float dx = xy.x - pxf, dy = xy.y - pyf;
+                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                const float G = __expf(power);
+                const float alpha = fminf(0.99f, co.w * G);
+                contrib = !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                if (contrib) {
+                    T = T / (1.f - alpha);
+                    const float dchannel_dcolor = alpha * T;
+                    const float4 cf = s_rgb[k];
+                    const float cc[3] = {cf.x, cf.y, cf.z};
+                    float dL_dalpha = 0.0f;
+#pragma unroll
+                    for (int ch = 0; ch < 3; ch++) {
+                        accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
+                        last_color[ch] = cc[ch];
+                        dL_dalpha += (cc[ch] - accum_rec[ch]) * dpx[ch];
+                        g[ch] = dchannel_dcolor * dpx[ch];
+                    }
+                    dL_dalpha *= T;
+                    last_alpha = alpha;
+                    dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
+                    const float dL_dG = co.w * dL_dalpha;
+                    const float gdx = G * dx;
+                    const float gdy = G * dy;
+                    const float dG_ddelx = -gdx * co.x - gdy * co.y;
+                    const float dG_ddely = -gdy * co.z - gdx * co.y;
+                    g[3] = dL_dG * dG_ddelx * ddelx_dx;
+                    g[4] = dL_dG * dG_ddely * ddely_dy;
+                    g[5] = -0.5f * gdx * dx * dL_dG;
+                    g[6] = -0.5f * gdx * dy * dL_dG;
+                    g[7] = -0.5f * gdy * dy * dL_dG;
+                    g[8] = G * dL_dalpha;
+                }
+            }
+            if (__ballot(contrib) != 0ull) {  // wave-uniform
+#pragma unroll
+                for (int q = 0; q < kNG; q++) g[q] = wave_sum(g[q]);
+                if (lane == 0) {
+#pragma unroll
+                    for (int q = 0; q < kNG; q++) atomicAdd(&s_acc[q * kBlk + k], g[q]);
+                }
+            }
+        }
+        __syncthreads();
+        // Flush: 16 lanes per Gaussian row, 4 rows per wave instruction.
+        const int wave = tid >> 6;
+        const int comp = lane & 15;
+        for (int r = wave * 4 + (lane >> 4); r < cnt; r += 16) {
+            if (comp < kNG) {
+                const float v = s_acc[comp * kBlk + r];
+                if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[r] * kGradRow + comp], v);
+            }
+        }
+    }
+}
+
+void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
+                            const float* colors, const float* bg, const float* dL_dpix, hipStream_t s) {
+    const int gx = (W + 15) / 16, gy = (H + 15) / 16;
+    if (gx == 0 || gy == 0) return;
+    hipLaunchKernelGGL(render_bwd_kernel, dim3(gx, gy), dim3(kBlk), 0, s, W, H, img.ranges, img.max_contrib,
+                       b.point_list, reinterpret_cast<const float2*>(g.means2D),
+                       reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,
+                       dL_dpix, bg, g.grad_accum);
+}
+
+// ------------------------------------------------------ per-Gaussian bwd ---
+__device__ __forceinline__ void dnormvdv3(float vx, float vy, float vz, float dx, float dy, float dz, float& ox,
+                                          float& oy, float& oz) {
+    // base/cr/auxiliary.h:107-117
+    const float sum2 = vx * vx + vy * vy + vz * vz;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    ox = ((+sum2 - vx * vx) * dx - vy * vx * dy - vz * vx * dz) * invsum32;
+    oy = (-vx * vy * dx + (sum2 - vy * vy) * dy - vz * vy * dz) * invsum32;
+    oz = (-vx * vz * dx - vy * vz * dy + (sum2 - vz * vz) * dz) * invsum32;
+}
+
+template <bool kHasSH, bool kHasScales>
+__global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussArgs a, const float* __restrict__ grad_accum,
+                                                                 const uint8_t* __restrict__ clamped_bits) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    const bool vis = a.radii[idx] > 0;
+    // Blend-stage gradients in the reference layout.
+    float acc[kNG];
+    if (vis) {
+        const float4* row = reinterpret_cast<const float4*>(grad_accum + (size_t)idx * kGradRow);
+        const float4 r0 = row[0], r1 = row[1];
+        const float r2 = grad_accum[(size_t)idx * kGradRow + 8];
+        acc[0] = r0.x; acc[1] = r0.y; acc[2] = r0.z; acc[3] = r0.w;
+        acc[4] = r1.x; acc[5] = r1.y; acc[6] = r1.z; acc[7] = r1.w; acc[8] = r2;
+    } else {
+#pragma unroll
+        for (int q = 0; q < kNG; q++) acc[q] = 0.f;
+    }
+    a.dL_dcolor[3 * idx + 0] = acc[0];
+    a.dL_dcolor[3 * idx + 1] = acc[1];
+    a.dL_dcolor[3 * idx + 2] = acc[2];
+    a.dL_dmean2D[3 * idx + 0] = acc[3];
+    a.dL_dmean2D[3 * idx + 1] = acc[4];
+    a.dL_dmean2D[3 * idx + 2] = 0.f;
+    reinterpret_cast<float4*>(a.dL_dconic)[idx] = make_float4(acc[5], acc[6], 0.f, acc[7]);
+    a.dL_dopacity[idx] = acc[8];
+
+    const int ncoef_out = a.M;  // dL_dsh is [P, M, 3]
+    if (!vis) {
+#pragma unroll
+        for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = 0.f;
+        if (kHasSH)
+            for (int i = 0; i < ncoef_out * 3; i++) a.dL_dsh[(size_t)idx * ncoef_out * 3 + i] = 0.f;
+        for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = 0.f;
+        for (int i = 0; i < 4; i++) a.dL_drot[4 * idx + i] = 0.f;
+        return;
+    }
+
+    const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
+    const Mat4 V = load_mat4(a.viewmatrix);
+    const Mat4 Pm = load_mat4(a.projmatrix);
+    float cov3D[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D[6 * idx + i];
+
+    // ---- computeCov2DCUDA (backward.cu:144-274)
+    float dmean[3];
+    float dcov[6];
+    {
+        const float h_x = a.focal_x, h_y = a.focal_y;
+        const float dcx = acc[5], dcy = acc[6], dcz = acc[7];  // dL_dconic (x, y, w)
+        float3 t = transform_point_4x3(mx, my, mz, V);
+        const float limx = 1.3f * a.tan_fovx;
+        const float limy = 1.3f * a.tan_fovy;
+        const float txtz = t.x / t.z;
+        const float tytz = t.y / t.z;
+        t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+        t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+        const float x_grad_mul = txtz < -limx || txtz > limx ? 0 : 1;
+        const float y_grad_mul = tytz < -limy || tytz > limy ? 0 : 1;
+        const Mat3 J = mat3_cols(h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z), 0.0f, h_y / t.z,
+                                 -(h_y * t.y) / (t.z * t.z), 0, 0, 0);
+        const float* v = V.m;
+        const Mat3 Wm = mat3_cols(v[0], v[4], v[8], v[1], v[5], v[9], v[2], v[6], v[10]);
+        const Mat3 Vrk = mat3_cols(cov3D[0], cov3D[1], cov3D[2], cov3D[1], cov3D[3], cov3D[4], cov3D[2], cov3D[4],
+                                   cov3D[5]);
+        const Mat3 T = mat3_mul(Wm, J);
+        Mat3 cov2D = mat3_mul(mat3_mul(mat3_transpose(T), mat3_transpose(Vrk)), T);
+        const float aa = cov2D.m[0][0] += 0.3f;
+        const float bb = cov2D.m[0][1];
+        const float cc = cov2D.m[1][1] += 0.3f;
+        const float denom = aa * cc - bb * bb;
+        float dL_da = 0, dL_db = 0, dL_dc = 0;
+        const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+        const auto& Tm = T.m;
+        const auto& Vm = Vrk.m;
+        if (denom2inv != 0) {
+            dL_da = denom2inv * (-cc * cc * dcx + 2 * bb * cc * dcy + (denom - aa * cc) * dcz);
+            dL_dc = denom2inv * (-aa * aa * dcz + 2 * aa * bb * dcy + (denom - aa * cc) * dcx);
+            dL_db = denom2inv * 2 * (bb * cc * dcx - (denom + 2 * bb * bb) * dcy + aa * bb * dcz);
+            dcov[0] = (Tm[0][0] * Tm[0][0] * dL_da + Tm[0][0] * Tm[1][0] * dL_db + Tm[1][0] * Tm[1][0] * dL_dc);
+            dcov[3] = (Tm[0][1] * Tm[0][1] * dL_da + Tm[0][1] * Tm[1][1] * dL_db + Tm[1][1] * Tm[1][1] * dL_dc);
+            dcov[5] = (Tm[0][2] * Tm[0][2] * dL_da + Tm[0][2] * Tm[1][2] * dL_db + Tm[1][2] * Tm[1][2] * dL_dc);
+            dcov[1] = 2 * Tm[0][0] * Tm[0][1] * dL_da + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_db +
+                      2 * Tm[1][0] * Tm[1][1] * dL_dc;
+            dcov[2] = 2 * Tm[0][0] * Tm[0][2] * dL_da + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_db +
+                      2 * Tm[1][0] * Tm[1][2] * dL_dc;
+            dcov[4] = 2 * Tm[0][2] * Tm[0][1] * dL_da + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_db +
+                      2 * Tm[1][1] * Tm[1][2] * dL_dc;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 6; i++) dcov[i] = 0;
+        }
+        const float dL_dT00 = 2 * (Tm[0][0] * Vm[0][0] + Tm[0][1] * Vm[0][1] + Tm[0][2] * Vm[0][2]) * dL_da +
+                              (Tm[1][0] * Vm[0][0] + Tm[1][1] * Vm[0][1] + Tm[1][2] * Vm[0][2]) * dL_db;
+        const float dL_dT01 = 2 * (Tm[0][0] * Vm[1][0] + Tm[0][1] * Vm[1][1] + Tm[0][2] * Vm[1][2]) * dL_da +
+                              (Tm[1][0] * Vm[1][0] + Tm[1][1] * Vm[1][1] + Tm[1][2] * Vm[1][2]) * dL_db;
+        const float dL_dT02 = 2 * (Tm[0][0] * Vm[2][0] + Tm[0][1] * Vm[2][1] + Tm[0][2] * Vm[2][2]) * dL_da +
+                              (Tm[1][0] * Vm[2][0] + Tm[1][1] * Vm[2][1] + Tm[1][2] * Vm[2][2]) * dL_db;
+        const float dL_dT10 = 2 * (Tm[1][0] * Vm[0][0] + Tm[1][1] * Vm[0][1] + Tm[1][2] * Vm[0][2]) * dL_dc +
+                              (Tm[0][0] * Vm[0][0] + Tm[0][1] * Vm[0][1] + Tm[0][2] * Vm[0][2]) * dL_db;
+        const float dL_dT11 = 2 * (Tm[1][0] * Vm[1][0] + Tm[1][1] * Vm[1][1] + Tm[1][2] * Vm[1][2]) * dL_dc +
+                              (Tm[0][0] * Vm[1][0] + Tm[0][1] * Vm[1][1] + Tm[0][2] * Vm[1][2]) * dL_db;
+        const float dL_dT12 = 2 * (Tm[1][0] * Vm[2][0] + Tm[1][1] * Vm[2][1] + Tm[1][2] * Vm[2][2]) * dL_dc +
+                              (Tm[0][0] * Vm[2][0] + Tm[0][1] * Vm[2][1] + Tm[0][2] * Vm[2][2]) * dL_db;
+        const auto& Wq = Wm.m;
+        const float dL_dJ00 = Wq[0][0] * dL_dT00 + Wq[0][1] * dL_dT01 + Wq[0][2] * dL_dT02;
+        const float dL_dJ02 = Wq[2][0] * dL_dT00 + Wq[2][1] * dL_dT01 + Wq[2][2] * dL_dT02;
+        const float dL_dJ11 = Wq[1][0] * dL_dT10 + Wq[1][1] * dL_dT11 + Wq[1][2] * dL_dT12;
+        const float dL_dJ12 = Wq[2][0] * dL_dT10 + Wq[2][1] * dL_dT11 + Wq[2][2] * dL_dT12;
+        const float tz = 1.f / t.z;
+        const float tz2 = tz * tz;
+        const float tz3 = tz2 * tz;
+        const float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
+        const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
+        const float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
+                             (2 * h_y * t.y) * tz3 * dL_dJ12;
+        // transformVec4x3Transpose (auxiliary.h:89-97): assign (=)
+        dmean[0] = v[0] * dL_dtx + v[1] * dL_dty + v[2] * dL_dtz;
+        dmean[1] = v[4] * dL_dtx + v[5] * dL_dty + v[6] * dL_dtz;
+        dmean[2] = v[8] * dL_dtx + v[9] * dL_dty + v[10] * dL_dtz;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = dcov[i];
+
+    // ---- preprocessCUDA backward (backward.cu:370-387): projection part (+=)
+    {
+        const float* proj = Pm.m;
+        const float4 m_hom = transform_point_4x4(mx, my, mz, Pm);
+        const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+        const float mul1 = (proj[0] * mx + proj[4] * my + proj[8] * mz + proj[12]) * m_w * m_w;
+        const float mul2 = (proj[1] * mx + proj[5] * my + proj[9] * mz + proj[13]) * m_w * m_w;
+        const float gx = acc[3], gy = acc[4];
+        dmean[0] += (proj[0] * m_w - proj[3] * mul1) * gx + (proj[1] * m_w - proj[3] * mul2) * gy;
+        dmean[1] += (proj[4] * m_w - proj[7] * mul1) * gx + (proj[5] * m_w - proj[7] * mul2) * gy;
+        dmean[2] += (proj[8] * m_w - proj[11] * mul1) * gx + (proj[9] * m_w - proj[11] * mul2) * gy;
+    }
+
+    // ---- computeColorFromSH backward (backward.cu:20-139)
+    if (kHasSH) {
+        const int deg = a.D;
+        const int ncoef = (deg + 1) * (deg + 1);
+        const float* sh = a.shs + (size_t)idx * a.M * 3;
+        float* dsh = a.dL_dsh + (size_t)idx * a.M * 3;
+        const float dox = mx - a.campos[0], doy = my - a.campos[1], doz = mz - a.campos[2];
+        const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
+        const float x = dox / len, y = doy / len, z = doz / len;
+        const uint8_t cb = clamped_bits[idx];
+        float dRGB[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) dRGB[c] = acc[c] * (((cb >> c) & 1) ? 0.0f : 1.0f);
+        float dx3[3] = {0, 0, 0}, dy3[3] = {0, 0, 0}, dz3[3] = {0, 0, 0};
+        float dsh_c[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) dsh_c[k] = 0.f;
+        dsh_c[0] = SH_C0;
+        float s[16][3];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) s[k][c] = (k < ncoef) ? sh[3 * k + c] : 0.f;
+        if (deg > 0) {
+            dsh_c[1] = -SH_C1 * y;
+            dsh_c[2] = SH_C1 * z;
+            dsh_c[3] = -SH_C1 * x;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                dx3[c] = -SH_C1 * s[3][c];
+                dy3[c] = -SH_C1 * s[1][c];
+                dz3[c] = SH_C1 * s[2][c];
+            }
+            if (deg > 1) {
+                const float xx = x * x, yy = y * y, zz = z * z;
+                const float xy = x * y, yz = y * z, xz = x * z;
+                dsh_c[4] = SH_C2_0 * xy;
+                dsh_c[5] = SH_C2_1 * yz;
+                dsh_c[6] = SH_C2_2 * (2.f * zz - xx - yy);
+                dsh_c[7] = SH_C2_3 * xz;
+                dsh_c[8] = SH_C2_4 * (xx - yy);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    dx3[c] += SH_C2_0 * y * s[4][c] + SH_C2_2 * 2.f * -x * s[6][c] + SH_C2_3 * z * s[7][c] +
+                              SH_C2_4 * 2.f * x * s[8][c];
+                    dy3[c] += SH_C2_0 * x * s[4][c] + SH_C2_1 * z * s[5][c] + SH_C2_2 * 2.f * -y * s[6][c] +
+                              SH_C2_4 * 2.f * -y * s[8][c];
+                    dz3[c] += SH_C2_1 * y * s[5][c] + SH_C2_2 * 2.f * 2.f * z * s[6][c] + SH_C2_3 * x * s[7][c];
+                }
+                if (deg > 2) {
+                    dsh_c[9] = SH_C3_0 * y * (3.f * xx - yy);
+                    dsh_c[10] = SH_C3_1 * xy * z;
+                    dsh_c[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
+                    dsh_c[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                    dsh_c[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
+                    dsh_c[14] = SH_C3_5 * z * (xx - yy);
+                    dsh_c[15] = SH_C3_6 * x * (xx - 3.f * yy);
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        dx3[c] += (SH_C3_0 * s[9][c] * 3.f * 2.f * xy + SH_C3_1 * s[10][c] * yz +
+                                   SH_C3_2 * s[11][c] * -2.f * xy + SH_C3_3 * s[12][c] * -3.f * 2.f * xz +
+                                   SH_C3_4 * s[13][c] * (-3.f * xx + 4.f * zz - yy) + SH_C3_5 * s[14][c] * 2.f * xz +
+                                   SH_C3_6 * s[15][c] * 3.f * (xx - yy));
+                        dy3[c] += (SH_C3_0 * s[9][c] * 3.f * (xx - yy) + SH_C3_1 * s[10][c] * xz +
+                                   SH_C3_2 * s[11][c] * (-3.f * yy + 4.f * zz - xx) +
+                                   SH_C3_3 * s[12][c] * -3.f * 2.f * yz + SH_C3_4 * s[13][c] * -2.f * xy +
+                                   SH_C3_5 * s[14][c] * -2.f * yz + SH_C3_6 * s[15][c] * -3.f * 2.f * xy);
+                        dz3[c] += (SH_C3_1 * s[10][c] * xy + SH_C3_2 * s[11][c] * 4.f * 2.f * yz +
+                                   SH_C3_3 * s[12][c] * 3.f * (2.f * zz - xx - yy) + SH_C3_4 * s[13][c] * 4.f * 2.f * xz +
+                                   SH_C3_5 * s[14][c] * (xx - yy));
+                    }
+                }
+            }
+        }
+        for (int k = 0; k < a.M; k++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) dsh[3 * k + c] = (k < ncoef) ? dsh_c[k] * dRGB[c] : 0.f;
+        const float ddx = dot3(dx3[0], dx3[1], dx3[2], dRGB[0], dRGB[1], dRGB[2]);
+        const float ddy = dot3(dy3[0], dy3[1], dy3[2], dRGB[0], dRGB[1], dRGB[2]);
+        const float ddz = dot3(dz3[0], dz3[1], dz3[2], dRGB[0], dRGB[1], dRGB[2]);
+        float ox, oy, oz;
+        dnormvdv3(dox, doy, doz, ddx, ddy, ddz, ox, oy, oz);
+        dmean[0] += ox;
+        dmean[1] += oy;
+        dmean[2] += oz;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = dmean[i];
+
+    // ---- computeCov3D backward (backward.cu:278-341)
+    if (kHasScales) {
+        const float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
+        const float r = q.x, x = q.y, y = q.z, z = q.w;
+        const Mat3 R = quat_to_R(r, x, y, z);
+        const float sx = a.scale_modifier * a.scales[3 * idx + 0];
+        const float sy = a.scale_modifier * a.scales[3 * idx + 1];
+        const float sz = a.scale_modifier * a.scales[3 * idx + 2];
+        Mat3 S = mat3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+        S.m[0][0] = sx; S.m[1][1] = sy; S.m[2][2] = sz;
+        const Mat3 Mm = mat3_mul(S, R);
+        const float* dc = dcov;
+        const Mat3 dL_dSigma = mat3_cols(dc[0], 0.5f * dc[1], 0.5f * dc[2], 0.5f * dc[1], dc[3], 0.5f * dc[4],
+                                         0.5f * dc[2], 0.5f * dc[4], dc[5]);
+        Mat3 M2;
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+#pragma unroll
+            for (int rr = 0; rr < 3; rr++) M2.m[c][rr] = 2.0f * Mm.m[c][rr];
+        const Mat3 dL_dM = mat3_mul(M2, dL_dSigma);
+        const Mat3 Rt = mat3_transpose(R);
+        Mat3 D = mat3_transpose(dL_dM);
+        a.dL_dscale[3 * idx + 0] = dot3(Rt.m[0][0], Rt.m[0][1], Rt.m[0][2], D.m[0][0], D.m[0][1], D.m[0][2]);
+        a.dL_dscale[3 * idx + 1] = dot3(Rt.m[1][0], Rt.m[1][1], Rt.m[1][2], D.m[1][0], D.m[1][1], D.m[1][2]);
+        a.dL_dscale[3 * idx + 2] = dot3(Rt.m[2][0], Rt.m[2][1], Rt.m[2][2], D.m[2][0], D.m[2][1], D.m[2][2]);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            D.m[0][k] *= sx;
+            D.m[1][k] *= sy;
+            D.m[2][k] *= sz;
+        }
+        const auto& Dm = D.m;
+        float4 dq;
+        dq.x = 2 * z * (Dm[0][1] - Dm[1][0]) + 2 * y * (Dm[2][0] - Dm[0][2]) + 2 * x * (Dm[1][2] - Dm[2][1]);
+        dq.y = 2 * y * (Dm[1][0] + Dm[0][1]) + 2 * z * (Dm[2][0] + Dm[0][2]) + 2 * r * (Dm[1][2] - Dm[2][1]) -
+               4 * x * (Dm[2][2] + Dm[1][1]);
+        dq.z = 2 * x * (Dm[1][0] + Dm[0][1]) + 2 * r * (Dm[2][0] - Dm[0][2]) + 2 * z * (Dm[1][2] + Dm[2][1]) -
+               4 * y * (Dm[2][2] + Dm[0][0]);
+        dq.w = 2 * r * (Dm[0][1] - Dm[1][0]) + 2 * x * (Dm[2][0] + Dm[0][2]) + 2 * y * (Dm[1][2] + Dm[2][1]) -
+               4 * z * (Dm[1][1] + Dm[0][0]);
+        reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
+    } else {
+        for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = 0.f;
+        for (int i = 0; i < 4; i++) a.dL_drot[4 * idx + i] = 0.f;
+    }
+}
+
+void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hipStream_t s) {
+    if (a.P == 0) return;
+    const dim3 grid((a.P + 255) / 256);
+    const bool sh = a.shs != nullptr;
+    const bool sc = a.scales != nullptr;
+    if (sh && sc)
+        hipLaunchKernelGGL((backward_gaussians_kernel<true, true>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
+    else if (sh)
+        hipLaunchKernelGGL((backward_gaussians_kernel<true, false>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
+    else if (sc)
+        hipLaunchKernelGGL((backward_gaussians_kernel<false, true>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
+    else
+        hipLaunchKernelGGL((backward_gaussians_kernel<false, false>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
+}
+
+}  // namespace gsamd

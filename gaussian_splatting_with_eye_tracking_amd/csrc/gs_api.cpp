@@ -1,0 +1,467 @@
+// gs_api.cpp -- C-ABI entry points (include/gsplat_amd.h): stage
+// orchestration on one HIP stream.
+//
+// Base forward follows base/cr/rasterizer_impl.cu:198-336, backward :340-434,
+// markVisible :141-153; the AMR forward amr/cr/rasterizer_impl.cu:296-694;
+// simple-knn knn/simple_knn.cu:185-221.  Differences that are deliberate
+// (all documented in DESIGN.md):
+//   * everything runs on the caller's stream (the reference uses the legacy
+//     default stream);
+//   * one blocking 16-byte read-back per forward (K plus the error and
+//     large-tile words) -- the reference does 1 (base) / 4 (AMR step 0) plus a
+//     cudaMalloc/cudaFree pair;
+//   * simple-knn has no host synchronisation at all (the reference has 2).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/gsplat_amd.h"
+#include "gs_kernels.h"
+#include "gs_layout.h"
+
+using namespace gsamd;
+
+namespace {
+
+thread_local std::string g_err;
+
+
+struct GsError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+
+#define GS_HIP_NOTHROW(expr) (void)(expr)
+#define GS_HIP(expr)                                                                                  \
+    do {                                                                                              \
+        hipError_t _e = (expr);                                                                       \
+        if (_e != hipSuccess)                                                                         \
+            throw GsError(std::string(#expr) + " failed: " + hipGetErrorString(_e) + " at " __FILE__ \
+                          ":" + std::to_string(__LINE__));                                            \
+    } while (0)
+
+// ---- optional per-stage timing (gs_profile_*): hipEvents recorded on the
+// launch stream around each stage; elapsed times are harvested lazily.
+constexpr int kStages = 12;
+const char* kStageNames[kStages] = {"preprocess", "tile_scan",    "duplicate",   "sort_tiles",
+                                    "render",     "render_bwd",   "bwd_gauss",   "amr_levels",
+                                    "amr_render", "amr_interp",   "knn",         "zero_accum"};
+enum Stage { kPre, kScan, kDup, kSort, kRender, kRenderBwd, kBwdGauss, kAmrLevels, kAmrRender, kAmrInterp, kKnn, kZero };
+struct Profiler {
+    bool on = false;
+    struct Pending { int stage; hipEvent_t a, b; };
+    std::vector<Pending> pending;
+    double total_ms[kStages] = {0};
+    long count[kStages] = {0};
+    std::vector<hipEvent_t> pool;
+    hipEvent_t get() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e; GS_HIP_NOTHROW(hipEventCreate(&e)); return e;
+    }
+    void harvest() {
+        for (auto& p : pending) {
+            float ms = 0.f;
+            if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+                total_ms[p.stage] += ms; count[p.stage] += 1;
+            }
+            pool.push_back(p.a); pool.push_back(p.b);
+        }
+        pending.clear();
+    }
+};
+Profiler g_prof;
+std::mutex g_prof_mu;
+
+struct StageTimer {
+    int stage; hipStream_t s; hipEvent_t a = nullptr, b = nullptr;
+    StageTimer(int st, hipStream_t str) : stage(st), s(str) {
+        if (!g_prof.on) return;
+        std::lock_guard<std::mutex> l(g_prof_mu);
+        a = g_prof.get(); b = g_prof.get();
+        hipEventRecord(a, s);
+    }
+    ~StageTimer() {
+        if (!a) return;
+        hipEventRecord(b, s);
+        std::lock_guard<std::mutex> l(g_prof_mu);
+        g_prof.pending.push_back({stage, a, b});
+    }
+};
+
+// CHECK_CUDA(A, debug) equivalent (base/cr/auxiliary.h:166-173): in debug
+// mode synchronise after every stage and raise on the first error.
+void stage_check(bool debug, hipStream_t s, const char* stage) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && debug) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) throw GsError(std::string("[HIP ERROR] in stage ") + stage + ": " + hipGetErrorString(e));
+}
+
+// Pinned 64-B landing zone for the single read-back per forward.
+uint32_t* pinned_words() {
+    thread_local uint32_t* p = nullptr;
+    if (!p) {
+        void* q = nullptr;
+        GS_HIP(hipHostMalloc(&q, 64, hipHostMallocDefault));
+        p = static_cast<uint32_t*>(q);
+    }
+    return p;
+}
+
+void read_header(const uint32_t* hdr_dev, uint32_t out[4], hipStream_t s) {
+    uint32_t* h = pinned_words();
+    GS_HIP(hipMemcpyAsync(h, hdr_dev, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    GS_HIP(hipStreamSynchronize(s));
+    std::memcpy(out, h, 4 * sizeof(uint32_t));
+}
+
+char* call_resize(const gs_buffer& b, size_t n, const char* what) {
+    if (!b.resize) throw GsError(std::string("no resize callback for ") + what);
+    char* p = b.resize(b.ctx, n);
+    if (!p && n > 0) throw GsError(std::string("resize failed for ") + what);
+    if (reinterpret_cast<uintptr_t>(p) % 16 != 0) throw GsError(std::string("unaligned buffer for ") + what);
+    return p;
+}
+
+template <typename F>
+int guarded(F&& f) {
+    try {
+        return f();
+    } catch (const std::exception& e) {
+        g_err = e.what();
+        return -1;
+    } catch (...) {
+        g_err = "unknown error";
+        return -1;
+    }
+}
+
+struct ForwardIn {
+    int P, D, M;
+    const float *background, *means3D, *shs, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp,
+        *viewmatrix, *projmatrix, *cam_pos;
+    int width, height;
+    float scale_modifier, tan_fovx, tan_fovy;
+    int prefiltered;
+};
+
+PreprocessArgs make_pp(const ForwardIn& in, int tile) {
+    PreprocessArgs a;
+    a.P = in.P;
+    a.D = in.D;
+    a.M = in.M;
+    a.means3D = in.means3D;
+    a.scales = in.scales;
+    a.scale_modifier = in.scale_modifier;
+    a.rotations = in.rotations;
+    a.opacities = in.opacities;
+    a.shs = in.shs;
+    a.cov3D_precomp = in.cov3D_precomp;
+    a.colors_precomp = in.colors_precomp;
+    a.viewmatrix = in.viewmatrix;
+    a.projmatrix = in.projmatrix;
+    a.cam_pos = in.cam_pos;
+    a.W = in.width;
+    a.H = in.height;
+    a.tan_fovx = in.tan_fovx;
+    a.tan_fovy = in.tan_fovy;
+    // rasterizer_impl.cu:222-223 (float arithmetic)
+    a.focal_y = (float)in.height / (2.0f * in.tan_fovy);
+    a.focal_x = (float)in.width / (2.0f * in.tan_fovx);
+    a.block = tile;
+    a.prefiltered = in.prefiltered;
+    return a;
+}
+
+struct Binned {
+    GeomView g;
+    ImageView img;
+    BinningView b;
+    int K;
+    int T;
+    int* radii;
+};
+
+// preprocess -> tile scan -> (K read-back) -> duplicate -> per-tile sort.
+Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const gs_buffer& binning,
+                          const gs_buffer& image, int* radii, int tile, bool debug, hipStream_t s) {
+    Binned r;
+    const int W = in.width, H = in.height;
+    const int gx = (W + tile - 1) / tile, gy = (H + tile - 1) / tile;
+    r.T = gx * gy;
+    const size_t N = (size_t)W * H;
+    char* gbase = call_resize(geometry, carve_geom(nullptr, in.P, nullptr), "geometry");
+    carve_geom(gbase, in.P, &r.g);
+    char* ibase = call_resize(image, carve_image(nullptr, N, r.T, nullptr), "image");
+    carve_image(ibase, N, r.T, &r.img);
+    r.radii = radii ? radii : r.g.radii;
+    GS_HIP(hipMemsetAsync(r.g.hdr, 0, kHdrWords * sizeof(uint32_t), s));
+    if (r.T > 0) GS_HIP(hipMemsetAsync(r.img.tile_count, 0, sizeof(uint32_t) * r.T, s));
+    { StageTimer _t(kPre, s); launch_preprocess(make_pp(in, tile), r.g, r.radii, r.img.tile_count, s); }
+    stage_check(debug, s, "preprocess");
+    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s); }
+    stage_check(debug, s, "tile_scan");
+    uint32_t hdr[4];
+    read_header(r.g.hdr, hdr, s);
+    if (hdr[kHdrError])
+        throw GsError("Point is filtered although prefiltered is set. This shouldn't happen!");
+    r.K = (int)hdr[kHdrNumRendered];
+    char* bbase = call_resize(binning, carve_binning(nullptr, r.K, nullptr), "binning");
+    carve_binning(bbase, r.K, &r.b);
+    if (r.K > 0) {
+        { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s); }
+        stage_check(debug, s, "duplicate");
+        { StageTimer _t(kSort, s); launch_sort_tiles(r.T, r.img, r.b, r.g.hdr, (int)hdr[kHdrNumLargeTiles], s); }
+        stage_check(debug, s, "sort_tiles");
+    }
+    return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gs_abi_version(void) { return GSPLAT_AMD_ABI_VERSION; }
+
+const char* gs_last_error(void) { return g_err.c_str(); }
+
+int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image, int P, int D, int M,
+                          const float* background, int width, int height, const float* means3D, const float* shs,
+                          const float* colors_precomp, const float* opacities, const float* scales,
+                          float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                          const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                          float tan_fovy, int prefiltered, float* out_color, int* radii, int debug, void* stream) {
+    return guarded([&]() -> int {
+        if (P <= 0) return 0;
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        ForwardIn in{P, D, M, background, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
+                     viewmatrix, projmatrix, cam_pos, width, height, scale_modifier, tan_fovx, tan_fovy, prefiltered};
+        Binned r = preprocess_and_bin(in, geometry, binning, image, radii, 16, debug != 0, s);
+        const float* feats = colors_precomp ? colors_precomp : r.g.rgb;
+        { StageTimer _t(kRender, s); launch_render_forward(width, height, r.img, r.b, r.g, feats, background, out_color, s); }
+        stage_check(debug != 0, s, "render");
+        return r.K;
+    });
+}
+
+int gs_rasterizer_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                           const float* means3D, const float* shs, const float* colors_precomp, const float* scales,
+                           float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                           const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                           float tan_fovy, const int* radii, char* geom_buffer, char* binning_buffer,
+                           char* img_buffer, const float* dL_dpix, float* dL_dmean2D, float* dL_dconic,
+                           float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
+                           float* dL_dsh, float* dL_dscale, float* dL_drot, int debug, void* stream) {
+    return guarded([&]() -> int {
+        if (P <= 0) return 0;
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        const int tile = 16;
+        const int T = ((width + tile - 1) / tile) * ((height + tile - 1) / tile);
+        GeomView g;
+        ImageView img;
+        BinningView b;
+        carve_geom(geom_buffer, P, &g);
+        carve_image(img_buffer, (size_t)width * height, T, &img);
+        carve_binning(binning_buffer, R, &b);
+        if (!radii) radii = g.radii;
+        { StageTimer _t(kZero, s); GS_HIP(hipMemsetAsync(g.grad_accum, 0, sizeof(float) * kGradRow * (size_t)P, s)); }
+        const float* colors = colors_precomp ? colors_precomp : g.rgb;
+        if (R > 0) { StageTimer _t(kRenderBwd, s); launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s); }
+        stage_check(debug != 0, s, "render_backward");
+        BackwardGaussArgs a;
+        a.P = P;
+        a.D = D;
+        a.M = M;
+        a.means3D = means3D;
+        a.radii = radii;
+        a.shs = shs;
+        a.scales = scales;
+        a.rotations = rotations;
+        a.scale_modifier = scale_modifier;
+        a.cov3D = cov3D_precomp ? cov3D_precomp : g.cov3D;
+        a.viewmatrix = viewmatrix;
+        a.projmatrix = projmatrix;
+        a.campos = campos;
+        a.focal_y = (float)height / (2.0f * tan_fovy);
+        a.focal_x = (float)width / (2.0f * tan_fovx);
+        a.tan_fovx = tan_fovx;
+        a.tan_fovy = tan_fovy;
+        a.has_cov_precomp = cov3D_precomp != nullptr;
+        a.dL_dmean2D = dL_dmean2D;
+        a.dL_dconic = dL_dconic;
+        a.dL_dopacity = dL_dopacity;
+        a.dL_dcolor = dL_dcolor;
+        a.dL_dmean3D = dL_dmean3D;
+        a.dL_dcov3D = dL_dcov3D;
+        a.dL_dsh = dL_dsh;
+        a.dL_dscale = dL_dscale;
+        a.dL_drot = dL_drot;
+        { StageTimer _t(kBwdGauss, s); launch_backward_gaussians(a, g, s); }
+        stage_check(debug != 0, s, "preprocess_backward");
+        return 0;
+    });
+}
+
+int gs_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                               uint8_t* present, void* stream) {
+    return guarded([&]() -> int {
+        launch_mark_visible(P, means3D, viewmatrix, projmatrix, reinterpret_cast<bool*>(present),
+                            static_cast<hipStream_t>(stream));
+        stage_check(false, static_cast<hipStream_t>(stream), "mark_visible");
+        return 0;
+    });
+}
+
+int gs_amr_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image, int P, int D, int M,
+                              const float* background, int width, int height, const float* means3D,
+                              const float* shs, const float* colors_precomp, const float* opacities,
+                              const float* scales, float scale_modifier, const float* rotations,
+                              const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                              const float* cam_pos, float tan_fovx, float tan_fovy, int prefiltered, int foveaStep,
+                              const float* out_color_precomp, char* geom_buffer_precomp,
+                              char* binning_buffer_precomp, char* image_buffer_precomp, float* out_color, int* radii,
+                              int interpolate_image, int debug, void* stream) {
+    return guarded([&]() -> int {
+        if (P <= 0) return 0;
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        const int tile = 32;
+        const int W = width, H = height;
+        const int T = ((W + tile - 1) / tile) * ((H + tile - 1) / tile);
+        const bool dbg = debug != 0;
+        if (foveaStep >= 1) {
+            // amr/cr/rasterizer_impl.cu:334-462: progressive step on precomputed buffers.
+            if (!geom_buffer_precomp || !binning_buffer_precomp || !image_buffer_precomp)
+                throw GsError("foveaStep >= 1 needs the buffers returned by foveaStep 0");
+            GeomView g;
+            ImageView img;
+            BinningView b;
+            carve_geom(geom_buffer_precomp, P, &g);
+            carve_image(image_buffer_precomp, (size_t)W * H, T, &img);
+            uint32_t hdr[4];
+            read_header(g.hdr, hdr, s);
+            const int K = (int)hdr[kHdrNumRendered];
+            carve_binning(binning_buffer_precomp, K, &b);
+            launch_fovea_levels(foveaStep, T, img, s);
+            stage_check(dbg, s, "fovea_levels");
+            const float* feats = colors_precomp ? colors_precomp : g.rgb;
+            { StageTimer _t(kAmrRender, s);
+              launch_amr_render(W, H, img, img.levels_current, img.levels_last, b, g, feats, background, out_color,
+                                foveaStep, s); }
+            stage_check(dbg, s, "amr_render");
+            if (interpolate_image) {
+                if (!out_color_precomp) throw GsError("interpolate_image at foveaStep >= 1 needs out_color_precomp");
+                launch_amr_interpolate(W, H, img, img.levels_current, img.levels_last, out_color, foveaStep,
+                                       out_color_precomp, s);
+                stage_check(dbg, s, "amr_interpolate");
+            }
+            return K;
+        }
+        ForwardIn in{P, D, M, background, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
+                     viewmatrix, projmatrix, cam_pos, width, height, scale_modifier, tan_fovx, tan_fovy, prefiltered};
+        Binned r = preprocess_and_bin(in, geometry, binning, image, radii, tile, dbg, s);
+        { StageTimer _t(kAmrLevels, s); launch_amr_levels(r.T, r.img, s); }
+        stage_check(dbg, s, "amr_levels");
+        if (foveaStep == 0) return r.K;  // step 0: buffers only (amr/cr/rasterizer_impl.cu:651)
+        launch_fovea_levels(foveaStep, r.T, r.img, s);
+        const float* feats = colors_precomp ? colors_precomp : r.g.rgb;
+        { StageTimer _t(kAmrRender, s);
+          launch_amr_render(W, H, r.img, r.img.levels, r.img.levels_last, r.b, r.g, feats, background, out_color,
+                            foveaStep, s); }
+        stage_check(dbg, s, "amr_render");
+        if (interpolate_image) {
+            launch_amr_interpolate(W, H, r.img, r.img.levels, r.img.levels_last, out_color, foveaStep,
+                                   out_color_precomp ? out_color_precomp : out_color, s);
+            stage_check(dbg, s, "amr_interpolate");
+        }
+        return r.K;
+    });
+}
+
+int gs_simple_knn(int P, const float* points, float* mean_dists, gs_buffer scratch, void* stream) {
+    return guarded([&]() -> int {
+        if (P <= 0) return 0;
+        char* ws = call_resize(scratch, knn_workspace_bytes(P), "knn scratch");
+        { StageTimer _t(kKnn, static_cast<hipStream_t>(stream)); launch_knn(P, points, mean_dists, ws, static_cast<hipStream_t>(stream)); }
+        stage_check(false, static_cast<hipStream_t>(stream), "knn");
+        return 0;
+    });
+}
+
+void gs_profile_enable(int on) {
+    std::lock_guard<std::mutex> l(g_prof_mu);
+    g_prof.on = on != 0;
+}
+
+int gs_profile_stage_count(void) { return kStages; }
+
+const char* gs_profile_stage_name(int i) { return (i >= 0 && i < kStages) ? kStageNames[i] : ""; }
+
+void gs_profile_read(double* total_ms, long* counts, int reset) {
+    std::lock_guard<std::mutex> l(g_prof_mu);
+    g_prof.harvest();
+    for (int i = 0; i < kStages; i++) {
+        if (total_ms) total_ms[i] = g_prof.total_ms[i];
+        if (counts) counts[i] = g_prof.count[i];
+        if (reset) {
+            g_prof.total_ms[i] = 0;
+            g_prof.count[i] = 0;
+        }
+    }
+}
+
+size_t gs_geom_bytes(int P) { return carve_geom(nullptr, (size_t)P, nullptr); }
+
+size_t gs_image_bytes(int width, int height, int tile) {
+    const size_t T = (size_t)((width + tile - 1) / tile) * ((height + tile - 1) / tile);
+    return carve_image(nullptr, (size_t)width * height, T, nullptr);
+}
+
+size_t gs_binning_bytes(int K) { return carve_binning(nullptr, (size_t)K, nullptr); }
+
+size_t gs_knn_workspace_bytes(int P) { return knn_workspace_bytes(P); }
+
+int gs_geom_view_of(char* base, int P, gs_geom_view* out) {
+    GeomView g;
+    carve_geom(base, (size_t)P, &g);
+    static_assert(sizeof(GeomView) == sizeof(gs_geom_view), "view layout");
+    std::memcpy(out, &g, sizeof(g));
+    return 0;
+}
+
+int gs_image_view_of(char* base, int width, int height, int tile, gs_image_view* out) {
+    const size_t T = (size_t)((width + tile - 1) / tile) * ((height + tile - 1) / tile);
+    ImageView v;
+    carve_image(base, (size_t)width * height, T, &v);
+    static_assert(sizeof(ImageView) == sizeof(gs_image_view), "view layout");
+    std::memcpy(out, &v, sizeof(v));
+    return 0;
+}
+
+int gs_binning_view_of(char* base, int K, gs_binning_view* out) {
+    BinningView v;
+    carve_binning(base, (size_t)K, &v);
+    static_assert(sizeof(BinningView) == sizeof(gs_binning_view), "view layout");
+    std::memcpy(out, &v, sizeof(v));
+    return 0;
+}
+
+int gs_reconstruct_keys(char* geom_buffer, char* binning_buffer, char* img_buffer, int P, int K, int width,
+                        int height, int tile, uint64_t* keys_out, void* stream) {
+    return guarded([&]() -> int {
+        const int T = ((width + tile - 1) / tile) * ((height + tile - 1) / tile);
+        GeomView g;
+        ImageView img;
+        BinningView b;
+        carve_geom(geom_buffer, P, &g);
+        carve_image(img_buffer, (size_t)width * height, T, &img);
+        carve_binning(binning_buffer, K, &b);
+        if (K > 0) launch_reconstruct_keys(T, img, b, g, keys_out, static_cast<hipStream_t>(stream));
+        stage_check(false, static_cast<hipStream_t>(stream), "reconstruct_keys");
+        return 0;
+    });
+}
+
+}  // extern "C"

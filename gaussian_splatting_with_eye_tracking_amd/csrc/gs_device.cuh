@@ -1,0 +1,141 @@
+// gs_device.cuh -- device-side helpers shared by the gfx950 kernels.
+//
+// Arithmetic contract (see DESIGN.md "Parity policy"): everything that feeds
+// the tile keys (depth bits, means2D, radius) is evaluated in the exact
+// operation order of the reference with FMA contraction OFF (the library is
+// compiled with -ffp-contract=off; blend loops opt back in locally with
+// `#pragma clang fp contract(fast)`).  Matrix products expand glm's
+// column-major operator* (glm/detail/type_mat3x3.inl:486-520).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsamd {
+
+constexpr int kChannels = 3;
+constexpr int kWave = 64;
+
+// base/cr/auxiliary.h:22-39
+__device__ constexpr float SH_C0 = 0.28209479177387814f;
+__device__ constexpr float SH_C1 = 0.4886025119029199f;
+__device__ constexpr float SH_C2_0 = 1.0925484305920792f;
+__device__ constexpr float SH_C2_1 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_2 = 0.31539156525252005f;
+__device__ constexpr float SH_C2_3 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_4 = 0.5462742152960396f;
+__device__ constexpr float SH_C3_0 = -0.5900435899266435f;
+__device__ constexpr float SH_C3_1 = 2.890611442640554f;
+__device__ constexpr float SH_C3_2 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_3 = 0.3731763325901154f;
+__device__ constexpr float SH_C3_4 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_5 = 1.445305721320277f;
+__device__ constexpr float SH_C3_6 = -0.5900435899266435f;
+
+// Column-major 3x3 (glm convention: m[c][r]).
+struct Mat3 {
+    float m[3][3];
+};
+
+__device__ __forceinline__ Mat3 mat3_cols(float a0, float a1, float a2, float a3, float a4, float a5,
+                                          float a6, float a7, float a8) {
+    Mat3 r;
+    r.m[0][0] = a0; r.m[0][1] = a1; r.m[0][2] = a2;
+    r.m[1][0] = a3; r.m[1][1] = a4; r.m[1][2] = a5;
+    r.m[2][0] = a6; r.m[2][1] = a7; r.m[2][2] = a8;
+    return r;
+}
+
+__device__ __forceinline__ Mat3 mat3_mul(const Mat3& A, const Mat3& B) {
+    Mat3 R;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+            R.m[c][r] = A.m[0][r] * B.m[c][0] + A.m[1][r] * B.m[c][1] + A.m[2][r] * B.m[c][2];
+    return R;
+}
+
+__device__ __forceinline__ Mat3 mat3_transpose(const Mat3& A) {
+    Mat3 R;
+#pragma unroll
+    for (int c = 0; c < 3; c++)
+#pragma unroll
+        for (int r = 0; r < 3; r++) R.m[c][r] = A.m[r][c];
+    return R;
+}
+
+__device__ __forceinline__ float dot3(float a0, float a1, float a2, float b0, float b1, float b2) {
+    float t0 = a0 * b0, t1 = a1 * b1, t2 = a2 * b2;
+    return t0 + t1 + t2;
+}
+
+// Quaternion (r,x,y,z) -> R, un-normalised as in base/cr/forward.cu:127-138.
+__device__ __forceinline__ Mat3 quat_to_R(float r, float x, float y, float z) {
+    return mat3_cols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                     2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                     2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+}
+
+// 4x4 matrices as 16 floats, column-major like the reference (auxiliary.h:58-77).
+struct Mat4 {
+    float m[16];
+};
+
+__device__ __forceinline__ Mat4 load_mat4(const float* __restrict__ p) {
+    Mat4 r;
+#pragma unroll
+    for (int i = 0; i < 16; i++) r.m[i] = p[i];
+    return r;
+}
+
+__device__ __forceinline__ float3 transform_point_4x3(float x, float y, float z, const Mat4& M) {
+    const float* m = M.m;
+    return make_float3(m[0] * x + m[4] * y + m[8] * z + m[12], m[1] * x + m[5] * y + m[9] * z + m[13],
+                       m[2] * x + m[6] * y + m[10] * z + m[14]);
+}
+
+__device__ __forceinline__ float4 transform_point_4x4(float x, float y, float z, const Mat4& M) {
+    const float* m = M.m;
+    return make_float4(m[0] * x + m[4] * y + m[8] * z + m[12], m[1] * x + m[5] * y + m[9] * z + m[13],
+                       m[2] * x + m[6] * y + m[10] * z + m[14], m[3] * x + m[7] * y + m[11] * z + m[15]);
+}
+
+// base/cr/auxiliary.h:41-44: the double literals promote the whole expression.
+__device__ __forceinline__ float ndc2pix(float v, int S) {
+    return (float)((((double)v + 1.0) * (double)S - 1.0) * 0.5);
+}
+
+struct Rect {
+    uint32_t x0, y0, x1, y1;
+};
+
+// base/cr/auxiliary.h:46-56 (tile size as template-free runtime args; the
+// division by a power of two is exact in either form).
+__device__ __forceinline__ Rect get_rect(float px, float py, int max_radius, int bx, int by, uint32_t gx,
+                                         uint32_t gy) {
+    const float fr = (float)max_radius;
+    int a = (int)((px - fr) / (float)bx);
+    int b = (int)((py - fr) / (float)by);
+    int c = (int)(((px + fr) + (float)bx - 1.0f) / (float)bx);
+    int d = (int)(((py + fr) + (float)by - 1.0f) / (float)by);
+    a = max(a, 0); b = max(b, 0); c = max(c, 0); d = max(d, 0);
+    Rect r;
+    r.x0 = min(gx, (uint32_t)a);
+    r.y0 = min(gy, (uint32_t)b);
+    r.x1 = min(gx, (uint32_t)c);
+    r.y1 = min(gy, (uint32_t)d);
+    return r;
+}
+
+__device__ __forceinline__ uint32_t float_bits(float f) { return __float_as_uint(f); }
+
+// ---------------------------------------------------------------- wave ops
+// Sum across the 64 lanes of a wave; every lane gets the total.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, kWave);
+    return v;
+}
+
+}  // namespace gsamd

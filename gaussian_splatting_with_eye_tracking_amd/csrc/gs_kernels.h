@@ -1,0 +1,103 @@
+// gs_kernels.h -- host-side launchers of the gfx950 kernels (one per stage).
+// Every launcher enqueues on `stream` and never synchronises; the C-ABI
+// orchestrators (gs_api.cpp) own the single K read-back.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gs_layout.h"
+
+namespace gsamd {
+
+struct PreprocessArgs {
+    int P, D, M;
+    const float* means3D;
+    const float* scales;
+    float scale_modifier;
+    const float* rotations;
+    const float* opacities;
+    const float* shs;
+    const float* cov3D_precomp;
+    const float* colors_precomp;
+    const float* viewmatrix;
+    const float* projmatrix;
+    const float* cam_pos;
+    int W, H;
+    float tan_fovx, tan_fovy, focal_x, focal_y;
+    int block;  // tile edge in pixels (16 base, 32 AMR)
+    int prefiltered;
+};
+
+// base/cr/forward.cu:155-256 (+ the tile histogram the binning needs).
+void launch_preprocess(const PreprocessArgs& a, const GeomView& g, int* radii, uint32_t* tile_count,
+                       hipStream_t s);
+// base/cr/rasterizer_impl.cu:54-66
+void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                         bool* present, hipStream_t s);
+
+// Binning (replaces scan + duplicateWithKeys + radix sort + identifyTileRanges,
+// base/cr/rasterizer_impl.cu:277-318, with identical outputs).
+void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s);
+void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
+                      const BinningView& b, hipStream_t s);
+void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, const uint32_t* hdr, int num_large_host,
+                       hipStream_t s);
+// (tile << 32 | depth) reconstruction of the reference's point_list_keys.
+void launch_reconstruct_keys(int T, const ImageView& img, const BinningView& b, const GeomView& g, uint64_t* keys,
+                             hipStream_t s);
+
+// Blend (base/cr/forward.cu:261-374).
+void launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
+                           const float* features, const float* bg, float* out_color, hipStream_t s);
+// Blend backward (base/cr/backward.cu:399-557) into g.grad_accum.
+void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
+                            const float* colors, const float* bg, const float* dL_dpix, hipStream_t s);
+
+struct BackwardGaussArgs {
+    int P, D, M;
+    const float* means3D;
+    const int* radii;
+    const float* shs;
+    const float* scales;
+    const float* rotations;
+    float scale_modifier;
+    const float* cov3D;  // precomp or geom
+    const float* viewmatrix;
+    const float* projmatrix;
+    const float* campos;
+    float focal_x, focal_y, tan_fovx, tan_fovy;
+    int has_cov_precomp;
+    // outputs (every element written; no memsets needed)
+    float* dL_dmean2D;
+    float* dL_dconic;
+    float* dL_dopacity;
+    float* dL_dcolor;
+    float* dL_dmean3D;
+    float* dL_dcov3D;
+    float* dL_dsh;
+    float* dL_dscale;
+    float* dL_drot;
+};
+// base/cr/backward.cu:144-396 fused into one per-Gaussian pass.
+void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hipStream_t s);
+
+// AMR (amr/cr/rasterizer_impl.cu:181-243, amr/cr/forward.cu:261-648).
+void launch_amr_levels(int T, const ImageView& img, hipStream_t s);
+void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s);
+void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
+                       const BinningView& b, const GeomView& g, const float* features, const float* bg,
+                       float* out_color, int foveaStep, hipStream_t s);
+void launch_amr_interpolate(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
+                            float* out_color, int foveaStep, const float* out_color_precomp, hipStream_t s);
+
+// simple-knn (knn/simple_knn.cu).
+size_t knn_workspace_bytes(int P);
+void launch_knn(int P, const float* points, float* mean_dists, char* workspace, hipStream_t s);
+
+// Generic stable LSD radix sort of (u32 key, u32 value) pairs.
+size_t radix_sort_u32_workspace(int n);
+void radix_sort_pairs_u32(int n, const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
+                          uint32_t* vals_out, int end_bit, char* workspace, hipStream_t s);
+
+}  // namespace gsamd

@@ -1,0 +1,128 @@
+// gs_layout.h -- how the three opaque byte buffers of the rasterizer are carved.
+//
+// The reference hands three uint8 tensors (geomBuffer / binningBuffer /
+// imgBuffer) between forward, backward and AMR steps and carves them with
+// GeometryState/ImageState/BinningState::fromChunk
+// (base/cr/rasterizer_impl.cu:155-194, amr/cr/rasterizer_impl.cu:245-292).
+// The contract is "opaque, round-trips unchanged" (SURVEY §8(a) A13), so this
+// build chooses its own MI355X layout: structure-of-arrays, every array
+// 256-B aligned (a wave's 64 x 4 B access is one 256-B segment), and
+//   * geom   (per Gaussian, P):  depths, radii, means2D (float2), conic_opacity
+//     (float4), rgb[3], cov3D[6], clamped (1 B bitmask), tiles_touched, and a
+//     64-B-row gradient accumulator grad_accum[P][16] for the backward blend
+//     (one 64-B memory-side atomic request per (tile, Gaussian) pair);
+//   * image  (per pixel N and per tile T): accum_alpha (final T), n_contrib,
+//     ranges (uint2), tile_count, tile_cursor, max_contrib, AMR levels;
+//   * binning (per instance K): point_list, the (depth|idx) sort keys, and a
+//     scratch copy for the large-tile merge sort.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+namespace gsamd {
+
+constexpr size_t kAlign = 256;
+constexpr int kGradRow = 16;  // floats per grad_accum row (9 used)
+
+// Header words (geom buffer, device side).
+enum HdrWord : int {
+    kHdrNumRendered = 0,  // K
+    kHdrError = 1,        // nonzero: a kernel raised (e.g. prefiltered violation)
+    kHdrMaxTileCount = 2,
+    kHdrNumLargeTiles = 3,
+    kHdrP = 4,
+    kHdrT = 5,
+    kHdrWords = 64,
+};
+
+inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) & ~(a - 1); }
+
+template <typename T>
+inline T* carve(char* base, size_t& off, size_t count) {
+    off = align_up(off);
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += sizeof(T) * count;
+    return p;
+}
+
+struct GeomView {
+    uint32_t* hdr;
+    float* depths;
+    int* radii;
+    float* means2D;        // [P][2]
+    float* conic_opacity;  // [P][4]
+    float* rgb;            // [P][3]
+    float* cov3D;          // [P][6]
+    uint8_t* clamped;      // [P] bit c = channel c clamped
+    uint32_t* tiles_touched;
+    float* grad_accum;  // [P][kGradRow]
+};
+
+// base is 256-B aligned by the caller (torch allocations are).
+inline size_t carve_geom(char* base, size_t P, GeomView* v) {
+    size_t off = 0;
+    GeomView g;
+    g.hdr = carve<uint32_t>(base, off, kHdrWords);
+    g.depths = carve<float>(base, off, P);
+    g.radii = carve<int>(base, off, P);
+    g.means2D = carve<float>(base, off, 2 * P);
+    g.conic_opacity = carve<float>(base, off, 4 * P);
+    g.rgb = carve<float>(base, off, 3 * P);
+    g.cov3D = carve<float>(base, off, 6 * P);
+    g.clamped = carve<uint8_t>(base, off, P);
+    g.tiles_touched = carve<uint32_t>(base, off, P);
+    g.grad_accum = carve<float>(base, off, (size_t)kGradRow * P);
+    if (v) *v = g;
+    return align_up(off);
+}
+
+struct ImageView {
+    float* accum_alpha;   // [N]
+    uint32_t* n_contrib;  // [N]
+    uint32_t* ranges;     // [T][2]
+    uint32_t* tile_count;  // [T] (= n_intersections for AMR)
+    uint32_t* tile_cursor;
+    uint32_t* max_contrib;
+    uint32_t* levels;          // tile_AMR_levels
+    uint32_t* levels_last;     // tile_AMR_levels_last
+    uint32_t* levels_current;  // tile_AMR_levels_current
+    uint32_t* pv;              // [4] percentile values (AMR)
+    uint32_t* large_tiles;     // [T] list of tiles needing the large sort
+};
+
+inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
+    size_t off = 0;
+    ImageView g;
+    g.accum_alpha = carve<float>(base, off, N);
+    g.n_contrib = carve<uint32_t>(base, off, N);
+    g.ranges = carve<uint32_t>(base, off, 2 * T);
+    g.tile_count = carve<uint32_t>(base, off, T);
+    g.tile_cursor = carve<uint32_t>(base, off, T);
+    g.max_contrib = carve<uint32_t>(base, off, T);
+    g.levels = carve<uint32_t>(base, off, T);
+    g.levels_last = carve<uint32_t>(base, off, T);
+    g.levels_current = carve<uint32_t>(base, off, T);
+    g.pv = carve<uint32_t>(base, off, 4);
+    g.large_tiles = carve<uint32_t>(base, off, T);
+    if (v) *v = g;
+    return align_up(off);
+}
+
+struct BinningView {
+    uint32_t* point_list;  // [K]
+    uint64_t* pair_keys;   // [K]  (depth_bits << 32 | gaussian idx), grouped by tile
+    uint64_t* scratch;     // [K]  merge-sort ping-pong
+};
+
+inline size_t carve_binning(char* base, size_t K, BinningView* v) {
+    size_t off = 0;
+    BinningView g;
+    g.point_list = carve<uint32_t>(base, off, K);
+    g.pair_keys = carve<uint64_t>(base, off, K);
+    g.scratch = carve<uint64_t>(base, off, K);
+    if (v) *v = g;
+    return align_up(off);
+}
+
+}  // namespace gsamd

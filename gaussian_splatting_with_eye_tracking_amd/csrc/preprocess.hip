@@ -1,0 +1,239 @@
+// preprocess.hip -- per-Gaussian forward preprocess for gfx950.
+//
+// Follows base/cr/forward.cu:155-256 (preprocessCUDA) and its helpers
+// computeCov3D (:118-152), computeCov2D (:74-113), computeColorFromSH
+// (:20-71), in_frustum (base/cr/auxiliary.h:139-164).  One thread per
+// Gaussian; HBM-bound (≈236 B read per visible Gaussian at SH degree 3).
+//
+// MI355X-specific:
+//   * the tile histogram the binning needs is fused here:
+//     each visible Gaussian adds 1 to every tile of its rect with a no-return
+//     global atomic, so the binning needs no P-wide scan;
+//   * SH rows are read as float4 when M == 16 (192-B rows are 16-B aligned);
+//   * no FMA contraction (file compiled with -ffp-contract=off): depth,
+//     means2D and radius are bit-identical to the oracle, which makes the
+//     tile keys bit-exact.
+#include "gs_device.cuh"
+#include "gs_kernels.h"
+
+namespace gsamd {
+
+// base/cr/forward.cu:20-71.  `sh` points at this Gaussian's first coeff.
+template <bool kSH16>
+__device__ __forceinline__ float3 eval_sh_color(int deg, const float* __restrict__ sh, float x, float y,
+                                                float z, uint8_t& clamped_bits) {
+    float c[16][3];
+    const int ncoef = (deg + 1) * (deg + 1);
+    if (kSH16) {
+        const float4* s4 = reinterpret_cast<const float4*>(sh);
+        float buf[48];
+#pragma unroll
+        for (int i = 0; i < 12; i++) {
+            float4 v = (i * 4 < ncoef * 3) ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            buf[4 * i + 0] = v.x; buf[4 * i + 1] = v.y; buf[4 * i + 2] = v.z; buf[4 * i + 3] = v.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) c[k][ch] = buf[3 * k + ch];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) c[k][ch] = (k < ncoef) ? sh[3 * k + ch] : 0.f;
+    }
+    float res[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) res[ch] = SH_C0 * c[0][ch];
+    if (deg > 0) {
+        const float k1 = SH_C1 * y, k2 = SH_C1 * z, k3 = SH_C1 * x;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) res[ch] = res[ch] - k1 * c[1][ch] + k2 * c[2][ch] - k3 * c[3][ch];
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            const float k4 = SH_C2_0 * xy;
+            const float k5 = SH_C2_1 * yz;
+            const float k6 = SH_C2_2 * (2.0f * zz - xx - yy);
+            const float k7 = SH_C2_3 * xz;
+            const float k8 = SH_C2_4 * (xx - yy);
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++)
+                res[ch] = res[ch] + k4 * c[4][ch] + k5 * c[5][ch] + k6 * c[6][ch] + k7 * c[7][ch] + k8 * c[8][ch];
+            if (deg > 2) {
+                const float k9 = SH_C3_0 * y * (3.0f * xx - yy);
+                const float k10 = SH_C3_1 * xy * z;
+                const float k11 = SH_C3_2 * y * (4.0f * zz - xx - yy);
+                const float k12 = SH_C3_3 * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+                const float k13 = SH_C3_4 * x * (4.0f * zz - xx - yy);
+                const float k14 = SH_C3_5 * z * (xx - yy);
+                const float k15 = SH_C3_6 * x * (xx - 3.0f * yy);
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++)
+                    res[ch] = res[ch] + k9 * c[9][ch] + k10 * c[10][ch] + k11 * c[11][ch] + k12 * c[12][ch] +
+                              k13 * c[13][ch] + k14 * c[14][ch] + k15 * c[15][ch];
+            }
+        }
+    }
+    clamped_bits = 0;
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        res[ch] += 0.5f;
+        if (res[ch] < 0) clamped_bits |= (uint8_t)(1u << ch);
+        res[ch] = fmaxf(res[ch], 0.0f);
+    }
+    return make_float3(res[0], res[1], res[2]);
+}
+
+template <bool kHasSH, bool kSH16, bool kCovPrecomp>
+__global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomView g, int* __restrict__ radii,
+                                                         uint32_t* __restrict__ tile_count) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    radii[idx] = 0;
+    g.tiles_touched[idx] = 0;
+
+    const float mx = a.means3D[3 * idx + 0];
+    const float my = a.means3D[3 * idx + 1];
+    const float mz = a.means3D[3 * idx + 2];
+    const Mat4 V = load_mat4(a.viewmatrix);
+    const Mat4 Pm = load_mat4(a.projmatrix);
+
+    // in_frustum (auxiliary.h:139-164): near plane only.
+    const float3 p_view = transform_point_4x3(mx, my, mz, V);
+    if (p_view.z <= 0.2f) {
+        if (a.prefiltered) atomicOr(&g.hdr[kHdrError], 1u);  // the reference __trap()s here
+        return;
+    }
+    const float4 p_hom = transform_point_4x4(mx, my, mz, Pm);
+    const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+    const float p_proj_x = p_hom.x * p_w;
+    const float p_proj_y = p_hom.y * p_w;
+
+    // computeCov3D (forward.cu:118-152)
+    float cov3D[6];
+    if (kCovPrecomp) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D_precomp[6 * idx + i];
+    } else {
+        Mat3 S = mat3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+        S.m[0][0] = a.scale_modifier * a.scales[3 * idx + 0];
+        S.m[1][1] = a.scale_modifier * a.scales[3 * idx + 1];
+        S.m[2][2] = a.scale_modifier * a.scales[3 * idx + 2];
+        const float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
+        const Mat3 R = quat_to_R(q.x, q.y, q.z, q.w);
+        const Mat3 Mm = mat3_mul(S, R);
+        const Mat3 Sigma = mat3_mul(mat3_transpose(Mm), Mm);
+        cov3D[0] = Sigma.m[0][0]; cov3D[1] = Sigma.m[0][1]; cov3D[2] = Sigma.m[0][2];
+        cov3D[3] = Sigma.m[1][1]; cov3D[4] = Sigma.m[1][2]; cov3D[5] = Sigma.m[2][2];
+#pragma unroll
+        for (int i = 0; i < 6; i++) g.cov3D[6 * idx + i] = cov3D[i];
+    }
+
+    // computeCov2D (forward.cu:74-113)
+    float3 t = transform_point_4x3(mx, my, mz, V);
+    const float limx = 1.3f * a.tan_fovx;
+    const float limy = 1.3f * a.tan_fovy;
+    const float txtz = t.x / t.z;
+    const float tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const Mat3 J = mat3_cols(a.focal_x / t.z, 0.0f, -(a.focal_x * t.x) / (t.z * t.z), 0.0f, a.focal_y / t.z,
+                             -(a.focal_y * t.y) / (t.z * t.z), 0, 0, 0);
+    const float* v = V.m;
+    const Mat3 Wm = mat3_cols(v[0], v[4], v[8], v[1], v[5], v[9], v[2], v[6], v[10]);
+    const Mat3 T = mat3_mul(Wm, J);
+    const Mat3 Vrk = mat3_cols(cov3D[0], cov3D[1], cov3D[2], cov3D[1], cov3D[3], cov3D[4], cov3D[2], cov3D[4],
+                               cov3D[5]);
+    Mat3 cov = mat3_mul(mat3_mul(mat3_transpose(T), mat3_transpose(Vrk)), T);
+    cov.m[0][0] += 0.3f;
+    cov.m[1][1] += 0.3f;
+    const float cx = cov.m[0][0], cy = cov.m[0][1], cz = cov.m[1][1];
+
+    // EWA inverse + extent (forward.cu:219-237)
+    const float det = (cx * cz - cy * cy);
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float conic_x = cz * det_inv, conic_y = -cy * det_inv, conic_z = cx * det_inv;
+    const float mid = 0.5f * (cx + cz);
+    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+    const float pix_x = ndc2pix(p_proj_x, a.W);
+    const float pix_y = ndc2pix(p_proj_y, a.H);
+    const uint32_t gx = (uint32_t)((a.W + a.block - 1) / a.block);
+    const uint32_t gy = (uint32_t)((a.H + a.block - 1) / a.block);
+    const int iradius = (int)my_radius;
+    const Rect r = get_rect(pix_x, pix_y, iradius, a.block, a.block, gx, gy);
+    const uint32_t area = (r.x1 - r.x0) * (r.y1 - r.y0);
+    if (area == 0) return;
+
+    if (kHasSH) {
+        // computeColorFromSH: dir = normalize(mean - campos)
+        float dx = mx - a.cam_pos[0], dy = my - a.cam_pos[1], dz = mz - a.cam_pos[2];
+        const float len = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
+        dx = dx / len; dy = dy / len; dz = dz / len;
+        uint8_t cbits;
+        const float3 rgb = eval_sh_color<kSH16>(a.D, a.shs + (size_t)idx * a.M * 3, dx, dy, dz, cbits);
+        g.rgb[3 * idx + 0] = rgb.x;
+        g.rgb[3 * idx + 1] = rgb.y;
+        g.rgb[3 * idx + 2] = rgb.z;
+        g.clamped[idx] = cbits;
+    }
+    g.depths[idx] = p_view.z;
+    radii[idx] = iradius;
+    reinterpret_cast<float2*>(g.means2D)[idx] = make_float2(pix_x, pix_y);
+    reinterpret_cast<float4*>(g.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, a.opacities[idx]);
+    g.tiles_touched[idx] = area;
+
+    // Fused tile histogram (no-return atomics).
+    for (uint32_t y = r.y0; y < r.y1; y++)
+        for (uint32_t x = r.x0; x < r.x1; x++) atomicAdd(&tile_count[y * gx + x], 1u);
+}
+
+template <bool A, bool B, bool C>
+static void launch_pp(const PreprocessArgs& a, const GeomView& g, int* radii, uint32_t* tile_count, hipStream_t s) {
+    const int blocks = (a.P + 255) / 256;
+    hipLaunchKernelGGL((preprocess_kernel<A, B, C>), dim3(blocks), dim3(256), 0, s, a, g, radii, tile_count);
+}
+
+void launch_preprocess(const PreprocessArgs& a, const GeomView& g, int* radii, uint32_t* tile_count,
+                       hipStream_t s) {
+    if (a.P == 0) return;
+    const bool has_sh = a.colors_precomp == nullptr;
+    const bool sh16 = has_sh && a.M == 16;
+    const bool covp = a.cov3D_precomp != nullptr;
+    if (has_sh) {
+        if (sh16) {
+            if (covp) launch_pp<true, true, true>(a, g, radii, tile_count, s);
+            else launch_pp<true, true, false>(a, g, radii, tile_count, s);
+        } else {
+            if (covp) launch_pp<true, false, true>(a, g, radii, tile_count, s);
+            else launch_pp<true, false, false>(a, g, radii, tile_count, s);
+        }
+    } else {
+        if (covp) launch_pp<false, false, true>(a, g, radii, tile_count, s);
+        else launch_pp<false, false, false>(a, g, radii, tile_count, s);
+    }
+}
+
+// base/cr/rasterizer_impl.cu:54-66 (checkFrustum)
+__global__ void __launch_bounds__(256) mark_visible_kernel(int P, const float* __restrict__ means3D,
+                                                           const float* __restrict__ viewmatrix,
+                                                           bool* __restrict__ present) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const Mat4 V = load_mat4(viewmatrix);
+    const float3 pv = transform_point_4x3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2], V);
+    present[idx] = !(pv.z <= 0.2f);
+}
+
+void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                         bool* present, hipStream_t s) {
+    (void)projmatrix;  // p_hom is computed but unused by the reference test
+    if (P == 0) return;
+    hipLaunchKernelGGL(mark_visible_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, viewmatrix,
+                       present);
+}
+
+}  // namespace gsamd

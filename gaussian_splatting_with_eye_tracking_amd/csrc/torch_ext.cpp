@@ -1,0 +1,301 @@
+// torch_ext.cpp -- PyTorch binding (`_C`) over the C ABI in include/gsplat_amd.h.
+//
+// Mirrors the reference bindings one for one:
+//   base/rasterize_points.cu:35-217 + base/ext.cpp:15-19
+//     rasterize_gaussians / rasterize_gaussians_backward / mark_visible
+//   amr/rasterize_points.cu:65-202 + amr/ext.cpp
+//     amr_rasterize_gaussians (exported to diff_gaussian_rasterization_amr._C
+//     as rasterize_gaussians)
+//   knn/spatial.cu:14-24 + knn/ext.cpp
+//     distCUDA2
+// Same argument order, same return tuples, same "empty tensor == nullptr"
+// convention (SURVEY §8(b) "Ownership"), same AT_ERROR on a bad means3D.
+// Differences: work is enqueued on torch's *current* HIP stream of the
+// input's device (the reference uses the legacy default stream and the
+// current device), and the library writes every output element, so outputs
+// are allocated with torch::empty instead of zero-filled.
+#include <torch/extension.h>
+
+#include <c10/hip/HIPStream.h>
+
+#include <string>
+#include <tuple>
+
+#include "gsplat_amd.h"
+
+namespace {
+
+using torch::Tensor;
+
+char* resize_tensor(void* ctx, size_t n) {
+    auto* t = static_cast<Tensor*>(ctx);
+    t->resize_({(int64_t)n});
+    return reinterpret_cast<char*>(t->data_ptr());
+}
+
+gs_buffer buf_of(Tensor& t) { return gs_buffer{&resize_tensor, &t}; }
+
+void* stream_of(const Tensor& t) {
+    return static_cast<void*>(c10::hip::getCurrentHIPStream(t.device().index()).stream());
+}
+
+void check(int rc, const char* what) {
+    if (rc < 0) TORCH_CHECK(false, what, ": ", gs_last_error());
+}
+
+void require_device(const Tensor& t, const char* name) {
+    if (t.numel() == 0) return;
+    TORCH_CHECK(t.is_cuda(), name, " must be a HIP device tensor (the MI355X rasterizer has no CPU path)");
+    TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32");
+}
+
+// Empty tensor -> nullptr (rasterize_points.cu: `.contiguous().data<float>()` of an empty tensor).
+const float* fptr(const Tensor& t) { return t.numel() ? t.data_ptr<float>() : nullptr; }
+float* fptr_mut(Tensor& t) { return t.numel() ? t.data_ptr<float>() : nullptr; }
+
+std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> rasterize_impl(
+    bool amr, const Tensor& background, const Tensor& means3D_in, const Tensor& colors_in, const Tensor& opacity_in,
+    const Tensor& scales_in, const Tensor& rotations_in, float scale_modifier, const Tensor& cov3D_precomp_in,
+    const Tensor& viewmatrix_in, const Tensor& projmatrix_in, float tan_fovx, float tan_fovy, int image_height,
+    int image_width, const Tensor& sh_in, int degree, const Tensor& campos_in, bool prefiltered, int foveaStep,
+    const Tensor& out_color_precomp_in, const Tensor& geom_pre, const Tensor& bin_pre, const Tensor& img_pre,
+    bool interpolate_image, bool debug) {
+    if (means3D_in.ndimension() != 2 || means3D_in.size(1) != 3) {
+        AT_ERROR("means3D must have dimensions (num_points, 3)");
+    }
+    const int P = (int)means3D_in.size(0);
+    const int H = image_height;
+    const int W = image_width;
+    const at::OptionalDeviceGuard guard(device_of(means3D_in));
+    require_device(means3D_in, "means3D");
+    auto float_opts = means3D_in.options().dtype(torch::kFloat32);
+    Tensor out_color = (amr || P == 0) ? torch::zeros({3, H, W}, float_opts) : torch::empty({3, H, W}, float_opts);
+    Tensor radii = (amr && foveaStep >= 1) || P == 0 ? torch::zeros({P}, means3D_in.options().dtype(torch::kInt32))
+                                                    : torch::empty({P}, means3D_in.options().dtype(torch::kInt32));
+    auto byte_opts = means3D_in.options().dtype(torch::kByte);
+    Tensor geomBuffer = torch::empty({0}, byte_opts);
+    Tensor binningBuffer = torch::empty({0}, byte_opts);
+    Tensor imgBuffer = torch::empty({0}, byte_opts);
+    int rendered = 0;
+    if (P != 0) {
+        const Tensor bg = background.contiguous(), means3D = means3D_in.contiguous(), colors = colors_in.contiguous(),
+                     opacity = opacity_in.contiguous(), scales = scales_in.contiguous(),
+                     rotations = rotations_in.contiguous(), cov3D_precomp = cov3D_precomp_in.contiguous(),
+                     viewmatrix = viewmatrix_in.contiguous(), projmatrix = projmatrix_in.contiguous(),
+                     sh = sh_in.contiguous(), campos = campos_in.contiguous();
+        for (auto& pr : {std::make_pair(&bg, "bg"), std::make_pair(&colors, "colors_precomp"),
+                         std::make_pair(&opacity, "opacities"), std::make_pair(&scales, "scales"),
+                         std::make_pair(&rotations, "rotations"), std::make_pair(&cov3D_precomp, "cov3D_precomp"),
+                         std::make_pair(&viewmatrix, "viewmatrix"), std::make_pair(&projmatrix, "projmatrix"),
+                         std::make_pair(&sh, "sh"), std::make_pair(&campos, "campos")})
+            require_device(*pr.first, pr.second);
+        const int M = sh.size(0) != 0 ? (int)sh.size(1) : 0;
+        void* stream = stream_of(means3D);
+        if (!amr) {
+            rendered = gs_rasterizer_forward(buf_of(geomBuffer), buf_of(binningBuffer), buf_of(imgBuffer), P, degree, M,
+                                             fptr(bg), W, H, fptr(means3D), fptr(sh), fptr(colors), fptr(opacity),
+                                             fptr(scales), scale_modifier, fptr(rotations), fptr(cov3D_precomp),
+                                             fptr(viewmatrix), fptr(projmatrix), fptr(campos), tan_fovx, tan_fovy,
+                                             prefiltered, out_color.data_ptr<float>(), radii.data_ptr<int>(), debug,
+                                             stream);
+            check(rendered, "rasterize_gaussians");
+        } else {
+            const Tensor pre = out_color_precomp_in.contiguous();
+            require_device(pre, "out_color_precomp");
+            Tensor g = geom_pre, b = bin_pre, im = img_pre;
+            rendered = gs_amr_rasterizer_forward(
+                buf_of(geomBuffer), buf_of(binningBuffer), buf_of(imgBuffer), P, degree, M, fptr(bg), W, H,
+                fptr(means3D), fptr(sh), fptr(colors), fptr(opacity), fptr(scales), scale_modifier, fptr(rotations),
+                fptr(cov3D_precomp), fptr(viewmatrix), fptr(projmatrix), fptr(campos), tan_fovx, tan_fovy, prefiltered,
+                foveaStep, fptr(pre), g.numel() ? reinterpret_cast<char*>(g.data_ptr()) : nullptr,
+                b.numel() ? reinterpret_cast<char*>(b.data_ptr()) : nullptr,
+                im.numel() ? reinterpret_cast<char*>(im.data_ptr()) : nullptr, out_color.data_ptr<float>(),
+                radii.data_ptr<int>(), interpolate_image, debug, stream);
+            check(rendered, "rasterize_gaussians (AMR)");
+        }
+    }
+    if (amr && foveaStep > 0)  // amr/rasterize_points.cu:182-190: hand the precomputed buffers back
+        return std::make_tuple(rendered, out_color, radii, geom_pre, bin_pre, img_pre);
+    return std::make_tuple(rendered, out_color, radii, geomBuffer, binningBuffer, imgBuffer);
+}
+
+// base/rasterize_points.cu:35-115
+std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> RasterizeGaussians(
+    const Tensor& background, const Tensor& means3D, const Tensor& colors, const Tensor& opacity,
+    const Tensor& scales, const Tensor& rotations, const float scale_modifier, const Tensor& cov3D_precomp,
+    const Tensor& viewmatrix, const Tensor& projmatrix, const float tan_fovx, const float tan_fovy,
+    const int image_height, const int image_width, const Tensor& sh, const int degree, const Tensor& campos,
+    const bool prefiltered, const bool debug) {
+    Tensor none;
+    auto e = torch::empty({0});
+    return rasterize_impl(false, background, means3D, colors, opacity, scales, rotations, scale_modifier,
+                          cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh,
+                          degree, campos, prefiltered, -1, e, e, e, e, false, debug);
+}
+
+// amr/rasterize_points.cu:65-202
+std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> AMRRasterizeGaussians(
+    const Tensor& background, const Tensor& means3D, const Tensor& colors, const Tensor& opacity,
+    const Tensor& scales, const Tensor& rotations, const float scale_modifier, const Tensor& cov3D_precomp,
+    const Tensor& viewmatrix, const Tensor& projmatrix, const float tan_fovx, const float tan_fovy,
+    const int image_height, const int image_width, const Tensor& sh, const int degree, const Tensor& campos,
+    const bool prefiltered, const int foveaStep, const Tensor& out_color_precomp, const Tensor& geomBuffer_precomp,
+    const Tensor& binningBuffer_precomp, const Tensor& imageBuffer_precomp, const bool interpolate_image,
+    const bool debug) {
+    return rasterize_impl(true, background, means3D, colors, opacity, scales, rotations, scale_modifier,
+                          cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh,
+                          degree, campos, prefiltered, foveaStep, out_color_precomp, geomBuffer_precomp,
+                          binningBuffer_precomp, imageBuffer_precomp, interpolate_image, debug);
+}
+
+// base/rasterize_points.cu:117-196
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> RasterizeGaussiansBackward(
+    const Tensor& background, const Tensor& means3D_in, const Tensor& radii_in, const Tensor& colors_in,
+    const Tensor& scales_in, const Tensor& rotations_in, const float scale_modifier, const Tensor& cov3D_precomp_in,
+    const Tensor& viewmatrix_in, const Tensor& projmatrix_in, const float tan_fovx, const float tan_fovy,
+    const Tensor& dL_dout_color_in, const Tensor& sh_in, const int degree, const Tensor& campos_in,
+    const Tensor& geomBuffer, const int R, const Tensor& binningBuffer, const Tensor& imageBuffer, const bool debug) {
+    const int P = (int)means3D_in.size(0);
+    const int H = (int)dL_dout_color_in.size(1);
+    const int W = (int)dL_dout_color_in.size(2);
+    const int M = sh_in.size(0) != 0 ? (int)sh_in.size(1) : 0;
+    const at::OptionalDeviceGuard guard(device_of(means3D_in));
+    auto opts = means3D_in.options();
+    Tensor dL_dmeans3D = torch::empty({P, 3}, opts);
+    Tensor dL_dmeans2D = torch::empty({P, 3}, opts);
+    Tensor dL_dcolors = torch::empty({P, 3}, opts);
+    Tensor dL_dconic = torch::empty({P, 2, 2}, opts);
+    Tensor dL_dopacity = torch::empty({P, 1}, opts);
+    Tensor dL_dcov3D = torch::empty({P, 6}, opts);
+    Tensor dL_dsh = torch::empty({P, M, 3}, opts);
+    Tensor dL_dscales = torch::empty({P, 3}, opts);
+    Tensor dL_drotations = torch::empty({P, 4}, opts);
+    if (P != 0) {
+        const Tensor bg = background.contiguous(), means3D = means3D_in.contiguous(), radii = radii_in.contiguous(),
+                     colors = colors_in.contiguous(), scales = scales_in.contiguous(),
+                     rotations = rotations_in.contiguous(), cov3D_precomp = cov3D_precomp_in.contiguous(),
+                     viewmatrix = viewmatrix_in.contiguous(), projmatrix = projmatrix_in.contiguous(),
+                     dL_dout = dL_dout_color_in.contiguous(), sh = sh_in.contiguous(), campos = campos_in.contiguous();
+        require_device(means3D, "means3D");
+        require_device(dL_dout, "dL_dout_color");
+        TORCH_CHECK(radii.scalar_type() == torch::kInt32, "radii must be int32");
+        const int rc = gs_rasterizer_backward(
+            P, degree, M, R, fptr(bg), W, H, fptr(means3D), fptr(sh), fptr(colors), fptr(scales), scale_modifier,
+            fptr(rotations), fptr(cov3D_precomp), fptr(viewmatrix), fptr(projmatrix), fptr(campos), tan_fovx,
+            tan_fovy, radii.data_ptr<int>(), reinterpret_cast<char*>(geomBuffer.data_ptr()),
+            reinterpret_cast<char*>(binningBuffer.data_ptr()), reinterpret_cast<char*>(imageBuffer.data_ptr()),
+            fptr(dL_dout), fptr_mut(dL_dmeans2D), fptr_mut(dL_dconic), fptr_mut(dL_dopacity), fptr_mut(dL_dcolors),
+            fptr_mut(dL_dmeans3D), fptr_mut(dL_dcov3D), fptr_mut(dL_dsh), fptr_mut(dL_dscales),
+            fptr_mut(dL_drotations), debug, stream_of(means3D));
+        check(rc, "rasterize_gaussians_backward");
+    }
+    return std::make_tuple(dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
+                           dL_drotations);
+}
+
+// base/rasterize_points.cu:198-217
+Tensor MarkVisible(Tensor& means3D_in, Tensor& viewmatrix_in, Tensor& projmatrix_in) {
+    const int P = (int)means3D_in.size(0);
+    const at::OptionalDeviceGuard guard(device_of(means3D_in));
+    Tensor present = torch::zeros({P}, means3D_in.options().dtype(at::kBool));
+    if (P != 0) {
+        const Tensor means3D = means3D_in.contiguous(), viewmatrix = viewmatrix_in.contiguous(),
+                     projmatrix = projmatrix_in.contiguous();
+        require_device(means3D, "means3D");
+        check(gs_rasterizer_mark_visible(P, fptr(means3D), fptr(viewmatrix), fptr(projmatrix),
+                                         reinterpret_cast<uint8_t*>(present.data_ptr<bool>()), stream_of(means3D)),
+              "mark_visible");
+    }
+    return present;
+}
+
+// knn/spatial.cu:14-24
+Tensor DistCUDA2(const Tensor& points_in) {
+    const int P = (int)points_in.size(0);
+    const at::OptionalDeviceGuard guard(device_of(points_in));
+    Tensor means = torch::empty({P}, points_in.options().dtype(torch::kFloat32));
+    if (P != 0) {
+        const Tensor points = points_in.contiguous();
+        require_device(points, "points");
+        Tensor scratch = torch::empty({0}, points.options().dtype(torch::kByte));
+        check(gs_simple_knn(P, fptr(points), means.data_ptr<float>(), buf_of(scratch), stream_of(points)),
+              "distCUDA2");
+    }
+    return means;
+}
+
+// Parity accessor (the idea of amr-debug's ParseBuffers,
+// amr-debug/rasterize_points.cu:37-61): copies of every internal buffer.
+py::dict ParseBuffers(const Tensor& geomBuffer, const Tensor& binningBuffer, const Tensor& imgBuffer, int P, int K,
+                      int width, int height, int tile) {
+    const at::OptionalDeviceGuard guard(device_of(geomBuffer));
+    auto o = geomBuffer.options();
+    auto f32 = o.dtype(torch::kFloat32);
+    auto i32 = o.dtype(torch::kInt32);
+    gs_geom_view g;
+    gs_image_view im;
+    gs_binning_view b;
+    gs_geom_view_of(reinterpret_cast<char*>(geomBuffer.data_ptr()), P, &g);
+    gs_image_view_of(reinterpret_cast<char*>(imgBuffer.data_ptr()), width, height, tile, &im);
+    gs_binning_view_of(binningBuffer.numel() ? reinterpret_cast<char*>(binningBuffer.data_ptr()) : nullptr, K, &b);
+    const int64_t T = (int64_t)((width + tile - 1) / tile) * ((height + tile - 1) / tile);
+    const int64_t N = (int64_t)width * height;
+    auto view = [&](void* p, std::vector<int64_t> shape, c10::TensorOptions opt) {
+        return torch::from_blob(p, shape, opt).clone();
+    };
+    py::dict d;
+    d["hdr"] = view(g.hdr, {64}, i32);
+    d["depths"] = view(g.depths, {P}, f32);
+    d["radii"] = view(g.radii, {P}, i32);
+    d["means2D"] = view(g.means2D, {P, 2}, f32);
+    d["conic_opacity"] = view(g.conic_opacity, {P, 4}, f32);
+    d["rgb"] = view(g.rgb, {P, 3}, f32);
+    d["cov3D"] = view(g.cov3D, {P, 6}, f32);
+    d["clamped_bits"] = view(g.clamped, {P}, o.dtype(torch::kUInt8));
+    d["tiles_touched"] = view(g.tiles_touched, {P}, i32);
+    d["accum_alpha"] = view(im.accum_alpha, {N}, f32);
+    d["n_contrib"] = view(im.n_contrib, {N}, i32);
+    d["ranges"] = view(im.ranges, {T, 2}, i32);
+    d["tile_count"] = view(im.tile_count, {T}, i32);
+    d["max_contrib"] = view(im.max_contrib, {T}, i32);
+    d["levels"] = view(im.levels, {T}, i32);
+    d["levels_last"] = view(im.levels_last, {T}, i32);
+    d["levels_current"] = view(im.levels_current, {T}, i32);
+    d["pv"] = view(im.pv, {4}, i32);
+    if (K > 0) {
+        d["point_list"] = view(b.point_list, {K}, i32);
+        Tensor keys = torch::empty({K}, o.dtype(torch::kInt64));
+        check(gs_reconstruct_keys(reinterpret_cast<char*>(geomBuffer.data_ptr()),
+                                  reinterpret_cast<char*>(binningBuffer.data_ptr()),
+                                  reinterpret_cast<char*>(imgBuffer.data_ptr()), P, K, width, height, tile,
+                                  reinterpret_cast<uint64_t*>(keys.data_ptr<int64_t>()), stream_of(geomBuffer)),
+              "reconstruct_keys");
+        d["point_list_keys"] = keys;
+    }
+    return d;
+}
+
+py::dict ProfileRead(bool reset) {
+    const int n = gs_profile_stage_count();
+    std::vector<double> ms(n);
+    std::vector<long> cnt(n);
+    gs_profile_read(ms.data(), cnt.data(), reset ? 1 : 0);
+    py::dict d;
+    for (int i = 0; i < n; i++) d[py::str(gs_profile_stage_name(i))] = py::make_tuple(ms[i], cnt[i]);
+    return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+    m.doc() = "MI355X (gfx950) Gaussian rasterizer -- PyTorch binding over include/gsplat_amd.h";
+    m.def("rasterize_gaussians", &RasterizeGaussians);
+    m.def("rasterize_gaussians_backward", &RasterizeGaussiansBackward);
+    m.def("mark_visible", &MarkVisible);
+    m.def("amr_rasterize_gaussians", &AMRRasterizeGaussians);
+    m.def("distCUDA2", &DistCUDA2);
+    m.def("parse_buffers", &ParseBuffers);
+    m.def("abi_version", []() { return gs_abi_version(); });
+    m.def("profile_enable", [](bool on) { gs_profile_enable(on ? 1 : 0); });
+    m.def("profile_read", &ProfileRead, py::arg("reset") = true);
+}

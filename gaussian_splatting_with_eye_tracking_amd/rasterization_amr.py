@@ -1,0 +1,94 @@
+"""Autograd wrapper of the AMR / foveated rasterizer -- the drop-in for
+``submodules/diff-gaussian-rasterization-amr/diff_gaussian_rasterization_amr/__init__.py``.
+
+Public surface identical to the reference (``amr/.../__init__.py:21-367``):
+
+* ``rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities,
+  scales, rotations, cov3Ds_precomp, foveaStep, out_color_precomp,
+  geomBuffer_precomp, binningBuffer_precomp, imageBuffer_precomp,
+  interpolate_image, raster_settings)``;
+* ``_RasterizeGaussians.apply(...) -> (color, radii, geomBuffer,
+  binningBuffer, imgBuffer)`` -- imported directly by
+  ``gaussian_renderer_amr/__init__.py:19``;
+* ``GaussianRasterizer.forward(..., foveaStep=0, out_color_precomp=None,
+  geomBuffer_precomp=None, binningBuffer_precomp=None,
+  imageBuffer_precomp=None, interpolate_image=True)``.
+
+foveaStep semantics (amr/cr/rasterizer_impl.cu:296-694): 0 = preprocess,
+binning and per-tile AMR levels only (blank image); 1..4 = render round k of
+every tile whose level reaches k, reusing the step-0 buffers (the image
+buffer is updated in place); < 0 = render every round up to each tile's level
+in one call (``render_once``).
+
+The reference's AMR backward is unreachable (its autograd forward has 15
+inputs/5 outputs while its backward takes 2 grads and returns 9, and its
+kernel misindexes the 2x render grid -- SURVEY §8(a) row B-AMR).  The AMR
+path is forward-only here as well; calling backward raises a RuntimeError
+that says so.
+"""
+from __future__ import annotations
+
+from typing import NamedTuple
+
+import torch
+import torch.nn as nn
+
+from . import _C
+from .rasterization import GaussianRasterizationSettings, _check_exactly_one, _or_empty  # noqa: F401
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                        foveaStep, out_color_precomp, geomBuffer_precomp, binningBuffer_precomp,
+                        imageBuffer_precomp, interpolate_image, raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                                     cov3Ds_precomp, foveaStep, out_color_precomp, geomBuffer_precomp,
+                                     binningBuffer_precomp, imageBuffer_precomp, interpolate_image, raster_settings)
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, foveaStep,
+                out_color_precomp, geomBuffer_precomp, binningBuffer_precomp, imageBuffer_precomp,
+                interpolate_image, raster_settings):
+        s = raster_settings
+        num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer = _C.amr_rasterize_gaussians(
+            s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
+            s.campos, s.prefiltered, int(foveaStep), out_color_precomp, geomBuffer_precomp, binningBuffer_precomp,
+            imageBuffer_precomp, bool(interpolate_image), s.debug)
+        ctx.num_rendered = num_rendered
+        ctx.mark_non_differentiable(radii, geomBuffer, binningBuffer, imgBuffer)
+        return color, radii, geomBuffer, binningBuffer, imgBuffer
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise RuntimeError("diff_gaussian_rasterization_amr is forward-only (as in the reference, whose AMR "
+                           "backward is unreachable); use diff_gaussian_rasterization for training.")
+
+
+def _empty_u8():
+    return torch.Tensor([]).to(torch.uint8)
+
+
+class GaussianRasterizer(nn.Module):
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):
+        with torch.no_grad():
+            s = self.raster_settings
+            visible = _C.mark_visible(positions, s.viewmatrix, s.projmatrix)
+        return visible
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                cov3D_precomp=None, foveaStep=int(0), out_color_precomp=None, geomBuffer_precomp=None,
+                binningBuffer_precomp=None, imageBuffer_precomp=None, interpolate_image=True):
+        _check_exactly_one(shs, colors_precomp, scales, rotations, cov3D_precomp)
+        return rasterize_gaussians(
+            means3D, means2D, _or_empty(shs), _or_empty(colors_precomp), opacities, _or_empty(scales),
+            _or_empty(rotations), _or_empty(cov3D_precomp), foveaStep, _or_empty(out_color_precomp),
+            _empty_u8() if geomBuffer_precomp is None else geomBuffer_precomp,
+            _empty_u8() if binningBuffer_precomp is None else binningBuffer_precomp,
+            _empty_u8() if imageBuffer_precomp is None else imageBuffer_precomp, interpolate_image,
+            self.raster_settings)

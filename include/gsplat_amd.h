@@ -1,0 +1,162 @@
+/*
+ * gsplat_amd.h -- C ABI of the MI355X (gfx950) Gaussian rasterizer.
+ *
+ * Plain pointers and sizes only (no torch types).  Every pointer argument
+ * that refers to per-Gaussian / per-pixel data is a DEVICE pointer (HBM);
+ * scalars are host values.  `stream` is a hipStream_t (NULL = legacy
+ * default stream).  Every call is asynchronous on `stream` except where a
+ * comment says it reads the instance count K back to the host (the
+ * reference performs that same blocking read, base/cr/rasterizer_impl.cu:281).
+ *
+ * Return value: >= 0 on success (the forward calls return num_rendered = K),
+ * negative on error; gs_last_error() then returns a message (thread-local).
+ *
+ * Buffer contract (SURVEY §8(b) "Ownership"): the three opaque byte buffers
+ * (geometry / binning / image) are allocated by the CALLER through
+ * gs_resize_fn callbacks, exactly like the reference's resizeFunctional
+ * (base/rasterize_points.cu:27-33), and must be handed back unchanged to the
+ * backward call or to the next AMR step.  Their internal layout is this
+ * library's own (see DESIGN.md "Data layout in HBM").
+ */
+#ifndef GSPLAT_AMD_H
+#define GSPLAT_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSPLAT_AMD_ABI_VERSION 1
+
+/* Resize the caller-owned byte buffer `ctx` to `nbytes` and return its
+ * (device, >=256-B aligned) base pointer, or NULL on failure.
+ * Mirrors std::function<char*(size_t)> resizeFunctional
+ * (base/rasterize_points.cu:27-33). */
+typedef char* (*gs_resize_fn)(void* ctx, size_t nbytes);
+
+typedef struct {
+    gs_resize_fn resize;
+    void* ctx;
+} gs_buffer;
+
+int gs_abi_version(void);
+const char* gs_last_error(void);
+
+/* Replaces CudaRasterizer::Rasterizer::forward
+ * (base/cr/rasterizer.h:35-59, base/cr/rasterizer_impl.cu:198-336).
+ * Reads K back to the host once (to size the binning buffer). */
+int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image, int P, int D, int M,
+                          const float* background, int width, int height, const float* means3D, const float* shs,
+                          const float* colors_precomp, const float* opacities, const float* scales,
+                          float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                          const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
+                          float tan_fovy, int prefiltered, float* out_color, int* radii, int debug, void* stream);
+
+/* Replaces CudaRasterizer::Rasterizer::backward
+ * (base/cr/rasterizer.h:61-84, base/cr/rasterizer_impl.cu:340-434).
+ * Unlike the reference, every output element is written (the reference
+ * relies on 9 zero-filled tensors, base/rasterize_points.cu:151-159), so
+ * the outputs may be uninitialised memory.  dL_dconic is [P][4] (a 2x2). */
+int gs_rasterizer_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                           const float* means3D, const float* shs, const float* colors_precomp, const float* scales,
+                           float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                           const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                           float tan_fovy, const int* radii, char* geom_buffer, char* binning_buffer,
+                           char* img_buffer, const float* dL_dpix, float* dL_dmean2D, float* dL_dconic,
+                           float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
+                           float* dL_dsh, float* dL_dscale, float* dL_drot, int debug, void* stream);
+
+/* Replaces CudaRasterizer::Rasterizer::markVisible
+ * (base/cr/rasterizer.h:24-29, base/cr/rasterizer_impl.cu:141-153). */
+int gs_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                               uint8_t* present, void* stream);
+
+/* Replaces the AMR CudaRasterizer::Rasterizer::forward
+ * (amr/cr/rasterizer.h:35-73, amr/cr/rasterizer_impl.cu:296-694).
+ * foveaStep 0: preprocess + binning + levels, no render (blank image);
+ * 1..4: progressive step on the *_precomp buffers (image buffer mutated in
+ * place), the geometry/binning/image callbacks are not called;
+ * <0: one-shot render of every level (render_once).
+ * Reads K back to the host once (both branches, as the reference does). */
+int gs_amr_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image, int P, int D, int M,
+                              const float* background, int width, int height, const float* means3D,
+                              const float* shs, const float* colors_precomp, const float* opacities,
+                              const float* scales, float scale_modifier, const float* rotations,
+                              const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                              const float* cam_pos, float tan_fovx, float tan_fovy, int prefiltered, int foveaStep,
+                              const float* out_color_precomp, char* geom_buffer_precomp,
+                              char* binning_buffer_precomp, char* image_buffer_precomp, float* out_color, int* radii,
+                              int interpolate_image, int debug, void* stream);
+
+/* Replaces SimpleKNN::knn (knn/simple_knn.h:16-19, knn/simple_knn.cu:185-221)
+ * behind simple_knn._C.distCUDA2.  `scratch` is resized to the workspace
+ * size; no host synchronisation. */
+int gs_simple_knn(int P, const float* points, float* mean_dists, gs_buffer scratch, void* stream);
+
+/* ------------------------------------------------ parity / debug accessors
+ * The reference exposes its internal buffers only in the AMR-debug variant
+ * (ParseBuffers, amr-debug/rasterize_points.cu:37-61).  These views let the
+ * tests compare every intermediate with the oracle. */
+typedef struct {
+    uint32_t* hdr; /* [64]: [0]=K, [1]=error flag, [2]=max tile count, [3]=#large tiles */
+    float* depths;
+    int* radii;
+    float* means2D;       /* [P][2] */
+    float* conic_opacity; /* [P][4] */
+    float* rgb;           /* [P][3] */
+    float* cov3D;         /* [P][6] */
+    uint8_t* clamped;     /* [P] bit c = channel c clamped */
+    uint32_t* tiles_touched;
+    float* grad_accum; /* [P][16] */
+} gs_geom_view;
+
+typedef struct {
+    float* accum_alpha; /* final T, [N] */
+    uint32_t* n_contrib;
+    uint32_t* ranges; /* [T][2] */
+    uint32_t* tile_count;
+    uint32_t* tile_cursor;
+    uint32_t* max_contrib;
+    uint32_t* levels;
+    uint32_t* levels_last;
+    uint32_t* levels_current;
+    uint32_t* pv; /* [4] */
+    uint32_t* large_tiles;
+} gs_image_view;
+
+typedef struct {
+    uint32_t* point_list;
+    uint64_t* pair_keys;
+    uint64_t* scratch;
+} gs_binning_view;
+
+size_t gs_geom_bytes(int P);
+size_t gs_image_bytes(int width, int height, int tile);
+size_t gs_binning_bytes(int K);
+size_t gs_knn_workspace_bytes(int P);
+int gs_geom_view_of(char* base, int P, gs_geom_view* out);
+int gs_image_view_of(char* base, int width, int height, int tile, gs_image_view* out);
+int gs_binning_view_of(char* base, int K, gs_binning_view* out);
+
+/* The reference's binningState.point_list_keys (tile << 32 | depth bits),
+ * rebuilt from point_list + ranges + depths into keys_out[K] (device). */
+int gs_reconstruct_keys(char* geom_buffer, char* binning_buffer, char* img_buffer, int P, int K, int width,
+                        int height, int tile, uint64_t* keys_out, void* stream);
+
+/* ---------------------------------------------------- per-stage timing
+ * When enabled, every stage records a pair of hipEvents on its launch stream;
+ * gs_profile_read() waits for them and returns the accumulated milliseconds
+ * and launch counts per stage (names from gs_profile_stage_name).  Used by
+ * bench.py for the live per-kernel roofline (cross-checked with rocprofv3). */
+void gs_profile_enable(int on);
+int gs_profile_stage_count(void);
+const char* gs_profile_stage_name(int i);
+void gs_profile_read(double* total_ms, long* counts, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSPLAT_AMD_H */

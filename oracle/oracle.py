@@ -1,0 +1,339 @@
+"""ctypes driver for the CPU oracle (gs_oracle.c) -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, bench.py's cpu_baseline leg and __graft_entry__.smoke() may
+import this module, and only as the checker: the product path
+(gaussian_splatting_with_eye_tracking_amd + the drop-in packages) never
+imports, links or executes anything under oracle/.
+
+The driver strings the restated stages together exactly like the reference
+orchestrators:
+  * base forward:  base/cr/rasterizer_impl.cu:198-336
+  * base backward: base/cr/rasterizer_impl.cu:340-434, base/rasterize_points.cu:117-196
+  * AMR forward:   amr/cr/rasterizer_impl.cu:296-694
+  * simple-knn:    knn/simple_knn.cu:185-221
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libgs_oracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(
+                os.path.join(_HERE, "gs_oracle.c")):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+    return _lib
+
+
+def _p(a):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "oracle arrays must be C-contiguous"
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _f32(a):
+    return None if a is None else np.ascontiguousarray(a, dtype=np.float32)
+
+
+@dataclass
+class Settings:
+    """Mirror of GaussianRasterizationSettings (base/.../__init__.py:157-169)."""
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: np.ndarray
+    scale_modifier: float
+    viewmatrix: np.ndarray
+    projmatrix: np.ndarray
+    sh_degree: int
+    campos: np.ndarray
+    prefiltered: bool = False
+    debug: bool = False
+
+
+def settings_from_camera(cam, bg=(0.0, 0.0, 0.0), sh_degree=3, scale_modifier=1.0) -> Settings:
+    return Settings(cam.image_height, cam.image_width, cam.tanfovx, cam.tanfovy,
+                    np.asarray(bg, np.float32), scale_modifier, cam.world_view_transform,
+                    cam.full_proj_transform, sh_degree, cam.camera_center)
+
+
+@dataclass
+class ForwardResult:
+    num_rendered: int
+    color: np.ndarray
+    radii: np.ndarray
+    means2D: np.ndarray
+    depths: np.ndarray
+    cov3D: np.ndarray
+    rgb: np.ndarray
+    clamped: np.ndarray
+    conic_opacity: np.ndarray
+    tiles_touched: np.ndarray
+    point_offsets: np.ndarray
+    point_list_keys: np.ndarray
+    point_list: np.ndarray
+    ranges: np.ndarray
+    final_T: np.ndarray
+    n_contrib: np.ndarray
+    block: int
+    extra: dict = field(default_factory=dict)
+
+
+def _c_float(x):
+    return ctypes.c_float(float(x))
+
+
+def preprocess_and_bin(s: Settings, means3D, opacities, shs=None, colors_precomp=None, scales=None,
+                       rotations=None, cov3D_precomp=None, block: int = 16) -> ForwardResult:
+    """base/cr/rasterizer_impl.cu:222-318 (everything before the blend)."""
+    L = lib()
+    means3D = _f32(means3D)
+    P = means3D.shape[0]
+    W, H = int(s.image_width), int(s.image_height)
+    focal_y = np.float32(H / (2.0 * np.float32(s.tanfovy)))
+    focal_x = np.float32(W / (2.0 * np.float32(s.tanfovx)))
+    # rasterizer_impl.cu:222-223: focal computed in float: height / (2.0f * tan_fovy)
+    tfx = np.float32(s.tanfovx)
+    tfy = np.float32(s.tanfovy)
+    focal_y = np.float32(np.float32(H) / (np.float32(2.0) * tfy))
+    focal_x = np.float32(np.float32(W) / (np.float32(2.0) * tfx))
+    shs = _f32(shs)
+    M = 0 if shs is None or shs.size == 0 else shs.shape[1]
+    if shs is not None and shs.size == 0:
+        shs = None
+    colors_precomp = _f32(colors_precomp)
+    if colors_precomp is not None and colors_precomp.size == 0:
+        colors_precomp = None
+    scales = _f32(scales)
+    if scales is not None and scales.size == 0:
+        scales = None
+    rotations = _f32(rotations)
+    if rotations is not None and rotations.size == 0:
+        rotations = None
+    cov3D_precomp = _f32(cov3D_precomp)
+    if cov3D_precomp is not None and cov3D_precomp.size == 0:
+        cov3D_precomp = None
+    opac = _f32(opacities).reshape(-1)
+    radii = np.zeros(P, np.int32)
+    means2D = np.zeros((P, 2), np.float32)
+    depths = np.zeros(P, np.float32)
+    cov3D = np.zeros((P, 6), np.float32)
+    rgb = np.zeros((P, 3), np.float32)
+    clamped = np.zeros((P, 3), np.uint8)
+    conic = np.zeros((P, 4), np.float32)
+    touched = np.zeros(P, np.uint32)
+    L.orc_preprocess(
+        ctypes.c_int(P), ctypes.c_int(int(s.sh_degree)), ctypes.c_int(M), _p(means3D), _p(scales),
+        _c_float(s.scale_modifier), _p(rotations), _p(opac), _p(shs), _p(clamped), _p(cov3D_precomp),
+        _p(colors_precomp), _p(_f32(s.viewmatrix)), _p(_f32(s.projmatrix)), _p(_f32(s.campos)),
+        ctypes.c_int(W), ctypes.c_int(H), ctypes.c_float(tfx), ctypes.c_float(tfy),
+        ctypes.c_float(focal_x), ctypes.c_float(focal_y), ctypes.c_int(block), ctypes.c_int(block),
+        _p(radii), _p(means2D), _p(depths), _p(cov3D), _p(rgb), _p(conic), _p(touched),
+        ctypes.c_int(int(s.prefiltered)))
+    offsets = np.zeros(P, np.uint32)
+    L.orc_inclusive_scan_u32(ctypes.c_int(P), _p(touched), _p(offsets))
+    K = int(offsets[-1]) if P > 0 else 0
+    keys = np.zeros(max(K, 1), np.uint64)
+    vals = np.zeros(max(K, 1), np.uint32)
+    L.orc_duplicate_with_keys(ctypes.c_int(P), _p(means2D), _p(depths), _p(offsets), _p(radii),
+                              ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(block), ctypes.c_int(block),
+                              _p(keys), _p(vals))
+    gx, gy = (W + block - 1) // block, (H + block - 1) // block
+    T = gx * gy
+    L.orc_get_higher_msb.restype = ctypes.c_uint32
+    bit = int(L.orc_get_higher_msb(ctypes.c_uint32(T)))
+    L.orc_sort_pairs_u64(ctypes.c_int(K), _p(keys), _p(vals), ctypes.c_int(32 + bit))
+    ranges = np.zeros((T, 2), np.uint32)
+    L.orc_identify_tile_ranges(ctypes.c_int(K), _p(keys), ctypes.c_int(T), _p(ranges))
+    return ForwardResult(K, np.zeros((3, H, W), np.float32), radii, means2D, depths, cov3D, rgb, clamped,
+                         conic, touched, offsets, keys[:K].copy(), vals[:K].copy(), ranges,
+                         np.zeros(H * W, np.float32), np.zeros(H * W, np.uint32), block,
+                         extra={"colors_precomp": colors_precomp, "M": M, "focal_x": focal_x,
+                                "focal_y": focal_y})
+
+
+def forward(s: Settings, means3D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+            cov3D_precomp=None) -> ForwardResult:
+    """Base forward (rasterizer_impl.cu:198-336)."""
+    r = preprocess_and_bin(s, means3D, opacities, shs, colors_precomp, scales, rotations, cov3D_precomp, 16)
+    W, H = int(s.image_width), int(s.image_height)
+    feats = r.extra["colors_precomp"] if r.extra["colors_precomp"] is not None else r.rgb
+    lib().orc_render_forward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(16), ctypes.c_int(16),
+                             _p(r.ranges), _p(r.point_list), _p(r.means2D), _p(np.ascontiguousarray(feats)),
+                             _p(r.conic_opacity), _p(r.final_T), _p(r.n_contrib), _p(_f32(s.bg)), _p(r.color))
+    return r
+
+
+def backward(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors_precomp=None, scales=None,
+             rotations=None, cov3D_precomp=None) -> dict:
+    """Base backward (rasterize_points.cu:117-196 + rasterizer_impl.cu:340-434).
+    Returns the 8 gradients of _C.rasterize_gaussians_backward plus dL_dconic."""
+    L = lib()
+    means3D = _f32(means3D)
+    P = means3D.shape[0]
+    W, H = int(s.image_width), int(s.image_height)
+    shs = None if shs is None or np.asarray(shs).size == 0 else _f32(shs)
+    M = 0 if shs is None else shs.shape[1]
+    colors_precomp = None if colors_precomp is None or np.asarray(colors_precomp).size == 0 else _f32(colors_precomp)
+    scales = None if scales is None or np.asarray(scales).size == 0 else _f32(scales)
+    rotations = None if rotations is None or np.asarray(rotations).size == 0 else _f32(rotations)
+    cov3D_precomp = None if cov3D_precomp is None or np.asarray(cov3D_precomp).size == 0 else _f32(cov3D_precomp)
+    dL_dpix = _f32(dL_dpix)
+    g_mean2D = np.zeros((P, 3), np.float32)
+    g_conic = np.zeros((P, 2, 2), np.float32)
+    g_opac = np.zeros((P, 1), np.float32)
+    g_col = np.zeros((P, 3), np.float32)
+    g_mean3D = np.zeros((P, 3), np.float32)
+    g_cov = np.zeros((P, 6), np.float32)
+    g_sh = np.zeros((P, M, 3), np.float32)
+    g_scale = np.zeros((P, 3), np.float32)
+    g_rot = np.zeros((P, 4), np.float32)
+    colors = colors_precomp if colors_precomp is not None else fwd.rgb
+    L.orc_render_backward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(16), ctypes.c_int(16), _p(fwd.ranges),
+                          _p(fwd.point_list), _p(_f32(s.bg)), _p(fwd.means2D), _p(fwd.conic_opacity),
+                          _p(np.ascontiguousarray(colors)), _p(fwd.final_T), _p(fwd.n_contrib), _p(dL_dpix),
+                          ctypes.c_int(P), _p(g_mean2D), _p(g_conic), _p(g_opac), _p(g_col))
+    cov_ptr = cov3D_precomp if cov3D_precomp is not None else fwd.cov3D
+    fx, fy = fwd.extra["focal_x"], fwd.extra["focal_y"]
+    L.orc_cov2d_backward(ctypes.c_int(P), _p(means3D), _p(fwd.radii), _p(np.ascontiguousarray(cov_ptr)),
+                         ctypes.c_float(fx), ctypes.c_float(fy), ctypes.c_float(np.float32(s.tanfovx)),
+                         ctypes.c_float(np.float32(s.tanfovy)), _p(_f32(s.viewmatrix)), _p(g_conic),
+                         _p(g_mean3D), _p(g_cov))
+    L.orc_preprocess_backward(ctypes.c_int(P), ctypes.c_int(int(s.sh_degree)), ctypes.c_int(M), _p(means3D),
+                              _p(fwd.radii), _p(shs), _p(fwd.clamped), _p(scales), _p(rotations),
+                              _c_float(s.scale_modifier), _p(_f32(s.projmatrix)), _p(_f32(s.campos)),
+                              _p(g_mean2D), _p(g_mean3D), _p(g_col), _p(g_cov), _p(g_sh), _p(g_scale),
+                              _p(g_rot))
+    return {"dL_dmeans2D": g_mean2D, "dL_dcolors": g_col, "dL_dopacity": g_opac, "dL_dmeans3D": g_mean3D,
+            "dL_dcov3D": g_cov, "dL_dsh": g_sh, "dL_dscales": g_scale, "dL_drotations": g_rot,
+            "dL_dconic": g_conic}
+
+
+def mark_visible(means3D, viewmatrix, projmatrix) -> np.ndarray:
+    means3D = _f32(means3D)
+    out = np.zeros(means3D.shape[0], np.uint8)
+    lib().orc_mark_visible(ctypes.c_int(means3D.shape[0]), _p(means3D), _p(_f32(viewmatrix)),
+                           _p(_f32(projmatrix)), _p(out))
+    return out.astype(bool)
+
+
+# ------------------------------------------------------------------- AMR ---
+@dataclass
+class AMRState:
+    """The opaque step-to-step state of the AMR path (geom/binning/image buffers)."""
+    fwd: ForwardResult
+    n_intersections: np.ndarray
+    n_intersections_sorted: np.ndarray
+    percentile_values: np.ndarray
+    levels: np.ndarray
+    levels_last: np.ndarray
+    levels_current: np.ndarray
+    final_T: np.ndarray
+    n_contrib: np.ndarray
+
+
+def amr_forward(s: Settings, means3D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                cov3D_precomp=None, foveaStep: int = 0, out_color_precomp=None, state: AMRState | None = None,
+                interpolate_image: bool = True):
+    """amr/cr/rasterizer_impl.cu:296-694. Returns (color, radii, state)."""
+    L = lib()
+    W, H = int(s.image_width), int(s.image_height)
+    N = W * H
+    if foveaStep >= 1:
+        st = state
+        fwd = st.fwd
+        T = fwd.ranges.shape[0]
+        orc_fovea(L, foveaStep, T, st)
+        color = np.zeros((3, H, W), np.float32)
+        feats = fwd.extra["colors_precomp"] if fwd.extra["colors_precomp"] is not None else fwd.rgb
+        L.orc_amr_render(ctypes.c_int(W), ctypes.c_int(H), _p(fwd.ranges), _p(st.levels_current),
+                         _p(st.levels_last), _p(fwd.point_list), _p(fwd.means2D), _p(np.ascontiguousarray(feats)),
+                         _p(fwd.conic_opacity), _p(st.final_T), _p(st.n_contrib), _p(_f32(s.bg)), _p(color),
+                         ctypes.c_int(foveaStep))
+        if interpolate_image:
+            pre = _f32(out_color_precomp)
+            L.orc_amr_interpolate(ctypes.c_int(W), ctypes.c_int(H), _p(st.levels_current), _p(st.levels_last),
+                                  _p(st.final_T), _p(st.n_contrib), _p(color), ctypes.c_int(foveaStep), _p(pre))
+        return color, np.zeros(fwd.radii.shape, np.int32), st
+    fwd = preprocess_and_bin(s, means3D, opacities, shs, colors_precomp, scales, rotations, cov3D_precomp, 32)
+    T = fwd.ranges.shape[0]
+    st = AMRState(fwd, np.zeros(T, np.uint32), np.zeros(T, np.uint32), np.zeros(3, np.uint32),
+                  np.zeros(T, np.uint32), np.zeros(T, np.uint32), np.zeros(T, np.uint32),
+                  np.zeros(N, np.float32), np.zeros(N, np.uint32))
+    L.orc_amr_levels(ctypes.c_int(T), _p(fwd.ranges), _p(st.n_intersections), _p(st.n_intersections_sorted),
+                     _p(st.percentile_values), _p(st.levels))
+    color = np.zeros((3, H, W), np.float32)
+    if foveaStep == 0:
+        return color, fwd.radii, st
+    orc_fovea(L, foveaStep, T, st)
+    feats = fwd.extra["colors_precomp"] if fwd.extra["colors_precomp"] is not None else fwd.rgb
+    L.orc_amr_render(ctypes.c_int(W), ctypes.c_int(H), _p(fwd.ranges), _p(st.levels), _p(st.levels_last),
+                     _p(fwd.point_list), _p(fwd.means2D), _p(np.ascontiguousarray(feats)), _p(fwd.conic_opacity),
+                     _p(st.final_T), _p(st.n_contrib), _p(_f32(s.bg)), _p(color), ctypes.c_int(foveaStep))
+    if interpolate_image:
+        L.orc_amr_interpolate(ctypes.c_int(W), ctypes.c_int(H), _p(st.levels), _p(st.levels_last),
+                              _p(st.final_T), _p(st.n_contrib), _p(color), ctypes.c_int(foveaStep), _p(color))
+    return color, fwd.radii, st
+
+
+def orc_fovea(L, step, T, st: AMRState):
+    L.orc_amr_fovea_levels(ctypes.c_int(step), ctypes.c_int(T), _p(st.levels_last), _p(st.levels_current),
+                           _p(st.levels))
+
+
+def amr_render_foveated(s: Settings, scene_kwargs: dict, interpolate_image: bool = False):
+    """gaussian_renderer_amr/__init__.py:24-608: steps 0..4, summing the partial images."""
+    c0, radii, st = amr_forward(s, foveaStep=0, **scene_kwargs)
+    acc = c0.copy()
+    steps = [c0]
+    for k in range(1, 5):
+        interp = interpolate_image if k == 4 else False
+        ck, _, st = amr_forward(s, foveaStep=k, out_color_precomp=acc, state=st, interpolate_image=interp,
+                                **scene_kwargs)
+        steps.append(ck)
+        acc = acc + ck
+    return acc, radii, st, steps
+
+
+def amr_render_once(s: Settings, scene_kwargs: dict):
+    """gaussian_renderer_amr/__init__.py:612-749: one call with foveaStep=-2, interpolate=True."""
+    return amr_forward(s, foveaStep=-2, interpolate_image=True, **scene_kwargs)
+
+
+# ------------------------------------------------------------- simple-knn ---
+def dist_cuda2(points) -> np.ndarray:
+    pts = _f32(points)
+    P = pts.shape[0]
+    out = np.zeros(P, np.float32)
+    lib().orc_knn(ctypes.c_int(P), _p(pts), _p(out), None, None, None)
+    return out
+
+
+def knn_intermediates(points):
+    pts = _f32(points)
+    P = pts.shape[0]
+    nb = (P + 1023) // 1024
+    out = np.zeros(P, np.float32)
+    morton = np.zeros(P, np.uint32)
+    idx = np.zeros(P, np.uint32)
+    boxes = np.zeros((max(nb, 1), 6), np.float32)
+    lib().orc_knn(ctypes.c_int(P), _p(pts), _p(out), _p(morton), _p(idx), _p(boxes))
+    return out, morton, idx, boxes[:nb]

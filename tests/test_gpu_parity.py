@@ -1,0 +1,276 @@
+"""GPU parity: the HIP path (through the drop-in API / C ABI) against the CPU
+oracle on identical seeded inputs.
+
+Bars (BASELINE.json north_star): tile keys / point_list / ranges and every
+integer buffer bit-exact; preprocess floats bit-exact (same op order, no
+contraction); image L1 < 1e-5; gradients within 1e-4 relative (L2 norm).
+"""
+import numpy as np
+import pytest
+
+import gs_helpers as G
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    ("g1_64_32x32", 64, 32, 32, 3),
+    ("cfg1_10k_256", 10000, 256, 256, 0),
+    ("ragged_3k_250x130", 3000, 250, 130, 7),
+    ("dense_20k_128", 20000, 128, 128, 11),  # large tiles: exercises the merge-sort path
+]
+
+
+def _gpu_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0.0, 0.0)):
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    s = G.torch_settings(cam, bg=bg)
+    t = G.scene_tensors(sc)
+    e = torch.Tensor([])
+    sh = t["shs"] if colors_precomp is None else e
+    col = e if colors_precomp is None else torch.from_numpy(colors_precomp).cuda()
+    scales = t["scales"] if cov3D_precomp is None else e
+    rots = t["rotations"] if cov3D_precomp is None else e
+    cov = e if cov3D_precomp is None else torch.from_numpy(cov3D_precomp).cuda()
+    out = C.rasterize_gaussians(s.bg, t["means3D"], col, t["opacities"], scales, rots, s.scale_modifier, cov,
+                                s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh,
+                                s.sh_degree, s.campos, s.prefiltered, s.debug)
+    torch.cuda.synchronize()
+    return s, t, out
+
+
+def _oracle_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0.0, 0.0)):
+    import oracle as O
+    s = O.settings_from_camera(cam, bg=bg)
+    kw = dict(shs=sc.shs if colors_precomp is None else None, colors_precomp=colors_precomp,
+              scales=sc.scales if cov3D_precomp is None else None,
+              rotations=sc.rotations if cov3D_precomp is None else None, cov3D_precomp=cov3D_precomp)
+    return s, O.forward(s, sc.means3D, sc.opacities, **kw), kw
+
+
+@pytest.mark.parametrize("name,P,W,H,seed", CASES)
+def test_forward_buffers_bit_exact(name, P, W, H, seed):
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
+    _, ref, _ = _oracle_forward(sc, cam)
+    assert K == ref.num_rendered
+    d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
+    np.testing.assert_array_equal(radii.cpu().numpy(), ref.radii)
+    vis = ref.radii > 0
+    np.testing.assert_array_equal(d["depths"].cpu().numpy()[vis], ref.depths[vis])
+    np.testing.assert_array_equal(d["means2D"].cpu().numpy()[vis], ref.means2D[vis])
+    np.testing.assert_array_equal(d["conic_opacity"].cpu().numpy()[vis], ref.conic_opacity[vis])
+    np.testing.assert_array_equal(d["rgb"].cpu().numpy()[vis], ref.rgb[vis])
+    np.testing.assert_array_equal(d["cov3D"].cpu().numpy()[vis], ref.cov3D[vis])
+    cb = d["clamped_bits"].cpu().numpy()[vis]
+    ref_cb = (ref.clamped[vis] * np.array([1, 2, 4], np.uint8)).sum(1)
+    np.testing.assert_array_equal(cb, ref_cb)
+    np.testing.assert_array_equal(d["tiles_touched"].cpu().numpy().astype(np.uint32), ref.tiles_touched)
+    np.testing.assert_array_equal(d["ranges"].cpu().numpy().astype(np.uint32), ref.ranges)
+    if K:
+        np.testing.assert_array_equal(d["point_list"].cpu().numpy().astype(np.uint32), ref.point_list)
+        np.testing.assert_array_equal(d["point_list_keys"].cpu().numpy().view(np.uint64), ref.point_list_keys)
+
+
+@pytest.mark.parametrize("name,P,W,H,seed", CASES)
+def test_forward_image(name, P, W, H, seed):
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam, bg=(0.1, 0.2, 0.3))
+    _, ref, _ = _oracle_forward(sc, cam, bg=(0.1, 0.2, 0.3))
+    assert G.image_l1(color.cpu().numpy(), ref.color) < G.IMAGE_L1_TOL
+    d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
+    ncont = d["n_contrib"].cpu().numpy().astype(np.uint32)
+    assert np.mean(ncont != ref.n_contrib) < 1e-3  # exp is hardware v_exp_f32 vs libm expf
+    assert G.image_l1(d["accum_alpha"].cpu().numpy(), ref.final_T) < G.IMAGE_L1_TOL
+
+
+@pytest.mark.parametrize("name,P,W,H,seed", CASES[:3])
+@pytest.mark.parametrize("variant", ["sh", "colors_precomp", "cov3D_precomp"])
+def test_backward_parity(name, P, W, H, seed, variant):
+    import oracle as O
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    colors = None
+    cov = None
+    if variant == "colors_precomp":
+        colors = np.random.default_rng(seed + 5).uniform(0, 1, (P, 3)).astype(np.float32)
+    if variant == "cov3D_precomp":
+        _, r0, _ = _oracle_forward(sc, cam)
+        cov = r0.cov3D.copy()
+        # invisible Gaussians have no computed cov3D: give them a valid one
+        cov[r0.radii <= 0] = np.array([1e-4, 0, 0, 1e-4, 0, 1e-4], np.float32)
+    bg = (0.2, 0.1, 0.05)
+    s, t, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam, colors, cov, bg=bg)
+    os_, ref, kw = _oracle_forward(sc, cam, colors, cov, bg=bg)
+    dpix = S.make_cotangent(H, W, seed + 1)
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    e = torch.Tensor([])
+    sh = t["shs"] if colors is None else e
+    colt = e if colors is None else torch.from_numpy(colors).cuda()
+    scales = t["scales"] if cov is None else e
+    rots = t["rotations"] if cov is None else e
+    covt = e if cov is None else torch.from_numpy(cov).cuda()
+    grads = C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, colt, scales, rots, s.scale_modifier, covt,
+                                           s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy,
+                                           torch.from_numpy(dpix).cuda(), sh, s.sh_degree, s.campos, geom, K, binning,
+                                           img, False)
+    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    rg = O.backward(os_, ref, sc.means3D, dpix, **kw)
+    for n, g in zip(names, grads):
+        gg = g.cpu().numpy()
+        assert gg.shape == rg[n].shape, n
+        assert np.all(np.isfinite(gg)), n
+        assert G.rel_err(gg, rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(gg, rg[n]))
+
+
+def test_autograd_dropin_matches_direct_call():
+    """The drop-in GaussianRasterizer (autograd) returns the same image and
+    gradients as the raw _C calls, in the reference's gradient order."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    sc, cam = G.scene_and_camera(2000, 96, 64, 2)
+    s = G.torch_settings(cam)
+    t = G.scene_tensors(sc, requires_grad=True)
+    means2D = torch.zeros_like(t["means3D"], requires_grad=True)
+    ras = GaussianRasterizer(s)
+    color, radii = ras(means3D=t["means3D"], means2D=means2D, opacities=t["opacities"], shs=t["shs"],
+                       scales=t["scales"], rotations=t["rotations"])
+    dpix = torch.randn_like(color)
+    (color * dpix).sum().backward()
+    assert means2D.grad is not None and torch.all(means2D.grad[:, 2] == 0)
+    for k in ("means3D", "opacities", "shs", "scales", "rotations"):
+        assert t[k].grad is not None and torch.isfinite(t[k].grad).all(), k
+    vis = ras.markVisible(t["means3D"].detach())
+    import oracle as O
+    np.testing.assert_array_equal(vis.cpu().numpy(),
+                                  O.mark_visible(sc.means3D, cam.world_view_transform, cam.full_proj_transform))
+
+
+def test_empty_scene():
+    from diff_gaussian_rasterization import GaussianRasterizer
+    sc, cam = G.scene_and_camera(0, 64, 48)
+    s = G.torch_settings(cam)
+    t = G.scene_tensors(sc)
+    color, radii = GaussianRasterizer(s)(means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]),
+                                          opacities=t["opacities"], shs=t["shs"], scales=t["scales"],
+                                          rotations=t["rotations"])
+    assert color.shape == (3, 48, 64) and torch.all(color == 0) and radii.numel() == 0
+
+
+def test_all_culled():
+    """Every Gaussian behind the near plane: K = 0, image = background."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(500, 64, 48)
+    sc.means3D[:, 2] = -5.0
+    s, t, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam, bg=(0.5, 0.25, 0.125))
+    assert K == 0 and torch.all(radii == 0)
+    np.testing.assert_allclose(color.cpu().numpy()[:, 0, 0], [0.5, 0.25, 0.125])
+
+
+def test_prefiltered_violation_raises():
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(100, 32, 32)
+    sc.means3D[0, 2] = -1.0
+    s = G.torch_settings(cam)
+    t = G.scene_tensors(sc)
+    with pytest.raises(RuntimeError, match="prefiltered"):
+        C.rasterize_gaussians(s.bg, t["means3D"], torch.Tensor([]), t["opacities"], t["scales"], t["rotations"], 1.0,
+                              torch.Tensor([]), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, 32, 32, t["shs"], 3,
+                              s.campos, True, False)
+
+
+# ---------------------------------------------------------------- AMR ----
+def _amr_gpu_steps(sc, cam, interpolate_last=False, bg=(0.0, 0.0, 0.0)):
+    from diff_gaussian_rasterization_amr import _RasterizeGaussians
+    s = G.torch_settings(cam, amr=True, bg=bg)
+    t = G.scene_tensors(sc)
+    e = torch.Tensor([])
+    u8 = torch.Tensor([]).to(torch.uint8)
+    means2D = torch.zeros_like(t["means3D"])
+    args = (t["means3D"], means2D, t["shs"], e, t["opacities"], t["scales"], t["rotations"], e)
+    c0, radii, gb, bb, ib = _RasterizeGaussians.apply(*args, 0, e, u8, u8, u8, False, s)
+    acc = c0
+    steps = [c0]
+    for k in range(1, 5):
+        ck, _, gb, bb, ib = _RasterizeGaussians.apply(*args, k, acc, gb, bb, ib, interpolate_last and k == 4, s)
+        steps.append(ck)
+        acc = acc + ck
+    torch.cuda.synchronize()
+    return acc, radii, steps, (gb, bb, ib)
+
+
+@pytest.mark.parametrize("name,P,W,H,seed", [("amr_10k_256", 10000, 256, 256, 0), ("amr_ragged", 4000, 200, 120, 3)])
+def test_amr_foveated_steps(name, P, W, H, seed):
+    import oracle as O
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.1, 0.1))
+    s = O.settings_from_camera(cam, bg=(0.1, 0.1, 0.1))
+    kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+    racc, rradii, st, rsteps = O.amr_render_foveated(s, kw)
+    np.testing.assert_array_equal(radii.cpu().numpy(), rradii)
+    K = st.fwd.num_rendered
+    d = C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
+    np.testing.assert_array_equal(d["ranges"].cpu().numpy().astype(np.uint32), st.fwd.ranges)
+    np.testing.assert_array_equal(d["point_list"].cpu().numpy().astype(np.uint32), st.fwd.point_list)
+    np.testing.assert_array_equal(d["pv"].cpu().numpy()[:3].astype(np.uint32), st.percentile_values)
+    np.testing.assert_array_equal(d["levels"].cpu().numpy().astype(np.uint32), st.levels)
+    np.testing.assert_array_equal(d["levels_last"].cpu().numpy().astype(np.uint32), st.levels_last)
+    np.testing.assert_array_equal(d["levels_current"].cpu().numpy().astype(np.uint32), st.levels_current)
+    assert torch.all(steps[0] == 0)
+    for k in range(5):
+        assert G.image_l1(steps[k].cpu().numpy(), rsteps[k]) < G.IMAGE_L1_TOL, k
+    assert G.image_l1(acc.cpu().numpy(), racc) < G.IMAGE_L1_TOL
+
+
+def test_amr_render_once_interpolated():
+    import oracle as O
+    from diff_gaussian_rasterization_amr import GaussianRasterizer
+    sc, cam = G.scene_and_camera(8000, 224, 160, 5)
+    s = G.torch_settings(cam, amr=True)
+    t = G.scene_tensors(sc)
+    color, radii, gb, bb, ib = GaussianRasterizer(s)(
+        means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"], shs=t["shs"],
+        scales=t["scales"], rotations=t["rotations"], foveaStep=-2, interpolate_image=True)
+    os_ = O.settings_from_camera(cam)
+    rcol, rrad, st = O.amr_render_once(os_, dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs,
+                                                  scales=sc.scales, rotations=sc.rotations))
+    assert G.image_l1(color.cpu().numpy(), rcol) < G.IMAGE_L1_TOL
+
+
+def test_amr_step4_interpolate():
+    """foveaStep 4 with interpolate_image=True (the reference's racy path,
+    defined here as precomp-copy-then-neighbour-copy)."""
+    import oracle as O
+    sc, cam = G.scene_and_camera(6000, 160, 96, 9)
+    acc, radii, steps, _ = _amr_gpu_steps(sc, cam, interpolate_last=True)
+    s = O.settings_from_camera(cam)
+    racc, _, _, rsteps = O.amr_render_foveated(
+        s, dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations),
+        interpolate_image=True)
+    assert G.image_l1(steps[4].cpu().numpy(), rsteps[4]) < G.IMAGE_L1_TOL
+    assert G.image_l1(acc.cpu().numpy(), racc) < G.IMAGE_L1_TOL
+
+
+def test_amr_backward_is_forward_only():
+    from diff_gaussian_rasterization_amr import GaussianRasterizer
+    sc, cam = G.scene_and_camera(500, 64, 64, 1)
+    s = G.torch_settings(cam, amr=True)
+    t = G.scene_tensors(sc, requires_grad=True)
+    color, *_ = GaussianRasterizer(s)(means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]),
+                                      opacities=t["opacities"], shs=t["shs"], scales=t["scales"],
+                                      rotations=t["rotations"], foveaStep=-1)
+    with pytest.raises(RuntimeError, match="forward-only"):
+        color.sum().backward()
+
+
+# ---------------------------------------------------------- simple-knn ----
+@pytest.mark.parametrize("P,seed", [(5, 0), (1000, 1), (5000, 2), (70000, 3)])
+def test_dist_cuda2_bit_exact(P, seed):
+    import oracle as O
+    from simple_knn._C import distCUDA2
+    pts = np.random.default_rng(seed).normal(0, 3.0, (P, 3)).astype(np.float32)
+    got = distCUDA2(torch.from_numpy(pts).cuda()).cpu().numpy()
+    np.testing.assert_array_equal(got, O.dist_cuda2(pts))

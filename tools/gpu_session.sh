@@ -1,0 +1,33 @@
+#!/usr/bin/env bash
+# Guarded GPU session for gpurun: every GPU step has its own time limit and
+# the script stops at the first fault-type exit (abort/segv/timeout).  A
+# pytest exit code of 1 (test failures) is not a fault and does not stop it.
+# usage: tools/gpu_session.sh <step> [<step> ...]   steps: tests smoke bench prof pmc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+fault() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "[gpu_session] $(date +%T) start $name"
+  timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "[gpu_session] $(date +%T) end $name rc=$rc"
+  tail -n 5 "gpurun_out/$name.log"
+  if fault "$rc"; then echo "[gpu_session] stopping after fault-type exit $rc in $name"; exit "$rc"; fi
+  return 0
+}
+for step in "$@"; do
+  case "$step" in
+    tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    benchq) run bench 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile ;;
+    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
+    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[gpu_session] done"
