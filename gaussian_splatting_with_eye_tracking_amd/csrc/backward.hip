@@ -6,13 +6,16 @@
 // terms.  What changes is where the sums go: the reference issues 9 global
 // float atomics per contributing (pixel, Gaussian) pair -- on MI355X those
 // are memory-side atomics at ~one 64-B request each, and 64 lanes hitting one
-// address serialise.  Here, per Gaussian j of the LDS batch:
-//   1. each wave sums its 64 lanes' 9 terms in registers (skipped when no lane
-//      of the wave contributes -- a wave-uniform ballot),
-//   2. one lane per wave adds the 9 sums into an LDS accumulator (ds_add_f32),
-//   3. at the end of the batch the block flushes each Gaussian's 9 sums as a
-//      single 64-B row of grad_accum[P][16] (16 lanes per row, 4 rows per
-//      wave instruction): one memory-side request per (tile, Gaussian).
+// address serialise.  Here one wave64 owns a whole 16x16 tile (4 pixels per
+// lane, gs_blend.cuh) and, per Gaussian j of the LDS batch:
+//   1. each lane sums its 4 pixels' terms, then the wave sums its 64 lanes'
+//      9 values with DPP row_shr/row_bcast adds (no LDS traffic) -- skipped
+//      when no pixel of the tile contributes (a wave-uniform ballot); one
+//      reduction therefore serves 256 pixels,
+//   2. lane 63 parks the 9 sums in an LDS row,
+//   3. at the end of each 64-Gaussian batch the wave flushes each Gaussian's
+//      9 sums as a single 64-B row of grad_accum[P][16] (16 lanes per row, 4
+//      rows per wave instruction): one memory-side request per (tile, Gaussian).
 // The backward also starts each tile at max(n_contrib) of its pixels
 // (recorded by the forward) instead of the end of the range: entries past it
 // are skipped by every pixel in the reference too.
@@ -22,133 +25,140 @@
 // computeCov3D (:278-341) into one per-Gaussian pass that also emits the
 // reference's dL_dmeans2D / dL_dconic / dL_dopacity / dL_dcolors layout from
 // grad_accum, and writes every output element (zeros included).
+#include "gs_blend.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
 
 namespace gsamd {
 
-constexpr int kBlk = 256;
-constexpr int kNG = 9;  // gradient terms per (pixel, Gaussian)
+constexpr int kNG = 9;      // gradient terms per (pixel, Gaussian)
+constexpr int kAccRow = 12;  // LDS accumulator row (floats, 48 B)
 
-__global__ void __launch_bounds__(kBlk) render_bwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
-                                                          const uint32_t* __restrict__ max_contrib,
-                                                          const uint32_t* __restrict__ point_list,
-                                                          const float2* __restrict__ means2D,
-                                                          const float4* __restrict__ conic_opacity,
-                                                          const float* __restrict__ colors,
-                                                          const float* __restrict__ final_Ts,
-                                                          const uint32_t* __restrict__ n_contrib,
-                                                          const float* __restrict__ dL_dpixels,
-                                                          const float* __restrict__ bg,
-                                                          float* __restrict__ grad_accum) {
+// One wave64 per 16x16 tile, 4 pixels per lane (gs_blend.cuh mapping).
+__global__ void __launch_bounds__(64) render_bwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
+                                                        const uint32_t* __restrict__ max_contrib,
+                                                        const uint32_t* __restrict__ point_list,
+                                                        const float2* __restrict__ means2D,
+                                                        const float4* __restrict__ conic_opacity,
+                                                        const float* __restrict__ colors,
+                                                        const float* __restrict__ final_Ts,
+                                                        const uint32_t* __restrict__ n_contrib,
+                                                        const float* __restrict__ dL_dpixels,
+                                                        const float* __restrict__ bg,
+                                                        float* __restrict__ grad_accum) {
 #pragma clang fp contract(fast)
-    __shared__ uint32_t s_id[kBlk];
-    __shared__ float2 s_xy[kBlk];
-    __shared__ float4 s_co[kBlk];
-    __shared__ float4 s_rgb[kBlk];
-    __shared__ float s_acc[kBlk * kNG];
+    __shared__ uint32_t s_id[kBatch];
+    __shared__ float2 s_xy[kBatch];
+    __shared__ float4 s_co[kBatch];
+    __shared__ float4 s_rgb[kBatch];
+    __shared__ float s_acc[kBatch * kAccRow];
 
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
+    const int lane = threadIdx.x;
     const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-    const uint32_t px = blockIdx.x * 16 + (tid & 15);
-    const uint32_t py = blockIdx.y * 16 + (tid >> 4);
-    const bool inside = px < (uint32_t)W && py < (uint32_t)H;
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const int n = (int)(range.y - range.x);
     const int m = min(n, (int)max_contrib[tile]);
-    if (m == 0) return;  // block-uniform
+    if (m == 0) return;  // wave-uniform
 
+    const PixelSet px = make_pixels(W, H, blockIdx.x * 16, blockIdx.y * 16, 1);
     const size_t plane = (size_t)H * W;
-    const uint32_t pid = inside ? (uint32_t)W * py + px : 0u;
-    const float T_final = inside ? final_Ts[pid] : 0.f;
-    float T = T_final;
-    const uint32_t last_contributor = inside ? n_contrib[pid] : 0u;
-    float dpx[3];
+    const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+    float T[kPix], nbg[kPix], dpx[kPix][3], acc_rec[kPix][3], last_col[kPix][3], last_alpha[kPix];
+    uint32_t last[kPix];
 #pragma unroll
-    for (int c = 0; c < 3; c++) dpx[c] = inside ? dL_dpixels[c * plane + pid] : 0.f;
-    float accum_rec[3] = {0.f, 0.f, 0.f}, last_color[3] = {0.f, 0.f, 0.f};
-    float last_alpha = 0.f;
-    const float bg_dot_dpixel = bg[0] * dpx[0] + bg[1] * dpx[1] + bg[2] * dpx[2];
+    for (int k = 0; k < kPix; k++) {
+        const uint32_t pid = px.pid[k];
+        const float Tf = px.inside[k] ? final_Ts[pid] : 0.f;
+        T[k] = Tf;
+        last[k] = px.inside[k] ? n_contrib[pid] : 0u;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            dpx[k][c] = px.inside[k] ? dL_dpixels[c * plane + pid] : 0.f;
+            acc_rec[k][c] = 0.f;
+            last_col[k][c] = 0.f;
+        }
+        last_alpha[k] = 0.f;
+        // (-T_final / (1 - alpha)) * bg.dL_dpix = nbg * 1/(1 - alpha)
+        nbg[k] = -Tf * (bg0 * dpx[k][0] + bg1 * dpx[k][1] + bg2 * dpx[k][2]);
+    }
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
-    const float pxf = (float)px, pyf = (float)py;
 
-    const int rounds = (m + kBlk - 1) / kBlk;
-    for (int b = 0; b < rounds; b++) {
-        const int top = m - b * kBlk;  // entries [top-cnt, top) in reverse
-        const int cnt = min(kBlk, top);
+    for (int top = m; top > 0; top -= kBatch) {  // entries [top-cnt, top), back to front
+        const int cnt = min(kBatch, top);
         __syncthreads();
-        if (tid < cnt) {
-            const uint32_t id = point_list[range.x + top - 1 - tid];
-            s_id[tid] = id;
-            s_xy[tid] = means2D[id];
-            s_co[tid] = conic_opacity[id];
-            s_rgb[tid] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2], 0.f);
+        if (lane < cnt) {
+            const uint32_t id = point_list[range.x + top - 1 - lane];
+            s_id[lane] = id;
+            s_xy[lane] = means2D[id];
+            s_co[lane] = conic_opacity[id];
+            s_rgb[lane] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2], 0.f);
         }
-#pragma unroll
-        for (int q = 0; q < kNG; q++) s_acc[q * kBlk + tid] = 0.f;
         __syncthreads();
-
-        for (int k = 0; k < cnt; k++) {
-            const uint32_t contributor = (uint32_t)(top - 1 - k);
+        unsigned long long written = 0ull;
+        for (int j = 0; j < cnt; j++) {
+            const uint32_t contributor = (uint32_t)(top - 1 - j);
+            const float2 xy = s_xy[j];
+            const float4 co = s_co[j];
+            const float dx = xy.x - px.x;
             float g[kNG];
 #pragma unroll
             for (int q = 0; q < kNG; q++) g[q] = 0.f;
-            bool contrib = contributor < last_contributor;
-            if (contrib) {
-                const float2 xy = s_xy[k];
-                const float4 co = s_co[k];
-                const float dx = xy.x - pxf, dy = xy.y - pyf;
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < kPix; k++) {
+                if (contributor >= last[k]) continue;  // also covers pixels outside the image
+                const float dy = xy.y - px.y[k];
                 const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                if (power > 0.0f) continue;
                 const float G = __expf(power);
                 const float alpha = fminf(0.99f, co.w * G);
-                contrib = !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-                if (contrib) {
-                    T = T / (1.f - alpha);
-                    const float dchannel_dcolor = alpha * T;
-                    const float4 cf = s_rgb[k];
-                    const float cc[3] = {cf.x, cf.y, cf.z};
-                    float dL_dalpha = 0.0f;
+                if (alpha < 1.0f / 255.0f) continue;
+                any = true;
+                const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
+                T[k] = T[k] * rinv;
+                const float dchannel_dcolor = alpha * T[k];
+                const float4 cf = s_rgb[j];
+                const float cc[3] = {cf.x, cf.y, cf.z};
+                float dL_dalpha = 0.0f;
 #pragma unroll
-                    for (int ch = 0; ch < 3; ch++) {
-                        accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
-                        last_color[ch] = cc[ch];
-                        dL_dalpha += (cc[ch] - accum_rec[ch]) * dpx[ch];
-                        g[ch] = dchannel_dcolor * dpx[ch];
-                    }
-                    dL_dalpha *= T;
-                    last_alpha = alpha;
-                    dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
-                    const float dL_dG = co.w * dL_dalpha;
-                    const float gdx = G * dx;
-                    const float gdy = G * dy;
-                    const float dG_ddelx = -gdx * co.x - gdy * co.y;
-                    const float dG_ddely = -gdy * co.z - gdx * co.y;
-                    g[3] = dL_dG * dG_ddelx * ddelx_dx;
-                    g[4] = dL_dG * dG_ddely * ddely_dy;
-                    g[5] = -0.5f * gdx * dx * dL_dG;
-                    g[6] = -0.5f * gdx * dy * dL_dG;
-                    g[7] = -0.5f * gdy * dy * dL_dG;
-                    g[8] = G * dL_dalpha;
+                for (int ch = 0; ch < 3; ch++) {
+                    acc_rec[k][ch] = last_alpha[k] * last_col[k][ch] + (1.f - last_alpha[k]) * acc_rec[k][ch];
+                    last_col[k][ch] = cc[ch];
+                    dL_dalpha += (cc[ch] - acc_rec[k][ch]) * dpx[k][ch];
+                    g[ch] += dchannel_dcolor * dpx[k][ch];
                 }
+                dL_dalpha *= T[k];
+                last_alpha[k] = alpha;
+                dL_dalpha += nbg[k] * rinv;
+                const float dL_dG = co.w * dL_dalpha;
+                const float gdx = G * dx;
+                const float gdy = G * dy;
+                g[3] += dL_dG * (-gdx * co.x - gdy * co.y) * ddelx_dx;
+                g[4] += dL_dG * (-gdy * co.z - gdx * co.y) * ddely_dy;
+                g[5] += -0.5f * gdx * dx * dL_dG;
+                g[6] += -0.5f * gdx * dy * dL_dG;
+                g[7] += -0.5f * gdy * dy * dL_dG;
+                g[8] += G * dL_dalpha;
             }
-            if (__ballot(contrib) != 0ull) {  // wave-uniform
+            if (__ballot(any) != 0ull) {  // wave-uniform: reduce the 9 sums into lane 63
 #pragma unroll
-                for (int q = 0; q < kNG; q++) g[q] = wave_sum(g[q]);
-                if (lane == 0) {
+                for (int q = 0; q < kNG; q++) g[q] = dpp_sum_lane63(g[q]);
+                if (lane == 63) {
 #pragma unroll
-                    for (int q = 0; q < kNG; q++) atomicAdd(&s_acc[q * kBlk + k], g[q]);
+                    for (int q = 0; q < kNG; q++) s_acc[j * kAccRow + q] = g[q];
                 }
+                written |= 1ull << j;
             }
         }
         __syncthreads();
-        // Flush: 16 lanes per Gaussian row, 4 rows per wave instruction.
-        const int wave = tid >> 6;
+        // Flush: 16 lanes per Gaussian row, 4 rows per wave instruction
+        // (one 64-B memory-side atomic request per (tile, Gaussian)).
         const int comp = lane & 15;
-        for (int r = wave * 4 + (lane >> 4); r < cnt; r += 16) {
-            if (comp < kNG) {
-                const float v = s_acc[comp * kBlk + r];
+#pragma unroll 4
+        for (int r = lane >> 4; r < cnt; r += 4) {
+            if (comp < kNG && ((written >> r) & 1ull)) {
+                const float v = s_acc[r * kAccRow + comp];
                 if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[r] * kGradRow + comp], v);
             }
         }
@@ -159,7 +169,7 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s) {
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return;
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(gx, gy), dim3(kBlk), 0, s, W, H, img.ranges, img.max_contrib,
+    hipLaunchKernelGGL(render_bwd_kernel, dim3(gx, gy), dim3(64), 0, s, W, H, img.ranges, img.max_contrib,
                        b.point_list, reinterpret_cast<const float2*>(g.means2D),
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,
                        dL_dpix, bg, g.grad_accum);

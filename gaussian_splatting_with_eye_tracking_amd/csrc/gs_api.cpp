@@ -390,6 +390,16 @@ int gs_simple_knn(int P, const float* points, float* mean_dists, gs_buffer scrat
     });
 }
 
+int gs_set_tuning(const char* key, int value) {
+    if (!key) return -1;
+    if (std::strcmp(key, "fwd_variant") == 0) {
+        set_forward_variant(value);
+        return 0;
+    }
+    g_err = std::string("unknown tuning key ") + key;
+    return -1;
+}
+
 void gs_profile_enable(int on) {
     std::lock_guard<std::mutex> l(g_prof_mu);
     g_prof.on = on != 0;

@@ -4,133 +4,99 @@
 // 261-518 (renderCUDA with per-tile level skip on the 2x2 sub-lattice) and
 // :520-648 (interpolateCUDA).
 //
-// One 256-thread workgroup (4 wave64s) per 16x16 pixel block; wave w owns
-// pixel rows 4w..4w+3 so a wave's 64 pixels are a compact 16x4 patch and its
-// lanes tend to finish together.  Gaussians are staged in LDS 256 at a time
-// (position, conic+opacity, colour -- the reference re-reads colour from
-// global memory per pixel-Gaussian pair; here it is staged too).  The
+// One wave64 per 16x16 pixel block, 4 pixels per lane (gs_blend.cuh).
+// Gaussians are staged in LDS 64 at a time (position, conic+opacity, colour
+// -- the reference re-reads colour from global memory per pixel-Gaussian
+// pair; here it is staged too).  The
 // per-pixel semantics (contributor / last_contributor / done, the alpha<1/255
 // and T<1e-4 tests) are the reference's; the forward additionally records the
 // per-tile maximum n_contrib so the backward can skip the tail of a range no
 // pixel of the tile consumed.
+#include "gs_blend.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
 
 namespace gsamd {
 
-constexpr int kBlk = 256;
-
-struct BlendOut {
-    float T;
-    uint32_t last;
-    float C[3];
-};
-
-// Blend `range` for pixel (pixf) -- the body shared by base and AMR kernels.
-// All 256 threads must call it (it contains barriers); `done` marks lanes that
-// do not blend (outside the image).
-__device__ __forceinline__ BlendOut blend_range(uint2 range, float2 pixf, bool done,
-                                                const uint32_t* __restrict__ point_list,
-                                                const float2* __restrict__ means2D,
-                                                const float* __restrict__ features,
-                                                const float4* __restrict__ conic_opacity, float2* s_xy,
-                                                float4* s_co, float4* s_rgb) {
-#pragma clang fp contract(fast)
-    const int tid = threadIdx.x;
-    const int rounds = (int)((range.y - range.x + kBlk - 1) / kBlk);
-    int toDo = (int)(range.y - range.x);
-    BlendOut o;
-    o.T = 1.0f;
-    o.last = 0;
-    o.C[0] = o.C[1] = o.C[2] = 0.f;
-    uint32_t contributor = 0;
-    for (int i = 0; i < rounds; i++, toDo -= kBlk) {
-        if (__syncthreads_count(done) == kBlk) break;
-        const uint32_t progress = (uint32_t)(i * kBlk + tid);
-        if (range.x + progress < range.y) {
-            const uint32_t id = point_list[range.x + progress];
-            s_xy[tid] = means2D[id];
-            s_co[tid] = conic_opacity[id];
-            s_rgb[tid] = make_float4(features[3 * id], features[3 * id + 1], features[3 * id + 2], 0.f);
-        }
-        __syncthreads();
-        const int cnt = min(kBlk, toDo);
-        for (int j = 0; j < cnt && !done; j++) {
-            contributor++;
-            const float2 xy = s_xy[j];
-            const float dx = xy.x - pixf.x, dy = xy.y - pixf.y;
-            const float4 co = s_co[j];
-            const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-            if (power > 0.0f) continue;
-            const float alpha = fminf(0.99f, co.w * __expf(power));
-            if (alpha < 1.0f / 255.0f) continue;
-            const float test_T = o.T * (1 - alpha);
-            if (test_T < 0.0001f) {
-                done = true;
-                continue;
-            }
-            const float4 f = s_rgb[j];
-            const float w = alpha * o.T;
-            o.C[0] += f.x * w;
-            o.C[1] += f.y * w;
-            o.C[2] += f.z * w;
-            o.T = test_T;
-            o.last = contributor;
-        }
-    }
-    return o;
-}
-
-__device__ __forceinline__ void block_max_to(uint32_t v, uint32_t* smax, uint32_t* dst) {
-    // wave max, then one LDS atomic per wave
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, kWave));
-    if ((threadIdx.x & (kWave - 1)) == 0) atomicMax(smax, v);
-    __syncthreads();
-    if (threadIdx.x == 0) *dst = *smax;
+    return v;
 }
 
-__global__ void __launch_bounds__(kBlk) render_fwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
-                                                          const uint32_t* __restrict__ point_list,
-                                                          const float2* __restrict__ means2D,
-                                                          const float* __restrict__ features,
-                                                          const float4* __restrict__ conic_opacity,
-                                                          float* __restrict__ final_T,
-                                                          uint32_t* __restrict__ n_contrib,
-                                                          uint32_t* __restrict__ max_contrib,
-                                                          const float* __restrict__ bg, float* __restrict__ out_color) {
-    __shared__ float2 s_xy[kBlk];
-    __shared__ float4 s_co[kBlk];
-    __shared__ float4 s_rgb[kBlk];
-    __shared__ uint32_t s_max;
-    const int tid = threadIdx.x;
-    if (tid == 0) s_max = 0;
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-    const uint32_t px = blockIdx.x * 16 + (tid & 15);
-    const uint32_t py = blockIdx.y * 16 + (tid >> 4);
-    const bool inside = px < (uint32_t)W && py < (uint32_t)H;
-    const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
-    const BlendOut o = blend_range(range, make_float2((float)px, (float)py), !inside, point_list, means2D, features,
-                                   conic_opacity, s_xy, s_co, s_rgb);
-    if (inside) {
-        const uint32_t pid = (uint32_t)W * py + px;
-        final_T[pid] = o.T;
-        n_contrib[pid] = o.last;
-        const size_t plane = (size_t)H * W;
+template <int kPPL>
+__device__ __forceinline__ void write_pixels(const PixelSetT<kPPL>& px, const BlendStateT<kPPL>& st, int W, int H,
+                                             float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+                                             const float* __restrict__ bg, float* __restrict__ out_color) {
+    const size_t plane = (size_t)H * W;
+    const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
 #pragma unroll
-        for (int ch = 0; ch < 3; ch++) out_color[ch * plane + pid] = o.C[ch] + o.T * bg[ch];
+    for (int k = 0; k < kPPL; k++) {
+        if (!px.inside[k]) continue;
+        const uint32_t pid = px.pid[k];
+        final_T[pid] = st.T[k];
+        n_contrib[pid] = st.last[k];
+        out_color[pid] = st.C[k][0] + st.T[k] * b0;
+        out_color[plane + pid] = st.C[k][1] + st.T[k] * b1;
+        out_color[2 * plane + pid] = st.C[k][2] + st.T[k] * b2;
     }
-    block_max_to(inside ? o.last : 0u, &s_max, &max_contrib[tile]);
 }
+
+// One 16x16 tile per workgroup of kWaves waves (kPPL pixels per lane).
+template <int kPPL, int kWaves>
+__global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
+                                                                 const uint32_t* __restrict__ point_list,
+                                                                 const float2* __restrict__ means2D,
+                                                                 const float* __restrict__ features,
+                                                                 const float4* __restrict__ conic_opacity,
+                                                                 float* __restrict__ final_T,
+                                                                 uint32_t* __restrict__ n_contrib,
+                                                                 uint32_t* __restrict__ max_contrib,
+                                                                 const float* __restrict__ bg,
+                                                                 float* __restrict__ out_color) {
+    __shared__ float2 s_xy[64 * kWaves];
+    __shared__ float4 s_co[64 * kWaves];
+    __shared__ float4 s_rgb[64 * kWaves];
+    __shared__ uint32_t s_max;
+    if (kWaves > 1 && threadIdx.x == 0) s_max = 0;
+    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, blockIdx.x * 16, blockIdx.y * 16, 1);
+    const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
+    const BlendStateT<kPPL> st = blend_tile_t<kPPL, kWaves>(range, px, point_list, means2D, features,
+                                                            conic_opacity, s_xy, s_co, s_rgb);
+    write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < kPPL; k++) m = max(m, px.inside[k] ? st.last[k] : 0u);
+    m = wave_max_u32(m);
+    if (kWaves == 1) {
+        if (threadIdx.x == 0) max_contrib[tile] = m;
+    } else {
+        if ((threadIdx.x & 63) == 0) atomicMax(&s_max, m);
+        __syncthreads();
+        if (threadIdx.x == 0) max_contrib[tile] = s_max;
+    }
+}
+
+int g_fwd_variant = 1;  // 0: 1 wave x 4 px/lane, 1: 2 waves x 2 px/lane, 2: 4 waves x 1 px/lane
+
+void set_forward_variant(int v) { g_fwd_variant = v; }
 
 void launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                            const float* features, const float* bg, float* out_color, hipStream_t s) {
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return;
-    hipLaunchKernelGGL(render_fwd_kernel, dim3(gx, gy), dim3(kBlk), 0, s, W, H, img.ranges, b.point_list,
-                       reinterpret_cast<const float2*>(g.means2D), features,
-                       reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,
-                       img.max_contrib, bg, out_color);
+#define GS_FWD_LAUNCH(PPL, WAVES)                                                                                \
+    hipLaunchKernelGGL((render_fwd_kernel<PPL, WAVES>), dim3(gx, gy), dim3(64 * WAVES), 0, s, W, H, img.ranges, \
+                       b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
+                       reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
+                       img.max_contrib, bg, out_color)
+    switch (g_fwd_variant) {
+        case 0: GS_FWD_LAUNCH(4, 1); break;
+        case 2: GS_FWD_LAUNCH(1, 4); break;
+        default: GS_FWD_LAUNCH(2, 2); break;
+    }
+#undef GS_FWD_LAUNCH
 }
 
 // ------------------------------------------------------------------- AMR ---
@@ -139,21 +105,21 @@ __device__ __forceinline__ uint32_t amr_round(uint32_t ox, uint32_t oy) {
     return ox == 0 ? (oy == 0 ? 1u : 4u) : (oy == 0 ? 3u : 2u);
 }
 
-// grid (2*tgx, 2*tgy) x 256: block -> (32-px tile, sub-lattice offset).
-__global__ void __launch_bounds__(kBlk) amr_render_kernel(int W, int H, int tgx, const uint32_t* __restrict__ ranges,
-                                                          const uint32_t* __restrict__ levels,
-                                                          const uint32_t* __restrict__ levels_last,
-                                                          const uint32_t* __restrict__ point_list,
-                                                          const float2* __restrict__ means2D,
-                                                          const float* __restrict__ features,
-                                                          const float4* __restrict__ conic_opacity,
-                                                          float* __restrict__ final_T,
-                                                          uint32_t* __restrict__ n_contrib,
-                                                          const float* __restrict__ bg, float* __restrict__ out_color,
-                                                          int foveaStep) {
-    __shared__ float2 s_xy[kBlk];
-    __shared__ float4 s_co[kBlk];
-    __shared__ float4 s_rgb[kBlk];
+// grid (2*tgx, 2*tgy) x one wave: block -> (32-px tile, sub-lattice offset);
+// the wave covers the tile's 16x16 sub-lattice with stride 2.
+__global__ void __launch_bounds__(64) amr_render_kernel(int W, int H, int tgx, const uint32_t* __restrict__ ranges,
+                                                        const uint32_t* __restrict__ levels,
+                                                        const uint32_t* __restrict__ levels_last,
+                                                        const uint32_t* __restrict__ point_list,
+                                                        const float2* __restrict__ means2D,
+                                                        const float* __restrict__ features,
+                                                        const float4* __restrict__ conic_opacity,
+                                                        float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+                                                        const float* __restrict__ bg, float* __restrict__ out_color,
+                                                        int foveaStep) {
+    __shared__ float2 s_xy[kBatch];
+    __shared__ float4 s_co[kBatch];
+    __shared__ float4 s_rgb[kBatch];
     const int tile = (blockIdx.y >> 1) * tgx + (blockIdx.x >> 1);
     const uint32_t L_last = levels_last[tile];
     uint32_t L = levels[tile];
@@ -164,21 +130,11 @@ __global__ void __launch_bounds__(kBlk) amr_render_kernel(int W, int H, int tgx,
     if (L > 4) L = 4;
     if (foveaStep > 0 && round <= L_last) return;
     if (round > L) return;
-    const int tid = threadIdx.x;
-    const uint32_t px = (blockIdx.x >> 1) * 32 + 2 * (tid & 15) + ox;
-    const uint32_t py = (blockIdx.y >> 1) * 32 + 2 * (tid >> 4) + oy;
-    const bool inside = px < (uint32_t)W && py < (uint32_t)H;
+    const PixelSet px = make_pixels(W, H, (blockIdx.x >> 1) * 32 + ox, (blockIdx.y >> 1) * 32 + oy, 2);
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
-    const BlendOut o = blend_range(range, make_float2((float)px, (float)py), !inside, point_list, means2D, features,
-                                   conic_opacity, s_xy, s_co, s_rgb);
-    if (inside) {
-        const uint32_t pid = (uint32_t)W * py + px;
-        final_T[pid] = o.T;
-        n_contrib[pid] = o.last;
-        const size_t plane = (size_t)H * W;
-#pragma unroll
-        for (int ch = 0; ch < 3; ch++) out_color[ch * plane + pid] = o.C[ch] + o.T * bg[ch];
-    }
+    const BlendStateT<kPix> st = blend_tile_t<kPix, 1>(range, px, point_list, means2D, features, conic_opacity,
+                                                       s_xy, s_co, s_rgb);
+    write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
 }
 
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
@@ -186,7 +142,7 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
                        float* out_color, int foveaStep, hipStream_t s) {
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0) return;
-    hipLaunchKernelGGL(amr_render_kernel, dim3(2 * tgx, 2 * tgy), dim3(kBlk), 0, s, W, H, tgx, img.ranges, levels,
+    hipLaunchKernelGGL(amr_render_kernel, dim3(2 * tgx, 2 * tgy), dim3(64), 0, s, W, H, tgx, img.ranges, levels,
                        levels_last, b.point_list, reinterpret_cast<const float2*>(g.means2D), features,
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib, bg,
                        out_color, foveaStep);

@@ -298,4 +298,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("abi_version", []() { return gs_abi_version(); });
     m.def("profile_enable", [](bool on) { gs_profile_enable(on ? 1 : 0); });
     m.def("profile_read", &ProfileRead, py::arg("reset") = true);
+    m.def("set_tuning", [](const std::string& k, int v) { check(gs_set_tuning(k.c_str(), v), "set_tuning"); });
 }

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Interleaved in-process A/B of kernel-geometry variants (guide §5.4 rule
+24): N variants x R rounds in ONE process on one device, per-stage HIP-event
+times from the library's profiler, median and min reported.
+
+usage: python tools/ab_tuning.py --key fwd_variant --values 0 1 2 --stage render [--backward]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--key", default="fwd_variant")
+    ap.add_argument("--values", type=int, nargs="+", default=[0, 1, 2])
+    ap.add_argument("--stage", default="render")
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--P", type=int, default=1_000_000)
+    ap.add_argument("--W", type=int, default=1920)
+    ap.add_argument("--H", type=int, default=1080)
+    ap.add_argument("--backward", action="store_true")
+    args = ap.parse_args()
+
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    dev = torch.device("cuda:0")
+    cam = S.make_camera(args.W, args.H)
+    sc = S.make_scene(args.P, cam, seed=0)
+    st = GaussianRasterizationSettings(
+        image_height=args.H, image_width=args.W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+        bg=torch.zeros(3, device=dev), scale_modifier=1.0,
+        viewmatrix=torch.from_numpy(cam.world_view_transform).to(dev),
+        projmatrix=torch.from_numpy(cam.full_proj_transform).to(dev), sh_degree=3,
+        campos=torch.from_numpy(cam.camera_center).to(dev), prefiltered=False, debug=False)
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(sc, k))).to(dev).requires_grad_(args.backward)
+         for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+    m2 = torch.zeros_like(t["means3D"], requires_grad=args.backward)
+    dpix = torch.from_numpy(S.make_cotangent(args.H, args.W, 1)).to(dev)
+    ras = GaussianRasterizer(st)
+
+    def run():
+        color, _ = ras(means3D=t["means3D"], means2D=m2, opacities=t["opacities"], shs=t["shs"],
+                       scales=t["scales"], rotations=t["rotations"])
+        if args.backward:
+            torch.autograd.backward(color, dpix)
+        return color
+
+    ref_img = None
+    results = {v: [] for v in args.values}
+    _C.profile_enable(True)
+    for r in range(args.rounds):
+        for v in args.values:
+            _C.set_tuning(args.key, v)
+            img = run()  # warm
+            torch.cuda.synchronize()
+            if ref_img is None:
+                ref_img = img.detach().clone()
+            else:
+                d = float((img.detach() - ref_img).abs().max())
+                if d > 1e-5:
+                    print(f"WARNING variant {v}: max image diff {d}")
+            _C.profile_read(True)
+            for _ in range(args.iters):
+                run()
+            torch.cuda.synchronize()
+            prof = _C.profile_read(True)
+            ms, cnt = prof[args.stage]
+            results[v].append(ms / max(cnt, 1))
+    _C.profile_enable(False)
+    out = {str(v): {"median_ms": float(np.median(x)), "min_ms": float(np.min(x)), "all": [round(a, 4) for a in x]}
+           for v, x in results.items()}
+    print(json.dumps({"key": args.key, "stage": args.stage, "results": out}))
+
+
+if __name__ == "__main__":
+    main()
