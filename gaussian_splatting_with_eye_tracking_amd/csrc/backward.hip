@@ -34,43 +34,45 @@ namespace gsamd {
 constexpr int kNG = 9;      // gradient terms per (pixel, Gaussian)
 constexpr int kAccRow = 12;  // LDS accumulator row (floats, 48 B)
 
-// One wave64 per 16x16 tile, 4 pixels per lane (gs_blend.cuh mapping).
-__global__ void __launch_bounds__(64) render_bwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
-                                                        const uint32_t* __restrict__ max_contrib,
-                                                        const uint32_t* __restrict__ point_list,
-                                                        const float2* __restrict__ means2D,
-                                                        const float4* __restrict__ conic_opacity,
-                                                        const float* __restrict__ colors,
-                                                        const float* __restrict__ final_Ts,
-                                                        const uint32_t* __restrict__ n_contrib,
-                                                        const float* __restrict__ dL_dpixels,
-                                                        const float* __restrict__ bg,
-                                                        float* __restrict__ grad_accum) {
+// One 16x16 tile per workgroup of kWaves wave64s, kPPL pixels per lane
+// (kWaves * 64 * kPPL = 256; gs_blend.cuh mapping).  kMinWaves: waves per
+// SIMD the register allocation must allow.
+template <int kPPL, int kWaves, int kMinWaves>
+__global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
+    int W, int H, const uint32_t* __restrict__ ranges, const uint32_t* __restrict__ max_contrib,
+    const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
+    const float4* __restrict__ conic_opacity, const float* __restrict__ colors, const float* __restrict__ final_Ts,
+    const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ bg,
+    float* __restrict__ grad_accum) {
 #pragma clang fp contract(fast)
-    __shared__ uint32_t s_id[kBatch];
-    __shared__ float2 s_xy[kBatch];
-    __shared__ float4 s_co[kBatch];
-    __shared__ float4 s_rgb[kBatch];
-    __shared__ float s_acc[kBatch * kAccRow];
+    constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
+    __shared__ uint32_t s_id[kB];
+    __shared__ float2 s_xy[kB];
+    __shared__ float4 s_co[kB];
+    __shared__ float4 s_rgb[kB];
+    __shared__ float s_acc[kB * kAccRow];
 
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
     const int tile = blockIdx.y * gridDim.x + blockIdx.x;
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const int n = (int)(range.y - range.x);
     const int m = min(n, (int)max_contrib[tile]);
-    if (m == 0) return;  // wave-uniform
+    if (m == 0) return;  // block-uniform
 
-    const PixelSet px = make_pixels(W, H, blockIdx.x * 16, blockIdx.y * 16, 1);
+    const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, blockIdx.x * 16, blockIdx.y * 16, 1);
     const size_t plane = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
-    float T[kPix], nbg[kPix], dpx[kPix][3], acc_rec[kPix][3], last_col[kPix][3], last_alpha[kPix];
-    uint32_t last[kPix];
+    float T[kPPL], nbg[kPPL], dpx[kPPL][3], acc_rec[kPPL][3], last_col[kPPL][3], last_alpha[kPPL];
+    uint32_t last[kPPL];
+    uint32_t wave_last = 0;
 #pragma unroll
-    for (int k = 0; k < kPix; k++) {
+    for (int k = 0; k < kPPL; k++) {
         const uint32_t pid = px.pid[k];
         const float Tf = px.inside[k] ? final_Ts[pid] : 0.f;
         T[k] = Tf;
         last[k] = px.inside[k] ? n_contrib[pid] : 0u;
+        wave_last = max(wave_last, last[k]);
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             dpx[k][c] = px.inside[k] ? dL_dpixels[c * plane + pid] : 0.f;
@@ -81,22 +83,27 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(int W, int H, const uint
         // (-T_final / (1 - alpha)) * bg.dL_dpix = nbg * 1/(1 - alpha)
         nbg[k] = -Tf * (bg0 * dpx[k][0] + bg1 * dpx[k][1] + bg2 * dpx[k][2]);
     }
+    // entries at or past the wave's max n_contrib are skipped by all its pixels
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) wave_last = max(wave_last, (uint32_t)__shfl_xor((int)wave_last, off, 64));
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
 
-    for (int top = m; top > 0; top -= kBatch) {  // entries [top-cnt, top), back to front
-        const int cnt = min(kBatch, top);
+    for (int top = m; top > 0; top -= kB) {  // entries [top-cnt, top), back to front
+        const int cnt = min(kB, top);
         __syncthreads();
-        if (lane < cnt) {
-            const uint32_t id = point_list[range.x + top - 1 - lane];
-            s_id[lane] = id;
-            s_xy[lane] = means2D[id];
-            s_co[lane] = conic_opacity[id];
-            s_rgb[lane] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2], 0.f);
+        if (tid < cnt) {
+            const uint32_t id = point_list[range.x + top - 1 - tid];
+            s_id[tid] = id;
+            s_xy[tid] = means2D[id];
+            s_co[tid] = conic_opacity[id];
+            s_rgb[tid] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2], 0.f);
         }
+        for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
         __syncthreads();
-        unsigned long long written = 0ull;
-        for (int j = 0; j < cnt; j++) {
+        // first batch slot this wave needs: contributor = top-1-j < wave_last
+        const int j0 = max(0, top - (int)wave_last);
+        for (int j = j0; j < cnt; j++) {
             const uint32_t contributor = (uint32_t)(top - 1 - j);
             const float2 xy = s_xy[j];
             const float4 co = s_co[j];
@@ -106,7 +113,7 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(int W, int H, const uint
             for (int q = 0; q < kNG; q++) g[q] = 0.f;
             bool any = false;
 #pragma unroll
-            for (int k = 0; k < kPix; k++) {
+            for (int k = 0; k < kPPL; k++) {
                 if (contributor >= last[k]) continue;  // also covers pixels outside the image
                 const float dy = xy.y - px.y[k];
                 const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
@@ -142,22 +149,24 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(int W, int H, const uint
                 g[8] += G * dL_dalpha;
             }
             if (__ballot(any) != 0ull) {  // wave-uniform: reduce the 9 sums into lane 63
-#pragma unroll
-                for (int q = 0; q < kNG; q++) g[q] = dpp_sum_lane63(g[q]);
+                dpp_sum9_lane63(g);
                 if (lane == 63) {
+                    if (kWaves == 1) {
 #pragma unroll
-                    for (int q = 0; q < kNG; q++) s_acc[j * kAccRow + q] = g[q];
+                        for (int q = 0; q < kNG; q++) s_acc[j * kAccRow + q] = g[q];
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < kNG; q++) atomicAdd(&s_acc[j * kAccRow + q], g[q]);
+                    }
                 }
-                written |= 1ull << j;
             }
         }
         __syncthreads();
         // Flush: 16 lanes per Gaussian row, 4 rows per wave instruction
         // (one 64-B memory-side atomic request per (tile, Gaussian)).
         const int comp = lane & 15;
-#pragma unroll 4
-        for (int r = lane >> 4; r < cnt; r += 4) {
-            if (comp < kNG && ((written >> r) & 1ull)) {
+        for (int r = (tid >> 4); r < cnt; r += 4 * kWaves) {
+            if (comp < kNG) {
                 const float v = s_acc[r * kAccRow + comp];
                 if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[r] * kGradRow + comp], v);
             }
@@ -165,14 +174,26 @@ __global__ void __launch_bounds__(64) render_bwd_kernel(int W, int H, const uint
     }
 }
 
+int g_bwd_variant = 1;  // 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave uncapped
+
+void set_backward_variant(int v) { g_bwd_variant = v; }
+
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s) {
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return;
-    hipLaunchKernelGGL(render_bwd_kernel, dim3(gx, gy), dim3(64), 0, s, W, H, img.ranges, img.max_contrib,
-                       b.point_list, reinterpret_cast<const float2*>(g.means2D),
-                       reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,
-                       dL_dpix, bg, g.grad_accum);
+#define GS_BWD_LAUNCH(PPL, WAVES, OCC)                                                                          \
+    hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC>), dim3(gx, gy), dim3(64 * WAVES), 0, s, W, H,       \
+                       img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
+                       reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
+                       dL_dpix, bg, g.grad_accum)
+    switch (g_bwd_variant) {
+        case 1: GS_BWD_LAUNCH(2, 2, 4); break;
+        case 2: GS_BWD_LAUNCH(1, 4, 4); break;
+        case 3: GS_BWD_LAUNCH(4, 1, 1); break;
+        default: GS_BWD_LAUNCH(4, 1, 4); break;
+    }
+#undef GS_BWD_LAUNCH
 }
 
 // ------------------------------------------------------ per-Gaussian bwd ---
@@ -226,12 +247,46 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
         return;
     }
 
+    // All loads up front (one memory round trip per thread).
     const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
-    const Mat4 V = load_mat4(a.viewmatrix);
-    const Mat4 Pm = load_mat4(a.projmatrix);
     float cov3D[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D[6 * idx + i];
+    float4 qrot = make_float4(0.f, 0.f, 0.f, 0.f);
+    float scl[3] = {0.f, 0.f, 0.f};
+    if (kHasScales) {
+        qrot = reinterpret_cast<const float4*>(a.rotations)[idx];
+        scl[0] = a.scales[3 * idx + 0];
+        scl[1] = a.scales[3 * idx + 1];
+        scl[2] = a.scales[3 * idx + 2];
+    }
+    float s[16][3];
+    uint8_t cb = 0;
+    if (kHasSH) {
+        const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
+        const float* sh = a.shs + (size_t)idx * a.M * 3;
+        if (a.M == 16) {
+            const float4* s4 = reinterpret_cast<const float4*>(sh);
+            float buf[48];
+#pragma unroll
+            for (int i = 0; i < 12; i++) {
+                const float4 v4 = (i * 4 < ncoef * 3) ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                buf[4 * i + 0] = v4.x; buf[4 * i + 1] = v4.y; buf[4 * i + 2] = v4.z; buf[4 * i + 3] = v4.w;
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) s[k][c] = buf[3 * k + c];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) s[k][c] = (k < ncoef) ? sh[3 * k + c] : 0.f;
+        }
+        cb = clamped_bits[idx];
+    }
+    const Mat4 V = load_mat4(a.viewmatrix);
+    const Mat4 Pm = load_mat4(a.projmatrix);
 
     // ---- computeCov2DCUDA (backward.cu:144-274)
     float dmean[3];
@@ -329,13 +384,11 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
     // ---- computeColorFromSH backward (backward.cu:20-139)
     if (kHasSH) {
         const int deg = a.D;
-        const int ncoef = (deg + 1) * (deg + 1);
-        const float* sh = a.shs + (size_t)idx * a.M * 3;
+        const int ncoef = min((deg + 1) * (deg + 1), a.M);
         float* dsh = a.dL_dsh + (size_t)idx * a.M * 3;
         const float dox = mx - a.campos[0], doy = my - a.campos[1], doz = mz - a.campos[2];
         const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
         const float x = dox / len, y = doy / len, z = doz / len;
-        const uint8_t cb = clamped_bits[idx];
         float dRGB[3];
 #pragma unroll
         for (int c = 0; c < 3; c++) dRGB[c] = acc[c] * (((cb >> c) & 1) ? 0.0f : 1.0f);
@@ -344,11 +397,6 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
 #pragma unroll
         for (int k = 0; k < 16; k++) dsh_c[k] = 0.f;
         dsh_c[0] = SH_C0;
-        float s[16][3];
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) s[k][c] = (k < ncoef) ? sh[3 * k + c] : 0.f;
         if (deg > 0) {
             dsh_c[1] = -SH_C1 * y;
             dsh_c[2] = SH_C1 * z;
@@ -417,12 +465,11 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
 
     // ---- computeCov3D backward (backward.cu:278-341)
     if (kHasScales) {
-        const float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
-        const float r = q.x, x = q.y, y = q.z, z = q.w;
+        const float r = qrot.x, x = qrot.y, y = qrot.z, z = qrot.w;
         const Mat3 R = quat_to_R(r, x, y, z);
-        const float sx = a.scale_modifier * a.scales[3 * idx + 0];
-        const float sy = a.scale_modifier * a.scales[3 * idx + 1];
-        const float sz = a.scale_modifier * a.scales[3 * idx + 2];
+        const float sx = a.scale_modifier * scl[0];
+        const float sy = a.scale_modifier * scl[1];
+        const float sz = a.scale_modifier * scl[2];
         Mat3 S = mat3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
         S.m[0][0] = sx; S.m[1][1] = sy; S.m[2][2] = sz;
         const Mat3 Mm = mat3_mul(S, R);

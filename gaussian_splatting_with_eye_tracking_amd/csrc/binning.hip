@@ -102,11 +102,28 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const float* __re
     const float2 xy = reinterpret_cast<const float2*>(means2D)[idx];
     const Rect r = get_rect(xy.x, xy.y, rad, block, block, gx, gy);
     const uint64_t key = ((uint64_t)float_bits(depths[idx]) << 32) | (uint32_t)idx;
-    for (uint32_t y = r.y0; y < r.y1; y++)
-        for (uint32_t x = r.x0; x < r.x1; x++) {
-            const uint32_t pos = atomicAdd(&cursor[y * gx + x], 1u);
-            pair_keys[pos] = key;
+    // Walk the rect row-major with kInFlight returning atomics outstanding
+    // (one round trip per kInFlight tiles instead of per tile).
+    constexpr int kInFlight = 8;
+    const uint32_t w = r.x1 - r.x0;
+    const uint32_t area = w * (r.y1 - r.y0);
+    uint32_t x = r.x0, y = r.y0;
+    for (uint32_t i0 = 0; i0 < area; i0 += kInFlight) {
+        uint32_t pos[kInFlight];
+#pragma unroll
+        for (int u = 0; u < kInFlight; u++) {
+            if (i0 + u < area) {
+                pos[u] = atomicAdd(&cursor[y * gx + x], 1u);
+                if (++x == r.x1) {
+                    x = r.x0;
+                    ++y;
+                }
+            }
         }
+#pragma unroll
+        for (int u = 0; u < kInFlight; u++)
+            if (i0 + u < area) pair_keys[pos[u]] = key;
+    }
 }
 
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,

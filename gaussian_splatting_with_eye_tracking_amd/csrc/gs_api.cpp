@@ -396,6 +396,10 @@ int gs_set_tuning(const char* key, int value) {
         set_forward_variant(value);
         return 0;
     }
+    if (std::strcmp(key, "bwd_variant") == 0) {
+        set_backward_variant(value);
+        return 0;
+    }
     g_err = std::string("unknown tuning key ") + key;
     return -1;
 }

@@ -18,18 +18,16 @@
 
 namespace gsamd {
 
-// base/cr/forward.cu:20-71.  `sh` points at this Gaussian's first coeff.
+// Load this Gaussian's SH coefficients (zero past the active degree).
 template <bool kSH16>
-__device__ __forceinline__ float3 eval_sh_color(int deg, const float* __restrict__ sh, float x, float y,
-                                                float z, uint8_t& clamped_bits) {
-    float c[16][3];
-    const int ncoef = (deg + 1) * (deg + 1);
+__device__ __forceinline__ void load_sh(int deg, int M, const float* __restrict__ sh, float (&c)[16][3]) {
+    const int ncoef = min((deg + 1) * (deg + 1), M);
     if (kSH16) {
         const float4* s4 = reinterpret_cast<const float4*>(sh);
         float buf[48];
 #pragma unroll
         for (int i = 0; i < 12; i++) {
-            float4 v = (i * 4 < ncoef * 3) ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const float4 v = (i * 4 < ncoef * 3) ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
             buf[4 * i + 0] = v.x; buf[4 * i + 1] = v.y; buf[4 * i + 2] = v.z; buf[4 * i + 3] = v.w;
         }
 #pragma unroll
@@ -42,6 +40,11 @@ __device__ __forceinline__ float3 eval_sh_color(int deg, const float* __restrict
 #pragma unroll
             for (int ch = 0; ch < 3; ch++) c[k][ch] = (k < ncoef) ? sh[3 * k + ch] : 0.f;
     }
+}
+
+// base/cr/forward.cu:20-71 on preloaded coefficients.
+__device__ __forceinline__ float3 eval_sh_color(int deg, const float (&c)[16][3], float x, float y, float z,
+                                                uint8_t& clamped_bits) {
     float res[3];
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) res[ch] = SH_C0 * c[0][ch];
@@ -93,9 +96,26 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
     radii[idx] = 0;
     g.tiles_touched[idx] = 0;
 
+    // Every global load of this Gaussian is issued up front (one memory round
+    // trip per thread); the math below then overlaps other waves' loads.
     const float mx = a.means3D[3 * idx + 0];
     const float my = a.means3D[3 * idx + 1];
     const float mz = a.means3D[3 * idx + 2];
+    float sc[3] = {0.f, 0.f, 0.f};
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    float cov3D[6];
+    if (kCovPrecomp) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D_precomp[6 * idx + i];
+    } else {
+        sc[0] = a.scales[3 * idx + 0];
+        sc[1] = a.scales[3 * idx + 1];
+        sc[2] = a.scales[3 * idx + 2];
+        q = reinterpret_cast<const float4*>(a.rotations)[idx];
+    }
+    const float opacity = a.opacities[idx];
+    float shc[16][3];
+    if (kHasSH) load_sh<kSH16>(a.D, a.M, a.shs + (size_t)idx * a.M * 3, shc);
     const Mat4 V = load_mat4(a.viewmatrix);
     const Mat4 Pm = load_mat4(a.projmatrix);
 
@@ -111,16 +131,11 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
     const float p_proj_y = p_hom.y * p_w;
 
     // computeCov3D (forward.cu:118-152)
-    float cov3D[6];
-    if (kCovPrecomp) {
-#pragma unroll
-        for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D_precomp[6 * idx + i];
-    } else {
+    if (!kCovPrecomp) {
         Mat3 S = mat3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
-        S.m[0][0] = a.scale_modifier * a.scales[3 * idx + 0];
-        S.m[1][1] = a.scale_modifier * a.scales[3 * idx + 1];
-        S.m[2][2] = a.scale_modifier * a.scales[3 * idx + 2];
-        const float4 q = reinterpret_cast<const float4*>(a.rotations)[idx];
+        S.m[0][0] = a.scale_modifier * sc[0];
+        S.m[1][1] = a.scale_modifier * sc[1];
+        S.m[2][2] = a.scale_modifier * sc[2];
         const Mat3 R = quat_to_R(q.x, q.y, q.z, q.w);
         const Mat3 Mm = mat3_mul(S, R);
         const Mat3 Sigma = mat3_mul(mat3_transpose(Mm), Mm);
@@ -174,7 +189,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
         const float len = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
         dx = dx / len; dy = dy / len; dz = dz / len;
         uint8_t cbits;
-        const float3 rgb = eval_sh_color<kSH16>(a.D, a.shs + (size_t)idx * a.M * 3, dx, dy, dz, cbits);
+        const float3 rgb = eval_sh_color(a.D, shc, dx, dy, dz, cbits);
         g.rgb[3 * idx + 0] = rgb.x;
         g.rgb[3 * idx + 1] = rgb.y;
         g.rgb[3 * idx + 2] = rgb.z;
@@ -183,7 +198,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
     g.depths[idx] = p_view.z;
     radii[idx] = iradius;
     reinterpret_cast<float2*>(g.means2D)[idx] = make_float2(pix_x, pix_y);
-    reinterpret_cast<float4*>(g.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, a.opacities[idx]);
+    reinterpret_cast<float4*>(g.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     g.tiles_touched[idx] = area;
 
     // Fused tile histogram (no-return atomics).

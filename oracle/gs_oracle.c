@@ -212,6 +212,38 @@ static void computeColorFromSH(int idx, int deg, int max_coeffs, const float* me
     }
 }
 
+/* Test hook: the SH polynomial of computeColorFromSH (forward.cu:30-62) for a
+ * given unit direction, before the +0.5 and the clamp.  sh is [max_coeffs][3]. */
+void orc_eval_sh(int deg, const float* dir, const float* sh, float* out) {
+    float x = dir[0], y = dir[1], z = dir[2];
+    float res[3];
+    for (int c = 0; c < 3; c++) res[c] = SH_C0 * sh[0 * 3 + c];
+    if (deg > 0) {
+        float k1 = SH_C1 * y, k2 = SH_C1 * z, k3 = SH_C1 * x;
+        for (int c = 0; c < 3; c++) res[c] = res[c] - k1 * sh[1 * 3 + c] + k2 * sh[2 * 3 + c] - k3 * sh[3 * 3 + c];
+        if (deg > 1) {
+            float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            float k4 = SH_C2[0] * xy, k5 = SH_C2[1] * yz, k6 = SH_C2[2] * (2.0f * zz - xx - yy);
+            float k7 = SH_C2[3] * xz, k8 = SH_C2[4] * (xx - yy);
+            for (int c = 0; c < 3; c++)
+                res[c] = res[c] + k4 * sh[4 * 3 + c] + k5 * sh[5 * 3 + c] + k6 * sh[6 * 3 + c] +
+                         k7 * sh[7 * 3 + c] + k8 * sh[8 * 3 + c];
+            if (deg > 2) {
+                float k9 = SH_C3[0] * y * (3.0f * xx - yy), k10 = SH_C3[1] * xy * z;
+                float k11 = SH_C3[2] * y * (4.0f * zz - xx - yy);
+                float k12 = SH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy);
+                float k13 = SH_C3[4] * x * (4.0f * zz - xx - yy), k14 = SH_C3[5] * z * (xx - yy);
+                float k15 = SH_C3[6] * x * (xx - 3.0f * yy);
+                for (int c = 0; c < 3; c++)
+                    res[c] = res[c] + k9 * sh[9 * 3 + c] + k10 * sh[10 * 3 + c] + k11 * sh[11 * 3 + c] +
+                             k12 * sh[12 * 3 + c] + k13 * sh[13 * 3 + c] + k14 * sh[14 * 3 + c] +
+                             k15 * sh[15 * 3 + c];
+            }
+        }
+    }
+    out[0] = res[0]; out[1] = res[1]; out[2] = res[2];
+}
+
 /* base/cr/forward.cu:74-113 */
 static void computeCov2D(const float* mean, float focal_x, float focal_y, float tan_fovx,
                          float tan_fovy, const float* cov3D, const float* viewmatrix, float* out) {

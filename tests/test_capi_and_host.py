@@ -1,0 +1,140 @@
+"""CPU-side checks of the product path that need no GPU compute:
+
+* the C-ABI library loads and exports every symbol include/gsplat_amd.h
+  declares, and its pure-host size/layout helpers are consistent;
+* the torch extension loads and exposes the reference's _C surface;
+* the drop-in packages expose the reference API with the reference's error
+  behaviour, and the product path fails loudly instead of falling back to the
+  CPU (there is no CPU path).
+"""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "gsplat_amd.h")
+LIB = os.path.join(ROOT, "gaussian_splatting_with_eye_tracking_amd", "libgsplat_amd.so")
+
+
+def _declared_functions():
+    src = open(HDR).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\*?\s*(gs_[a-z0-9_]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_the_boundary():
+    names = _declared_functions()
+    for must in ("gs_rasterizer_forward", "gs_rasterizer_backward", "gs_rasterizer_mark_visible",
+                 "gs_amr_rasterizer_forward", "gs_simple_knn", "gs_last_error"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(LIB)
+    missing = [n for n in _declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_host_layout_helpers():
+    lib = ctypes.CDLL(LIB)
+    lib.gs_geom_bytes.restype = ctypes.c_size_t
+    lib.gs_image_bytes.restype = ctypes.c_size_t
+    lib.gs_binning_bytes.restype = ctypes.c_size_t
+    lib.gs_knn_workspace_bytes.restype = ctypes.c_size_t
+    assert lib.gs_abi_version() == 1
+    g1, g2 = lib.gs_geom_bytes(1000), lib.gs_geom_bytes(2000)
+    assert g2 > g1 > 1000 * (4 + 4 + 8 + 16 + 12 + 24 + 1 + 4 + 64)
+    assert lib.gs_image_bytes(1920, 1080, 16) >= 1920 * 1080 * 8 + 120 * 68 * 8
+    assert lib.gs_binning_bytes(4096) >= 4096 * 20
+    assert lib.gs_knn_workspace_bytes(10000) > 10000 * 16
+    # views carve 256-B aligned arrays out of a base pointer (no device access)
+    class GeomView(ctypes.Structure):
+        _fields_ = [(n, ctypes.c_void_p) for n in ("hdr", "depths", "radii", "means2D", "conic_opacity", "rgb",
+                                                   "cov3D", "clamped", "tiles_touched", "grad_accum")]
+    v = GeomView()
+    base = 1 << 20
+    assert lib.gs_geom_view_of(ctypes.c_void_p(base), 1000, ctypes.byref(v)) == 0
+    ptrs = [getattr(v, f[0]) for f in GeomView._fields_]
+    assert ptrs[0] == base and all(p % 256 == 0 for p in ptrs) and ptrs == sorted(ptrs)
+    assert v.grad_accum + 1000 * 64 - base <= g1
+
+
+def test_torch_extension_surface():
+    from gaussian_splatting_with_eye_tracking_amd import _C, native_library_paths
+    for n in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "amr_rasterize_gaussians",
+              "distCUDA2", "parse_buffers", "profile_enable", "profile_read", "set_tuning"):
+        assert hasattr(_C, n), n
+    assert _C.abi_version() == 1
+    assert all(os.path.exists(p) and p.startswith(ROOT) for p in native_library_paths())
+
+
+def test_dropin_packages_export_reference_names():
+    import diff_gaussian_rasterization as base
+    import diff_gaussian_rasterization_amr as amr
+    from simple_knn._C import distCUDA2  # noqa: F401
+    for m in (base, amr):
+        for n in ("GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_RasterizeGaussians",
+                  "_C"):
+            assert hasattr(m, n), (m.__name__, n)
+    assert base.GaussianRasterizationSettings._fields == (
+        "image_height", "image_width", "tanfovx", "tanfovy", "bg", "scale_modifier", "viewmatrix", "projmatrix",
+        "sh_degree", "campos", "prefiltered", "debug")
+    assert amr.GaussianRasterizationSettings._fields == base.GaussianRasterizationSettings._fields
+
+
+def _settings():
+    from diff_gaussian_rasterization import GaussianRasterizationSettings
+    e = torch.eye(4)
+    return GaussianRasterizationSettings(8, 8, 0.5, 0.5, torch.zeros(3), 1.0, e, e, 3, torch.zeros(3), False, False)
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(), "excatly one of either SHs or precomputed colors"),
+    (dict(shs=torch.zeros(1, 16, 3), colors_precomp=torch.zeros(1, 3)), "excatly one"),
+    (dict(shs=torch.zeros(1, 16, 3)), "scale/rotation pair or precomputed 3D covariance"),
+    (dict(shs=torch.zeros(1, 16, 3), scales=torch.ones(1, 3), rotations=torch.ones(1, 4), cov3D_precomp=torch.ones(1, 6)),
+     "exactly one of either scale/rotation"),
+])
+def test_exactly_one_checks_raise_like_reference(kw, msg):
+    """base/.../__init__.py:191-195 raise a bare Exception (before any native call)."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    m = torch.zeros(1, 3)
+    with pytest.raises(Exception, match=msg):
+        GaussianRasterizer(_settings())(means3D=m, means2D=m, opacities=torch.ones(1, 1), **kw)
+
+
+def test_bad_means3D_shape_raises_runtime_error():
+    """rasterize_points.cu:57-59: AT_ERROR -> RuntimeError."""
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    s = _settings()
+    e = torch.Tensor([])
+    with pytest.raises(RuntimeError, match="means3D must have dimensions"):
+        _C.rasterize_gaussians(s.bg, torch.zeros(4, 2), e, torch.ones(4, 1), e, e, 1.0, e, s.viewmatrix,
+                               s.projmatrix, 0.5, 0.5, 8, 8, torch.zeros(4, 16, 3), 3, s.campos, False, False)
+
+
+def test_no_cpu_fallback():
+    """Host tensors are refused loudly: the product path has no CPU route."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    m = torch.zeros(5, 3)
+    with pytest.raises(RuntimeError, match="HIP device tensor"):
+        GaussianRasterizer(_settings())(means3D=m, means2D=m, opacities=torch.ones(5, 1), shs=torch.zeros(5, 16, 3),
+                                        scales=torch.ones(5, 3), rotations=torch.ones(5, 4))
+    from simple_knn._C import distCUDA2
+    with pytest.raises(RuntimeError, match="HIP device tensor"):
+        distCUDA2(torch.zeros(5, 3))
+
+
+def test_amr_wrapper_defaults_match_reference():
+    import inspect
+
+    from diff_gaussian_rasterization_amr import GaussianRasterizer
+    sig = inspect.signature(GaussianRasterizer.forward)
+    assert sig.parameters["foveaStep"].default == 0
+    assert sig.parameters["interpolate_image"].default is True
+    for n in ("out_color_precomp", "geomBuffer_precomp", "binningBuffer_precomp", "imageBuffer_precomp"):
+        assert sig.parameters[n].default is None

@@ -1,0 +1,104 @@
+"""World-size-2 gloo test of the multi-view data-parallel exchange (CPU).
+
+Each rank renders + back-propagates its own view (the CPU oracle stands in
+for the GPU backward here), writes its gradients into the flat buffer, and
+the all-reduce must deliver sum-over-views on every rank, bit-identically
+("the 8-GPU summed grad equals the sum of the single-GPU
+per-view grads").  The densification statistics are summed / max-reduced.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _view_grads(rank):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    W, H = 64, 48
+    cam0 = S.make_camera(W, H)
+    sc = S.make_scene(800, cam0, seed=0)
+    cam = S.make_orbit_camera(W, H, yaw_deg=(rank - 0.5) * 5.0)
+    s = O.settings_from_camera(cam)
+    kw = dict(shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+    r = O.forward(s, sc.means3D, sc.opacities, **kw)
+    g = O.backward(s, r, sc.means3D, S.make_cotangent(H, W, 100 + rank), **kw)
+    return sc, g, r
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+        sc, g, r = _view_grads(rank)
+        params = {"means3D": torch.from_numpy(sc.means3D), "shs": torch.from_numpy(sc.shs),
+                  "opacities": torch.from_numpy(sc.opacities), "scales": torch.from_numpy(sc.scales),
+                  "rotations": torch.from_numpy(sc.rotations)}
+        fg = DP.FlatGrads(params)
+        assert fg.flat.numel() == sc.P * DP.flat_numel_per_gaussian()
+        fg.load({"means3D": torch.from_numpy(g["dL_dmeans3D"]), "shs": torch.from_numpy(g["dL_dsh"]),
+                 "opacities": torch.from_numpy(g["dL_dopacity"]), "scales": torch.from_numpy(g["dL_dscales"]),
+                 "rotations": torch.from_numpy(g["dL_drotations"])})
+        DP.allreduce_(fg.flat)
+        acc = torch.from_numpy(np.linalg.norm(g["dL_dmeans2D"][:, :2], axis=1)).float()
+        denom = torch.from_numpy((r.radii > 0).astype(np.float32))
+        radii = torch.from_numpy(r.radii.astype(np.float32))
+        DP.densification_stats_allreduce_(acc, denom, radii)
+        q.put((rank, fg.flat.numpy().copy(), acc.numpy(), denom.numpy(), radii.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gradient_allreduce():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = {}
+    for _ in range(world):
+        rank, flat, acc, denom, radii = q.get(timeout=240)
+        outs[rank] = (flat, acc, denom, radii)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # replicas bit-identical
+    for i in range(4):
+        np.testing.assert_array_equal(outs[0][i], outs[1][i])
+    # == sum over views computed locally
+    exp = []
+    accs, dens, rads = [], [], []
+    for rank in range(world):
+        sc, g, r = _view_grads(rank)
+        exp.append(np.concatenate([g["dL_dmeans3D"].ravel(), g["dL_dsh"].ravel(), g["dL_dopacity"].ravel(),
+                                   g["dL_dscales"].ravel(), g["dL_drotations"].ravel()]))
+        accs.append(np.linalg.norm(g["dL_dmeans2D"][:, :2], axis=1).astype(np.float32))
+        dens.append((r.radii > 0).astype(np.float32))
+        rads.append(r.radii.astype(np.float32))
+    np.testing.assert_allclose(outs[0][0], exp[0] + exp[1], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(outs[0][1], accs[0] + accs[1], rtol=1e-6)
+    np.testing.assert_array_equal(outs[0][2], dens[0] + dens[1])
+    np.testing.assert_array_equal(outs[0][3], np.maximum(rads[0], rads[1]))

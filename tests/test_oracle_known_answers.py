@@ -1,0 +1,162 @@
+"""Known-answer tests of the oracle's CUDA-only stages (CPU only).  The
+reference ships no tests for them, so these hand-computed cases
+pin the semantics: blending order, the alpha < 1/255 skip, the T < 1e-4
+stop, near-plane culling, empty-tile ranges, getHigherMsb, the AMR
+percentile levels and fovea schedule, and simple-knn distances."""
+import ctypes
+import math
+
+import numpy as np
+import pytest
+
+import oracle as O
+from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+
+
+def _scene_at(cam, pts_pix_z, opac, rgb, scale=0.002):
+    """Gaussians whose centres project to given (px, py) at depth z (identity camera)."""
+    W, H = cam.image_width, cam.image_height
+    means = []
+    for (px, py, z) in pts_pix_z:
+        ndc_x = (2.0 * px + 1.0) / W - 1.0
+        ndc_y = (2.0 * py + 1.0) / H - 1.0
+        means.append([ndc_x * z * cam.tanfovx, ndc_y * z * cam.tanfovy, z])
+    P = len(means)
+    means = np.array(means, np.float32)
+    scales = np.full((P, 3), scale, np.float32)
+    rots = np.tile(np.array([1, 0, 0, 0], np.float32), (P, 1))
+    op = np.array(opac, np.float32).reshape(P, 1)
+    cols = np.array(rgb, np.float32).reshape(P, 3)
+    return means, scales, rots, op, cols
+
+
+def _fwd(cam, means, scales, rots, op, cols, bg=(0, 0, 0)):
+    s = O.settings_from_camera(cam, bg=bg)
+    return O.forward(s, means, op, colors_precomp=cols, scales=scales, rotations=rots)
+
+
+def test_single_gaussian_at_pixel_centre():
+    cam = S.make_camera(32, 32)
+    r = _fwd(cam, *_scene_at(cam, [(16, 16, 5.0)], [0.5], [[0.2, 0.4, 0.8]]), bg=(0.1, 0.1, 0.1))
+    pid = 16 * 32 + 16
+    # alpha = min(0.99, 0.5 * exp(~0)) = 0.5; C = f * alpha * 1; out = C + 0.5 * bg
+    np.testing.assert_allclose(r.color[:, 16, 16], [0.2 * 0.5 + 0.05, 0.4 * 0.5 + 0.05, 0.8 * 0.5 + 0.05],
+                               atol=1e-5)
+    assert r.n_contrib[pid] == 1
+    assert abs(r.final_T[pid] - 0.5) < 1e-5
+
+
+def test_two_gaussians_blend_front_to_back():
+    cam = S.make_camera(32, 32)
+    m, s, q, o, c = _scene_at(cam, [(16, 16, 7.0), (16, 16, 5.0)], [0.5, 0.5], [[1, 0, 0], [0, 1, 0]])
+    r = _fwd(cam, m, s, q, o, c)
+    # the nearer (green, idx 1) first: C = g*0.5 + r*0.5*0.5
+    np.testing.assert_allclose(r.color[:, 16, 16], [0.25, 0.5, 0.0], atol=1e-5)
+    t = (16 // 16) * 2 + (16 // 16)
+    beg, end = r.ranges[t]
+    assert list(r.point_list[beg:end]) == [1, 0]  # depth order
+    assert r.n_contrib[16 * 32 + 16] == 2
+
+
+def test_alpha_below_threshold_is_skipped():
+    cam = S.make_camera(32, 32)
+    r = _fwd(cam, *_scene_at(cam, [(16, 16, 5.0)], [0.003], [[1, 1, 1]]))
+    pid = 16 * 32 + 16
+    assert r.final_T[pid] == 1.0 and r.n_contrib[pid] == 0 and np.all(r.color[:, 16, 16] == 0)
+
+
+def test_transmittance_stop():
+    """alpha = 0.99: the second Gaussian would take T below 1e-4, so it is not
+    blended and the pixel is done (base/cr/forward.cu:346-351)."""
+    cam = S.make_camera(32, 32)
+    r = _fwd(cam, *_scene_at(cam, [(16, 16, 5.0), (16, 16, 6.0), (16, 16, 7.0)], [1, 1, 1],
+                             [[1, 0, 0], [0, 1, 0], [0, 0, 1]]))
+    pid = 16 * 32 + 16
+    assert r.n_contrib[pid] == 1
+    np.testing.assert_allclose(r.final_T[pid], 1 - np.float32(0.99), rtol=1e-6)
+    np.testing.assert_allclose(r.color[:, 16, 16], [0.99, 0, 0], atol=1e-6)
+
+
+def test_near_plane_cull_and_empty_ranges():
+    cam = S.make_camera(64, 48)
+    m, s, q, o, c = _scene_at(cam, [(10, 10, 0.1), (40, 20, 5.0)], [0.9, 0.9], [[1, 1, 1], [1, 1, 1]])
+    r = _fwd(cam, m, s, q, o, c)
+    assert r.radii[0] == 0 and r.radii[1] > 0
+    T = r.ranges.shape[0]
+    cnt = r.ranges[:, 1] - r.ranges[:, 0]
+    assert cnt.sum() == r.num_rendered == r.tiles_touched[1]
+    empty = cnt == 0
+    assert np.all(r.ranges[empty] == 0) and empty.sum() < T
+
+
+@pytest.mark.parametrize("n,bits", [(1, 1), (2, 2), (3, 2), (2040, 11), (6700, 13), (8160, 13), (8192, 14)])
+def test_get_higher_msb(n, bits):
+    L = O.lib()
+    L.orc_get_higher_msb.restype = ctypes.c_uint32
+    assert L.orc_get_higher_msb(ctypes.c_uint32(n)) == bits == n.bit_length()
+
+
+def test_amr_percentile_levels():
+    T = 8
+    counts = np.arange(T, dtype=np.uint32)[::-1].copy()
+    ranges = np.zeros((T, 2), np.uint32)
+    ranges[:, 1] = counts
+    L = O.lib()
+    ni, srt, pv, lv = (np.zeros(T, np.uint32) for _ in range(4))
+    pv = np.zeros(3, np.uint32)
+    L.orc_amr_levels(ctypes.c_int(T), O._p(ranges), O._p(ni), O._p(srt), O._p(pv), O._p(lv))
+    # idx = int(p * T) in float32: 2, 4, 7 -> sorted values 2, 4, 7
+    assert list(pv) == [2, 4, 7]
+    exp = [1 if c <= 2 else 2 if c <= 4 else 3 if c <= 7 else 4 for c in counts]
+    assert list(lv) == exp
+    assert list(srt) == sorted(counts)
+
+
+def test_amr_fovea_schedule():
+    L = O.lib()
+    levels = np.array([1, 2, 3, 4], np.uint32)
+    last = np.zeros(4, np.uint32)
+    cur = np.zeros(4, np.uint32)
+    seen = []
+    for step in (1, 2, 3, 4):
+        L.orc_amr_fovea_levels(ctypes.c_int(step), ctypes.c_int(4), O._p(last), O._p(cur), O._p(levels))
+        seen.append((list(last), list(cur)))
+    assert seen == [([0, 0, 0, 0], [1, 1, 1, 1]), ([1, 1, 1, 1], [1, 2, 2, 2]), ([1, 2, 2, 2], [1, 2, 3, 3]),
+                    ([1, 2, 3, 3], [1, 2, 3, 4])]
+    L.orc_amr_fovea_levels(ctypes.c_int(-2), ctypes.c_int(4), O._p(last), O._p(cur), O._p(levels))
+    assert list(last) == [0, 0, 0, 0] and list(cur) == [1, 2, 3, 4]
+
+
+def test_amr_rounds_cover_each_pixel_once():
+    """Summed over steps 1..4 every pixel with round <= level is rendered once
+    and the rest stay 0 (gaussian_renderer_amr/__init__.py:24-608)."""
+    cam = S.make_camera(96, 64)
+    sc = S.make_scene(3000, cam, seed=2)
+    s = O.settings_from_camera(cam, bg=(1.0, 1.0, 1.0))
+    kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+    acc, radii, st, steps = O.amr_render_foveated(s, kw)
+    assert np.all(steps[0] == 0)
+    covered = sum((st_ != 0).astype(int) for st_ in steps[1:])  # bg = 1 makes every rendered pixel nonzero
+    assert covered.max() <= 1
+    tgx = (96 + 31) // 32
+    for py in range(64):
+        for px in range(96):
+            t = (py // 32) * tgx + px // 32
+            rnd = {(0, 0): 1, (1, 1): 2, (1, 0): 3, (0, 1): 4}[(px % 2, py % 2)]
+            assert covered[0, py, px] == (1 if rnd <= st.levels[t] else 0)
+
+
+def test_knn_unit_grid():
+    g = np.stack(np.meshgrid(np.arange(3), np.arange(3), np.arange(3), indexing="ij"), -1).reshape(-1, 3)
+    d = O.dist_cuda2(g.astype(np.float32) + 0.5)
+    np.testing.assert_array_equal(d, np.ones(27, np.float32))
+
+
+def test_knn_bbox_zero_init_quirk():
+    """minn/maxx reductions start from {0,0,0} (knn/simple_knn.cu:189): a cloud
+    far from the origin still gets Morton codes relative to the origin box."""
+    pts = (np.random.default_rng(0).uniform(10, 11, (50, 3))).astype(np.float32)
+    d, morton, idx, boxes = O.knn_intermediates(pts)
+    q = np.floor((pts - 0.0) / (pts.max(0) - 0.0) * 1023).astype(np.uint32)
+    assert q.min() > 900  # all codes are near the top of the [0, max] box
+    assert np.all(np.isfinite(d)) and np.all(d > 0)
