@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
     const float4* __restrict__ conic_opacity, const float* __restrict__ colors, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ bg,
-    float* __restrict__ grad_accum) {
+    float* __restrict__ grad_accum, int cull) {
 #pragma clang fp contract(fast)
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[kB];
@@ -51,9 +51,11 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     __shared__ float4 s_co[kB];
     __shared__ float4 s_rgb[kB];
     __shared__ float s_acc[kB * kAccRow];
+    __shared__ uint64_t s_bal[4 * kWaves];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    const int wave = tid >> 6;
     const int tile = blockIdx.y * gridDim.x + blockIdx.x;
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const int n = (int)(range.y - range.x);
@@ -92,18 +94,37 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     for (int top = m; top > 0; top -= kB) {  // entries [top-cnt, top), back to front
         const int cnt = min(kB, top);
         __syncthreads();
+        uint32_t gm = 0;
         if (tid < cnt) {
             const uint32_t id = point_list[range.x + top - 1 - tid];
+            const float2 xy = means2D[id];
+            const float4 co = conic_opacity[id];
             s_id[tid] = id;
-            s_xy[tid] = means2D[id];
-            s_co[tid] = conic_opacity[id];
+            s_xy[tid] = xy;
+            s_co[tid] = co;
             s_rgb[tid] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2], 0.f);
+            gm = cull ? splat_group_mask(xy, co, (float)(blockIdx.x * 16), (float)(blockIdx.y * 16), 1.0f) : 0xfu;
         }
+        publish_group_masks<kWaves>(gm, s_bal);
         for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
         __syncthreads();
         // first batch slot this wave needs: contributor = top-1-j < wave_last
         const int j0 = max(0, top - (int)wave_last);
-        for (int j = j0; j < cnt; j++) {
+#pragma unroll 1
+        for (int c = 0; c < kWaves; c++) {
+          if (64 * c + 64 <= j0) continue;
+          uint64_t mk[kPPL];
+          uint64_t todo = 0;
+          const uint64_t lo_cut = (j0 > 64 * c) ? ~0ull << (j0 - 64 * c) : ~0ull;
+#pragma unroll
+          for (int k = 0; k < kPPL; k++) {
+              mk[k] = uniform_u64(s_bal[c * 4 + wave * kPPL + k]) & lo_cut;
+              todo |= mk[k];
+          }
+          while (todo) {
+            const int bit = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int j = 64 * c + bit;
             const uint32_t contributor = (uint32_t)(top - 1 - j);
             const float2 xy = s_xy[j];
             const float4 co = s_co[j];
@@ -114,6 +135,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             bool any = false;
 #pragma unroll
             for (int k = 0; k < kPPL; k++) {
+                if (!((mk[k] >> bit) & 1ull)) continue;  // wave-uniform: culled for this row group
                 if (contributor >= last[k]) continue;  // also covers pixels outside the image
                 const float dy = xy.y - px.y[k];
                 const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
@@ -160,6 +182,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                     }
                 }
             }
+          }
         }
         __syncthreads();
         // Flush: 16 lanes per Gaussian row, 4 rows per wave instruction
@@ -174,6 +197,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     }
 }
 
+extern int g_cull;  // render.hip
 int g_bwd_variant = 1;  // 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave uncapped
 
 void set_backward_variant(int v) { g_bwd_variant = v; }
@@ -186,7 +210,7 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
     hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC>), dim3(gx, gy), dim3(64 * WAVES), 0, s, W, H,       \
                        img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
-                       dL_dpix, bg, g.grad_accum)
+                       dL_dpix, bg, g.grad_accum, g_cull)
     switch (g_bwd_variant) {
         case 1: GS_BWD_LAUNCH(2, 2, 4); break;
         case 2: GS_BWD_LAUNCH(1, 4, 4); break;

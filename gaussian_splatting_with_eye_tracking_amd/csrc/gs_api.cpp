@@ -400,6 +400,10 @@ int gs_set_tuning(const char* key, int value) {
         set_backward_variant(value);
         return 0;
     }
+    if (std::strcmp(key, "cull") == 0) {
+        set_cull(value);
+        return 0;
+    }
     g_err = std::string("unknown tuning key ") + key;
     return -1;
 }

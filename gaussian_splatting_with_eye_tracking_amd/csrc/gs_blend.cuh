@@ -18,7 +18,10 @@ constexpr int kPix = 4;      // pixels per lane of the single-wave (backward) ge
 constexpr int kBatch = 64;   // Gaussians staged per LDS batch in the single-wave geometry
 
 // A 16x16 block is covered by kWaves wave64s with kPPL pixels per lane
-// (kWaves * 64 * kPPL = 256): thread t owns (x, y) = (t & 15, (t >> 4) + 4*kWaves*k).
+// (kWaves * 64 * kPPL = 256).  The block is 4 row groups of 16x4 pixels;
+// wave w owns the contiguous groups r = w*kPPL + k (k < kPPL), lane l pixel
+// (x, y) = (l & 15, 4r + (l >> 4)) of group r, so a wave's pixels form one
+// 16 x 4*kPPL band (the cull below works per row group).
 template <int kPPL>
 struct PixelSetT {
     float x;  // shared by the lane's pixels
@@ -32,12 +35,13 @@ using PixelSet = PixelSetT<kPix>;
 template <int kPPL, int kWaves>
 __device__ __forceinline__ PixelSetT<kPPL> make_pixels_t(int W, int H, uint32_t ox, uint32_t oy, uint32_t st) {
     const uint32_t t = threadIdx.x;
+    const uint32_t w = t >> 6, l = t & 63;
     PixelSetT<kPPL> p;
-    const uint32_t px = ox + st * (t & 15);
+    const uint32_t px = ox + st * (l & 15);
     p.x = (float)px;
 #pragma unroll
     for (int k = 0; k < kPPL; k++) {
-        const uint32_t py = oy + st * ((t >> 4) + 4 * kWaves * k);
+        const uint32_t py = oy + st * (4 * (w * kPPL + k) + (l >> 4));
         p.y[k] = (float)py;
         p.inside[k] = px < (uint32_t)W && py < (uint32_t)H;
         p.pid[k] = p.inside[k] ? (uint32_t)W * py + px : 0u;
@@ -49,6 +53,68 @@ __device__ __forceinline__ PixelSet make_pixels(int W, int H, uint32_t ox, uint3
     return make_pixels_t<kPix, 1>(W, H, ox, oy, st);
 }
 
+
+// ------------------------------------------------------------ row-group cull
+// A (pixel, Gaussian) pair is blended only if alpha = min(0.99, o*exp(power))
+// >= 1/255 with power = -Q/2, Q = d^T C d (C = conic, d = mean - pixel), i.e.
+// only if Q <= 2 ln(255 o).  That set is an ellipse; its bounding box has
+// half-widths sqrt(thr * C_yy / det C) and sqrt(thr * C_xx / det C).  A
+// Gaussian whose box misses all pixels of a 16x4 row group is skipped by
+// every pixel of the group in the reference too (the alpha < 1/255
+// `continue`, base/cr/forward.cu:341-343, backward.cu:480-482), so skipping
+// it is exact, provided the box is conservative w.r.t. the kernel's own
+// float evaluation of Q, exp and the threshold:
+//   * thr = 2.04 ln(255 o) + 2e-3 (2 % + absolute slack), box widths x1.001
+//     + 0.02 px;
+//   * the rounding of the kernel's Q is <= ~4 eps (1+rho)/(1-rho) Q, with
+//     rho = |C_xy| / sqrt(C_xx C_yy); the cull is used only for rho^2 <
+//     0.998 (error < 5e-4 Q, well inside the 2 % slack), otherwise and for
+//     any non-finite value the Gaussian is kept ("hit");
+//   * o*255 < 0.999 means alpha <= o < 1/255 for every pixel (exp(power) <= 1
+//     once power <= 0, and power > 0 is skipped anyway): never blended.
+// Returns bit r set when the box meets row group r of the 16x16 block at
+// (ox, oy) with pixel stride st (1 = base, 2 = AMR sub-lattice).
+__device__ __forceinline__ uint32_t splat_group_mask(float2 xy, float4 co, float ox, float oy, float st) {
+    const float o = co.w;
+    if (o * 255.0f < 0.999f) return 0u;  // false for NaN: kept
+    const float lt = fmaxf(__logf(255.0f * o), 0.0f);
+    const float thr = 2.04f * lt + 2e-3f;
+    const float cxz = co.x * co.z;
+    const bool ok = co.x > 0.0f && co.z > 0.0f && co.y * co.y < 0.998f * cxz;
+    const float det = cxz - co.y * co.y;
+    const float hx = ok ? sqrtf(thr * co.z / det) * 1.001f + 0.02f : __builtin_inff();
+    const float hy = ok ? sqrtf(thr * co.x / det) * 1.001f + 0.02f : __builtin_inff();
+    // "misses" comparisons are false for NaN / inf widths -> kept
+    if (xy.x + hx < ox || xy.x - hx > ox + 15.0f * st) return 0u;
+    uint32_t m = 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const float y0 = oy + st * (4.0f * r), y1 = oy + st * (4.0f * r + 3.0f);
+        if (!(xy.y + hy < y0 || xy.y - hy > y1)) m |= 1u << r;
+    }
+    return m;
+}
+
+// Scalar copy of a wave-uniform 64-bit value held in VGPRs.
+__device__ __forceinline__ uint64_t uniform_u64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Per batch: s_bal[c * 4 + r] = 64-bit mask over batch slots 64c..64c+63 of
+// the Gaussians meeting row group r.  Called by every thread after it has
+// computed the mask of its own slot (0 for empty slots).
+template <int kWaves>
+__device__ __forceinline__ void publish_group_masks(uint32_t my_mask, uint64_t* s_bal) {
+    const uint32_t c = threadIdx.x >> 6;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const uint64_t b = __ballot((my_mask >> r) & 1u);
+        if ((threadIdx.x & 63) == 0) s_bal[c * 4 + r] = b;
+    }
+}
+
 template <int kPPL>
 struct BlendStateT {
     float T[kPPL];
@@ -58,23 +124,26 @@ struct BlendStateT {
 
 // Front-to-back blend of `range` for the thread's kPPL pixels.  Called by the
 // whole workgroup (kWaves waves); LDS batches hold 64*kWaves Gaussians.
+// (ox, oy, st): the block origin and pixel stride, for the row-group cull.
 template <int kPPL, int kWaves>
-__device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const PixelSetT<kPPL>& px,
-                                                          const uint32_t* __restrict__ point_list,
+__device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const PixelSetT<kPPL>& px, float ox, float oy,
+                                                          float st, const uint32_t* __restrict__ point_list,
                                                           const float2* __restrict__ means2D,
                                                           const float* __restrict__ features,
                                                           const float4* __restrict__ conic_opacity, float2* s_xy,
-                                                          float4* s_co, float4* s_rgb) {
+                                                          float4* s_co, float4* s_rgb, uint64_t* s_bal,
+                                                          bool cull) {
 #pragma clang fp contract(fast)
     constexpr uint32_t kB = 64 * kWaves;
     const uint32_t tid = threadIdx.x;
-    BlendStateT<kPPL> st;
+    const uint32_t wave = tid >> 6;
+    BlendStateT<kPPL> st_;
     bool done[kPPL];
 #pragma unroll
     for (int k = 0; k < kPPL; k++) {
-        st.T[k] = 1.0f;
-        st.C[k][0] = st.C[k][1] = st.C[k][2] = 0.f;
-        st.last[k] = 0;
+        st_.T[k] = 1.0f;
+        st_.C[k][0] = st_.C[k][1] = st_.C[k][2] = 0.f;
+        st_.last[k] = 0;
         done[k] = !px.inside[k];
     }
     const uint32_t n = range.y - range.x;
@@ -88,47 +157,69 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
         } else {
             if (!__syncthreads_or(any)) break;
         }
+        uint32_t gm = 0;
         if (b0 + tid < n) {
             const uint32_t id = point_list[range.x + b0 + tid];
-            s_xy[tid] = means2D[id];
-            s_co[tid] = conic_opacity[id];
+            const float2 xy = means2D[id];
+            const float4 co = conic_opacity[id];
+            s_xy[tid] = xy;
+            s_co[tid] = co;
             s_rgb[tid] = make_float4(features[3 * id], features[3 * id + 1], features[3 * id + 2], 0.f);
+            gm = cull ? splat_group_mask(xy, co, ox, oy, st) : 0xfu;
         }
+        publish_group_masks<kWaves>(gm, s_bal);
         __syncthreads();
-        const int cnt = (int)min(kB, n - b0);
         if (__ballot(any) == 0ull) continue;  // this wave is done; keep joining the barriers
-        for (int j = 0; j < cnt; j++) {
-            const float2 xy = s_xy[j];
-            const float4 co = s_co[j];
-            const float dx = xy.x - px.x;
-            const uint32_t contributor = b0 + (uint32_t)j + 1;
-            bool alive = false;
+        bool wave_alive = true;
+#pragma unroll 1
+        for (uint32_t c = 0; c < (uint32_t)kWaves && wave_alive; c++) {
+            uint64_t mk[kPPL];
+            uint64_t todo = 0;
 #pragma unroll
             for (int k = 0; k < kPPL; k++) {
-                if (done[k]) continue;
-                alive = true;
-                const float dy = xy.y - px.y[k];
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                if (power > 0.0f) continue;
-                const float alpha = fminf(0.99f, co.w * __expf(power));
-                if (alpha < 1.0f / 255.0f) continue;
-                const float test_T = st.T[k] * (1 - alpha);
-                if (test_T < 0.0001f) {
-                    done[k] = true;
-                    continue;
-                }
-                const float4 f = s_rgb[j];
-                const float w = alpha * st.T[k];
-                st.C[k][0] += f.x * w;
-                st.C[k][1] += f.y * w;
-                st.C[k][2] += f.z * w;
-                st.T[k] = test_T;
-                st.last[k] = contributor;
+                mk[k] = uniform_u64(s_bal[c * 4 + wave * kPPL + k]);
+                todo |= mk[k];
             }
-            if (__ballot(alive) == 0ull) break;
+            while (todo) {
+                const uint32_t bit = (uint32_t)__builtin_ctzll(todo);
+                todo &= todo - 1;
+                const uint32_t j = c * 64 + bit;
+                const float2 xy = s_xy[j];
+                const float4 co = s_co[j];
+                const float dx = xy.x - px.x;
+                const uint32_t contributor = b0 + j + 1;
+                bool alive = false;
+#pragma unroll
+                for (int k = 0; k < kPPL; k++) {
+                    if (done[k]) continue;
+                    alive = true;
+                    if (!((mk[k] >> bit) & 1ull)) continue;  // wave-uniform: culled for this row group
+                    const float dy = xy.y - px.y[k];
+                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                    if (power > 0.0f) continue;
+                    const float alpha = fminf(0.99f, co.w * __expf(power));
+                    if (alpha < 1.0f / 255.0f) continue;
+                    const float test_T = st_.T[k] * (1 - alpha);
+                    if (test_T < 0.0001f) {
+                        done[k] = true;
+                        continue;
+                    }
+                    const float4 f = s_rgb[j];
+                    const float w = alpha * st_.T[k];
+                    st_.C[k][0] += f.x * w;
+                    st_.C[k][1] += f.y * w;
+                    st_.C[k][2] += f.z * w;
+                    st_.T[k] = test_T;
+                    st_.last[k] = contributor;
+                }
+                if (__ballot(alive) == 0ull) {
+                    wave_alive = false;
+                    break;
+                }
+            }
         }
     }
-    return st;
+    return st_;
 }
 
 // ------------------------------------------------------------ DPP reduce

@@ -53,17 +53,19 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
                                                                  uint32_t* __restrict__ n_contrib,
                                                                  uint32_t* __restrict__ max_contrib,
                                                                  const float* __restrict__ bg,
-                                                                 float* __restrict__ out_color) {
+                                                                 float* __restrict__ out_color, int cull) {
     __shared__ float2 s_xy[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
     __shared__ float4 s_rgb[64 * kWaves];
+    __shared__ uint64_t s_bal[4 * kWaves];
     __shared__ uint32_t s_max;
     if (kWaves > 1 && threadIdx.x == 0) s_max = 0;
     const int tile = blockIdx.y * gridDim.x + blockIdx.x;
     const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, blockIdx.x * 16, blockIdx.y * 16, 1);
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
-    const BlendStateT<kPPL> st = blend_tile_t<kPPL, kWaves>(range, px, point_list, means2D, features,
-                                                            conic_opacity, s_xy, s_co, s_rgb);
+    const BlendStateT<kPPL> st =
+        blend_tile_t<kPPL, kWaves>(range, px, (float)(blockIdx.x * 16), (float)(blockIdx.y * 16), 1.0f, point_list,
+                                   means2D, features, conic_opacity, s_xy, s_co, s_rgb, s_bal, cull != 0);
     write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
     uint32_t m = 0;
 #pragma unroll
@@ -78,7 +80,10 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
     }
 }
 
-int g_fwd_variant = 1;  // 0: 1 wave x 4 px/lane, 1: 2 waves x 2 px/lane, 2: 4 waves x 1 px/lane
+int g_cull = 1;         // row-group cull on (gs_blend.cuh); 0 only for the exactness A/B test
+void set_cull(int v) { g_cull = v; }
+
+int g_fwd_variant = 2;  // 0: 1 wave x 4 px/lane, 1: 2 waves x 2 px/lane, 2: 4 waves x 1 px/lane
 
 void set_forward_variant(int v) { g_fwd_variant = v; }
 
@@ -90,11 +95,11 @@ void launch_render_forward(int W, int H, const ImageView& img, const BinningView
     hipLaunchKernelGGL((render_fwd_kernel<PPL, WAVES>), dim3(gx, gy), dim3(64 * WAVES), 0, s, W, H, img.ranges, \
                        b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
-                       img.max_contrib, bg, out_color)
+                       img.max_contrib, bg, out_color, g_cull)
     switch (g_fwd_variant) {
         case 0: GS_FWD_LAUNCH(4, 1); break;
-        case 2: GS_FWD_LAUNCH(1, 4); break;
-        default: GS_FWD_LAUNCH(2, 2); break;
+        case 1: GS_FWD_LAUNCH(2, 2); break;
+        default: GS_FWD_LAUNCH(1, 4); break;
     }
 #undef GS_FWD_LAUNCH
 }
@@ -116,10 +121,11 @@ __global__ void __launch_bounds__(64) amr_render_kernel(int W, int H, int tgx, c
                                                         const float4* __restrict__ conic_opacity,
                                                         float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
                                                         const float* __restrict__ bg, float* __restrict__ out_color,
-                                                        int foveaStep) {
+                                                        int foveaStep, int cull) {
     __shared__ float2 s_xy[kBatch];
     __shared__ float4 s_co[kBatch];
     __shared__ float4 s_rgb[kBatch];
+    __shared__ uint64_t s_bal[4];
     const int tile = (blockIdx.y >> 1) * tgx + (blockIdx.x >> 1);
     const uint32_t L_last = levels_last[tile];
     uint32_t L = levels[tile];
@@ -130,10 +136,11 @@ __global__ void __launch_bounds__(64) amr_render_kernel(int W, int H, int tgx, c
     if (L > 4) L = 4;
     if (foveaStep > 0 && round <= L_last) return;
     if (round > L) return;
-    const PixelSet px = make_pixels(W, H, (blockIdx.x >> 1) * 32 + ox, (blockIdx.y >> 1) * 32 + oy, 2);
+    const uint32_t bx = (blockIdx.x >> 1) * 32 + ox, by = (blockIdx.y >> 1) * 32 + oy;
+    const PixelSet px = make_pixels(W, H, bx, by, 2);
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
-    const BlendStateT<kPix> st = blend_tile_t<kPix, 1>(range, px, point_list, means2D, features, conic_opacity,
-                                                       s_xy, s_co, s_rgb);
+    const BlendStateT<kPix> st = blend_tile_t<kPix, 1>(range, px, (float)bx, (float)by, 2.0f, point_list, means2D,
+                                                       features, conic_opacity, s_xy, s_co, s_rgb, s_bal, cull != 0);
     write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
 }
 
@@ -145,7 +152,7 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
     hipLaunchKernelGGL(amr_render_kernel, dim3(2 * tgx, 2 * tgy), dim3(64), 0, s, W, H, tgx, img.ranges, levels,
                        levels_last, b.point_list, reinterpret_cast<const float2*>(g.means2D), features,
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib, bg,
-                       out_color, foveaStep);
+                       out_color, foveaStep, g_cull);
 }
 
 // amr/cr/forward.cu:520-648, per pixel.  pass 0 = the precomp copy of the

@@ -152,8 +152,11 @@ int gs_reconstruct_keys(char* geom_buffer, char* binning_buffer, char* img_buffe
  * bench.py for the live per-kernel roofline (cross-checked with rocprofv3). */
 void gs_profile_enable(int on);
 /* Kernel-geometry knobs for A/B measurements ("fwd_variant": 0 = one wave
- * per tile x 4 px/lane, 1 = 2 waves x 2 px/lane (default), 2 = 4 waves x
- * 1 px/lane).  Returns 0, or -1 for an unknown key. */
+ * per tile x 4 px/lane, 1 = 2 waves x 2 px/lane, 2 = 4 waves x
+ * 1 px/lane, the default), "bwd_variant" (same geometries; default 1), "cull" (1 =
+ * skip Gaussians whose alpha >= 1/255 box misses a 16x4 row group, the
+ * default; 0 only to verify that the cull is exact).  Returns 0, or -1 for
+ * an unknown key. */
 int gs_set_tuning(const char* key, int value);
 int gs_profile_stage_count(void);
 const char* gs_profile_stage_name(int i);
