@@ -45,22 +45,25 @@ CONFIGS = {
 
 
 def algorithmic_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: int) -> float:
-    """Compulsory HBM bytes of one launch of `stage`."""
-    if stage == "preprocess":
-        return 20.0 * P + 289.0 * V + 4.0 * K
-    if stage == "render":
-        return 40.0 * K + 20.0 * N + 12.0 * T
-    if stage == "render_bwd":
-        return 76.0 * Kb + 20.0 * N + 12.0 * T
-    if stage == "bwd_gauss":
-        return 24.0 * P + 64.0 * V + 236.0 * P + 300.0 * P + 44.0 * V
-    if stage == "duplicate":
-        return 16.0 * V + 12.0 * K
-    if stage == "sort_tiles":
+    """Compulsory HBM bytes of one launch of `stage`: the bytes
+    the reference algorithm must read or write once, whatever the kernel.
+    P Gaussians, V visible, K instances, Kb instances up to each tile's last
+    contributor (what any blend must read), N pixels, T tiles."""
+    if stage == "preprocess":   # means 12 + radii 4 + tiles_touched 4 per P; per V: scales 12, rot 16,
+        return 20.0 * P + 289.0 * V  # opacity 4, SH 192 in; depth 4, xy 8, conic 16, rgb 12, cov 24, clamped 1 out
+    if stage == "render":       # per entry: id 4 + xy 8 + conic/opacity 16 + rgb 12; per pixel: colour 12,
+        return 40.0 * Kb + 20.0 * N + 12.0 * T  # final T 4, n_contrib 4; per tile: range 8 + max_contrib 4
+    if stage == "render_bwd":   # per entry: the same 40 B + 9 accumulated floats 36; per pixel: dL/dpix 12,
+        return 76.0 * Kb + 20.0 * N + 12.0 * T  # final T 4, n_contrib 4; per tile 12
+    if stage == "bwd_gauss":    # radii 4 + all 75 gradient floats 300 per P; per V: accum 36, means 12,
+        return 304.0 * P + 293.0 * V  # cov3D 24, scales 12, rot 16, SH 192, clamped 1
+    if stage == "duplicate":    # per V: xy 8, radius 4, depth 4; per instance: one 8-B key
+        return 16.0 * V + 8.0 * K
+    if stage == "sort_tiles":   # per instance: key in 8, point_list out 4; per tile: range 8
         return 12.0 * K + 8.0 * T
-    if stage == "zero_accum":
+    if stage == "zero_accum":   # the 64-B accumulator rows (this design's own buffer)
         return 64.0 * P
-    if stage == "tile_scan":
+    if stage == "tile_scan":    # count in, range + cursor + max_contrib out
         return 28.0 * T
     return 0.0
 
