@@ -59,6 +59,8 @@ def algorithmic_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: in
         return 304.0 * P + 293.0 * V  # cov3D 24, scales 12, rot 16, SH 192, clamped 1
     if stage == "duplicate":    # per V: xy 8, radius 4, depth 4; per instance: one 8-B key
         return 16.0 * V + 8.0 * K
+    if stage == "count_tiles":  # radius per P, xy per V in; T counts out
+        return 4.0 * P + 8.0 * V + 4.0 * T
     if stage == "sort_tiles":   # per instance: key in 8, point_list out 4; per tile: range 8
         return 12.0 * K + 8.0 * T
     if stage == "zero_accum":   # the 64-B accumulator rows (this design's own buffer)

@@ -126,10 +126,109 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const float* __re
     }
 }
 
+// ------------------------------------------- LDS-privatised binning ---
+// Device-scope atomics execute at the memory side, one 64-B request each
+// when scattered (MI355X_MICROARCH.md "Global float atomics"): 4.4M per-pair
+// histogram increments plus 4.4M returning cursor bumps at config 2 cost
+// ~0.2 ms apiece.  Instead a workgroup of kBinThreads threads takes a chunk
+// of g_bin_chunk consecutive Gaussians and counts its (Gaussian, tile) pairs
+// in an LDS histogram over all T tiles, then
+//   count_tiles: adds the histogram to tile_count with consecutive-tile
+//                (coalesced, no-return) atomics, one per non-empty tile;
+//   duplicate:   reserves each non-empty tile's run with ONE coalesced
+//                returning atomic on the tile cursor, then hands out slots
+//                inside the run with LDS atomics and writes the keys.
+// Slot order inside a bucket stays arbitrary; sort_tiles makes it exact.
+constexpr int kBinThreads = 1024;
+int g_bin_chunk = 4096;
+void set_bin_chunk(int v) { g_bin_chunk = max(kBinThreads, v); }
+
+__device__ __forceinline__ bool gaussian_rect(int idx, const float* __restrict__ means2D,
+                                              const int* __restrict__ radii, int block, uint32_t gx, uint32_t gy,
+                                              Rect& r) {
+    const int rad = radii[idx];
+    if (rad <= 0) return false;
+    const float2 xy = reinterpret_cast<const float2*>(means2D)[idx];
+    r = get_rect(xy.x, xy.y, rad, block, block, gx, gy);
+    return true;
+}
+
+__global__ void __launch_bounds__(kBinThreads) count_tiles_kernel(int P, int chunk, const float* __restrict__ means2D,
+                                                                  const int* __restrict__ radii, int block,
+                                                                  uint32_t gx, uint32_t gy,
+                                                                  uint32_t* __restrict__ tile_count) {
+    extern __shared__ uint32_t hist[];
+    const int T = (int)(gx * gy);
+    for (int i = threadIdx.x; i < T; i += kBinThreads) hist[i] = 0;
+    __syncthreads();
+    const int beg = blockIdx.x * chunk, end = min(P, beg + chunk);
+    for (int idx = beg + threadIdx.x; idx < end; idx += kBinThreads) {
+        Rect r;
+        if (!gaussian_rect(idx, means2D, radii, block, gx, gy, r)) continue;
+        for (uint32_t y = r.y0; y < r.y1; y++)
+            for (uint32_t x = r.x0; x < r.x1; x++) atomicAdd(&hist[y * gx + x], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < T; i += kBinThreads) {
+        const uint32_t c = hist[i];
+        if (c) atomicAdd(&tile_count[i], c);
+    }
+}
+
+__global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int chunk,
+                                                                    const float* __restrict__ means2D,
+                                                                    const float* __restrict__ depths,
+                                                                    const int* __restrict__ radii, int block,
+                                                                    uint32_t gx, uint32_t gy,
+                                                                    uint32_t* __restrict__ cursor,
+                                                                    uint64_t* __restrict__ pair_keys) {
+    extern __shared__ uint32_t slot[];
+    const int T = (int)(gx * gy);
+    for (int i = threadIdx.x; i < T; i += kBinThreads) slot[i] = 0;
+    __syncthreads();
+    const int beg = blockIdx.x * chunk, end = min(P, beg + chunk);
+    for (int idx = beg + threadIdx.x; idx < end; idx += kBinThreads) {
+        Rect r;
+        if (!gaussian_rect(idx, means2D, radii, block, gx, gy, r)) continue;
+        for (uint32_t y = r.y0; y < r.y1; y++)
+            for (uint32_t x = r.x0; x < r.x1; x++) atomicAdd(&slot[y * gx + x], 1u);
+    }
+    __syncthreads();
+    // one returning atomic per non-empty tile: the chunk's run in the bucket
+    for (int i = threadIdx.x; i < T; i += kBinThreads) {
+        const uint32_t c = slot[i];
+        if (c) slot[i] = atomicAdd(&cursor[i], c);
+    }
+    __syncthreads();
+    for (int idx = beg + threadIdx.x; idx < end; idx += kBinThreads) {
+        Rect r;
+        if (!gaussian_rect(idx, means2D, radii, block, gx, gy, r)) continue;
+        const uint64_t key = ((uint64_t)float_bits(depths[idx]) << 32) | (uint32_t)idx;
+        for (uint32_t y = r.y0; y < r.y1; y++)
+            for (uint32_t x = r.x0; x < r.x1; x++) pair_keys[atomicAdd(&slot[y * gx + x], 1u)] = key;
+    }
+}
+
+void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
+                        hipStream_t s) {
+    const uint32_t gx = (uint32_t)((W + block - 1) / block), gy = (uint32_t)((H + block - 1) / block);
+    if (P == 0 || gx * gy == 0) return;
+    const int chunk = g_bin_chunk;
+    hipLaunchKernelGGL(count_tiles_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
+                       sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, radii, block, gx, gy, img.tile_count);
+}
+
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
                       const BinningView& b, hipStream_t s) {
     if (P == 0) return;
     const uint32_t gx = (uint32_t)((W + block - 1) / block), gy = (uint32_t)((H + block - 1) / block);
+    if (gx * gy <= (uint32_t)kLdsTiles) {
+        const int chunk = g_bin_chunk;
+        hipLaunchKernelGGL(duplicate_lds_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
+                           sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, g.depths, radii, block, gx, gy,
+                           img.tile_cursor, b.pair_keys);
+        return;
+    }
     hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, g.means2D, g.depths, radii,
                        block, gx, gy, img.tile_cursor, b.pair_keys);
 }

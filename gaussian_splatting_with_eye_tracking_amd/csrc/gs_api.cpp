@@ -46,11 +46,14 @@ struct GsError : std::runtime_error {
 
 // ---- optional per-stage timing (gs_profile_*): hipEvents recorded on the
 // launch stream around each stage; elapsed times are harvested lazily.
-constexpr int kStages = 12;
+constexpr int kStages = 13;
 const char* kStageNames[kStages] = {"preprocess", "tile_scan",    "duplicate",   "sort_tiles",
                                     "render",     "render_bwd",   "bwd_gauss",   "amr_levels",
-                                    "amr_render", "amr_interp",   "knn",         "zero_accum"};
-enum Stage { kPre, kScan, kDup, kSort, kRender, kRenderBwd, kBwdGauss, kAmrLevels, kAmrRender, kAmrInterp, kKnn, kZero };
+                                    "amr_render", "amr_interp",   "knn",         "zero_accum",
+                                    "count_tiles"};
+enum Stage {
+    kPre, kScan, kDup, kSort, kRender, kRenderBwd, kBwdGauss, kAmrLevels, kAmrRender, kAmrInterp, kKnn, kZero, kCount
+};
 struct Profiler {
     bool on = false;
     struct Pending { int stage; hipEvent_t a, b; };
@@ -200,8 +203,11 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     r.radii = radii ? radii : r.g.radii;
     GS_HIP(hipMemsetAsync(r.g.hdr, 0, kHdrWords * sizeof(uint32_t), s));
     if (r.T > 0) GS_HIP(hipMemsetAsync(r.img.tile_count, 0, sizeof(uint32_t) * r.T, s));
-    { StageTimer _t(kPre, s); launch_preprocess(make_pp(in, tile), r.g, r.radii, r.img.tile_count, s); }
+    const bool lds_bin = r.T <= kLdsTiles;
+    { StageTimer _t(kPre, s); launch_preprocess(make_pp(in, tile), r.g, r.radii, lds_bin ? nullptr : r.img.tile_count, s); }
     stage_check(debug, s, "preprocess");
+    if (lds_bin) { StageTimer _t(kCount, s); launch_count_tiles(in.P, r.g, r.radii, W, H, tile, r.img, s); }
+    stage_check(debug, s, "count_tiles");
     if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s); }
     stage_check(debug, s, "tile_scan");
     uint32_t hdr[4];
@@ -398,6 +404,10 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "bwd_variant") == 0) {
         set_backward_variant(value);
+        return 0;
+    }
+    if (std::strcmp(key, "bin_chunk") == 0) {
+        set_bin_chunk(value);
         return 0;
     }
     if (std::strcmp(key, "cull") == 0) {

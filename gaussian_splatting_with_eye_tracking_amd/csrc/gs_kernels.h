@@ -41,6 +41,12 @@ void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, c
 void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s);
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
                       const BinningView& b, hipStream_t s);
+// Tile grids up to kLdsTiles are binned with workgroup-private LDS histograms
+// (count_tiles + chunked duplicate); larger grids use device atomics.
+constexpr int kLdsTiles = 16384;
+void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
+                        hipStream_t s);
+void set_bin_chunk(int gaussians_per_workgroup);
 void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, const uint32_t* hdr, int num_large_host,
                        hipStream_t s);
 // (tile << 32 | depth) reconstruction of the reference's point_list_keys.

@@ -201,9 +201,11 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
     reinterpret_cast<float4*>(g.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     g.tiles_touched[idx] = area;
 
-    // Fused tile histogram (no-return atomics).
-    for (uint32_t y = r.y0; y < r.y1; y++)
-        for (uint32_t x = r.x0; x < r.x1; x++) atomicAdd(&tile_count[y * gx + x], 1u);
+    // Tile histogram with device atomics only when the tile grid is too large
+    // for the LDS-privatised count_tiles kernel (binning.hip); wave-uniform.
+    if (tile_count)
+        for (uint32_t y = r.y0; y < r.y1; y++)
+            for (uint32_t x = r.x0; x < r.x1; x++) atomicAdd(&tile_count[y * gx + x], 1u);
 }
 
 template <bool A, bool B, bool C>

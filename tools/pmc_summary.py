@@ -26,6 +26,8 @@ STAGES = {
     "render_bwd_kernel": "render_bwd",
     "render_fwd_kernel": "render",
     "duplicate_kernel": "duplicate",
+    "duplicate_lds_kernel": "duplicate",
+    "count_tiles_kernel": "count_tiles",
     "backward_gaussians_kernel": "bwd_gauss",
     "preprocess_kernel": "preprocess",
     "sort_tiles_small_kernel": "sort_tiles",
