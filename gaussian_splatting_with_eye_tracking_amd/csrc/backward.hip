@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
     const float4* __restrict__ conic_opacity, const float* __restrict__ colors, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ bg,
-    float* __restrict__ grad_accum, int cull) {
+    float* __restrict__ grad_accum, int cull, const uint32_t* __restrict__ order, int gx) {
 #pragma clang fp contract(fast)
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[kB];
@@ -56,13 +56,14 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+    const int tile = order ? (int)order[blockIdx.x] : (int)blockIdx.x;
+    const uint32_t ox = (uint32_t)(tile % gx) * 16, oy = (uint32_t)(tile / gx) * 16;
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const int n = (int)(range.y - range.x);
     const int m = min(n, (int)max_contrib[tile]);
     if (m == 0) return;  // block-uniform
 
-    const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, blockIdx.x * 16, blockIdx.y * 16, 1);
+    const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, 1);
     const size_t plane = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
     float T[kPPL], nbg[kPPL], dpx[kPPL][3], acc_rec[kPPL][3], last_col[kPPL][3], last_alpha[kPPL];
@@ -103,7 +104,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             s_xy[tid] = xy;
             s_co[tid] = co;
             s_rgb[tid] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2], 0.f);
-            gm = cull ? splat_group_mask(xy, co, (float)(blockIdx.x * 16), (float)(blockIdx.y * 16), 1.0f) : 0xfu;
+            gm = cull ? splat_group_mask(xy, co, (float)ox, (float)oy, 1.0f) : 0xfu;
         }
         publish_group_masks<kWaves>(gm, s_bal);
         for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
@@ -170,13 +171,16 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 g[7] += -0.5f * gdy * dy * dL_dG;
                 g[8] += G * dL_dalpha;
             }
-            if (__ballot(any) != 0ull) {  // wave-uniform: reduce the 9 sums into lane 63
-                dpp_sum9_lane63(g);
-                if (lane == 63) {
-                    if (kWaves == 1) {
+            if (__ballot(any) != 0ull) {  // wave-uniform
+                if (kWaves == 1) {  // reduce the 9 sums into lane 63, park them
+                    dpp_sum9_lane63(g);
+                    if (lane == 63) {
 #pragma unroll
                         for (int q = 0; q < kNG; q++) s_acc[j * kAccRow + q] = g[q];
-                    } else {
+                    }
+                } else {  // 16-lane row sums; the 4 row leaders add them into LDS
+                    dpp_sum9_rows(g);
+                    if ((lane & 15) == 15) {
 #pragma unroll
                         for (int q = 0; q < kNG; q++) atomicAdd(&s_acc[j * kAccRow + q], g[q]);
                     }
@@ -206,11 +210,16 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s) {
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return;
+    const uint32_t* order = nullptr;
+    if (tile_order_enabled()) {
+        launch_order_tiles(gx * gy, img, true, s);
+        order = img.tile_order;
+    }
 #define GS_BWD_LAUNCH(PPL, WAVES, OCC)                                                                          \
-    hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC>), dim3(gx, gy), dim3(64 * WAVES), 0, s, W, H,       \
+    hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H,      \
                        img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
-                       dL_dpix, bg, g.grad_accum, g_cull)
+                       dL_dpix, bg, g.grad_accum, g_cull, order, gx)
     switch (g_bwd_variant) {
         case 1: GS_BWD_LAUNCH(2, 2, 4); break;
         case 2: GS_BWD_LAUNCH(1, 4, 4); break;

@@ -233,6 +233,60 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
                        block, gx, gy, img.tile_cursor, b.pair_keys);
 }
 
+// ------------------------------------------------------- launch order ---
+// One workgroup: counting sort of the tiles by descending work (12-bit
+// buckets, order inside a bucket arbitrary -- it only steers scheduling).
+constexpr int kOrderThreads = 1024;
+constexpr int kOrderBuckets = 4096;
+int g_tile_order = 1;
+void set_tile_order(int v) { g_tile_order = v; }
+bool tile_order_enabled() { return g_tile_order != 0; }
+
+__global__ void __launch_bounds__(kOrderThreads) order_tiles_kernel(int T, const uint32_t* __restrict__ ranges,
+                                                                    const uint32_t* __restrict__ max_contrib,
+                                                                    uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[kOrderBuckets];
+    __shared__ uint32_t part[kOrderThreads];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < kOrderBuckets; i += kOrderThreads) hist[i] = 0;
+    __syncthreads();
+    auto bucket = [&](int t) -> uint32_t {
+        uint32_t w = ranges[2 * t + 1] - ranges[2 * t];
+        if (max_contrib) w = min(w, max_contrib[t]);
+        return (uint32_t)(kOrderBuckets - 1) - min(w, (uint32_t)(kOrderBuckets - 1));  // heaviest first
+    };
+    for (int t = tid; t < T; t += kOrderThreads) atomicAdd(&hist[bucket(t)], 1u);
+    __syncthreads();
+    // exclusive scan of 4096 buckets: 4 per thread + Hillis-Steele over threads
+    constexpr int kPer = kOrderBuckets / kOrderThreads;
+    uint32_t loc[kPer], sum = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+        loc[i] = sum;
+        sum += hist[tid * kPer + i];
+    }
+    part[tid] = sum;
+    __syncthreads();
+    for (int off = 1; off < kOrderThreads; off <<= 1) {
+        const uint32_t v = tid >= off ? part[tid - off] : 0u;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    const uint32_t base = part[tid] - sum;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kPer; i++) hist[tid * kPer + i] = base + loc[i];
+    __syncthreads();
+    for (int t = tid; t < T; t += kOrderThreads) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
+}
+
+void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s) {
+    if (T <= 0) return;
+    hipLaunchKernelGGL(order_tiles_kernel, dim3(1), dim3(kOrderThreads), 0, s, T, img.ranges,
+                       use_max_contrib ? img.max_contrib : nullptr, img.tile_order);
+}
+
 // --------------------------------------------------------- tile sorting ---
 // In-LDS bitonic sort of S (power of two) u64 keys by `nthreads` threads.
 template <int kThreads>

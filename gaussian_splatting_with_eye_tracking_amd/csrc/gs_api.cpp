@@ -406,6 +406,10 @@ int gs_set_tuning(const char* key, int value) {
         set_backward_variant(value);
         return 0;
     }
+    if (std::strcmp(key, "tile_order") == 0) {
+        set_tile_order(value);
+        return 0;
+    }
     if (std::strcmp(key, "bin_chunk") == 0) {
         set_bin_chunk(value);
         return 0;

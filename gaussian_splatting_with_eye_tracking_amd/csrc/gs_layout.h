@@ -89,6 +89,7 @@ struct ImageView {
     uint32_t* levels_current;  // tile_AMR_levels_current
     uint32_t* pv;              // [4] percentile values (AMR)
     uint32_t* large_tiles;     // [T] list of tiles needing the large sort
+    uint32_t* tile_order;      // [T] tiles by descending blend work (launch order)
 };
 
 inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
@@ -105,6 +106,7 @@ inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
     g.levels_current = carve<uint32_t>(base, off, T);
     g.pv = carve<uint32_t>(base, off, 4);
     g.large_tiles = carve<uint32_t>(base, off, T);
+    g.tile_order = carve<uint32_t>(base, off, T);
     if (v) *v = g;
     return align_up(off);
 }

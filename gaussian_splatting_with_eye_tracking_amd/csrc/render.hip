@@ -53,18 +53,20 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
                                                                  uint32_t* __restrict__ n_contrib,
                                                                  uint32_t* __restrict__ max_contrib,
                                                                  const float* __restrict__ bg,
-                                                                 float* __restrict__ out_color, int cull) {
+                                                                 float* __restrict__ out_color, int cull,
+                                                                 const uint32_t* __restrict__ order, int gx) {
     __shared__ float2 s_xy[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
     __shared__ float4 s_rgb[64 * kWaves];
     __shared__ uint64_t s_bal[4 * kWaves];
     __shared__ uint32_t s_max;
     if (kWaves > 1 && threadIdx.x == 0) s_max = 0;
-    const int tile = blockIdx.y * gridDim.x + blockIdx.x;
-    const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, blockIdx.x * 16, blockIdx.y * 16, 1);
+    const int tile = order ? (int)order[blockIdx.x] : (int)blockIdx.x;
+    const uint32_t ox = (uint32_t)(tile % gx) * 16, oy = (uint32_t)(tile / gx) * 16;
+    const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, 1);
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const BlendStateT<kPPL> st =
-        blend_tile_t<kPPL, kWaves>(range, px, (float)(blockIdx.x * 16), (float)(blockIdx.y * 16), 1.0f, point_list,
+        blend_tile_t<kPPL, kWaves>(range, px, (float)ox, (float)oy, 1.0f, point_list,
                                    means2D, features, conic_opacity, s_xy, s_co, s_rgb, s_bal, cull != 0);
     write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
     uint32_t m = 0;
@@ -91,11 +93,15 @@ void launch_render_forward(int W, int H, const ImageView& img, const BinningView
                            const float* features, const float* bg, float* out_color, hipStream_t s) {
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return;
+    // Row-major launch: heaviest-first by range length measured slower here
+    // (early termination makes the range a poor work estimate); the backward
+    // orders by max_contrib instead (backward.hip).
+    const uint32_t* order = nullptr;
 #define GS_FWD_LAUNCH(PPL, WAVES)                                                                                \
-    hipLaunchKernelGGL((render_fwd_kernel<PPL, WAVES>), dim3(gx, gy), dim3(64 * WAVES), 0, s, W, H, img.ranges, \
+    hipLaunchKernelGGL((render_fwd_kernel<PPL, WAVES>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H, img.ranges, \
                        b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
-                       img.max_contrib, bg, out_color, g_cull)
+                       img.max_contrib, bg, out_color, g_cull, order, gx)
     switch (g_fwd_variant) {
         case 0: GS_FWD_LAUNCH(4, 1); break;
         case 1: GS_FWD_LAUNCH(2, 2); break;

@@ -124,6 +124,7 @@ typedef struct {
     uint32_t* levels_current;
     uint32_t* pv; /* [4] */
     uint32_t* large_tiles;
+    uint32_t* tile_order; /* [T] blend launch order (descending work) */
 } gs_image_view;
 
 typedef struct {

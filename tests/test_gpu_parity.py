@@ -18,6 +18,7 @@ CASES = [
     ("cfg1_10k_256", 10000, 256, 256, 0),
     ("ragged_3k_250x130", 3000, 250, 130, 7),
     ("dense_20k_128", 20000, 128, 128, 11),  # large tiles: exercises the merge-sort path
+    ("grid_17k_tiles", 3000, 2112, 2080, 5),  # T = 17160 > kLdsTiles: device-atomic binning path
 ]
 
 
