@@ -110,7 +110,10 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
         __syncthreads();
         // first batch slot this wave needs: contributor = top-1-j < wave_last
-        const int j0 = max(0, top - (int)wave_last);
+        // (readfirstlane: wave_last is uniform after the xor-shuffle max, but the
+        // compiler cannot prove it; without this the bit-scan loop below is
+        // compiled as a divergent VALU loop)
+        const int j0 = __builtin_amdgcn_readfirstlane(max(0, top - (int)wave_last));
 #pragma unroll 1
         for (int c = 0; c < kWaves; c++) {
           if (64 * c + 64 <= j0) continue;
@@ -137,13 +140,16 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
 #pragma unroll
             for (int k = 0; k < kPPL; k++) {
                 if (!((mk[k] >> bit) & 1ull)) continue;  // wave-uniform: culled for this row group
-                if (contributor >= last[k]) continue;  // also covers pixels outside the image
                 const float dy = xy.y - px.y[k];
                 const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                if (power > 0.0f) continue;
                 const float G = __expf(power);
                 const float alpha = fminf(0.99f, co.w * G);
-                if (alpha < 1.0f / 255.0f) continue;
+                // The reference's three per-pixel `continue`s (backward.cu:466-482)
+                // as one predicate: only wave-uniform branches save SIMD time, and
+                // nested ones make the compiler re-zero g[] on every skip path.
+                // (contributor >= last also covers pixels outside the image.)
+                const bool ok = contributor < last[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                if (!ok) continue;
                 any = true;
                 const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
                 T[k] = T[k] * rinv;
@@ -202,7 +208,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
 }
 
 extern int g_cull;  // render.hip
-int g_bwd_variant = 1;  // 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave uncapped
+int g_bwd_variant = 0;  // 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave uncapped
 
 void set_backward_variant(int v) { g_bwd_variant = v; }
 

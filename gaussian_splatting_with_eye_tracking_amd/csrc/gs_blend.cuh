@@ -191,19 +191,18 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 bool alive = false;
 #pragma unroll
                 for (int k = 0; k < kPPL; k++) {
-                    if (done[k]) continue;
-                    alive = true;
+                    alive |= !done[k];
                     if (!((mk[k] >> bit) & 1ull)) continue;  // wave-uniform: culled for this row group
                     const float dy = xy.y - px.y[k];
                     const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
-                    if (power > 0.0f) continue;
                     const float alpha = fminf(0.99f, co.w * __expf(power));
-                    if (alpha < 1.0f / 255.0f) continue;
                     const float test_T = st_.T[k] * (1 - alpha);
-                    if (test_T < 0.0001f) {
-                        done[k] = true;
-                        continue;
-                    }
+                    // forward.cu:333-352's per-pixel continues as predicates (only
+                    // wave-uniform branches save SIMD time)
+                    const bool hit = !done[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                    const bool stop = hit && test_T < 0.0001f;
+                    done[k] = done[k] || stop;
+                    if (!hit || stop) continue;
                     const float4 f = s_rgb[j];
                     const float w = alpha * st_.T[k];
                     st_.C[k][0] += f.x * w;

@@ -154,7 +154,7 @@ int gs_reconstruct_keys(char* geom_buffer, char* binning_buffer, char* img_buffe
 void gs_profile_enable(int on);
 /* Kernel-geometry knobs for A/B measurements ("fwd_variant": 0 = one wave
  * per tile x 4 px/lane, 1 = 2 waves x 2 px/lane, 2 = 4 waves x
- * 1 px/lane, the default), "bwd_variant" (same geometries; default 1), "cull" (1 =
+ * 1 px/lane, the default), "bwd_variant" (0 = 1 wave x 4 px/lane, the default; 1 = 2 x 2; 2 = 4 x 1; 3 = 1 x 4 uncapped registers), "cull" (1 =
  * skip Gaussians whose alpha >= 1/255 box misses a 16x4 row group, the
  * default; 0 only to verify that the cull is exact).  Returns 0, or -1 for
  * an unknown key. */

@@ -126,6 +126,38 @@ def test_backward_parity(name, P, W, H, seed, variant):
         assert G.rel_err(gg, rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(gg, rg[n]))
 
 
+@pytest.mark.parametrize("bwd_variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("fwd_variant", [0, 1, 2])
+def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
+    """Every forward / backward blend geometry (gs_set_tuning) against the oracle."""
+    import oracle as O
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    P, W, H, seed = 10000, 256, 256, 0
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    try:
+        C.set_tuning("fwd_variant", fwd_variant)
+        C.set_tuning("bwd_variant", bwd_variant)
+        s, t, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam, bg=(0.2, 0.1, 0.05))
+        dpix = S.make_cotangent(H, W, seed + 1)
+        e = torch.Tensor([])
+        grads = C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, e, t["scales"], t["rotations"],
+                                               s.scale_modifier, e, s.viewmatrix, s.projmatrix, s.tanfovx,
+                                               s.tanfovy, torch.from_numpy(dpix).cuda(), t["shs"], s.sh_degree,
+                                               s.campos, geom, K, binning, img, False)
+        torch.cuda.synchronize()
+    finally:
+        C.set_tuning("fwd_variant", 2)
+        C.set_tuning("bwd_variant", 0)
+    os_, ref, kw = _oracle_forward(sc, cam, bg=(0.2, 0.1, 0.05))
+    assert G.image_l1(color.cpu().numpy(), ref.color) < G.IMAGE_L1_TOL
+    rg = O.backward(os_, ref, sc.means3D, dpix, **kw)
+    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    for n, g in zip(names, grads):
+        assert G.rel_err(g.cpu().numpy(), rg[n]) < G.GRAD_REL_TOL, (n, fwd_variant, bwd_variant)
+
+
 def test_autograd_dropin_matches_direct_call():
     """The drop-in GaussianRasterizer (autograd) returns the same image and
     gradients as the raw _C calls, in the reference's gradient order."""
