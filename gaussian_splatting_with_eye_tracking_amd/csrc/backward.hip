@@ -246,7 +246,9 @@ __device__ __forceinline__ void dnormvdv3(float vx, float vy, float vz, float dx
     oz = (-vx * vz * dx - vy * vz * dy + (sum2 - vz * vz) * dz) * invsum32;
 }
 
-template <bool kHasSH, bool kHasScales>
+// kSH16: SH with M = 16 coefficients (degree-3 models): compile-time loops,
+// 16-B loads and stores of the 192-B SH rows.
+template <bool kHasSH, bool kHasScales, bool kSH16>
 __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussArgs a, const float* __restrict__ grad_accum,
                                                                  const uint8_t* __restrict__ clamped_bits) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -279,8 +281,13 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
         for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = 0.f;
 #pragma unroll
         for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = 0.f;
-        if (kHasSH)
+        if (kHasSH && kSH16) {
+#pragma unroll
+            for (int i = 0; i < 12; i++)
+                reinterpret_cast<float4*>(a.dL_dsh)[(size_t)idx * 12 + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else if (kHasSH) {
             for (int i = 0; i < ncoef_out * 3; i++) a.dL_dsh[(size_t)idx * ncoef_out * 3 + i] = 0.f;
+        }
         for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = 0.f;
         for (int i = 0; i < 4; i++) a.dL_drot[4 * idx + i] = 0.f;
         return;
@@ -304,7 +311,7 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
     if (kHasSH) {
         const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
         const float* sh = a.shs + (size_t)idx * a.M * 3;
-        if (a.M == 16) {
+        if (kSH16) {
             const float4* s4 = reinterpret_cast<const float4*>(sh);
             float buf[48];
 #pragma unroll
@@ -487,9 +494,25 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
                 }
             }
         }
-        for (int k = 0; k < a.M; k++)
+        if (kSH16) {
+            float o[48];
 #pragma unroll
-            for (int c = 0; c < 3; c++) dsh[3 * k + c] = (k < ncoef) ? dsh_c[k] * dRGB[c] : 0.f;
+            for (int k = 0; k < 16; k++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) o[3 * k + c] = (k < ncoef) ? dsh_c[k] * dRGB[c] : 0.f;
+#pragma unroll
+            for (int i = 0; i < 12; i++)
+                reinterpret_cast<float4*>(dsh)[i] = make_float4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+        } else {
+            for (int k = 0; k < a.M; k++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    float v = 0.f;
+#pragma unroll
+                    for (int kk = 0; kk < 16; kk++) v = (kk == k && k < ncoef) ? dsh_c[kk] * dRGB[c] : v;
+                    dsh[3 * k + c] = v;
+                }
+        }
         const float ddx = dot3(dx3[0], dx3[1], dx3[2], dRGB[0], dRGB[1], dRGB[2]);
         const float ddy = dot3(dy3[0], dy3[1], dy3[2], dRGB[0], dRGB[1], dRGB[2]);
         const float ddz = dot3(dz3[0], dz3[1], dz3[2], dRGB[0], dRGB[1], dRGB[2]);
@@ -552,15 +575,17 @@ void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hi
     if (a.P == 0) return;
     const dim3 grid((a.P + 255) / 256);
     const bool sh = a.shs != nullptr;
+    const bool sh16 = sh && a.M == 16;
     const bool sc = a.scales != nullptr;
-    if (sh && sc)
-        hipLaunchKernelGGL((backward_gaussians_kernel<true, true>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
-    else if (sh)
-        hipLaunchKernelGGL((backward_gaussians_kernel<true, false>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
-    else if (sc)
-        hipLaunchKernelGGL((backward_gaussians_kernel<false, true>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
-    else
-        hipLaunchKernelGGL((backward_gaussians_kernel<false, false>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
+#define GS_BG_LAUNCH(A, B, C) \
+    hipLaunchKernelGGL((backward_gaussians_kernel<A, B, C>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped)
+    if (sh16 && sc) GS_BG_LAUNCH(true, true, true);
+    else if (sh16) GS_BG_LAUNCH(true, false, true);
+    else if (sh && sc) GS_BG_LAUNCH(true, true, false);
+    else if (sh) GS_BG_LAUNCH(true, false, false);
+    else if (sc) GS_BG_LAUNCH(false, true, false);
+    else GS_BG_LAUNCH(false, false, false);
+#undef GS_BG_LAUNCH
 }
 
 }  // namespace gsamd
