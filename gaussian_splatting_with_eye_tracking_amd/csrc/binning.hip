@@ -309,25 +309,111 @@ __device__ __forceinline__ void bitonic_lds(uint64_t* s, int S) {
     }
 }
 
-__global__ void __launch_bounds__(kSortThreads) sort_tiles_small_kernel(int T, const uint32_t* __restrict__ ranges,
+// ---- register-resident bitonic sort of one tile (S <= 256 * kEmax keys).
+// Thread-major: thread t holds keys t*E .. t*E+E-1 (E = S/256, S = padded
+// size).  A compare-exchange stage (k, j) pairs key i with i ^ j:
+//   j < E          partner in the same thread's registers;
+//   j < 64 E       partner in lane ^ (j/E) of the same wave (cross-lane shuffle);
+//   j >= 64 E      partner in another wave: one LDS exchange + 2 barriers.
+// Only log2(S/64E)... the last few stages of each merge touch LDS, so a
+// 1024-key tile does 3 LDS stages instead of 55 LDS round trips.
+__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
+    const int lo = __shfl_xor((int)(uint32_t)v, m, 64);
+    const int hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+template <int E, int kWavesUsed>
+__device__ __forceinline__ void bitonic_regs(uint64_t (&v)[E], uint64_t* lds) {
+    constexpr int S = 64 * kWavesUsed * E;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int k = 2; k <= S; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            if (j < E) {
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    if (e & j) continue;
+                    const int i = tid * E + e;
+                    const bool up = (i & k) == 0;
+                    const uint64_t a = v[e], b = v[e | j];
+                    const bool sw = (a > b) == up;
+                    v[e] = sw ? b : a;
+                    v[e | j] = sw ? a : b;
+                }
+            } else if (j < 64 * E) {
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int i = tid * E + e;
+                    const uint64_t p = shfl_xor_u64(v[e], j / E);
+                    const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+                    v[e] = keep_min ? (v[e] < p ? v[e] : p) : (v[e] < p ? p : v[e]);
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < E; e++) lds[tid * E + e] = v[e];
+                __syncthreads();
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const int i = tid * E + e;
+                    const uint64_t p = lds[i ^ j];
+                    const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+                    v[e] = keep_min ? (v[e] < p ? v[e] : p) : (v[e] < p ? p : v[e]);
+                }
+                __syncthreads();
+            }
+        }
+    }
+}
+
+template <int E, int kWavesUsed>
+__device__ __forceinline__ void sort_tile_regs(const uint64_t* __restrict__ keys, int n,
+                                               uint32_t* __restrict__ out, uint64_t* lds) {
+    const int tid = threadIdx.x;
+    uint64_t v[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = tid * E + e;
+        v[e] = i < n ? keys[i] : ~0ull;
+    }
+    bitonic_regs<E, kWavesUsed>(v, lds);
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = tid * E + e;
+        if (i < n) out[i] = (uint32_t)v[e];
+    }
+}
+
+// Tiles with lo < n <= hi (hi <= 256 * kEmax), one 256-thread workgroup each.
+template <int kEmax>
+__global__ void __launch_bounds__(kSortThreads) sort_tiles_small_kernel(int lo, int hi,
+                                                                         const uint32_t* __restrict__ ranges,
                                                                          const uint64_t* __restrict__ pair_keys,
                                                                          uint32_t* __restrict__ point_list) {
-    __shared__ uint64_t s[kSmallCap];
+    __shared__ uint64_t lds[256 * kEmax];
     const int tile = blockIdx.x;
     const uint32_t beg = ranges[2 * tile], end = ranges[2 * tile + 1];
     const int n = (int)(end - beg);
-    if (n == 0 || n > kSmallCap) return;
-    const int tid = threadIdx.x;
+    if (n <= lo || n > hi) return;
+    const uint64_t* keys = pair_keys + beg;
+    uint32_t* out = point_list + beg;
     if (n == 1) {
-        if (tid == 0) point_list[beg] = (uint32_t)pair_keys[beg];
+        if (threadIdx.x == 0) out[0] = (uint32_t)keys[0];
         return;
     }
-    int S = 2;
-    while (S < n) S <<= 1;
-    for (int i = tid; i < S; i += kSortThreads) s[i] = i < n ? pair_keys[beg + i] : ~0ull;
-    __syncthreads();
-    bitonic_lds<kSortThreads>(s, S);
-    for (int i = tid; i < n; i += kSortThreads) point_list[beg + i] = (uint32_t)s[i];
+    if (n <= 64) {  // one wave, shuffles only
+        if (threadIdx.x < 64) sort_tile_regs<1, 1>(keys, n, out, lds);
+        return;
+    }
+    if (kEmax == 4) {
+        if (n <= 256) sort_tile_regs<1, 4>(keys, n, out, lds);
+        else if (n <= 512) sort_tile_regs<2, 4>(keys, n, out, lds);
+        else sort_tile_regs<4, 4>(keys, n, out, lds);
+    } else {
+        if (n <= 2048) sort_tile_regs<8, 4>(keys, n, out, lds);
+        else sort_tile_regs<16, 4>(keys, n, out, lds);
+    }
 }
 
 // Merge-path split: number of elements taken from A for the first `diag`
@@ -392,12 +478,16 @@ __global__ void __launch_bounds__(kLargeThreads) sort_tiles_large_kernel(const u
     for (int i = tid; i < n; i += kLargeThreads) point_list[beg + i] = (uint32_t)src[i];
 }
 
-void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, const uint32_t* hdr, int num_large_host,
+void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int max_count_host, int num_large_host,
                        hipStream_t s) {
-    (void)hdr;
     if (T == 0) return;
-    hipLaunchKernelGGL(sort_tiles_small_kernel, dim3(T), dim3(kSortThreads), 0, s, T, img.ranges, b.pair_keys,
-                       b.point_list);
+    // n <= 1024 with 8 KiB of LDS; 1024 < n <= 4096 with 32 KiB (launched
+    // only if such a tile exists: the forward read back the maximum count)
+    hipLaunchKernelGGL(sort_tiles_small_kernel<4>, dim3(T), dim3(kSortThreads), 0, s, 0, 1024, img.ranges,
+                       b.pair_keys, b.point_list);
+    if (max_count_host > 1024)
+        hipLaunchKernelGGL(sort_tiles_small_kernel<16>, dim3(T), dim3(kSortThreads), 0, s, 1024, kSmallCap,
+                           img.ranges, b.pair_keys, b.point_list);
     if (num_large_host > 0)
         hipLaunchKernelGGL(sort_tiles_large_kernel, dim3(num_large_host), dim3(kLargeThreads), 0, s,
                            img.large_tiles, img.ranges, b.pair_keys, b.scratch, b.point_list);

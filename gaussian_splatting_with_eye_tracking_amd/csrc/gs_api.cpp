@@ -220,7 +220,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     if (r.K > 0) {
         { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s); }
         stage_check(debug, s, "duplicate");
-        { StageTimer _t(kSort, s); launch_sort_tiles(r.T, r.img, r.b, r.g.hdr, (int)hdr[kHdrNumLargeTiles], s); }
+        { StageTimer _t(kSort, s); launch_sort_tiles(r.T, r.img, r.b, (int)hdr[kHdrMaxTileCount], (int)hdr[kHdrNumLargeTiles], s); }
         stage_check(debug, s, "sort_tiles");
     }
     return r;

@@ -54,7 +54,7 @@ void set_bin_chunk(int gaussians_per_workgroup);
 void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s);
 bool tile_order_enabled();
 void set_tile_order(int v);
-void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, const uint32_t* hdr, int num_large_host,
+void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int max_count_host, int num_large_host,
                        hipStream_t s);
 // (tile << 32 | depth) reconstruction of the reference's point_list_keys.
 void launch_reconstruct_keys(int T, const ImageView& img, const BinningView& b, const GeomView& g, uint64_t* keys,
