@@ -39,6 +39,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 CONFIGS = {
     # name: (P, W, H)
     "cfg2_1080p_1M": (1_000_000, 1920, 1080),
+    "cfg3_amr_1080p_1M": (1_000_000, 1920, 1080),   # forward-only foveated AMR (32-px tiles)
     "cfg4_bicycle_6M": (6_100_000, 1600, 1063),
     "small": (100_000, 640, 360),
 }
@@ -103,6 +104,165 @@ def cpu_baseline_views_per_s(P: int, W: int, H: int, seed: int = 0):
     return 1.0 / dt, dt
 
 
+def cpu_amr_test_path(seed: int = 0):
+    """BASELINE.json north_star: the reference's CPU path, AMR_test.py, timed
+    on the host (oracle/amr_test_path.py restates it) on config 1: 10k
+    Gaussians at 256x256; its input image is the CPU oracle's forward render."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import amr_test_path as A
+    import oracle as O
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    W = H = 256
+    cam = S.make_camera(W, H)
+    sc = S.make_scene(10_000, cam, seed=seed)
+    t0 = time.perf_counter()
+    r = O.forward(O.settings_from_camera(cam), sc.means3D, sc.opacities, shs=sc.shs, scales=sc.scales,
+                  rotations=sc.rotations)
+    t_render = time.perf_counter() - t0
+    out = A.run(sc.means3D, cam.world_view_transform, cam.full_proj_transform, r.color, W, H)
+    sec = {k: round(v, 4) for k, v in out["seconds"].items()}
+    sec["render_cpu_oracle"] = round(t_render, 4)
+    total = sec["total"] + t_render
+    return {"value": 1.0 / total, "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": "config 1 (10k Gaussians, 256x256): AMR_test.py CPU section (projection, per-tile count "
+                      "loop, log10 levels, stride lattice, 3x scipy griddata linear) + CPU oracle render",
+            "seconds": sec}
+
+
+def amr_algorithmic_bytes(ranges: np.ndarray, levels: np.ndarray) -> float:
+    """Compulsory bytes of one 5-step frame's amr_render launches (DESIGN.md
+    §4): every rendered (tile, round) block reads its tile's entries (id 4 +
+    xy 8 + conic/opacity 16 + rgb 12 B) and writes its 256 sub-lattice pixels
+    (colour 12 + final T 4 + n_contrib 4 B); a tile of level L renders L rounds."""
+    n = (ranges[:, 1] - ranges[:, 0]).astype(np.float64)
+    L = np.minimum(levels.astype(np.float64), 4.0)
+    return float((L * (40.0 * n + 20.0 * 256)).sum())
+
+
+def run_amr(args, world, rank, local_rank, distributed, dev):
+    """Config 3: forward-only foveated rendering (gaussian_renderer_amr's
+    render(): foveaStep 0..4 through _RasterizeGaussians, summing the step
+    images; and render_once(): foveaStep -2 with interpolation).  Per-frame and
+    single-GPU: for N > 1 every rank renders its own frames (replicas only)."""
+    from diff_gaussian_rasterization_amr import GaussianRasterizationSettings, GaussianRasterizer, _RasterizeGaussians
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+
+    P, W, H = CONFIGS[args.config]
+    cam = S.make_camera(W, H)
+    sc = S.make_scene(P, cam, seed=args.seed)
+    st = GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+        bg=torch.zeros(3, device=dev), scale_modifier=1.0,
+        viewmatrix=torch.from_numpy(cam.world_view_transform).to(dev),
+        projmatrix=torch.from_numpy(cam.full_proj_transform).to(dev), sh_degree=3,
+        campos=torch.from_numpy(cam.camera_center).to(dev), prefiltered=False, debug=False)
+    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(sc, k))).to(dev)
+         for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+    e = torch.empty(0, device=dev)
+    u8 = torch.empty(0, dtype=torch.uint8, device=dev)
+    means2D = torch.zeros_like(t["means3D"])
+    a = (t["means3D"], means2D, t["shs"], e, t["opacities"], t["scales"], t["rotations"], e)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+
+    def frame_5step(record=False):
+        if record:
+            ev[0].record()
+        c, radii, gb, bb, ib = _RasterizeGaussians.apply(*a, 0, e, u8, u8, u8, False, st)
+        acc = c
+        if record:
+            ev[1].record()
+        for k in range(1, 5):
+            c, _, gb, bb, ib = _RasterizeGaussians.apply(*a, k, acc, gb, bb, ib, False, st)
+            acc = acc + c
+            if record:
+                ev[k + 1].record()
+        return acc, gb, bb, ib
+
+    rast = GaussianRasterizer(st)
+
+    def frame_once():
+        return rast(means3D=t["means3D"], means2D=means2D, opacities=t["opacities"], shs=t["shs"],
+                    scales=t["scales"], rotations=t["rotations"], foveaStep=-2, interpolate_image=True)[0]
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            frame_5step()
+            frame_once()
+        torch.cuda.synchronize()
+        if not args.no_profile:
+            _C.profile_enable(True)
+            _C.profile_read(True)
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        step_ms = np.zeros(5)
+        for _ in range(args.steps):
+            frame_5step(record=True)
+            torch.cuda.synchronize()
+            step_ms += np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(5)])
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        el5 = time.perf_counter() - t0
+        prof = {}
+        if not args.no_profile:
+            prof = _C.profile_read(True)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            frame_once()
+        torch.cuda.synchronize()
+        if distributed:
+            dist.barrier()
+        el1 = time.perf_counter() - t0
+        if not args.no_profile:
+            _C.profile_enable(False)
+        if distributed:
+            tt = torch.tensor([el5, el1], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el5, el1 = float(tt[0].item()), float(tt[1].item())
+        result = None
+        if rank == 0:
+            acc, gb, bb, ib = frame_5step()
+            torch.cuda.synchronize()
+            K = int(_C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)["hdr"][0].item())
+            d = _C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
+            rng = d["ranges"].cpu().numpy().astype(np.int64)
+            lv = d["levels"].cpu().numpy().astype(np.int64)
+            stages = {n: {"avg_ms": ms / c, "launches": c, "ms_per_frame": ms / args.steps}
+                      for n, (ms, c) in prof.items() if c}
+            roofline = None
+            if "amr_render" in stages:
+                by = amr_algorithmic_bytes(rng, lv)
+                ms = stages["amr_render"]["ms_per_frame"]
+                ach = by / (ms * 1e-3) / 1e9
+                roofline = {"kernel": "amr_render", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("amr_render"),
+                            "algorithmic_bytes_per_frame": by, "ms_per_frame": round(ms, 4)}
+            cpu = None
+            if not args.no_cpu_baseline and world == 1:
+                cpu = cpu_amr_test_path(args.seed)
+            result = {
+                "metric": "foveated AMR frames/sec (forward-only render(), 5 fovea steps) at 1080p, 1M Gaussians",
+                "value": world * args.steps / el5, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": 1000.0 * el5 / args.steps, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+                "data": "synthetic (SURVEY §8(d) generator, seed 0)",
+                "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, 32x32 AMR tiles, 5-step foveated "
+                                       f"render() per frame" + (", replicas" if world > 1 else ""),
+                           "P": P, "width": W, "height": H, "K_instances": K, "parallelism": f"replicas{world}",
+                           "levels_hist": np.bincount(lv, minlength=5)[1:].tolist()},
+                "render_once_fps": world * args.steps / el1,
+                "per_step_ms": [round(x / args.steps, 4) for x in step_ms],
+                "roofline": roofline,
+                "cpu_baseline": cpu,
+                "stages": stages,
+            }
+            print(json.dumps(result), flush=True)
+    return result
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,6 +284,12 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
+    if args.config.startswith("cfg3"):
+        result = run_amr(args, world, rank, local_rank, distributed, dev)
+        if distributed:
+            dist.barrier()
+            dist.destroy_process_group()
+        return result
 
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     from gaussian_splatting_with_eye_tracking_amd import _C
@@ -241,6 +407,7 @@ def main():
                        "parallelism": f"dp{world}", "K_instances": K, "V_visible": V, "K_bwd_entries": Kb},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "cpu_amr_test_path": cpu_amr_test_path(args.seed) if (cpu is not None) else None,
             "stages": stages,
         }
         print(json.dumps(result), flush=True)
