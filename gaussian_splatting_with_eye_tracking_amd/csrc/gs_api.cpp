@@ -406,6 +406,10 @@ int gs_set_tuning(const char* key, int value) {
         set_backward_variant(value);
         return 0;
     }
+    if (std::strcmp(key, "amr_variant") == 0) {
+        set_amr_variant(value);
+        return 0;
+    }
     if (std::strcmp(key, "tile_order") == 0) {
         set_tile_order(value);
         return 0;

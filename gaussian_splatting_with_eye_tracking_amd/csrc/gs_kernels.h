@@ -65,7 +65,8 @@ void launch_render_forward(int W, int H, const ImageView& img, const BinningView
                            const float* features, const float* bg, float* out_color, hipStream_t s);
 // Tuning knob for A/B runs (gs_set_tuning("fwd_variant", v)).
 void set_forward_variant(int v);
-void set_cull(int v);  // row-group cull in the blend kernels (default on)
+void set_cull(int v);
+void set_amr_variant(int v);  // AMR blend geometry (as fwd_variant)  // row-group cull in the blend kernels (default on)
 void set_backward_variant(int v);
 // Blend backward (base/cr/backward.cu:399-557) into g.grad_accum.
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,

@@ -116,22 +116,27 @@ __device__ __forceinline__ uint32_t amr_round(uint32_t ox, uint32_t oy) {
     return ox == 0 ? (oy == 0 ? 1u : 4u) : (oy == 0 ? 3u : 2u);
 }
 
-// grid (2*tgx, 2*tgy) x one wave: block -> (32-px tile, sub-lattice offset);
-// the wave covers the tile's 16x16 sub-lattice with stride 2.
-__global__ void __launch_bounds__(64) amr_render_kernel(int W, int H, int tgx, const uint32_t* __restrict__ ranges,
-                                                        const uint32_t* __restrict__ levels,
-                                                        const uint32_t* __restrict__ levels_last,
-                                                        const uint32_t* __restrict__ point_list,
-                                                        const float2* __restrict__ means2D,
-                                                        const float* __restrict__ features,
-                                                        const float4* __restrict__ conic_opacity,
-                                                        float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-                                                        const float* __restrict__ bg, float* __restrict__ out_color,
-                                                        int foveaStep, int cull) {
-    __shared__ float2 s_xy[kBatch];
-    __shared__ float4 s_co[kBatch];
-    __shared__ float4 s_rgb[kBatch];
-    __shared__ uint64_t s_bal[4];
+// grid (2*tgx, 2*tgy) x kWaves waves: block -> (32-px tile, sub-lattice
+// offset); the block covers the tile's 16x16 sub-lattice with stride 2, in the
+// gs_blend.cuh geometry (kPPL pixels per lane).
+template <int kPPL, int kWaves>
+__global__ void __launch_bounds__(64 * kWaves) amr_render_kernel(int W, int H, int tgx,
+                                                                 const uint32_t* __restrict__ ranges,
+                                                                 const uint32_t* __restrict__ levels,
+                                                                 const uint32_t* __restrict__ levels_last,
+                                                                 const uint32_t* __restrict__ point_list,
+                                                                 const float2* __restrict__ means2D,
+                                                                 const float* __restrict__ features,
+                                                                 const float4* __restrict__ conic_opacity,
+                                                                 float* __restrict__ final_T,
+                                                                 uint32_t* __restrict__ n_contrib,
+                                                                 const float* __restrict__ bg,
+                                                                 float* __restrict__ out_color, int foveaStep,
+                                                                 int cull) {
+    __shared__ float2 s_xy[64 * kWaves];
+    __shared__ float4 s_co[64 * kWaves];
+    __shared__ float4 s_rgb[64 * kWaves];
+    __shared__ uint64_t s_bal[4 * kWaves];
     const int tile = (blockIdx.y >> 1) * tgx + (blockIdx.x >> 1);
     const uint32_t L_last = levels_last[tile];
     uint32_t L = levels[tile];
@@ -143,22 +148,33 @@ __global__ void __launch_bounds__(64) amr_render_kernel(int W, int H, int tgx, c
     if (foveaStep > 0 && round <= L_last) return;
     if (round > L) return;
     const uint32_t bx = (blockIdx.x >> 1) * 32 + ox, by = (blockIdx.y >> 1) * 32 + oy;
-    const PixelSet px = make_pixels(W, H, bx, by, 2);
+    const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, bx, by, 2);
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
-    const BlendStateT<kPix> st = blend_tile_t<kPix, 1>(range, px, (float)bx, (float)by, 2.0f, point_list, means2D,
-                                                       features, conic_opacity, s_xy, s_co, s_rgb, s_bal, cull != 0);
+    const BlendStateT<kPPL> st =
+        blend_tile_t<kPPL, kWaves>(range, px, (float)bx, (float)by, 2.0f, point_list, means2D, features,
+                                   conic_opacity, s_xy, s_co, s_rgb, s_bal, cull != 0);
     write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
 }
+
+int g_amr_variant = 2;  // same geometries as the forward: 0 = 1 x 4 px, 1 = 2 x 2, 2 = 4 x 1
+void set_amr_variant(int v) { g_amr_variant = v; }
 
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const GeomView& g, const float* features, const float* bg,
                        float* out_color, int foveaStep, hipStream_t s) {
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0) return;
-    hipLaunchKernelGGL(amr_render_kernel, dim3(2 * tgx, 2 * tgy), dim3(64), 0, s, W, H, tgx, img.ranges, levels,
-                       levels_last, b.point_list, reinterpret_cast<const float2*>(g.means2D), features,
-                       reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib, bg,
-                       out_color, foveaStep, g_cull);
+#define GS_AMR_LAUNCH(PPL, WAVES)                                                                                  \
+    hipLaunchKernelGGL((amr_render_kernel<PPL, WAVES>), dim3(2 * tgx, 2 * tgy), dim3(64 * WAVES), 0, s, W, H, tgx, \
+                       img.ranges, levels, levels_last, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
+                       features, reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib, \
+                       bg, out_color, foveaStep, g_cull)
+    switch (g_amr_variant) {
+        case 0: GS_AMR_LAUNCH(4, 1); break;
+        case 1: GS_AMR_LAUNCH(2, 2); break;
+        default: GS_AMR_LAUNCH(1, 4); break;
+    }
+#undef GS_AMR_LAUNCH
 }
 
 // amr/cr/forward.cu:520-648, per pixel.  pass 0 = the precomp copy of the

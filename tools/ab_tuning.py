@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--W", type=int, default=1920)
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--backward", action="store_true")
+    ap.add_argument("--amr", action="store_true", help="time a 5-step foveated AMR frame instead")
     args = ap.parse_args()
 
     from gaussian_splatting_with_eye_tracking_amd import _C
@@ -54,6 +55,22 @@ def main():
         if args.backward:
             torch.autograd.backward(color, dpix)
         return color
+
+    if args.amr:
+        from diff_gaussian_rasterization_amr import GaussianRasterizationSettings as AS, _RasterizeGaussians as AR
+        ast = AS(**st._asdict())
+        e = torch.empty(0, device=dev)
+        u8 = torch.empty(0, dtype=torch.uint8, device=dev)
+        a = (t["means3D"], m2, t["shs"], e, t["opacities"], t["scales"], t["rotations"], e)
+
+        def run():  # noqa: F811  (gaussian_renderer_amr render(): fovea steps 0..4)
+            with torch.no_grad():
+                c, _, gb, bb, ib = AR.apply(*a, 0, e, u8, u8, u8, False, ast)
+                acc = c
+                for k in range(1, 5):
+                    c, _, gb, bb, ib = AR.apply(*a, k, acc, gb, bb, ib, False, ast)
+                    acc = acc + c
+            return acc
 
     ref_img = None
     results = {v: [] for v in args.values}

@@ -37,6 +37,7 @@ for step in "$@"; do
               run ab_chunk_cnt 400 python tools/ab_tuning.py --key bin_chunk --values 2048 4096 8192 16384 --stage count_tiles ;;
     ab_order) run ab_order_fwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render &&
               run ab_order_bwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render_bwd --backward ;;
+    ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 0 1 2 --stage amr_render --amr ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_sq -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_sq2) run pmc_sq2 600 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     *) echo "unknown step $step"; exit 2 ;;
