@@ -27,8 +27,14 @@ HIP_SOURCES = ["preprocess.hip", "binning.hip", "render.hip", "backward.hip", "a
 ARCH = os.environ.get("GSAMD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off is part of the parity contract (see gs_device.cuh).
+# -fno-slp-vectorize: the SLP pass packs independent f32 ops into v_pk_* and then
+# needs v_mov pairs to form the operand registers; in the blend loops that cost
+# more than it saved (render_bwd 0.90 -> 0.68 ms at config 2).
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off", "-munsafe-fp-atomics",
+             "-fno-slp-vectorize",
              "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}"]
+# extra flags for code-generation experiments (e.g. GSAMD_EXTRA_HIPFLAGS=-fno-slp-vectorize)
+HIP_FLAGS += shlex.split(os.environ.get("GSAMD_EXTRA_HIPFLAGS", ""))
 
 
 def _run(cmd: list[str]) -> None:
