@@ -31,38 +31,61 @@ constexpr int kSortThreads = 256;
 constexpr int kLargeThreads = 1024;
 constexpr int kChunk = 4096;
 
+// Exclusive prefix sum of one value per thread over a workgroup of kThreads
+// (<= 1024) threads: wave-level shuffle scans, one LDS exchange of the wave
+// totals, two barriers.  Also returns the workgroup total.
+template <int kThreads>
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+    constexpr int kW = kThreads / 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)inc, off, 64);
+        if (lane >= off) inc += t;
+    }
+    if (lane == 63) s_wave[wave] = inc;
+    __syncthreads();
+    if (wave == 0) {
+        uint32_t w = lane < kW ? s_wave[lane] : 0u;
+        uint32_t wi = w;
+#pragma unroll
+        for (int off = 1; off < kW; off <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)wi, off, 64);
+            if (lane >= off) wi += t;
+        }
+        if (lane < kW) s_wave[lane] = wi - w;  // exclusive wave offsets
+        if (lane == kW - 1) s_wave[kW] = wi;   // total
+    }
+    __syncthreads();
+    total = s_wave[kW];
+    return s_wave[wave] + inc - v;
+}
+
 // ------------------------------------------------------------ tile scan ---
 __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const uint32_t* __restrict__ count,
                                                                  uint32_t* __restrict__ ranges,
                                                                  uint32_t* __restrict__ cursor,
                                                                  uint32_t* __restrict__ large_tiles,
                                                                  uint32_t* __restrict__ hdr) {
-    __shared__ uint32_t sums[kScanThreads];
-    __shared__ uint32_t smax[kScanThreads];
+    __shared__ uint32_t s_wave[kScanThreads / 64 + 1];
+    __shared__ uint32_t s_max[kScanThreads / 64];
     __shared__ uint32_t nlarge;
     const int tid = threadIdx.x;
     const int per = (T + kScanThreads - 1) / kScanThreads;
     const int beg = min(T, tid * per), end = min(T, beg + per);
-    uint32_t s = 0, mx = 0;
+    uint32_t sum = 0, mx = 0;
     for (int i = beg; i < end; i++) {
         const uint32_t c = count[i];
-        s += c;
+        sum += c;
         mx = max(mx, c);
     }
-    sums[tid] = s;
-    smax[tid] = mx;
     if (tid == 0) nlarge = 0;
-    __syncthreads();
-    // Hillis-Steele inclusive scan over 1024 partial sums.
-    for (int off = 1; off < kScanThreads; off <<= 1) {
-        const uint32_t v = tid >= off ? sums[tid - off] : 0u;
-        const uint32_t m = tid >= off ? smax[tid - off] : 0u;
-        __syncthreads();
-        sums[tid] += v;
-        smax[tid] = max(smax[tid], m);
-        __syncthreads();
-    }
-    uint32_t run = sums[tid] - s;  // exclusive prefix
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    if ((tid & 63) == 0) s_max[tid >> 6] = mx;
+    uint32_t total;
+    uint32_t run = block_exclusive_scan<kScanThreads>(sum, s_wave, total);
     for (int i = beg; i < end; i++) {
         const uint32_t c = count[i];
         // identifyTileRanges leaves empty tiles at (0,0) (rasterizer_impl.cu:310).
@@ -76,9 +99,11 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const ui
         run += c;
     }
     __syncthreads();
-    if (tid == kScanThreads - 1) {
-        hdr[kHdrNumRendered] = sums[tid];
-        hdr[kHdrMaxTileCount] = smax[tid];
+    if (tid == 0) {
+        uint32_t m = 0;
+        for (int w = 0; w < kScanThreads / 64; w++) m = max(m, s_max[w]);
+        hdr[kHdrNumRendered] = total;
+        hdr[kHdrMaxTileCount] = m;
         hdr[kHdrNumLargeTiles] = nlarge;
         hdr[kHdrT] = (uint32_t)T;
     }
@@ -237,7 +262,7 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
 // One workgroup: counting sort of the tiles by descending work (12-bit
 // buckets, order inside a bucket arbitrary -- it only steers scheduling).
 constexpr int kOrderThreads = 1024;
-constexpr int kOrderBuckets = 4096;
+constexpr int kOrderBuckets = 1024;  // one per thread: bucket b = 64 log2(work + 1), heaviest first
 int g_tile_order = 1;
 void set_tile_order(int v) { g_tile_order = v; }
 bool tile_order_enabled() { return g_tile_order != 0; }
@@ -246,37 +271,22 @@ __global__ void __launch_bounds__(kOrderThreads) order_tiles_kernel(int T, const
                                                                     const uint32_t* __restrict__ max_contrib,
                                                                     uint32_t* __restrict__ order) {
     __shared__ uint32_t hist[kOrderBuckets];
-    __shared__ uint32_t part[kOrderThreads];
+    __shared__ uint32_t s_wave[kOrderThreads / 64 + 1];
     const int tid = threadIdx.x;
-    for (int i = tid; i < kOrderBuckets; i += kOrderThreads) hist[i] = 0;
+    hist[tid] = 0;
     __syncthreads();
     auto bucket = [&](int t) -> uint32_t {
         uint32_t w = ranges[2 * t + 1] - ranges[2 * t];
         if (max_contrib) w = min(w, max_contrib[t]);
-        return (uint32_t)(kOrderBuckets - 1) - min(w, (uint32_t)(kOrderBuckets - 1));  // heaviest first
+        const uint32_t b = min((uint32_t)(64.0f * __log2f((float)w + 1.0f)), (uint32_t)(kOrderBuckets - 1));
+        return (uint32_t)(kOrderBuckets - 1) - b;  // heaviest first
     };
     for (int t = tid; t < T; t += kOrderThreads) atomicAdd(&hist[bucket(t)], 1u);
     __syncthreads();
-    // exclusive scan of 4096 buckets: 4 per thread + Hillis-Steele over threads
-    constexpr int kPer = kOrderBuckets / kOrderThreads;
-    uint32_t loc[kPer], sum = 0;
-#pragma unroll
-    for (int i = 0; i < kPer; i++) {
-        loc[i] = sum;
-        sum += hist[tid * kPer + i];
-    }
-    part[tid] = sum;
+    uint32_t total;
+    const uint32_t base = block_exclusive_scan<kOrderThreads>(hist[tid], s_wave, total);
     __syncthreads();
-    for (int off = 1; off < kOrderThreads; off <<= 1) {
-        const uint32_t v = tid >= off ? part[tid - off] : 0u;
-        __syncthreads();
-        part[tid] += v;
-        __syncthreads();
-    }
-    const uint32_t base = part[tid] - sum;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < kPer; i++) hist[tid * kPer + i] = base + loc[i];
+    hist[tid] = base;
     __syncthreads();
     for (int t = tid; t < T; t += kOrderThreads) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
 }
