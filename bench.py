@@ -280,9 +280,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    # GS_BENCH_SHARE_DEVICE=1 / GS_BENCH_BACKEND=gloo only rehearse the N>1 path
+    # on a one-GPU box (every rank on device 0); real runs use one GPU per rank
+    # and RCCL ("nccl").
+    if os.environ.get("GS_BENCH_SHARE_DEVICE") == "1":
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     if distributed:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        backend = os.environ.get("GS_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local_rank)
     if args.config.startswith("cfg3"):
         result = run_amr(args, world, rank, local_rank, distributed, dev)
