@@ -89,6 +89,16 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // entries at or past the wave's max n_contrib are skipped by all its pixels
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) wave_last = max(wave_last, (uint32_t)__shfl_xor((int)wave_last, off, 64));
+    // per row group (the lane's k-th pixel): max n_contrib of its 64 pixels;
+    // entries at or past it are skipped by every pixel of the group
+    int group_last[kPPL];
+#pragma unroll
+    for (int k = 0; k < kPPL; k++) {
+        uint32_t g = last[k];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) g = max(g, (uint32_t)__shfl_xor((int)g, off, 64));
+        group_last[k] = __builtin_amdgcn_readfirstlane((int)g);
+    }
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
 
@@ -122,7 +132,10 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
           const uint64_t lo_cut = (j0 > 64 * c) ? ~0ull << (j0 - 64 * c) : ~0ull;
 #pragma unroll
           for (int k = 0; k < kPPL; k++) {
-              mk[k] = uniform_u64(s_bal[c * 4 + wave * kPPL + k]) & lo_cut;
+              // slots j with contributor = top-1-j < group_last[k], i.e. j >= top - group_last[k]
+              const int jk = top - group_last[k] - 64 * c;
+              const uint64_t gcut = jk <= 0 ? ~0ull : (jk >= 64 ? 0ull : ~0ull << jk);
+              mk[k] = uniform_u64(s_bal[c * 4 + wave * kPPL + k]) & lo_cut & gcut;
               todo |= mk[k];
           }
           while (todo) {
@@ -246,6 +259,132 @@ __device__ __forceinline__ void dnormvdv3(float vx, float vy, float vz, float dx
     oz = (-vx * vz * dx - vy * vz * dy + (sum2 - vz * vz) * dz) * invsum32;
 }
 
+// SH rows of Gaussian idx into s[16][3] (zero past (D+1)^2 and M).
+template <bool kSH16>
+__device__ __forceinline__ void load_sh_rows(const BackwardGaussArgs& a, int idx, float (&s)[16][3]) {
+    const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
+    const float* sh = a.shs + (size_t)idx * a.M * 3;
+    if (kSH16) {
+        const float4* s4 = reinterpret_cast<const float4*>(sh);
+        float buf[48];
+#pragma unroll
+        for (int i = 0; i < 12; i++) {
+            const float4 v4 = (i * 4 < ncoef * 3) ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+            buf[4 * i + 0] = v4.x; buf[4 * i + 1] = v4.y; buf[4 * i + 2] = v4.z; buf[4 * i + 3] = v4.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) s[k][c] = buf[3 * k + c];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) s[k][c] = (k < ncoef) ? sh[3 * k + c] : 0.f;
+    }
+}
+
+// computeColorFromSH backward (backward.cu:20-139) for one Gaussian: writes
+// its dL_dsh row and adds the view-direction term to dmean (+=, after the
+// cov2D (=) and projection (+=) terms, the reference's order).
+template <bool kSH16>
+__device__ __forceinline__ void sh_backward(const BackwardGaussArgs& a, int idx, float mx, float my, float mz,
+                                            const float (&s)[16][3], uint8_t cb, const float* acc,
+                                            float (&dmean)[3]) {
+    const int deg = a.D;
+    const int ncoef = min((deg + 1) * (deg + 1), a.M);
+    float* dsh = a.dL_dsh + (size_t)idx * a.M * 3;
+    const float dox = mx - a.campos[0], doy = my - a.campos[1], doz = mz - a.campos[2];
+    const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
+    const float x = dox / len, y = doy / len, z = doz / len;
+    float dRGB[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) dRGB[c] = acc[c] * (((cb >> c) & 1) ? 0.0f : 1.0f);
+    float dx3[3] = {0, 0, 0}, dy3[3] = {0, 0, 0}, dz3[3] = {0, 0, 0};
+    float dsh_c[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) dsh_c[k] = 0.f;
+    dsh_c[0] = SH_C0;
+    if (deg > 0) {
+        dsh_c[1] = -SH_C1 * y;
+        dsh_c[2] = SH_C1 * z;
+        dsh_c[3] = -SH_C1 * x;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            dx3[c] = -SH_C1 * s[3][c];
+            dy3[c] = -SH_C1 * s[1][c];
+            dz3[c] = SH_C1 * s[2][c];
+        }
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            dsh_c[4] = SH_C2_0 * xy;
+            dsh_c[5] = SH_C2_1 * yz;
+            dsh_c[6] = SH_C2_2 * (2.f * zz - xx - yy);
+            dsh_c[7] = SH_C2_3 * xz;
+            dsh_c[8] = SH_C2_4 * (xx - yy);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                dx3[c] += SH_C2_0 * y * s[4][c] + SH_C2_2 * 2.f * -x * s[6][c] + SH_C2_3 * z * s[7][c] +
+                          SH_C2_4 * 2.f * x * s[8][c];
+                dy3[c] += SH_C2_0 * x * s[4][c] + SH_C2_1 * z * s[5][c] + SH_C2_2 * 2.f * -y * s[6][c] +
+                          SH_C2_4 * 2.f * -y * s[8][c];
+                dz3[c] += SH_C2_1 * y * s[5][c] + SH_C2_2 * 2.f * 2.f * z * s[6][c] + SH_C2_3 * x * s[7][c];
+            }
+            if (deg > 2) {
+                dsh_c[9] = SH_C3_0 * y * (3.f * xx - yy);
+                dsh_c[10] = SH_C3_1 * xy * z;
+                dsh_c[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
+                dsh_c[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                dsh_c[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
+                dsh_c[14] = SH_C3_5 * z * (xx - yy);
+                dsh_c[15] = SH_C3_6 * x * (xx - 3.f * yy);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    dx3[c] += (SH_C3_0 * s[9][c] * 3.f * 2.f * xy + SH_C3_1 * s[10][c] * yz +
+                               SH_C3_2 * s[11][c] * -2.f * xy + SH_C3_3 * s[12][c] * -3.f * 2.f * xz +
+                               SH_C3_4 * s[13][c] * (-3.f * xx + 4.f * zz - yy) + SH_C3_5 * s[14][c] * 2.f * xz +
+                               SH_C3_6 * s[15][c] * 3.f * (xx - yy));
+                    dy3[c] += (SH_C3_0 * s[9][c] * 3.f * (xx - yy) + SH_C3_1 * s[10][c] * xz +
+                               SH_C3_2 * s[11][c] * (-3.f * yy + 4.f * zz - xx) +
+                               SH_C3_3 * s[12][c] * -3.f * 2.f * yz + SH_C3_4 * s[13][c] * -2.f * xy +
+                               SH_C3_5 * s[14][c] * -2.f * yz + SH_C3_6 * s[15][c] * -3.f * 2.f * xy);
+                    dz3[c] += (SH_C3_1 * s[10][c] * xy + SH_C3_2 * s[11][c] * 4.f * 2.f * yz +
+                               SH_C3_3 * s[12][c] * 3.f * (2.f * zz - xx - yy) + SH_C3_4 * s[13][c] * 4.f * 2.f * xz +
+                               SH_C3_5 * s[14][c] * (xx - yy));
+                }
+            }
+        }
+    }
+    if (kSH16) {
+        float o[48];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) o[3 * k + c] = (k < ncoef) ? dsh_c[k] * dRGB[c] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 12; i++)
+            reinterpret_cast<float4*>(dsh)[i] = make_float4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
+    } else {
+        for (int k = 0; k < a.M; k++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                float v = 0.f;
+#pragma unroll
+                for (int kk = 0; kk < 16; kk++) v = (kk == k && k < ncoef) ? dsh_c[kk] * dRGB[c] : v;
+                dsh[3 * k + c] = v;
+            }
+    }
+    const float ddx = dot3(dx3[0], dx3[1], dx3[2], dRGB[0], dRGB[1], dRGB[2]);
+    const float ddy = dot3(dy3[0], dy3[1], dy3[2], dRGB[0], dRGB[1], dRGB[2]);
+    const float ddz = dot3(dz3[0], dz3[1], dz3[2], dRGB[0], dRGB[1], dRGB[2]);
+    float ox, oy, oz;
+    dnormvdv3(dox, doy, doz, ddx, ddy, ddz, ox, oy, oz);
+    dmean[0] += ox;
+    dmean[1] += oy;
+    dmean[2] += oz;
+}
+
 // kSH16: SH with M = 16 coefficients (degree-3 models): compile-time loops,
 // 16-B loads and stores of the 192-B SH rows.
 template <bool kHasSH, bool kHasScales, bool kSH16>
@@ -309,26 +448,7 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
     float s[16][3];
     uint8_t cb = 0;
     if (kHasSH) {
-        const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
-        const float* sh = a.shs + (size_t)idx * a.M * 3;
-        if (kSH16) {
-            const float4* s4 = reinterpret_cast<const float4*>(sh);
-            float buf[48];
-#pragma unroll
-            for (int i = 0; i < 12; i++) {
-                const float4 v4 = (i * 4 < ncoef * 3) ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-                buf[4 * i + 0] = v4.x; buf[4 * i + 1] = v4.y; buf[4 * i + 2] = v4.z; buf[4 * i + 3] = v4.w;
-            }
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) s[k][c] = buf[3 * k + c];
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) s[k][c] = (k < ncoef) ? sh[3 * k + c] : 0.f;
-        }
+        load_sh_rows<kSH16>(a, idx, s);
         cb = clamped_bits[idx];
     }
     const Mat4 V = load_mat4(a.viewmatrix);
@@ -428,100 +548,7 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
     }
 
     // ---- computeColorFromSH backward (backward.cu:20-139)
-    if (kHasSH) {
-        const int deg = a.D;
-        const int ncoef = min((deg + 1) * (deg + 1), a.M);
-        float* dsh = a.dL_dsh + (size_t)idx * a.M * 3;
-        const float dox = mx - a.campos[0], doy = my - a.campos[1], doz = mz - a.campos[2];
-        const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
-        const float x = dox / len, y = doy / len, z = doz / len;
-        float dRGB[3];
-#pragma unroll
-        for (int c = 0; c < 3; c++) dRGB[c] = acc[c] * (((cb >> c) & 1) ? 0.0f : 1.0f);
-        float dx3[3] = {0, 0, 0}, dy3[3] = {0, 0, 0}, dz3[3] = {0, 0, 0};
-        float dsh_c[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++) dsh_c[k] = 0.f;
-        dsh_c[0] = SH_C0;
-        if (deg > 0) {
-            dsh_c[1] = -SH_C1 * y;
-            dsh_c[2] = SH_C1 * z;
-            dsh_c[3] = -SH_C1 * x;
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                dx3[c] = -SH_C1 * s[3][c];
-                dy3[c] = -SH_C1 * s[1][c];
-                dz3[c] = SH_C1 * s[2][c];
-            }
-            if (deg > 1) {
-                const float xx = x * x, yy = y * y, zz = z * z;
-                const float xy = x * y, yz = y * z, xz = x * z;
-                dsh_c[4] = SH_C2_0 * xy;
-                dsh_c[5] = SH_C2_1 * yz;
-                dsh_c[6] = SH_C2_2 * (2.f * zz - xx - yy);
-                dsh_c[7] = SH_C2_3 * xz;
-                dsh_c[8] = SH_C2_4 * (xx - yy);
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    dx3[c] += SH_C2_0 * y * s[4][c] + SH_C2_2 * 2.f * -x * s[6][c] + SH_C2_3 * z * s[7][c] +
-                              SH_C2_4 * 2.f * x * s[8][c];
-                    dy3[c] += SH_C2_0 * x * s[4][c] + SH_C2_1 * z * s[5][c] + SH_C2_2 * 2.f * -y * s[6][c] +
-                              SH_C2_4 * 2.f * -y * s[8][c];
-                    dz3[c] += SH_C2_1 * y * s[5][c] + SH_C2_2 * 2.f * 2.f * z * s[6][c] + SH_C2_3 * x * s[7][c];
-                }
-                if (deg > 2) {
-                    dsh_c[9] = SH_C3_0 * y * (3.f * xx - yy);
-                    dsh_c[10] = SH_C3_1 * xy * z;
-                    dsh_c[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
-                    dsh_c[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                    dsh_c[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
-                    dsh_c[14] = SH_C3_5 * z * (xx - yy);
-                    dsh_c[15] = SH_C3_6 * x * (xx - 3.f * yy);
-#pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        dx3[c] += (SH_C3_0 * s[9][c] * 3.f * 2.f * xy + SH_C3_1 * s[10][c] * yz +
-                                   SH_C3_2 * s[11][c] * -2.f * xy + SH_C3_3 * s[12][c] * -3.f * 2.f * xz +
-                                   SH_C3_4 * s[13][c] * (-3.f * xx + 4.f * zz - yy) + SH_C3_5 * s[14][c] * 2.f * xz +
-                                   SH_C3_6 * s[15][c] * 3.f * (xx - yy));
-                        dy3[c] += (SH_C3_0 * s[9][c] * 3.f * (xx - yy) + SH_C3_1 * s[10][c] * xz +
-                                   SH_C3_2 * s[11][c] * (-3.f * yy + 4.f * zz - xx) +
-                                   SH_C3_3 * s[12][c] * -3.f * 2.f * yz + SH_C3_4 * s[13][c] * -2.f * xy +
-                                   SH_C3_5 * s[14][c] * -2.f * yz + SH_C3_6 * s[15][c] * -3.f * 2.f * xy);
-                        dz3[c] += (SH_C3_1 * s[10][c] * xy + SH_C3_2 * s[11][c] * 4.f * 2.f * yz +
-                                   SH_C3_3 * s[12][c] * 3.f * (2.f * zz - xx - yy) + SH_C3_4 * s[13][c] * 4.f * 2.f * xz +
-                                   SH_C3_5 * s[14][c] * (xx - yy));
-                    }
-                }
-            }
-        }
-        if (kSH16) {
-            float o[48];
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) o[3 * k + c] = (k < ncoef) ? dsh_c[k] * dRGB[c] : 0.f;
-#pragma unroll
-            for (int i = 0; i < 12; i++)
-                reinterpret_cast<float4*>(dsh)[i] = make_float4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
-        } else {
-            for (int k = 0; k < a.M; k++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    float v = 0.f;
-#pragma unroll
-                    for (int kk = 0; kk < 16; kk++) v = (kk == k && k < ncoef) ? dsh_c[kk] * dRGB[c] : v;
-                    dsh[3 * k + c] = v;
-                }
-        }
-        const float ddx = dot3(dx3[0], dx3[1], dx3[2], dRGB[0], dRGB[1], dRGB[2]);
-        const float ddy = dot3(dy3[0], dy3[1], dy3[2], dRGB[0], dRGB[1], dRGB[2]);
-        const float ddz = dot3(dz3[0], dz3[1], dz3[2], dRGB[0], dRGB[1], dRGB[2]);
-        float ox, oy, oz;
-        dnormvdv3(dox, doy, doz, ddx, ddy, ddz, ox, oy, oz);
-        dmean[0] += ox;
-        dmean[1] += oy;
-        dmean[2] += oz;
-    }
+    if (kHasSH) sh_backward<kSH16>(a, idx, mx, my, mz, s, cb, acc, dmean);
 #pragma unroll
     for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = dmean[i];
 
@@ -571,6 +598,37 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
     }
 }
 
+// Split mode, second kernel: the SH part alone (its ~50 live SH registers no
+// longer limit the occupancy of the geometry part).  Reads dL_dcolor and the
+// partial dL_dmeans3D the geometry kernel wrote, adds the SH term, writes
+// dL_dsh (zeros for culled Gaussians).
+template <bool kSH16>
+__global__ void __launch_bounds__(256) sh_backward_kernel(BackwardGaussArgs a, const uint8_t* __restrict__ clamped_bits) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    if (a.radii[idx] <= 0) {
+        if (kSH16) {
+#pragma unroll
+            for (int i = 0; i < 12; i++)
+                reinterpret_cast<float4*>(a.dL_dsh)[(size_t)idx * 12 + i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+            for (int i = 0; i < a.M * 3; i++) a.dL_dsh[(size_t)idx * a.M * 3 + i] = 0.f;
+        }
+        return;
+    }
+    const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
+    float acc[3] = {a.dL_dcolor[3 * idx], a.dL_dcolor[3 * idx + 1], a.dL_dcolor[3 * idx + 2]};
+    float dmean[3] = {a.dL_dmean3D[3 * idx], a.dL_dmean3D[3 * idx + 1], a.dL_dmean3D[3 * idx + 2]};
+    float s[16][3];
+    load_sh_rows<kSH16>(a, idx, s);
+    sh_backward<kSH16>(a, idx, mx, my, mz, s, clamped_bits[idx], acc, dmean);
+#pragma unroll
+    for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = dmean[i];
+}
+
+int g_bwd_gauss_split = 0;
+void set_bwd_gauss_split(int v) { g_bwd_gauss_split = v; }
+
 void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hipStream_t s) {
     if (a.P == 0) return;
     const dim3 grid((a.P + 255) / 256);
@@ -579,6 +637,13 @@ void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hi
     const bool sc = a.scales != nullptr;
 #define GS_BG_LAUNCH(A, B, C) \
     hipLaunchKernelGGL((backward_gaussians_kernel<A, B, C>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped)
+    if (sh && g_bwd_gauss_split) {
+        if (sc) GS_BG_LAUNCH(false, true, false);
+        else GS_BG_LAUNCH(false, false, false);
+        if (sh16) hipLaunchKernelGGL((sh_backward_kernel<true>), grid, dim3(256), 0, s, a, g.clamped);
+        else hipLaunchKernelGGL((sh_backward_kernel<false>), grid, dim3(256), 0, s, a, g.clamped);
+        return;
+    }
     if (sh16 && sc) GS_BG_LAUNCH(true, true, true);
     else if (sh16) GS_BG_LAUNCH(true, false, true);
     else if (sh && sc) GS_BG_LAUNCH(true, true, false);

@@ -406,6 +406,10 @@ int gs_set_tuning(const char* key, int value) {
         set_backward_variant(value);
         return 0;
     }
+    if (std::strcmp(key, "bwd_gauss_split") == 0) {
+        set_bwd_gauss_split(value);
+        return 0;
+    }
     if (std::strcmp(key, "amr_variant") == 0) {
         set_amr_variant(value);
         return 0;

@@ -40,6 +40,8 @@ for step in "$@"; do
     ab_order) run ab_order_fwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render &&
               run ab_order_bwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render_bwd --backward ;;
     ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 0 1 2 --stage amr_render --amr ;;
+    ab_split) run ab_split2 400 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward &&
+              run ab_split4 600 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_sq -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_sq2) run pmc_sq2 600 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     *) echo "unknown step $step"; exit 2 ;;
