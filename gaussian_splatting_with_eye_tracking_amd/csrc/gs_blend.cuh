@@ -86,11 +86,42 @@ __device__ __forceinline__ uint32_t splat_group_mask(float2 xy, float4 co, float
     const float hy = ok ? sqrtf(thr * co.x / det) * 1.001f + 0.02f : __builtin_inff();
     // "misses" comparisons are false for NaN / inf widths -> kept
     if (xy.x + hx < ox || xy.x - hx > ox + 15.0f * st) return 0u;
+    // Exact second stage: the minimum of Q over the group's rectangle (grown
+    // by 0.02 px) against the same threshold; a box that only grazes the
+    // group with a corner the ellipse does not reach is culled too.  The
+    // minimum lies inside (Q = 0) or on an edge, where Q is a 1-D quadratic
+    // minimised at a clamped point; rounding of that point moves Q by
+    // O(c * (1e-4 px)^2), far inside the margins above.
+    const float x0 = ox - 0.02f, x1 = ox + 15.0f * st + 0.02f;
+    const float kyx = -co.y / co.z, kxy = -co.y / co.x;
     uint32_t m = 0;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const float y0 = oy + st * (4.0f * r), y1 = oy + st * (4.0f * r + 3.0f);
-        if (!(xy.y + hy < y0 || xy.y - hy > y1)) m |= 1u << r;
+        if (xy.y + hy < y0 || xy.y - hy > y1) continue;
+        bool hit = !ok;  // ill-conditioned or non-finite: box test only
+        if (!hit) {
+            const float ya = y0 - 0.02f, yb = y1 + 0.02f;
+            if (xy.x >= x0 && xy.x <= x1 && xy.y >= ya && xy.y <= yb) {
+                hit = true;
+            } else {
+                float q = __builtin_inff();
+#pragma unroll
+                for (int e = 0; e < 2; e++) {  // vertical edges x = x0, x1
+                    const float dx = xy.x - (e ? x1 : x0);
+                    const float dy = fminf(fmaxf(kyx * dx, xy.y - yb), xy.y - ya);
+                    q = fminf(q, co.x * dx * dx + 2.0f * co.y * dx * dy + co.z * dy * dy);
+                }
+#pragma unroll
+                for (int e = 0; e < 2; e++) {  // horizontal edges y = ya, yb
+                    const float dy = xy.y - (e ? yb : ya);
+                    const float dx = fminf(fmaxf(kxy * dy, xy.x - x1), xy.x - x0);
+                    q = fminf(q, co.x * dx * dx + 2.0f * co.y * dx * dy + co.z * dy * dy);
+                }
+                hit = !(q > thr);  // NaN -> kept
+            }
+        }
+        if (hit) m |= 1u << r;
     }
     return m;
 }
