@@ -330,6 +330,22 @@ int gs_amr_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer i
                               const float* out_color_precomp, char* geom_buffer_precomp,
                               char* binning_buffer_precomp, char* image_buffer_precomp, float* out_color, int* radii,
                               int interpolate_image, int debug, void* stream) {
+    return gs_amr_rasterizer_forward_ex(geometry, binning, image, P, D, M, background, width, height, means3D, shs,
+                                        colors_precomp, opacities, scales, scale_modifier, rotations, cov3D_precomp,
+                                        viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered, foveaStep,
+                                        out_color_precomp, geom_buffer_precomp, binning_buffer_precomp,
+                                        image_buffer_precomp, out_color, radii, interpolate_image, debug, -1, stream);
+}
+
+int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffer image, int P, int D, int M,
+                                 const float* background, int width, int height, const float* means3D,
+                                 const float* shs, const float* colors_precomp, const float* opacities,
+                                 const float* scales, float scale_modifier, const float* rotations,
+                                 const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                                 const float* cam_pos, float tan_fovx, float tan_fovy, int prefiltered,
+                                 int foveaStep, const float* out_color_precomp, char* geom_buffer_precomp,
+                                 char* binning_buffer_precomp, char* image_buffer_precomp, float* out_color,
+                                 int* radii, int interpolate_image, int debug, int num_rendered_hint, void* stream) {
     return guarded([&]() -> int {
         if (P <= 0) return 0;
         hipStream_t s = static_cast<hipStream_t>(stream);
@@ -339,16 +355,21 @@ int gs_amr_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer i
         const bool dbg = debug != 0;
         if (foveaStep >= 1) {
             // amr/cr/rasterizer_impl.cu:334-462: progressive step on precomputed buffers.
-            if (!geom_buffer_precomp || !binning_buffer_precomp || !image_buffer_precomp)
+            if (!geom_buffer_precomp || !image_buffer_precomp)
                 throw GsError("foveaStep >= 1 needs the buffers returned by foveaStep 0");
             GeomView g;
             ImageView img;
             BinningView b;
             carve_geom(geom_buffer_precomp, P, &g);
             carve_image(image_buffer_precomp, (size_t)W * H, T, &img);
-            uint32_t hdr[4];
-            read_header(g.hdr, hdr, s);
-            const int K = (int)hdr[kHdrNumRendered];
+            int K = num_rendered_hint;
+            if (K < 0) {  // the reference reads K back here (amr/cr/rasterizer_impl.cu:337-340)
+                uint32_t hdr[4];
+                read_header(g.hdr, hdr, s);
+                K = (int)hdr[kHdrNumRendered];
+            }
+            if (K > 0 && !binning_buffer_precomp)
+                throw GsError("foveaStep >= 1 needs the binning buffer returned by foveaStep 0");
             carve_binning(binning_buffer_precomp, K, &b);
             launch_fovea_levels(foveaStep, T, img, s);
             stage_check(dbg, s, "fovea_levels");
@@ -460,6 +481,16 @@ size_t gs_image_bytes(int width, int height, int tile) {
 }
 
 size_t gs_binning_bytes(int K) { return carve_binning(nullptr, (size_t)K, nullptr); }
+
+int gs_binning_count_of_bytes(size_t nbytes) {
+    long lo = 0, hi = (long)std::min<size_t>(nbytes / 8 + 1, (size_t)INT32_MAX);
+    while (lo < hi) {  // smallest K with bytes(K) >= nbytes (bytes() is strictly increasing)
+        const long mid = (lo + hi) / 2;
+        if (carve_binning(nullptr, (size_t)mid, nullptr) < nbytes) lo = mid + 1;
+        else hi = mid;
+    }
+    return carve_binning(nullptr, (size_t)lo, nullptr) == nbytes ? (int)lo : -1;
+}
 
 size_t gs_knn_workspace_bytes(int P) { return knn_workspace_bytes(P); }
 

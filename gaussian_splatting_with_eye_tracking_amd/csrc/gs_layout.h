@@ -124,7 +124,10 @@ inline size_t carve_binning(char* base, size_t K, BinningView* v) {
     g.pair_keys = carve<uint64_t>(base, off, K);
     g.scratch = carve<uint64_t>(base, off, K);
     if (v) *v = g;
-    return align_up(off);
+    // Unpadded end: strictly increasing in K (>= 8 B per instance), so the
+    // caller can recover K from the buffer size (gs_binning_count_of_bytes)
+    // without a device read-back.
+    return off;
 }
 
 }  // namespace gsamd

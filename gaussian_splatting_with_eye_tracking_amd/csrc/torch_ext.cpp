@@ -103,14 +103,16 @@ std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> rasterize_impl(
             const Tensor pre = out_color_precomp_in.contiguous();
             require_device(pre, "out_color_precomp");
             Tensor g = geom_pre, b = bin_pre, im = img_pre;
-            rendered = gs_amr_rasterizer_forward(
+            // K of the precomputed buffers from the binning buffer's size (no sync)
+            const int hint = foveaStep >= 1 ? gs_binning_count_of_bytes((size_t)b.numel()) : -1;
+            rendered = gs_amr_rasterizer_forward_ex(
                 buf_of(geomBuffer), buf_of(binningBuffer), buf_of(imgBuffer), P, degree, M, fptr(bg), W, H,
                 fptr(means3D), fptr(sh), fptr(colors), fptr(opacity), fptr(scales), scale_modifier, fptr(rotations),
                 fptr(cov3D_precomp), fptr(viewmatrix), fptr(projmatrix), fptr(campos), tan_fovx, tan_fovy, prefiltered,
                 foveaStep, fptr(pre), g.numel() ? reinterpret_cast<char*>(g.data_ptr()) : nullptr,
                 b.numel() ? reinterpret_cast<char*>(b.data_ptr()) : nullptr,
                 im.numel() ? reinterpret_cast<char*>(im.data_ptr()) : nullptr, out_color.data_ptr<float>(),
-                radii.data_ptr<int>(), interpolate_image, debug, stream);
+                radii.data_ptr<int>(), interpolate_image, debug, hint, stream);
             check(rendered, "rasterize_gaussians (AMR)");
         }
     }

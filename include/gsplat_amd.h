@@ -90,6 +90,21 @@ int gs_amr_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer i
                               char* binning_buffer_precomp, char* image_buffer_precomp, float* out_color, int* radii,
                               int interpolate_image, int debug, void* stream);
 
+/* gs_amr_rasterizer_forward with num_rendered_hint: for foveaStep >= 1, a
+ * hint >= 0 is taken as K (the caller recovered it from the binning buffer's
+ * size with gs_binning_count_of_bytes) and the device read-back of K is
+ * skipped, so the progressive steps run without host synchronisation; -1
+ * reads it back like the reference. */
+int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffer image, int P, int D, int M,
+                                 const float* background, int width, int height, const float* means3D,
+                                 const float* shs, const float* colors_precomp, const float* opacities,
+                                 const float* scales, float scale_modifier, const float* rotations,
+                                 const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                                 const float* cam_pos, float tan_fovx, float tan_fovy, int prefiltered,
+                                 int foveaStep, const float* out_color_precomp, char* geom_buffer_precomp,
+                                 char* binning_buffer_precomp, char* image_buffer_precomp, float* out_color,
+                                 int* radii, int interpolate_image, int debug, int num_rendered_hint, void* stream);
+
 /* Replaces SimpleKNN::knn (knn/simple_knn.h:16-19, knn/simple_knn.cu:185-221)
  * behind simple_knn._C.distCUDA2.  `scratch` is resized to the workspace
  * size; no host synchronisation. */
@@ -136,6 +151,8 @@ typedef struct {
 size_t gs_geom_bytes(int P);
 size_t gs_image_bytes(int width, int height, int tile);
 size_t gs_binning_bytes(int K);
+/* Inverse of gs_binning_bytes (exact; -1 if nbytes is not a binning size). */
+int gs_binning_count_of_bytes(size_t nbytes);
 size_t gs_knn_workspace_bytes(int P);
 int gs_geom_view_of(char* base, int P, gs_geom_view* out);
 int gs_image_view_of(char* base, int width, int height, int tile, gs_image_view* out);

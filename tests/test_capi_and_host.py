@@ -63,6 +63,24 @@ def test_host_layout_helpers():
     assert v.grad_accum + 1000 * 64 - base <= g1
 
 
+def test_binning_size_inverse_is_exact():
+    """gs_binning_count_of_bytes inverts gs_binning_bytes (the AMR steps >= 1
+    recover K from the binning buffer's size instead of a device read-back)."""
+    lib = ctypes.CDLL(LIB)
+    lib.gs_binning_bytes.restype = ctypes.c_size_t
+    lib.gs_binning_bytes.argtypes = [ctypes.c_int]
+    lib.gs_binning_count_of_bytes.restype = ctypes.c_int
+    lib.gs_binning_count_of_bytes.argtypes = [ctypes.c_size_t]
+    ks = list(range(0, 700)) + [4095, 4096, 4097, 123457, 2205067, 4437743, 22303484]
+    prev = -1
+    for k in ks:
+        b = lib.gs_binning_bytes(k)
+        assert b > prev or k == 0
+        prev = b
+        assert lib.gs_binning_count_of_bytes(b) == k, k
+    assert lib.gs_binning_count_of_bytes(lib.gs_binning_bytes(1000) + 1) == -1
+
+
 def test_torch_extension_surface():
     from gaussian_splatting_with_eye_tracking_amd import _C, native_library_paths
     for n in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "amr_rasterize_gaussians",

@@ -269,6 +269,23 @@ def test_amr_foveated_steps(name, P, W, H, seed):
     assert G.image_l1(acc.cpu().numpy(), racc) < G.IMAGE_L1_TOL
 
 
+def test_amr_steps_with_nothing_in_front():
+    """K = 0 (every Gaussian behind the near plane): the progressive steps run
+    on an empty binning buffer and match the oracle (background on the
+    rendered sub-lattices)."""
+    import oracle as O
+    sc, cam = G.scene_and_camera(500, 96, 64, 2)
+    sc.means3D[:, 2] = -5.0
+    acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.3, 0.2, 0.1))
+    assert bb.numel() == 0 and int((radii > 0).sum()) == 0
+    s = O.settings_from_camera(cam, bg=(0.3, 0.2, 0.1))
+    kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+    racc, _, _, rsteps = O.amr_render_foveated(s, kw)
+    for k in range(5):
+        np.testing.assert_allclose(steps[k].cpu().numpy(), rsteps[k], atol=1e-6)
+    np.testing.assert_allclose(acc.cpu().numpy(), racc, atol=1e-6)
+
+
 def test_amr_render_once_interpolated():
     import oracle as O
     from diff_gaussian_rasterization_amr import GaussianRasterizer
