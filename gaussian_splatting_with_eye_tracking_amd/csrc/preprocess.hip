@@ -114,8 +114,6 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
         q = reinterpret_cast<const float4*>(a.rotations)[idx];
     }
     const float opacity = a.opacities[idx];
-    float shc[16][3];
-    if (kHasSH) load_sh<kSH16>(a.D, a.M, a.shs + (size_t)idx * a.M * 3, shc);
     const Mat4 V = load_mat4(a.viewmatrix);
     const Mat4 Pm = load_mat4(a.projmatrix);
 
@@ -184,6 +182,10 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
     if (area == 0) return;
 
     if (kHasSH) {
+        // SH only for Gaussians that survive the cull (computeColorFromSH runs
+        // after the rect test in the reference too, forward.cu:240-247)
+        float shc[16][3];
+        load_sh<kSH16>(a.D, a.M, a.shs + (size_t)idx * a.M * 3, shc);
         // computeColorFromSH: dir = normalize(mean - campos)
         float dx = mx - a.cam_pos[0], dy = my - a.cam_pos[1], dz = mz - a.cam_pos[2];
         const float len = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
