@@ -261,10 +261,16 @@ __device__ __forceinline__ void dnormvdv3(float vx, float vy, float vz, float dx
 
 // SH rows of Gaussian idx into s[16][3] (zero past (D+1)^2 and M).
 template <bool kSH16>
-__device__ __forceinline__ void load_sh_rows(const BackwardGaussArgs& a, int idx, float (&s)[16][3]) {
+__device__ __forceinline__ void load_sh_rows(const BackwardGaussArgs& a, int idx, float (&s)[16][3],
+                                             const float* lrow = nullptr) {
     const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
     const float* sh = a.shs + (size_t)idx * a.M * 3;
-    if (kSH16) {
+    if (kSH16 && lrow) {  // row staged in LDS by the workgroup's coalesced load
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) s[k][c] = (k < ncoef) ? lrow[3 * k + c] : 0.f;
+    } else if (kSH16) {
         const float4* s4 = reinterpret_cast<const float4*>(sh);
         float buf[48];
 #pragma unroll
@@ -453,7 +459,7 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     float s[16][3];
     uint8_t cb = 0;
     if (kHasSH) {
-        load_sh_rows<kSH16>(a, idx, s);
+        load_sh_rows<kSH16>(a, idx, s, lrow);
         cb = clamped_bits[idx];
     }
     const Mat4 V = load_mat4(a.viewmatrix);
@@ -616,6 +622,17 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
     constexpr bool kStage = kHasSH && kSH16;
     __shared__ float s_dsh[kStage ? 256 * kShRow : 1];
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if constexpr (kStage) {  // the workgroup's 256 SH rows in, wave-contiguous
+        const int g0 = blockIdx.x * blockDim.x;
+        const int n = min(256, a.P - g0);
+        const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)g0 * 12;
+        for (int f = threadIdx.x; f < n * 12; f += 256) {
+            const float4 v = in[f];
+            float* r = s_dsh + (f / 12) * kShRow + 4 * (f % 12);
+            r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+        }
+        __syncthreads();
+    }
     backward_gaussian_body<kHasSH, kHasScales, kSH16>(a, grad_accum, clamped_bits, idx,
                                                       kStage ? s_dsh + threadIdx.x * kShRow : nullptr);
     if constexpr (kStage) {
