@@ -28,6 +28,7 @@ for step in "$@"; do
     dist2) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 ;;
     dist2amr) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2amr 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 5 --warmup 2 --config cfg3_amr_1080p_1M ;;
     benchq) run bench 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    prof4) run rocprof4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- python3 bench.py --config cfg4_bicycle_6M --steps 5 --warmup 2 --no-cpu-baseline --no-profile ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
