@@ -85,6 +85,23 @@ def load_traffic(stage: str):
     return None
 
 
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
+# instruction (MI355X_MICROARCH.md, execution model).
+VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2
+
+
+def load_valu_instructions(stage: str):
+    """SQ_INSTS_VALU per launch of `stage` from a committed PMC summary, or None."""
+    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))):
+        try:
+            d = json.load(open(f))
+            if stage in d.get("per_launch_valu_instructions", {}):
+                return float(d["per_launch_valu_instructions"][stage])
+        except Exception:
+            continue
+    return None
+
+
 def cpu_baseline_views_per_s(P: int, W: int, H: int, seed: int = 0):
     """The CPU oracle (scalar C port of the reference path) timed on one full
     view, forward + backward, single thread."""
@@ -396,6 +413,12 @@ def main():
             roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic(dom),
                         "algorithmic_bytes": by, "avg_ms": round(stages[dom]["avg_ms"], 4)}
+            vi = load_valu_instructions(dom)
+            if vi is not None:  # the blend kernels' real bound
+                a_ = vi / (stages[dom]["avg_ms"] * 1e-3)
+                roofline["valu_issue"] = {"instructions_per_launch": vi, "achieved": round(a_, 1),
+                                          "peak": VALU_PEAK_WAVE_INSTR_PER_S, "unit": "wave-instr/s",
+                                          "frac": round(a_ / VALU_PEAK_WAVE_INSTR_PER_S, 4)}
             for n, st in stages.items():
                 b = algorithmic_bytes(n, P, V, K, Kb, N, T)
                 st["algorithmic_GBps"] = round(b / (st["avg_ms"] * 1e-3) / 1e9, 1) if b else None

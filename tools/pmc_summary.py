@@ -79,6 +79,14 @@ def main():
             wk = sum(wv[st]) / len(wv[st])
             res["raw_kib"][st] = {"FETCH_SIZE": fk, "WRITE_SIZE": wk, "launches": len(fv[st])}
             res["per_launch_hbm_bytes"][st] = (2.0 * fk + wk) * 1024.0
+    # VALU issue: SQ_INSTS_VALU per launch (wave-instructions; own pass, see
+    # tools/gpu_session.sh pmc_valu) -- the roofline of the blend kernels.
+    v = os.path.join(args.src, "pmc_valu", "run_counter_collection.csv")
+    if os.path.exists(v):
+        res["per_launch_valu_instructions"] = {}
+        vv, _ = per_kernel(v, "SQ_INSTS_VALU")
+        for st, xs in vv.items():
+            res["per_launch_valu_instructions"][st] = sum(xs) / len(xs)
     stats = os.path.join(args.src, "prof", "run_kernel_stats.csv")
     if os.path.exists(stats):
         shutil.copy(stats, os.path.join(args.out, f"{args.tag}_kernel_stats.csv"))
