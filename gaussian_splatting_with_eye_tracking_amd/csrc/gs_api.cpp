@@ -417,6 +417,18 @@ int gs_simple_knn(int P, const float* points, float* mean_dists, gs_buffer scrat
     });
 }
 
+int gs_l1_ssim_loss(const float* image, const float* gt, int C, int H, int W, float lambda_dssim, float* grad,
+                    float* out3, gs_buffer workspace, void* stream) {
+    return guarded([&]() -> int {
+        if (C <= 0 || H <= 0 || W <= 0) return 0;
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        char* ws = call_resize(workspace, l1_ssim_workspace_bytes(C, H, W), "loss workspace");
+        launch_l1_ssim(image, gt, C, H, W, lambda_dssim, grad, out3, reinterpret_cast<float*>(ws), s);
+        stage_check(false, s, "l1_ssim");
+        return 0;
+    });
+}
+
 int gs_set_tuning(const char* key, int value) {
     if (!key) return -1;
     if (std::strcmp(key, "fwd_variant") == 0) {

@@ -119,4 +119,9 @@ size_t radix_sort_u32_workspace(int n);
 void radix_sort_pairs_u32(int n, const uint32_t* keys_in, uint32_t* keys_out, const uint32_t* vals_in,
                           uint32_t* vals_out, int end_bit, char* workspace, hipStream_t s);
 
+// Training loss of train.py:91-93 (loss.hip): grad <- dloss/dimg, out3 <- {loss, l1, ssim}.
+size_t l1_ssim_workspace_bytes(int C, int H, int W);
+void launch_l1_ssim(const float* img, const float* gt, int C, int H, int W, float lambda, float* grad, float* out3,
+                    float* workspace, hipStream_t s);
+
 }  // namespace gsamd

@@ -290,6 +290,23 @@ py::dict ProfileRead(bool reset) {
 
 }  // namespace
 
+// Fused L1 + D-SSIM training loss (loss.hip): returns (out3 = [loss, l1, ssim], grad).
+std::tuple<Tensor, Tensor> L1SsimLoss(const Tensor& image, const Tensor& gt, double lambda_dssim) {
+    TORCH_CHECK(image.sizes() == gt.sizes() && image.dim() == 3, "image and gt must both be [C, H, W]");
+    require_device(image, "image");
+    require_device(gt, "gt");
+    const at::OptionalDeviceGuard guard(device_of(image));
+    const Tensor x = image.contiguous(), y = gt.contiguous();
+    Tensor grad = torch::empty_like(x);
+    Tensor out3 = torch::empty({3}, x.options());
+    Tensor ws = torch::empty({0}, x.options().dtype(torch::kByte));
+    check(gs_l1_ssim_loss(x.data_ptr<float>(), y.data_ptr<float>(), (int)x.size(0), (int)x.size(1), (int)x.size(2),
+                          (float)lambda_dssim, grad.data_ptr<float>(), out3.data_ptr<float>(), buf_of(ws),
+                          stream_of(x)),
+          "l1_ssim_loss");
+    return std::make_tuple(out3, grad);
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "MI355X (gfx950) Gaussian rasterizer -- PyTorch binding over include/gsplat_amd.h";
     m.def("rasterize_gaussians", &RasterizeGaussians);
@@ -298,6 +315,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("amr_rasterize_gaussians", &AMRRasterizeGaussians);
     m.def("distCUDA2", &DistCUDA2);
     m.def("parse_buffers", &ParseBuffers);
+    m.def("l1_ssim_loss", &L1SsimLoss);
     m.def("abi_version", []() { return gs_abi_version(); });
     m.def("profile_enable", [](bool on) { gs_profile_enable(on ? 1 : 0); });
     m.def("profile_read", &ProfileRead, py::arg("reset") = true);

@@ -110,6 +110,14 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
  * size; no host synchronisation. */
 int gs_simple_knn(int P, const float* points, float* mean_dists, gs_buffer scratch, void* stream);
 
+/* Training loss of the reference (train.py:91-93, utils/loss_utils.py:17-63):
+ *   loss = (1 - lambda_dssim) * mean|image - gt| + lambda_dssim * (1 - SSIM(image, gt))
+ * image, gt: [C][H][W] float32 (device).  Writes grad = dloss/dimage
+ * ([C][H][W]) and out3 = {loss, l1, ssim} (device); one fused pass plus a
+ * fixed-order reduction (deterministic); no host synchronisation. */
+int gs_l1_ssim_loss(const float* image, const float* gt, int C, int H, int W, float lambda_dssim, float* grad,
+                    float* out3, gs_buffer workspace, void* stream);
+
 /* ------------------------------------------------ parity / debug accessors
  * The reference exposes its internal buffers only in the AMR-debug variant
  * (ParseBuffers, amr-debug/rasterize_points.cu:37-61).  These views let the
