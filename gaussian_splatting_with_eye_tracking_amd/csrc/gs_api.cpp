@@ -429,6 +429,31 @@ int gs_l1_ssim_loss(const float* image, const float* gt, int C, int H, int W, fl
     });
 }
 
+int gs_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, long long n, int nseg,
+                 const long long* seg_end, const double* lr, const long long* step, double beta1, double beta2, double eps,
+                 void* stream) {
+    return guarded([&]() -> int {
+        if (nseg < 1 || nseg > 8) throw GsError("gs_adam_step: 1..8 segments");
+        for (int i = 0; i < nseg; i++)
+            if (step[i] < 0 || (i > 0 && seg_end[i] < seg_end[i - 1])) throw GsError("gs_adam_step: bad segments");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_adam(params, grads, exp_avg, exp_avg_sq, n, nseg, seg_end, lr, step, beta1, beta2, eps, s);
+        stage_check(false, s, "adam");
+        return 0;
+    });
+}
+
+int gs_densify_stats(int P, const int* radii, const float* grad_means2D, int grad_stride, float* xyz_gradient_accum,
+                     float* denom, float* max_radii2D, void* stream) {
+    return guarded([&]() -> int {
+        if (P < 0 || grad_stride < 2) throw GsError("gs_densify_stats: bad sizes");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_densify_stats(P, radii, grad_means2D, grad_stride, xyz_gradient_accum, denom, max_radii2D, s);
+        stage_check(false, s, "densify_stats");
+        return 0;
+    });
+}
+
 int gs_set_tuning(const char* key, int value) {
     if (!key) return -1;
     if (std::strcmp(key, "fwd_variant") == 0) {

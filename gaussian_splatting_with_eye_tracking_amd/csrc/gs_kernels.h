@@ -123,5 +123,11 @@ void radix_sort_pairs_u32(int n, const uint32_t* keys_in, uint32_t* keys_out, co
 size_t l1_ssim_workspace_bytes(int C, int H, int W);
 void launch_l1_ssim(const float* img, const float* gt, int C, int H, int W, float lambda, float* grad, float* out3,
                     float* workspace, hipStream_t s);
+// torch.optim.Adam step over a flat buffer with per-segment learning rates.
+void launch_adam(float* p, const float* g, float* m, float* v, long long N, int nseg, const long long* seg_end,
+                 const double* lr, const long long* step, double beta1, double beta2, double eps, hipStream_t s);
+// train.py:111-113 densification statistics for the visible Gaussians.
+void launch_densify_stats(int P, const int* radii, const float* grad_means2D, int g_stride, float* accum,
+                          float* denom, float* max_radii, hipStream_t s);
 
 }  // namespace gsamd

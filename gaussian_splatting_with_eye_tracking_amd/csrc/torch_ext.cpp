@@ -20,6 +20,7 @@
 
 #include <string>
 #include <tuple>
+#include <vector>
 
 #include "gsplat_amd.h"
 
@@ -307,6 +308,45 @@ std::tuple<Tensor, Tensor> L1SsimLoss(const Tensor& image, const Tensor& gt, dou
     return std::make_tuple(out3, grad);
 }
 
+// Fused Adam over flat buffers: seg_end / lr per segment (host lists).
+void AdamStep(Tensor& params, const Tensor& grads, Tensor& exp_avg, Tensor& exp_avg_sq,
+              const std::vector<int64_t>& seg_end, const std::vector<double>& lr, const std::vector<int64_t>& step, double beta1,
+              double beta2, double eps) {
+    for (const Tensor* t : std::initializer_list<const Tensor*>{&params, &grads, &exp_avg, &exp_avg_sq}) {
+        require_device(*t, "adam buffer");
+        TORCH_CHECK(t->is_contiguous() && t->numel() == params.numel(), "adam buffers: contiguous, same size");
+    }
+    TORCH_CHECK(seg_end.size() == lr.size() && step.size() == lr.size() && !seg_end.empty() && seg_end.back() == params.numel(),
+                "adam segments must cover the buffer");
+    const at::OptionalDeviceGuard guard(device_of(params));
+    std::vector<long long> ends(seg_end.begin(), seg_end.end()), steps(step.begin(), step.end());
+    check(gs_adam_step(params.data_ptr<float>(), grads.data_ptr<float>(), exp_avg.data_ptr<float>(),
+                       exp_avg_sq.data_ptr<float>(), params.numel(), (int)ends.size(), ends.data(), lr.data(), steps.data(),
+                       beta1, beta2, eps, stream_of(params)),
+          "adam_step");
+}
+
+// train.py:111-113: in-place statistics update (accum / denom [P, 1], max_radii [P]).
+void DensifyStats(const Tensor& radii, const Tensor& grad_means2D, Tensor& accum, Tensor& denom, Tensor& max_radii) {
+    const int64_t P = radii.size(0);
+    TORCH_CHECK(radii.is_cuda() && radii.scalar_type() == torch::kInt32 && radii.is_contiguous(),
+                "radii: int32 contiguous HIP device tensor");
+    require_device(grad_means2D, "grad_means2D");
+    TORCH_CHECK(grad_means2D.dim() == 2 && grad_means2D.size(0) == P && grad_means2D.size(1) >= 2 &&
+                    grad_means2D.stride(1) == 1 && grad_means2D.scalar_type() == torch::kFloat32,
+                "grad_means2D: [P, >=2] f32 rows");
+    for (const Tensor* t : std::initializer_list<const Tensor*>{&accum, &denom, &max_radii}) {
+        require_device(*t, "densification statistic");
+        TORCH_CHECK(t->numel() == P && t->is_contiguous() && t->scalar_type() == torch::kFloat32,
+                    "densification statistics: P contiguous f32");
+    }
+    const at::OptionalDeviceGuard guard(device_of(radii));
+    check(gs_densify_stats((int)P, radii.data_ptr<int>(), grad_means2D.data_ptr<float>(), (int)grad_means2D.stride(0),
+                           accum.data_ptr<float>(), denom.data_ptr<float>(), max_radii.data_ptr<float>(),
+                           stream_of(radii)),
+          "densify_stats");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "MI355X (gfx950) Gaussian rasterizer -- PyTorch binding over include/gsplat_amd.h";
     m.def("rasterize_gaussians", &RasterizeGaussians);
@@ -316,6 +356,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("distCUDA2", &DistCUDA2);
     m.def("parse_buffers", &ParseBuffers);
     m.def("l1_ssim_loss", &L1SsimLoss);
+    m.def("adam_step", &AdamStep);
+    m.def("densify_stats", &DensifyStats);
     m.def("abi_version", []() { return gs_abi_version(); });
     m.def("profile_enable", [](bool on) { gs_profile_enable(on ? 1 : 0); });
     m.def("profile_read", &ProfileRead, py::arg("reset") = true);

@@ -118,6 +118,24 @@ int gs_simple_knn(int P, const float* points, float* mean_dists, gs_buffer scrat
 int gs_l1_ssim_loss(const float* image, const float* gt, int C, int H, int W, float lambda_dssim, float* grad,
                     float* out3, gs_buffer workspace, void* stream);
 
+/* One torch.optim.Adam step (scene/gaussian_model.py:154-163: per-group
+ * learning rates, betas (0.9, 0.999), eps 1e-15) over a flat f32 buffer of n
+ * parameters split into nseg <= 8 segments [seg_end[i-1], seg_end[i]) with
+ * learning rate lr[i] and 1-based step count step[i] after this update
+ * (0 = the segment has no gradient this iteration and is left untouched, as
+ * torch skips a parameter whose .grad is None).  Element-wise in torch's
+ * operation order; one pass over p, g, m, v. */
+int gs_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, long long n, int nseg,
+                 const long long* seg_end, const double* lr, const long long* step, double beta1, double beta2, double eps,
+                 void* stream);
+
+/* Densification statistics of train.py:111-113 and
+ * scene/gaussian_model.py:405-407 for the Gaussians with radii > 0:
+ * max_radii2D = max(max_radii2D, radii), xyz_gradient_accum +=
+ * ||grad_means2D[:2]|| (rows of grad_stride floats), denom += 1. */
+int gs_densify_stats(int P, const int* radii, const float* grad_means2D, int grad_stride, float* xyz_gradient_accum,
+                     float* denom, float* max_radii2D, void* stream);
+
 /* ------------------------------------------------ parity / debug accessors
  * The reference exposes its internal buffers only in the AMR-debug variant
  * (ParseBuffers, amr-debug/rasterize_points.cu:37-61).  These views let the
