@@ -454,6 +454,35 @@ int gs_densify_stats(int P, const int* radii, const float* grad_means2D, int gra
     });
 }
 
+int gs_activate_gaussians(int P, int M, const float* features_dc, const float* features_rest, const float* opacity_raw,
+                          const float* scaling_raw, const float* rotation_raw, float* shs, float* opacities,
+                          float* scales, float* rotations, void* stream) {
+    return guarded([&]() -> int {
+        if (P < 0 || M < 1 || M > 16) throw GsError("gs_activate_gaussians: bad sizes");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_activate(P, M, features_dc, features_rest, opacity_raw, scaling_raw, rotation_raw, shs, opacities,
+                        scales, rotations, s);
+        stage_check(false, s, "activate");
+        return 0;
+    });
+}
+
+int gs_activation_backward(int P, int M, int accumulate, const float* dL_dshs, const float* dL_dopacities,
+                           const float* dL_dscales, const float* dL_drotations, const float* dL_dmeans3D,
+                           const float* opacity_raw, const float* scaling_raw, const float* rotation_raw,
+                           float* grad_xyz, float* grad_features_dc, float* grad_features_rest, float* grad_opacity,
+                           float* grad_scaling, float* grad_rotation, void* stream) {
+    return guarded([&]() -> int {
+        if (P < 0 || M < 1 || M > 16) throw GsError("gs_activation_backward: bad sizes");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_activation_backward(P, M, accumulate, dL_dshs, dL_dopacities, dL_dscales, dL_drotations, dL_dmeans3D,
+                                   opacity_raw, scaling_raw, rotation_raw, grad_xyz, grad_features_dc,
+                                   grad_features_rest, grad_opacity, grad_scaling, grad_rotation, s);
+        stage_check(false, s, "activation_backward");
+        return 0;
+    });
+}
+
 int gs_set_tuning(const char* key, int value) {
     if (!key) return -1;
     if (std::strcmp(key, "fwd_variant") == 0) {

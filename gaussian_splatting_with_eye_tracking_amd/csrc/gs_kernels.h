@@ -129,5 +129,14 @@ void launch_adam(float* p, const float* g, float* m, float* v, long long N, int 
 // train.py:111-113 densification statistics for the visible Gaussians.
 void launch_densify_stats(int P, const int* radii, const float* grad_means2D, int g_stride, float* accum,
                           float* denom, float* max_radii, hipStream_t s);
+// scene/gaussian_model.py:93-113 activations from raw segments, and their backward.
+void launch_activate(int P, int M, const float* dc, const float* rest, const float* opacity_raw,
+                     const float* scaling_raw, const float* rotation_raw, float* shs, float* opacity, float* scales,
+                     float* rotations, hipStream_t s);
+void launch_activation_backward(int P, int M, int accumulate, const float* d_shs, const float* d_opac,
+                                const float* d_scales, const float* d_rot, const float* d_means3D,
+                                const float* opacity_raw, const float* scaling_raw, const float* rotation_raw,
+                                float* g_xyz, float* g_dc, float* g_rest, float* g_opacity, float* g_scaling,
+                                float* g_rotation, hipStream_t s);
 
 }  // namespace gsamd

@@ -347,6 +347,60 @@ void DensifyStats(const Tensor& radii, const Tensor& grad_means2D, Tensor& accum
           "densify_stats");
 }
 
+void check_f32_rows(const Tensor& t, int64_t P, int64_t n, const char* name) {
+    require_device(t, name);
+    TORCH_CHECK(t.is_contiguous() && t.numel() == P * n, name, ": contiguous, ", n, " floats per Gaussian");
+}
+
+// scene/gaussian_model.py:93-113: raw groups -> rasterizer inputs (outputs preallocated).
+void Activate(const Tensor& dc, const Tensor& rest, const Tensor& opacity_raw, const Tensor& scaling_raw,
+              const Tensor& rotation_raw, Tensor& shs, Tensor& opacities, Tensor& scales, Tensor& rotations) {
+    const int64_t P = dc.size(0);
+    const int64_t M = rest.numel() / std::max<int64_t>(P, 1) / 3 + 1;
+    check_f32_rows(dc, P, 3, "features_dc");
+    check_f32_rows(rest, P, 3 * (M - 1), "features_rest");
+    check_f32_rows(opacity_raw, P, 1, "opacity");
+    check_f32_rows(scaling_raw, P, 3, "scaling");
+    check_f32_rows(rotation_raw, P, 4, "rotation");
+    check_f32_rows(shs, P, 3 * M, "shs");
+    check_f32_rows(opacities, P, 1, "opacities");
+    check_f32_rows(scales, P, 3, "scales");
+    check_f32_rows(rotations, P, 4, "rotations");
+    const at::OptionalDeviceGuard guard(device_of(dc));
+    check(gs_activate_gaussians((int)P, (int)M, fptr(dc), fptr(rest), fptr(opacity_raw), fptr(scaling_raw),
+                                fptr(rotation_raw), fptr_mut(shs), fptr_mut(opacities), fptr_mut(scales),
+                                fptr_mut(rotations), stream_of(dc)),
+          "activate");
+}
+
+void ActivationBackward(const Tensor& d_shs, const Tensor& d_opac, const Tensor& d_scales, const Tensor& d_rot,
+                        const Tensor& d_means3D, const Tensor& opacity_raw, const Tensor& scaling_raw,
+                        const Tensor& rotation_raw, Tensor& g_xyz, Tensor& g_dc, Tensor& g_rest, Tensor& g_opacity,
+                        Tensor& g_scaling, Tensor& g_rotation, bool accumulate) {
+    const int64_t P = d_means3D.size(0);
+    const int64_t M = d_shs.numel() / std::max<int64_t>(P, 1) / 3;
+    check_f32_rows(d_shs, P, 3 * M, "dL_dshs");
+    check_f32_rows(d_opac, P, 1, "dL_dopacities");
+    check_f32_rows(d_scales, P, 3, "dL_dscales");
+    check_f32_rows(d_rot, P, 4, "dL_drotations");
+    check_f32_rows(d_means3D, P, 3, "dL_dmeans3D");
+    check_f32_rows(opacity_raw, P, 1, "opacity");
+    check_f32_rows(scaling_raw, P, 3, "scaling");
+    check_f32_rows(rotation_raw, P, 4, "rotation");
+    check_f32_rows(g_xyz, P, 3, "grad xyz");
+    check_f32_rows(g_dc, P, 3, "grad features_dc");
+    check_f32_rows(g_rest, P, 3 * (M - 1), "grad features_rest");
+    check_f32_rows(g_opacity, P, 1, "grad opacity");
+    check_f32_rows(g_scaling, P, 3, "grad scaling");
+    check_f32_rows(g_rotation, P, 4, "grad rotation");
+    const at::OptionalDeviceGuard guard(device_of(d_shs));
+    check(gs_activation_backward((int)P, (int)M, accumulate ? 1 : 0, fptr(d_shs), fptr(d_opac), fptr(d_scales),
+                                 fptr(d_rot), fptr(d_means3D), fptr(opacity_raw), fptr(scaling_raw),
+                                 fptr(rotation_raw), fptr_mut(g_xyz), fptr_mut(g_dc), fptr_mut(g_rest),
+                                 fptr_mut(g_opacity), fptr_mut(g_scaling), fptr_mut(g_rotation), stream_of(d_shs)),
+          "activation_backward");
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "MI355X (gfx950) Gaussian rasterizer -- PyTorch binding over include/gsplat_amd.h";
     m.def("rasterize_gaussians", &RasterizeGaussians);
@@ -358,6 +412,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("l1_ssim_loss", &L1SsimLoss);
     m.def("adam_step", &AdamStep);
     m.def("densify_stats", &DensifyStats);
+    m.def("activate", &Activate);
+    m.def("activation_backward", &ActivationBackward);
     m.def("abi_version", []() { return gs_abi_version(); });
     m.def("profile_enable", [](bool on) { gs_profile_enable(on ? 1 : 0); });
     m.def("profile_read", &ProfileRead, py::arg("reset") = true);

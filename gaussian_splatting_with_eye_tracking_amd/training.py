@@ -161,6 +161,9 @@ class FlatGaussianModel:
             self.param[g] = p
             self._gview[g] = self.grads[off:end].view(shape)
             off = end
+        M = (self.max_sh_degree + 1) ** 2
+        self._act = {"shs": torch.empty((P, M, 3), device=dev), "opacities": torch.empty((P, 1), device=dev),
+                     "scales": torch.empty((P, 3), device=dev), "rotations": torch.empty((P, 4), device=dev)}
         self.xyz_gradient_accum = torch.zeros((P, 1), device=dev)
         self.denom = torch.zeros((P, 1), device=dev)
         self.max_radii2D = torch.zeros((P,), device=dev)
@@ -203,13 +206,22 @@ class FlatGaussianModel:
         return self.lr["xyz"]
 
     # --------------------------------------------------------- optimiser ---
-    def zero_grad(self) -> None:
+    def zero_grad(self, memset: bool = True) -> None:
         """optimizer.zero_grad(set_to_none=True): the buffer is zeroed and
-        re-attached (autograd accumulates into an existing .grad in place)."""
-        self.grads.zero_()
+        re-attached (autograd accumulates into an existing .grad in place).
+        memset=False defers the zeroing: the fused backward overwrites every
+        gradient, and the paths that accumulate zero a stale buffer first."""
+        if memset:
+            self.grads.zero_()
+        self._grads_stale = not memset
         for g in GROUPS:
             self.param[g].grad = self._gview[g]
             self.has_grad[g] = False
+
+    def _fresh_grads(self) -> None:
+        if self._grads_stale:
+            self.grads.zero_()
+            self._grads_stale = False
 
     def mark_backward(self) -> None:
         """Every group reaches the loss through the renderer, so after a
@@ -325,6 +337,7 @@ class FlatGaussianModel:
     def render(self, settings: GaussianRasterizationSettings):
         """gaussian_renderer/__init__.py:18-114 (default pipe: SH and the 3D
         covariance evaluated by the rasterizer)."""
+        self._fresh_grads()
         screenspace_points = torch.zeros_like(self.param["xyz"], requires_grad=True) + 0
         screenspace_points.retain_grad()
         s = settings._replace(sh_degree=self.active_sh_degree)
@@ -333,6 +346,43 @@ class FlatGaussianModel:
             scales=self.get_scaling, rotations=self.get_rotation)
         return {"render": image, "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
                 "radii": radii}
+
+
+    def render_and_backward(self, settings: GaussianRasterizationSettings, gt_image: torch.Tensor,
+                            lambda_dssim: float, accumulate: bool = False):
+        """render -> L1 + D-SSIM -> backward without autograd: the activation
+        kernel fills the rasterizer inputs from the raw segments, the fused
+        loss kernel hands dL/dimage straight to the rasterizer backward, and
+        the activation backward writes the raw-parameter gradients into the
+        flat gradient buffer (gaussian_renderer/__init__.py:18-114 +
+        train.py:89-93 + loss.backward()).  Same results as render() +
+        l1_ssim_loss + autograd (tests/test_gpu_training.py)."""
+        if accumulate:
+            self._fresh_grads()
+        s = settings._replace(sh_degree=self.active_sh_degree)
+        raw = {g: self.group_view(self.params, g) for g in GROUPS}
+        a = self._act
+        _C.activate(raw["f_dc"], raw["f_rest"], raw["opacity"], raw["scaling"], raw["rotation"], a["shs"],
+                    a["opacities"], a["scales"], a["rotations"])
+        e = torch.empty(0, device=self.device)
+        xyz = raw["xyz"]
+        num_rendered, color, radii, geom, binning, img = _C.rasterize_gaussians(
+            s.bg, xyz, e, a["opacities"], a["scales"], a["rotations"], s.scale_modifier, e, s.viewmatrix,
+            s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, a["shs"], s.sh_degree, s.campos,
+            s.prefiltered, s.debug)
+        out3, d_image = _C.l1_ssim_loss(color, gt_image, float(lambda_dssim))
+        (d_means2D, _d_colors, d_opac, d_means3D, _d_cov3D, d_shs, d_scales, d_rot) = _C.rasterize_gaussians_backward(
+            s.bg, xyz, radii, e, a["scales"], a["rotations"], s.scale_modifier, e, s.viewmatrix, s.projmatrix,
+            s.tanfovx, s.tanfovy, d_image, a["shs"], s.sh_degree, s.campos, geom, num_rendered, binning, img,
+            s.debug)
+        gv = {g: self.group_view(self.grads, g) for g in GROUPS}
+        _C.activation_backward(d_shs, d_opac, d_scales, d_rot, d_means3D, raw["opacity"], raw["scaling"],
+                               raw["rotation"], gv["xyz"], gv["f_dc"], gv["f_rest"], gv["opacity"], gv["scaling"],
+                               gv["rotation"], bool(accumulate))
+        self._grads_stale = False
+        self.mark_backward()
+        pkg = {"render": color, "viewspace_grad": d_means2D, "visibility_filter": radii > 0, "radii": radii}
+        return pkg, {"loss": out3[0], "l1": out3[1], "ssim": out3[2]}
 
 
 def allreduce_training_grads(model: FlatGaussianModel, group=None) -> None:
@@ -353,30 +403,38 @@ def reduce_densification_stats(model: FlatGaussianModel, group=None) -> None:
 
 
 def forward_backward(model: FlatGaussianModel, iteration: int, settings: GaussianRasterizationSettings,
-                     gt_image: torch.Tensor, group=None):
+                     gt_image: torch.Tensor, group=None, fused: bool = True):
     """train.py:76-93 + the backward: learning-rate schedule, SH degree step,
     render, fused L1 + D-SSIM loss, backward into the flat gradient buffer,
-    all-reduce over the data-parallel ranks.  Returns (render package, loss
-    terms as device tensors)."""
+    all-reduce over the data-parallel ranks.  fused=True runs the
+    autograd-free native sequence (render_and_backward); fused=False the
+    reference-shaped one (torch activations + the drop-in autograd
+    rasterizer + autograd).  Returns (render package, loss terms as device
+    tensors); pkg["viewspace_grad"] is dL/dmeans2D."""
     model.update_learning_rate(iteration)
     if iteration % 1000 == 0:
         model.oneupSHdegree()
-    pkg = model.render(settings)
-    loss, l1, ssim = l1_ssim_loss_terms(pkg["render"], gt_image, model.opt.lambda_dssim)
-    loss.backward()
-    model.mark_backward()
+    if fused:
+        pkg, terms = model.render_and_backward(settings, gt_image, model.opt.lambda_dssim)
+    else:
+        pkg = model.render(settings)
+        loss, l1, ssim = l1_ssim_loss_terms(pkg["render"], gt_image, model.opt.lambda_dssim)
+        loss.backward()
+        model.mark_backward()
+        pkg["viewspace_grad"] = pkg["viewspace_points"].grad
+        terms = {"loss": loss.detach(), "l1": l1, "ssim": ssim}
     allreduce_training_grads(model, group)
-    return pkg, {"loss": loss.detach(), "l1": l1, "ssim": ssim}
+    return pkg, terms
 
 
 @torch.no_grad()
 def post_backward(model: FlatGaussianModel, iteration: int, pkg, scene_extent: float, white_background: bool = False,
-                  group=None) -> None:
+                  group=None, fused: bool = False) -> None:
     """train.py:108-125: densification statistics, densify / prune / opacity
     reset on the reference's schedule, Adam, zero_grad."""
     o = model.opt
     if iteration < o.densify_until_iter:
-        model.add_densification_stats(pkg["viewspace_points"].grad, pkg["radii"])
+        model.add_densification_stats(pkg["viewspace_grad"], pkg["radii"])
         if iteration > o.densify_from_iter and iteration % o.densification_interval == 0:
             reduce_densification_stats(model, group)
             size_threshold = 20 if iteration > o.opacity_reset_interval else None
@@ -385,14 +443,14 @@ def post_backward(model: FlatGaussianModel, iteration: int, pkg, scene_extent: f
             model.reset_opacity()
     if iteration < o.iterations:
         model.optimizer_step()
-        model.zero_grad()
+        model.zero_grad(memset=not fused)
 
 
 def training_iteration(model: FlatGaussianModel, iteration: int, settings: GaussianRasterizationSettings,
                        gt_image: torch.Tensor, scene_extent: float, white_background: bool = False,
-                       group=None) -> Dict[str, torch.Tensor]:
+                       group=None, fused: bool = True) -> Dict[str, torch.Tensor]:
     """One iteration of train.py:67-125 (minus logging / saving / the GUI).
     Returns the loss terms as device tensors (no host sync)."""
-    pkg, terms = forward_backward(model, iteration, settings, gt_image, group)
-    post_backward(model, iteration, pkg, scene_extent, white_background, group)
+    pkg, terms = forward_backward(model, iteration, settings, gt_image, group, fused)
+    post_backward(model, iteration, pkg, scene_extent, white_background, group, fused)
     return terms

@@ -136,6 +136,22 @@ int gs_adam_step(float* params, const float* grads, float* exp_avg, float* exp_a
 int gs_densify_stats(int P, const int* radii, const float* grad_means2D, int grad_stride, float* xyz_gradient_accum,
                      float* denom, float* max_radii2D, void* stream);
 
+/* The rasterizer inputs from the raw parameters (scene/gaussian_model.py:
+ * 93-113): shs [P][M][3] = cat(features_dc [P][1][3], features_rest
+ * [P][M-1][3]), opacities = sigmoid(opacity_raw), scales = exp(scaling_raw),
+ * rotations = rotation_raw / max(|rotation_raw|, 1e-12). */
+int gs_activate_gaussians(int P, int M, const float* features_dc, const float* features_rest, const float* opacity_raw,
+                          const float* scaling_raw, const float* rotation_raw, float* shs, float* opacities,
+                          float* scales, float* rotations, void* stream);
+/* Backward of gs_activate_gaussians (the gradients torch autograd would give
+ * the raw parameters) plus dL/dxyz = dL/dmeans3D, stored into (accumulate =
+ * 0) or added to (accumulate = 1) the raw-parameter gradient arrays. */
+int gs_activation_backward(int P, int M, int accumulate, const float* dL_dshs, const float* dL_dopacities,
+                           const float* dL_dscales, const float* dL_drotations, const float* dL_dmeans3D,
+                           const float* opacity_raw, const float* scaling_raw, const float* rotation_raw,
+                           float* grad_xyz, float* grad_features_dc, float* grad_features_rest, float* grad_opacity,
+                           float* grad_scaling, float* grad_rotation, void* stream);
+
 /* ------------------------------------------------ parity / debug accessors
  * The reference exposes its internal buffers only in the AMR-debug variant
  * (ParseBuffers, amr-debug/rasterize_points.cu:37-61).  These views let the

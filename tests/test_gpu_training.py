@@ -138,8 +138,9 @@ def test_densify_stats_kernel_matches_reference():
     torch.testing.assert_close(m.max_radii2D, o.max_radii2D, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("iteration", [2999, 3000, 3100, 4000])
-def test_post_backward_lockstep_with_reference(iteration):
+def test_post_backward_lockstep_with_reference(iteration, fused):
     """train.py:108-125 at a plain step (2999), densify + opacity reset
     (3000), densify with the screen-size prune (3100) and a step after
     densification (4000, opacity step count lagging)."""
@@ -156,10 +157,10 @@ def test_post_backward_lockstep_with_reference(iteration):
     m.xyz_gradient_accum.copy_(torch.rand(m.P, 1, generator=gen) * 0.002)
     m.denom.copy_(torch.randint(0, 8, (m.P, 1), generator=gen).float())
     gt = torch.rand(3, cam.image_height, cam.image_width, generator=gen).cuda()
-    pkg, terms = T.forward_backward(m, iteration, s, gt)
+    pkg, terms = T.forward_backward(m, iteration, s, gt, fused=fused)
     assert math.isfinite(float(terms["loss"]))
     o = oracle_from(m)
-    g2d = pkg["viewspace_points"].grad.clone()
+    g2d = pkg["viewspace_grad"].clone()
     radii = pkg["radii"].clone()
     torch.manual_seed(7)
     T.post_backward(m, iteration, pkg, scene_extent=5.0)
@@ -168,6 +169,36 @@ def test_post_backward_lockstep_with_reference(iteration):
     if iteration in (3000, 3100):
         assert m.P != 3000
     assert_close_state(m, o)
+
+
+@pytest.mark.parametrize("active_sh", [0, 3])
+def test_fused_path_matches_autograd_path(active_sh):
+    """render_and_backward (activation kernels, fused loss gradient straight
+    into the rasterizer backward, no autograd) against torch activations +
+    the drop-in autograd rasterizer + l1_ssim_loss + loss.backward(): image
+    and radii identical, raw-parameter gradients within 1e-5 relative."""
+    T = _T()
+    sc, cam, s = _render_case(P=5000, W=160, H=120, seed=9)
+    raw = raw_from_scene(sc)
+    raw["rotation"] = raw["rotation"] * torch.linspace(0.5, 2.0, 5000, device="cuda")[:, None]  # unnormalised
+    gt = torch.rand(3, 120, 160, device="cuda", generator=torch.Generator("cuda").manual_seed(1))
+    out = []
+    for fused in (True, False):
+        m = T.FlatGaussianModel(raw, 3, spatial_lr_scale=5.0)
+        m.active_sh_degree = active_sh
+        pkg, terms = T.forward_backward(m, 1, s, gt, fused=fused)
+        out.append((m, pkg, terms))
+    (mf, pf, tf), (ma, pa, ta) = out
+    torch.testing.assert_close(pf["render"], pa["render"].detach(), rtol=0, atol=1e-6)
+    assert torch.equal(pf["radii"], pa["radii"])
+    assert abs(float(tf["loss"]) - float(ta["loss"])) < 1e-6
+    torch.testing.assert_close(pf["viewspace_grad"], pa["viewspace_grad"], rtol=1e-5, atol=1e-9)
+    for g in T.GROUPS:
+        a, b = mf.group_view(mf.grads, g), ma.group_view(ma.grads, g)
+        rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
+        assert rel < 1e-5, (g, rel)
+        if g == "f_rest" and active_sh == 0:
+            assert float(a.abs().max()) == 0.0
 
 
 def test_training_run_fits_a_target():

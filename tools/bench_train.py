@@ -71,38 +71,40 @@ def main():
         iteration()
     t_iter = timed(iteration, args.reps)
 
-    # phases
-    ev = {}
+    # the reference-shaped sequence: torch activations + drop-in autograd rasterizer + autograd
+    def iteration_autograd():
+        it[0] += 1
+        T.training_iteration(m, it[0], st, gt, scene_extent=5.0, fused=False)
 
+    for _ in range(2):
+        iteration_autograd()
+    t_iter_autograd = timed(iteration_autograd, args.reps)
+
+    # phases of the fused sequence
     def phases():
         it[0] += 1
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         e[0].record()
         m.update_learning_rate(it[0])
-        pkg = m.render(st)
+        pkg, _ = m.render_and_backward(st, gt, 0.2)
         e[1].record()
-        loss, _, _ = T.l1_ssim_loss_terms(pkg["render"], gt, 0.2)
-        e[2].record()
-        loss.backward()
-        m.mark_backward()
-        e[3].record()
         with torch.no_grad():
-            m.add_densification_stats(pkg["viewspace_points"].grad, pkg["radii"])
-            e[4].record()
+            m.add_densification_stats(pkg["viewspace_grad"], pkg["radii"])
+            e[2].record()
             m.optimizer_step()
-            m.zero_grad()
-        e[5].record()
+            m.zero_grad(memset=False)
+        e[3].record()
         return e
 
     for _ in range(2):
         phases()
-    acc = np.zeros(5)
+    acc = np.zeros(3)
     for _ in range(args.reps):
         e = phases()
         torch.cuda.synchronize()
-        acc += [e[i].elapsed_time(e[i + 1]) for i in range(5)]
+        acc += [e[i].elapsed_time(e[i + 1]) for i in range(3)]
     acc /= args.reps
-    names = ["render_fwd+activations", "loss_fused", "backward", "densify_stats", "adam+zero_grad"]
+    names = ["activate+render+loss+backward", "densify_stats", "adam+zero_grad"]
 
     # the reference's pieces on the same GPU
     o_params = {k: torch.nn.Parameter(m.param[k].detach().clone()) for k in T.GROUPS}
@@ -151,8 +153,9 @@ def main():
 
     out = {
         "workload": f"training iteration (train.py:67-125), {args.P} Gaussians, {args.W}x{args.H}, SH3, "
-                    "no densify step", "iteration_ms": round(t_iter, 4),
+                    "no densify step; fused native sequence (autograd-path time alongside)", "iteration_ms": round(t_iter, 4),
         "iterations_per_s": round(1000.0 / t_iter, 1),
+        "iteration_ms_autograd_path": round(t_iter_autograd, 4),
         "phases_ms": {k: round(float(v), 4) for k, v in zip(names, acc)},
         "adam": {"fused_ms": round(t_fused_adam, 4), "torch_optim_adam_ms": round(t_torch_adam, 4),
                  "speedup": round(t_torch_adam / t_fused_adam, 2), "params": n,
