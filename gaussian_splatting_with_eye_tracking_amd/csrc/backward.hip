@@ -46,11 +46,15 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     float* __restrict__ grad_accum, int cull, const uint32_t* __restrict__ order, int gx) {
 #pragma clang fp contract(fast)
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
-    __shared__ uint32_t s_id[kB];
+    __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
     __shared__ float2 s_xy[kB];
     __shared__ float4 s_co[kB];
     __shared__ float4 s_rgb[kB];
-    __shared__ float s_acc[kB * kAccRow];
+    // per-Gaussian sums: one wave parks its two half-wave partials (summed by
+    // the flush; 4 row partials would double the LDS footprint and cost
+    // workgroups per CU); several waves add into one row with LDS atomics
+    constexpr int kRowsPerG = kWaves == 1 ? 2 : 1;
+    __shared__ float s_acc[kB * kRowsPerG * kAccRow];
     __shared__ uint64_t s_bal[4 * kWaves];
 
     const int tid = threadIdx.x;
@@ -66,7 +70,10 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, 1);
     const size_t plane = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
-    float T[kPPL], nbg[kPPL], dpx[kPPL][3], acc_rec[kPPL][3], last_col[kPPL][3], last_alpha[kPPL];
+    // acc_rec . dL_dpix and last_colour . dL_dpix are all the reference's
+    // accum_rec / last_color recurrences (backward.cu:500-507) feed into
+    // dL_dalpha, so each pixel carries those two scalars instead of 2 x 3.
+    float T[kPPL], nbg[kPPL], dpx[kPPL][3], acc_dot[kPPL], last_dot[kPPL], last_alpha[kPPL];
     uint32_t last[kPPL];
     uint32_t wave_last = 0;
 #pragma unroll
@@ -77,11 +84,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         last[k] = px.inside[k] ? n_contrib[pid] : 0u;
         wave_last = max(wave_last, last[k]);
 #pragma unroll
-        for (int c = 0; c < 3; c++) {
-            dpx[k][c] = px.inside[k] ? dL_dpixels[c * plane + pid] : 0.f;
-            acc_rec[k][c] = 0.f;
-            last_col[k][c] = 0.f;
-        }
+        for (int c = 0; c < 3; c++) dpx[k][c] = px.inside[k] ? dL_dpixels[c * plane + pid] : 0.f;
+        acc_dot[k] = 0.f;
+        last_dot[k] = 0.f;
         last_alpha[k] = 0.f;
         // (-T_final / (1 - alpha)) * bg.dL_dpix = nbg * 1/(1 - alpha)
         nbg[k] = -Tf * (bg0 * dpx[k][0] + bg1 * dpx[k][1] + bg2 * dpx[k][2]);
@@ -101,23 +106,48 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     }
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
+    // The per-pixel terms are summed without their constant factors; the
+    // flush applies them: g3 * -ddelx_dx, g4 * -ddely_dy, g5..g7 * -0.5.
+    const int comp = lane & 15;
+    const float comp_scale = comp == 3 ? -ddelx_dx : comp == 4 ? -ddely_dy : (comp >= 5 && comp <= 7) ? -0.5f : 1.0f;
 
-    for (int top = m; top > 0; top -= kB) {  // entries [top-cnt, top), back to front
+    // Software pipeline over the batches (vector-memory counters retire in
+    // issue order, so issue order decides what each wait covers): the next
+    // batch's point_list ids are loaded while this batch is blended, its
+    // Gaussian records are gathered before this batch's flush atomics are
+    // issued, so neither the id round trip nor the atomics' completion is
+    // waited for at the top of the next batch.
+    uint32_t nid = 0;
+    float2 nxy = make_float2(0.f, 0.f);
+    float4 nco = make_float4(0.f, 0.f, 0.f, 0.f);
+    float nrgb[3] = {0.f, 0.f, 0.f};
+    if (tid < min(kB, m)) {
+        nid = point_list[range.x + m - 1 - tid];
+        nxy = means2D[nid];
+        nco = conic_opacity[nid];
+        nrgb[0] = colors[3 * nid]; nrgb[1] = colors[3 * nid + 1]; nrgb[2] = colors[3 * nid + 2];
+        s_id[0][tid] = nid;
+    }
+    int par = 0;
+    for (int top = m; top > 0; top -= kB, par ^= 1) {  // entries [top-cnt, top), back to front
         const int cnt = min(kB, top);
         __syncthreads();
         uint32_t gm = 0;
         if (tid < cnt) {
-            const uint32_t id = point_list[range.x + top - 1 - tid];
-            const float2 xy = means2D[id];
-            const float4 co = conic_opacity[id];
-            s_id[tid] = id;
+            const float2 xy = nxy;
+            const float4 co = nco;
             s_xy[tid] = xy;
             s_co[tid] = co;
-            s_rgb[tid] = make_float4(colors[3 * id], colors[3 * id + 1], colors[3 * id + 2], 0.f);
+            s_rgb[tid] = make_float4(nrgb[0], nrgb[1], nrgb[2], 0.f);
             gm = cull ? splat_group_mask(xy, co, (float)ox, (float)oy, 1.0f) : 0xfu;
         }
+        const int ntop = top - kB;  // the next batch: entries [ntop - ncnt, ntop)
+        const bool has_next = ntop > 0 && tid < min(kB, ntop);
+        if (has_next) nid = point_list[range.x + ntop - 1 - tid];
         publish_group_masks<kWaves>(gm, s_bal);
-        for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
+        if (kWaves > 1)
+            for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
+        uint64_t written = 0;  // kWaves == 1: batch slots whose partial rows were stored
         __syncthreads();
         // first batch slot this wave needs: contributor = top-1-j < wave_last
         // (readfirstlane: wave_last is uniform after the xor-shuffle max, but the
@@ -145,7 +175,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             const uint32_t contributor = (uint32_t)(top - 1 - j);
             const float2 xy = s_xy[j];
             const float4 co = s_co[j];
+            const float4 cf = s_rgb[j];
             const float dx = xy.x - px.x;
+            const float dx_cx = dx * co.x, dx_cy = dx * co.y;
             float g[kNG];
 #pragma unroll
             for (int q = 0; q < kNG; q++) g[q] = 0.f;
@@ -167,36 +199,34 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
                 T[k] = T[k] * rinv;
                 const float dchannel_dcolor = alpha * T[k];
-                const float4 cf = s_rgb[j];
-                const float cc[3] = {cf.x, cf.y, cf.z};
-                float dL_dalpha = 0.0f;
-#pragma unroll
-                for (int ch = 0; ch < 3; ch++) {
-                    acc_rec[k][ch] = last_alpha[k] * last_col[k][ch] + (1.f - last_alpha[k]) * acc_rec[k][ch];
-                    last_col[k][ch] = cc[ch];
-                    dL_dalpha += (cc[ch] - acc_rec[k][ch]) * dpx[k][ch];
-                    g[ch] += dchannel_dcolor * dpx[k][ch];
-                }
-                dL_dalpha *= T[k];
+                // sum_ch (c - accum_rec) dL_dpix, with accum_rec . dL_dpix
+                // advanced by the reference's recurrence
+                const float c_dot = cf.x * dpx[k][0] + cf.y * dpx[k][1] + cf.z * dpx[k][2];
+                acc_dot[k] = last_alpha[k] * last_dot[k] + (1.f - last_alpha[k]) * acc_dot[k];
+                last_dot[k] = c_dot;
                 last_alpha[k] = alpha;
-                dL_dalpha += nbg[k] * rinv;
-                const float dL_dG = co.w * dL_dalpha;
-                const float gdx = G * dx;
-                const float gdy = G * dy;
-                g[3] += dL_dG * (-gdx * co.x - gdy * co.y) * ddelx_dx;
-                g[4] += dL_dG * (-gdy * co.z - gdx * co.y) * ddely_dy;
-                g[5] += -0.5f * gdx * dx * dL_dG;
-                g[6] += -0.5f * gdx * dy * dL_dG;
-                g[7] += -0.5f * gdy * dy * dL_dG;
+                const float dL_dalpha = (c_dot - acc_dot[k]) * T[k] + nbg[k] * rinv;
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) g[ch] += dchannel_dcolor * dpx[k][ch];
+                // dL_dG * G times the unscaled mean2D / conic factors
+                const float h = G * (co.w * dL_dalpha);
+                const float hdx = h * dx, hdy = h * dy;
+                g[3] += h * (dx_cx + dy * co.y);
+                g[4] += h * (dy * co.z + dx_cy);
+                g[5] += hdx * dx;
+                g[6] += hdx * dy;
+                g[7] += hdy * dy;
                 g[8] += G * dL_dalpha;
             }
             if (__ballot(any) != 0ull) {  // wave-uniform
-                if (kWaves == 1) {  // reduce the 9 sums into lane 63, park them
-                    dpp_sum9_lane63(g);
-                    if (lane == 63) {
+                if (kWaves == 1) {  // half-wave sums, parked by lanes 31 and 63
+                    dpp_sum9_halves(g);
+                    if ((lane & 31) == 31) {
+                        float* row = &s_acc[(j * 2 + (lane >> 5)) * kAccRow];
 #pragma unroll
-                        for (int q = 0; q < kNG; q++) s_acc[j * kAccRow + q] = g[q];
+                        for (int q = 0; q < kNG; q++) row[q] = g[q];
                     }
+                    written |= 1ull << j;
                 } else {  // 16-lane row sums; the 4 row leaders add them into LDS
                     dpp_sum9_rows(g);
                     if ((lane & 15) == 15) {
@@ -208,20 +238,38 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
           }
         }
         __syncthreads();
+        if (has_next) {  // gathers for the next batch, ahead of the flush atomics
+            s_id[par ^ 1][tid] = nid;
+            nxy = means2D[nid];
+            nco = conic_opacity[nid];
+            nrgb[0] = colors[3 * nid]; nrgb[1] = colors[3 * nid + 1]; nrgb[2] = colors[3 * nid + 2];
+        }
         // Flush: 16 lanes per Gaussian row, 4 rows per wave instruction
-        // (one 64-B memory-side atomic request per (tile, Gaussian)).
-        const int comp = lane & 15;
-        for (int r = (tid >> 4); r < cnt; r += 4 * kWaves) {
-            if (comp < kNG) {
-                const float v = s_acc[r * kAccRow + comp];
-                if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[r] * kGradRow + comp], v);
+        // (one 64-B memory-side atomic request per (tile, Gaussian)).  (A full
+        // unroll lets the scheduler hoist all 64 LDS reads: 163 VGPRs.)
+#pragma unroll 4
+        for (int i = 0; i < kB / (4 * kWaves); i++) {
+            const int r = (tid >> 4) + 4 * kWaves * i;
+            bool live = r < cnt && comp < kNG;
+            if (kWaves == 1) live = live && ((written >> (r & 63)) & 1ull);
+            if (live) {
+                float v;
+                if (kWaves == 1) {
+                    const float* rows = &s_acc[r * 2 * kAccRow + comp];
+                    v = (rows[0] + rows[kAccRow]) * comp_scale;
+                } else {
+                    v = s_acc[r * kAccRow + comp] * comp_scale;
+                }
+                if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[par][r] * kGradRow + comp], v);
             }
         }
     }
 }
 
 extern int g_cull;  // render.hip
-int g_bwd_variant = 0;  // 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave uncapped
+// 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave uncapped,
+// 4 / 5: 1 wave x 4 px with <= 102 / <= 85 VGPRs (5 / 6 waves per SIMD)
+int g_bwd_variant = 0;
 
 void set_backward_variant(int v) { g_bwd_variant = v; }
 
@@ -243,6 +291,8 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         case 1: GS_BWD_LAUNCH(2, 2, 4); break;
         case 2: GS_BWD_LAUNCH(1, 4, 4); break;
         case 3: GS_BWD_LAUNCH(4, 1, 1); break;
+        case 4: GS_BWD_LAUNCH(4, 1, 5); break;
+        case 5: GS_BWD_LAUNCH(4, 1, 6); break;
         default: GS_BWD_LAUNCH(4, 1, 4); break;
     }
 #undef GS_BWD_LAUNCH
