@@ -169,9 +169,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
               todo |= mk[k];
           }
           while (todo) {
-            const int bit = __builtin_ctzll(todo);
+            const int cbit = __builtin_ctzll(todo);
             todo &= todo - 1;
-            const int j = 64 * c + bit;
+            const int j = 64 * c + cbit;
             const uint32_t contributor = (uint32_t)(top - 1 - j);
             const float2 xy = s_xy[j];
             const float4 co = s_co[j];
@@ -184,9 +184,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             bool any = false;
 #pragma unroll
             for (int k = 0; k < kPPL; k++) {
-                if (!((mk[k] >> bit) & 1ull)) continue;  // wave-uniform: culled for this row group
+                if (!((mk[k] >> cbit) & 1ull)) continue;  // wave-uniform: culled for this row group
                 const float dy = xy.y - px.y[k];
-                const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                const float power = splat_power(dx, dy, co);  // the forward's bits
                 const float G = __expf(power);
                 const float alpha = fminf(0.99f, co.w * G);
                 // The reference's three per-pixel `continue`s (backward.cu:466-482)
@@ -267,8 +267,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
 }
 
 extern int g_cull;  // render.hip
-// 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave uncapped,
-// 4 / 5: 1 wave x 4 px with <= 102 / <= 85 VGPRs (5 / 6 waves per SIMD)
+// 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave uncapped
+// (1 wave x 4 px capped at 5 or 6 waves per SIMD spills: measured slower)
 int g_bwd_variant = 0;
 
 void set_backward_variant(int v) { g_bwd_variant = v; }
@@ -291,8 +291,6 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         case 1: GS_BWD_LAUNCH(2, 2, 4); break;
         case 2: GS_BWD_LAUNCH(1, 4, 4); break;
         case 3: GS_BWD_LAUNCH(4, 1, 1); break;
-        case 4: GS_BWD_LAUNCH(4, 1, 5); break;
-        case 5: GS_BWD_LAUNCH(4, 1, 6); break;
         default: GS_BWD_LAUNCH(4, 1, 4); break;
     }
 #undef GS_BWD_LAUNCH

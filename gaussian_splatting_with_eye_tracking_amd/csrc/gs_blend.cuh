@@ -31,6 +31,15 @@ struct PixelSetT {
 };
 using PixelSet = PixelSetT<kPix>;
 
+// power = -0.5 (c.x dx^2 + c.z dy^2) - c.y dx dy (forward.cu:331-333,
+// backward.cu:466-468) with its fused multiply-adds written out: every
+// Gaussian gets the same bits wherever the compiler schedules it (the
+// two-Gaussian forward loop, the backward's replay), so the backward's alpha
+// is the forward's and the row-group cull leaves the image bit-identical.
+__device__ __forceinline__ float splat_power(float dx, float dy, float4 co) {
+    return __builtin_fmaf(-0.5f, __builtin_fmaf(co.x * dx, dx, (co.z * dy) * dy), -((co.y * dx) * dy));
+}
+
 // 16x16 block at (ox, oy) with pixel stride `st` (1 = base, 2 = AMR sub-lattice).
 template <int kPPL, int kWaves>
 __device__ __forceinline__ PixelSetT<kPPL> make_pixels_t(int W, int H, uint32_t ox, uint32_t oy, uint32_t st) {
@@ -211,6 +220,63 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 mk[k] = uniform_u64(s_bal[c * 4 + wave * kPPL + k]);
                 todo |= mk[k];
             }
+            if constexpr (kPPL == 1) {
+                // One row group per wave: every set bit of todo is a visit.  Two
+                // Gaussians per iteration: their LDS reads share one wait and
+                // their alpha chains (independent of T) interleave; the blend
+                // itself stays front to back.
+                while (todo) {
+                    const uint32_t bA = (uint32_t)__builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    const bool two = todo != 0;  // wave-uniform
+                    const uint32_t bB = two ? (uint32_t)__builtin_ctzll(todo) : bA;
+                    if (two) todo &= todo - 1;
+                    const uint32_t jA = c * 64 + bA, jB = c * 64 + bB;
+                    const float2 xyA = s_xy[jA], xyB = s_xy[jB];
+                    const float4 coA = s_co[jA], coB = s_co[jB];
+                    const float4 fA = s_rgb[jA], fB = s_rgb[jB];
+                    const float dxA = xyA.x - px.x, dxB = xyB.x - px.x;
+                    const float dyA = xyA.y - px.y[0], dyB = xyB.y - px.y[0];
+                    const float pA = splat_power(dxA, dyA, coA);
+                    const float pB = splat_power(dxB, dyB, coB);
+                    const float aA = fminf(0.99f, coA.w * __expf(pA));
+                    const float aB = fminf(0.99f, coB.w * __expf(pB));
+                    const bool alive = !done[0];
+                    {
+                        const float test_T = st_.T[0] * (1 - aA);
+                        const bool hit = !done[0] && !(pA > 0.0f) && !(aA < 1.0f / 255.0f);
+                        const bool stop = hit && test_T < 0.0001f;
+                        done[0] = done[0] || stop;
+                        if (hit && !stop) {
+                            const float w = aA * st_.T[0];
+                            st_.C[0][0] = __builtin_fmaf(fA.x, w, st_.C[0][0]);
+                            st_.C[0][1] = __builtin_fmaf(fA.y, w, st_.C[0][1]);
+                            st_.C[0][2] = __builtin_fmaf(fA.z, w, st_.C[0][2]);
+                            st_.T[0] = test_T;
+                            st_.last[0] = b0 + jA + 1;
+                        }
+                    }
+                    if (two) {
+                        const float test_T = st_.T[0] * (1 - aB);
+                        const bool hit = !done[0] && !(pB > 0.0f) && !(aB < 1.0f / 255.0f);
+                        const bool stop = hit && test_T < 0.0001f;
+                        done[0] = done[0] || stop;
+                        if (hit && !stop) {
+                            const float w = aB * st_.T[0];
+                            st_.C[0][0] = __builtin_fmaf(fB.x, w, st_.C[0][0]);
+                            st_.C[0][1] = __builtin_fmaf(fB.y, w, st_.C[0][1]);
+                            st_.C[0][2] = __builtin_fmaf(fB.z, w, st_.C[0][2]);
+                            st_.T[0] = test_T;
+                            st_.last[0] = b0 + jB + 1;
+                        }
+                    }
+                    if (__ballot(alive) == 0ull) {
+                        wave_alive = false;
+                        break;
+                    }
+                }
+                continue;
+            }
             while (todo) {
                 const uint32_t bit = (uint32_t)__builtin_ctzll(todo);
                 todo &= todo - 1;
@@ -225,7 +291,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                     alive |= !done[k];
                     if (!((mk[k] >> bit) & 1ull)) continue;  // wave-uniform: culled for this row group
                     const float dy = xy.y - px.y[k];
-                    const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+                    const float power = splat_power(dx, dy, co);
                     const float alpha = fminf(0.99f, co.w * __expf(power));
                     const float test_T = st_.T[k] * (1 - alpha);
                     // forward.cu:333-352's per-pixel continues as predicates (only
@@ -236,9 +302,9 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                     if (!hit || stop) continue;
                     const float4 f = s_rgb[j];
                     const float w = alpha * st_.T[k];
-                    st_.C[k][0] += f.x * w;
-                    st_.C[k][1] += f.y * w;
-                    st_.C[k][2] += f.z * w;
+                    st_.C[k][0] = __builtin_fmaf(f.x, w, st_.C[k][0]);
+                    st_.C[k][1] = __builtin_fmaf(f.y, w, st_.C[k][1]);
+                    st_.C[k][2] = __builtin_fmaf(f.z, w, st_.C[k][2]);
                     st_.T[k] = test_T;
                     st_.last[k] = contributor;
                 }
