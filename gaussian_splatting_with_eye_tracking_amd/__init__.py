@@ -9,8 +9,8 @@ The drop-in packages ``diff_gaussian_rasterization``,
 re-export the reference API from here.
 
 There is no CPU fallback: importing ``_C`` fails loudly if the native
-extension has not been built (run ``python -m
-gaussian_splatting_with_eye_tracking_amd.build`` or
+extension has not been built (run ``python
+gaussian_splatting_with_eye_tracking_amd/build.py`` or
 ``__graft_entry__.build()``).
 """
 from __future__ import annotations
@@ -30,7 +30,7 @@ def _load_native():
     except ImportError as e:  # pragma: no cover - exercised only when unbuilt
         raise ImportError(
             "gaussian_splatting_with_eye_tracking_amd: the native HIP extension is not built "
-            f"({e}). Build it with `python -m gaussian_splatting_with_eye_tracking_amd.build`.") from e
+            f"({e}). Build it with `python gaussian_splatting_with_eye_tracking_amd/build.py` or `__graft_entry__.build()`.") from e
 
 
 _C = _load_native()
