@@ -106,10 +106,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     }
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
-    // The per-pixel terms are summed without their constant factors; the
-    // flush applies them: g3 * -ddelx_dx, g4 * -ddely_dy, g5..g7 * -0.5.
     const int comp = lane & 15;
-    const float comp_scale = comp == 3 ? -ddelx_dx : comp == 4 ? -ddely_dy : (comp >= 5 && comp <= 7) ? -0.5f : 1.0f;
+    // flush: the accumulator-row entry each output component starts from
+    const int ia = comp < 3 ? comp : comp == 8 ? 3 : comp < 5 ? 4 : comp + 1;
 
     // Software pipeline over the batches (vector-memory counters retire in
     // issue order, so issue order decides what each wait covers): the next
@@ -137,7 +136,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             const float2 xy = nxy;
             const float4 co = nco;
             s_xy[tid] = xy;
-            s_co[tid] = co;
+            s_co[tid] = splat_coef(co);
             s_rgb[tid] = make_float4(nrgb[0], nrgb[1], nrgb[2], 0.f);
             gm = cull ? splat_group_mask(xy, co, (float)ox, (float)oy, 1.0f) : 0xfu;
         }
@@ -174,50 +173,59 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             const int j = 64 * c + cbit;
             const uint32_t contributor = (uint32_t)(top - 1 - j);
             const float2 xy = s_xy[j];
-            const float4 co = s_co[j];
+            const float4 pc = s_co[j];
             const float4 cf = s_rgb[j];
             const float dx = xy.x - px.x;
-            const float dx_cx = dx * co.x, dx_cy = dx * co.y;
+            const float pa = (pc.x * dx) * dx, pb = pc.y * dx;  // the lane's pixels share x
+            // Per pixel with t = G dL_dalpha the reference adds (backward.cu:
+            // 518-545) dL_dopacity += t; dL_dmean2D += -o t (C d) * (W/2, H/2);
+            // dL_dconic += -o/2 t (dx^2, dx dy, dy^2).  A lane's pixels share dx,
+            // so it sums s0 = sum t, s1 = sum t dy, s2 = sum t dy^2 and forms
+            // the six moments (s0, dx s0, s1, dx^2 s0, dx s1, s2) once; the flush
+            // applies o, the conic and the constants.
             float g[kNG];
 #pragma unroll
             for (int q = 0; q < kNG; q++) g[q] = 0.f;
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
             bool any = false;
 #pragma unroll
             for (int k = 0; k < kPPL; k++) {
                 if (!((mk[k] >> cbit) & 1ull)) continue;  // wave-uniform: culled for this row group
                 const float dy = xy.y - px.y[k];
-                const float power = splat_power(dx, dy, co);  // the forward's bits
-                const float G = __expf(power);
-                const float alpha = fminf(0.99f, co.w * G);
+                const float p2 = splat_p2(pa, pb, dy, pc);  // the forward's bits
+                const float G = splat_exp(p2);
+                const float alpha = fminf(0.99f, pc.w * G);
                 // The reference's three per-pixel `continue`s (backward.cu:466-482)
                 // as one predicate: only wave-uniform branches save SIMD time, and
                 // nested ones make the compiler re-zero g[] on every skip path.
                 // (contributor >= last also covers pixels outside the image.)
-                const bool ok = contributor < last[k] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                const bool ok = contributor < last[k] && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
                 if (!ok) continue;
                 any = true;
                 const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
                 T[k] = T[k] * rinv;
                 const float dchannel_dcolor = alpha * T[k];
                 // sum_ch (c - accum_rec) dL_dpix, with accum_rec . dL_dpix
-                // advanced by the reference's recurrence
+                // advanced by the reference's recurrence (backward.cu:500-507)
                 const float c_dot = cf.x * dpx[k][0] + cf.y * dpx[k][1] + cf.z * dpx[k][2];
-                acc_dot[k] = last_alpha[k] * last_dot[k] + (1.f - last_alpha[k]) * acc_dot[k];
+                acc_dot[k] = __builtin_fmaf(last_alpha[k], last_dot[k] - acc_dot[k], acc_dot[k]);
                 last_dot[k] = c_dot;
                 last_alpha[k] = alpha;
                 const float dL_dalpha = (c_dot - acc_dot[k]) * T[k] + nbg[k] * rinv;
 #pragma unroll
                 for (int ch = 0; ch < 3; ch++) g[ch] += dchannel_dcolor * dpx[k][ch];
-                // dL_dG * G times the unscaled mean2D / conic factors
-                const float h = G * (co.w * dL_dalpha);
-                const float hdx = h * dx, hdy = h * dy;
-                g[3] += h * (dx_cx + dy * co.y);
-                g[4] += h * (dy * co.z + dx_cy);
-                g[5] += hdx * dx;
-                g[6] += hdx * dy;
-                g[7] += hdy * dy;
-                g[8] += G * dL_dalpha;
+                const float t = G * dL_dalpha;
+                const float tdy = t * dy;
+                s0 += t;
+                s1 += tdy;
+                s2 = __builtin_fmaf(tdy, dy, s2);
             }
+            g[3] = s0;
+            g[4] = dx * s0;
+            g[5] = s1;
+            g[6] = dx * g[4];
+            g[7] = dx * s1;
+            g[8] = s2;
             if (__ballot(any) != 0ull) {  // wave-uniform
                 if (kWaves == 1) {  // half-wave sums, parked by lanes 31 and 63
                     dpp_sum9_halves(g);
@@ -253,13 +261,24 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             bool live = r < cnt && comp < kNG;
             if (kWaves == 1) live = live && ((written >> (r & 63)) & 1ull);
             if (live) {
-                float v;
+                // row sums (c0, c1, c2, s0, sx, sy, sxx, sxy, syy) -> the
+                // reference's nine terms: v = ka * row[ia] + kb * sy, with o and
+                // the conic from the staged log2(e)-scaled record
+                const float* row0 = &s_acc[r * kRowsPerG * kAccRow];
+                float qa = row0[ia], qb = row0[5];
                 if (kWaves == 1) {
-                    const float* rows = &s_acc[r * 2 * kAccRow + comp];
-                    v = (rows[0] + rows[kAccRow]) * comp_scale;
-                } else {
-                    v = s_acc[r * kAccRow + comp] * comp_scale;
+                    qa += row0[kAccRow + ia];
+                    qb += row0[kAccRow + 5];
                 }
+                const float4 pc = s_co[r];
+                const float o = pc.w;
+                const float cx = pc.x * (-1.0f / kHalfLog2e), cy = pc.y * (-1.0f / kLog2e),
+                            cz = pc.z * (-1.0f / kHalfLog2e);
+                const float ka = comp == 3 ? -o * cx * ddelx_dx
+                               : comp == 4 ? -o * cy * ddely_dy
+                               : (comp >= 5 && comp <= 7) ? -0.5f * o : 1.0f;
+                const float kb = comp == 3 ? -o * cy * ddelx_dx : comp == 4 ? -o * cz * ddely_dy : 0.0f;
+                const float v = ka * qa + kb * qb;
                 if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[par][r] * kGradRow + comp], v);
             }
         }

@@ -32,13 +32,33 @@ struct PixelSetT {
 using PixelSet = PixelSetT<kPix>;
 
 // power = -0.5 (c.x dx^2 + c.z dy^2) - c.y dx dy (forward.cu:331-333,
-// backward.cu:466-468) with its fused multiply-adds written out: every
-// Gaussian gets the same bits wherever the compiler schedules it (the
-// two-Gaussian forward loop, the backward's replay), so the backward's alpha
-// is the forward's and the row-group cull leaves the image bit-identical.
-__device__ __forceinline__ float splat_power(float dx, float dy, float4 co) {
-    return __builtin_fmaf(-0.5f, __builtin_fmaf(co.x * dx, dx, (co.z * dy) * dy), -((co.y * dx) * dy));
+// backward.cu:466-468), evaluated pre-scaled by log2(e) so exp(power) is one
+// v_exp_f32 (exp2) and as a quadratic in dy: p2 = (hz dy + ny dx) dy + hx dx^2
+// with (hx, ny, hz) = log2(e) (-c.x/2, -c.y, -c.z/2) computed once per
+// Gaussian when it is staged (splat_coef).  For the backward's 4 pixels per
+// lane (same x) hx dx^2 and ny dx are per-lane terms, so each pixel costs two
+// fmas.  Every kernel evaluates the same expression with explicit fmas, so
+// the backward's alpha carries the forward's bits.  sign(p2) = sign(power):
+// the reference's `power > 0` skip is `p2 > 0`.
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kHalfLog2e = 0.5f * kLog2e;
+
+__device__ __forceinline__ float4 splat_coef(float4 co) {
+    return make_float4(-kHalfLog2e * co.x, -kLog2e * co.y, -kHalfLog2e * co.z, co.w);
 }
+
+// p2 from the per-lane terms a = (hx dx) dx and b = ny dx.
+__device__ __forceinline__ float splat_p2(float a, float b, float dy, float4 pc) {
+    return __builtin_fmaf(__builtin_fmaf(pc.z, dy, b), dy, a);
+}
+
+__device__ __forceinline__ float splat_p2(float dx, float dy, float4 pc) {
+    return splat_p2((pc.x * dx) * dx, pc.y * dx, dy, pc);
+}
+
+// G = exp(power) = 2^p2 (the hardware exp2; the reference's expf within a
+// few ulp).
+__device__ __forceinline__ float splat_exp(float p2) { return __builtin_amdgcn_exp2f(p2); }
 
 // 16x16 block at (ox, oy) with pixel stride `st` (1 = base, 2 = AMR sub-lattice).
 template <int kPPL, int kWaves>
@@ -203,7 +223,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
             const float2 xy = means2D[id];
             const float4 co = conic_opacity[id];
             s_xy[tid] = xy;
-            s_co[tid] = co;
+            s_co[tid] = splat_coef(co);
             s_rgb[tid] = make_float4(features[3 * id], features[3 * id + 1], features[3 * id + 2], 0.f);
             gm = cull ? splat_group_mask(xy, co, ox, oy, st) : 0xfu;
         }
@@ -237,10 +257,10 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                     const float4 fA = s_rgb[jA], fB = s_rgb[jB];
                     const float dxA = xyA.x - px.x, dxB = xyB.x - px.x;
                     const float dyA = xyA.y - px.y[0], dyB = xyB.y - px.y[0];
-                    const float pA = splat_power(dxA, dyA, coA);
-                    const float pB = splat_power(dxB, dyB, coB);
-                    const float aA = fminf(0.99f, coA.w * __expf(pA));
-                    const float aB = fminf(0.99f, coB.w * __expf(pB));
+                    const float pA = splat_p2(dxA, dyA, coA);
+                    const float pB = splat_p2(dxB, dyB, coB);
+                    const float aA = fminf(0.99f, coA.w * splat_exp(pA));
+                    const float aB = fminf(0.99f, coB.w * splat_exp(pB));
                     const bool alive = !done[0];
                     {
                         const float test_T = st_.T[0] * (1 - aA);
@@ -284,6 +304,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 const float2 xy = s_xy[j];
                 const float4 co = s_co[j];
                 const float dx = xy.x - px.x;
+                const float pa = (co.x * dx) * dx, pb = co.y * dx;
                 const uint32_t contributor = b0 + j + 1;
                 bool alive = false;
 #pragma unroll
@@ -291,8 +312,8 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                     alive |= !done[k];
                     if (!((mk[k] >> bit) & 1ull)) continue;  // wave-uniform: culled for this row group
                     const float dy = xy.y - px.y[k];
-                    const float power = splat_power(dx, dy, co);
-                    const float alpha = fminf(0.99f, co.w * __expf(power));
+                    const float power = splat_p2(pa, pb, dy, co);
+                    const float alpha = fminf(0.99f, co.w * splat_exp(power));
                     const float test_T = st_.T[k] * (1 - alpha);
                     // forward.cu:333-352's per-pixel continues as predicates (only
                     // wave-uniform branches save SIMD time)
