@@ -32,12 +32,12 @@
 namespace gsamd {
 
 constexpr int kNG = 9;      // gradient terms per (pixel, Gaussian)
-constexpr int kAccRow = 12;  // LDS accumulator row (floats, 48 B)
+constexpr int kAccRow = 9;   // LDS accumulator row (floats; odd stride: 9 scalar stores per row)
 
 // One 16x16 tile per workgroup of kWaves wave64s, kPPL pixels per lane
 // (kWaves * 64 * kPPL = 256; gs_blend.cuh mapping).  kMinWaves: waves per
 // SIMD the register allocation must allow.
-template <int kPPL, int kWaves, int kMinWaves>
+template <int kPPL, int kWaves, int kMinWaves, bool kSwap>
 __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     int W, int H, const uint32_t* __restrict__ ranges, const uint32_t* __restrict__ max_contrib,
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // per-Gaussian sums: one wave parks its two half-wave partials (summed by
     // the flush; 4 row partials would double the LDS footprint and cost
     // workgroups per CU); several waves add into one row with LDS atomics
-    constexpr int kRowsPerG = kWaves == 1 ? 2 : 1;
+    constexpr int kRowsPerG = (kWaves == 1 && !kSwap) ? 2 : 1;
     __shared__ float s_acc[kB * kRowsPerG * kAccRow];
     __shared__ uint64_t s_bal[4 * kWaves];
 
@@ -183,10 +183,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             // so it sums s0 = sum t, s1 = sum t dy, s2 = sum t dy^2 and forms
             // the six moments (s0, dx s0, s1, dx^2 s0, dx s1, s2) once; the flush
             // applies o, the conic and the constants.
-            float g[kNG];
-#pragma unroll
-            for (int q = 0; q < kNG; q++) g[q] = 0.f;
-            float s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            float c0 = 0.f, c1 = 0.f, c2 = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f;
             bool any = false;
 #pragma unroll
             for (int k = 0; k < kPPL; k++) {
@@ -212,14 +209,19 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 last_dot[k] = c_dot;
                 last_alpha[k] = alpha;
                 const float dL_dalpha = (c_dot - acc_dot[k]) * T[k] + nbg[k] * rinv;
-#pragma unroll
-                for (int ch = 0; ch < 3; ch++) g[ch] += dchannel_dcolor * dpx[k][ch];
+                c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
+                c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
+                c2 = __builtin_fmaf(dchannel_dcolor, dpx[k][2], c2);
                 const float t = G * dL_dalpha;
                 const float tdy = t * dy;
                 s0 += t;
                 s1 += tdy;
                 s2 = __builtin_fmaf(tdy, dy, s2);
             }
+            float g[kNG];
+            g[0] = c0;
+            g[1] = c1;
+            g[2] = c2;
             g[3] = s0;
             g[4] = dx * s0;
             g[5] = s1;
@@ -227,7 +229,24 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             g[7] = dx * s1;
             g[8] = s2;
             if (__ballot(any) != 0ull) {  // wave-uniform
-                if (kWaves == 1) {  // half-wave sums, parked by lanes 31 and 63
+                if (kSwap) {  // full sums by transposition: 2 values per row leader + g8 in lane 63
+                    float za, zb;
+                    swap_sum9(g, za, zb);
+                    if ((lane & 15) == 15) {
+                        float* row = &s_acc[j * kAccRow];
+                        const int q = swap_sum_slot(lane >> 4);
+                        if (kWaves == 1) {
+                            row[q] = za;
+                            row[4 + q] = zb;
+                            if (lane == 63) row[8] = g[8];
+                        } else {
+                            atomicAdd(&row[q], za);
+                            atomicAdd(&row[4 + q], zb);
+                            if (lane == 63) atomicAdd(&row[8], g[8]);
+                        }
+                    }
+                    written |= 1ull << j;
+                } else if (kWaves == 1) {  // half-wave sums, parked by lanes 31 and 63
                     dpp_sum9_halves(g);
                     if ((lane & 31) == 31) {
                         float* row = &s_acc[(j * 2 + (lane >> 5)) * kAccRow];
@@ -266,7 +285,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 // the conic from the staged log2(e)-scaled record
                 const float* row0 = &s_acc[r * kRowsPerG * kAccRow];
                 float qa = row0[ia], qb = row0[5];
-                if (kWaves == 1) {
+                if (kRowsPerG == 2) {
                     qa += row0[kAccRow + ia];
                     qb += row0[kAccRow + 5];
                 }
@@ -301,16 +320,17 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         launch_order_tiles(gx * gy, img, true, s);
         order = img.tile_order;
     }
-#define GS_BWD_LAUNCH(PPL, WAVES, OCC)                                                                          \
-    hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H,      \
+#define GS_BWD_LAUNCH(PPL, WAVES, OCC, SWAP)                                                                    \
+    hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H,      \
                        img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
                        dL_dpix, bg, g.grad_accum, g_cull, order, gx)
     switch (g_bwd_variant) {
-        case 1: GS_BWD_LAUNCH(2, 2, 4); break;
-        case 2: GS_BWD_LAUNCH(1, 4, 4); break;
-        case 3: GS_BWD_LAUNCH(4, 1, 1); break;
-        default: GS_BWD_LAUNCH(4, 1, 4); break;
+        case 1: GS_BWD_LAUNCH(2, 2, 4, true); break;
+        case 2: GS_BWD_LAUNCH(1, 4, 4, true); break;
+        case 3: GS_BWD_LAUNCH(4, 1, 4, false); break;
+        case 4: GS_BWD_LAUNCH(4, 1, 5, true); break;
+        default: GS_BWD_LAUNCH(4, 1, 4, true); break;
     }
 #undef GS_BWD_LAUNCH
 }

@@ -482,4 +482,63 @@ __device__ __forceinline__ void dpp_sum9_halves(float (&g)[9]) {
           "+v"(g[8]));
 }
 
+// Full 64-lane sums of 9 values by transposition (gfx950 v_permlane32_swap /
+// v_permlane16_swap) instead of 9 independent DPP trees.  For a group of 4
+// registers (a, b, c, d), rows = 16-lane quarters:
+//   permlane32_swap(a, b); a + b  -> [a0+a2, a1+a3, b0+b2, b1+b3]   (same for c, d)
+//   permlane16_swap(ab, cd); sum  -> [a, c, b, d] row partials in ONE register
+//   row_shr 1, 2, 4, 8            -> lane 15 of row r holds the total of
+//                                    value ((r & 1) << 1 | r >> 1) of the group.
+// Two groups (g0..g3, g4..g7) cost 6 swaps + 6 adds + 8 DPP adds; g8 takes
+// the plain tree (6 DPP adds, total in lane 63): 26 VALU ops instead of the
+// 45 of dpp_sum9_halves, and one full sum per value (no half-wave partials).
+// After it: lane 16r + 15 holds za = g[q(r)] and zb = g[4 + q(r)]; lane 63
+// also holds g8.  Must run with all 64 lanes active.
+__device__ __forceinline__ int swap_sum_slot(int row) { return ((row & 1) << 1) | (row >> 1); }
+
+__device__ __forceinline__ float pl_add32(float a, float b) {
+    // (the two halves go through named scalars: subscripting the returned
+    // vector directly inside the expression miscompiles to r[0] + r[0] with
+    // ROCm 7.2's clang)
+    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
+                                                    false, false);
+    const uint32_t r0 = r[0], r1 = r[1];
+    return __builtin_bit_cast(float, r0) + __builtin_bit_cast(float, r1);
+}
+
+__device__ __forceinline__ float pl_add16(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
+                                                    false, false);
+    const uint32_t r0 = r[0], r1 = r[1];
+    return __builtin_bit_cast(float, r0) + __builtin_bit_cast(float, r1);
+}
+
+__device__ __forceinline__ void swap_sum9(float (&g)[9], float& za, float& zb) {
+    const float ab = pl_add32(g[0], g[1]), cd = pl_add32(g[2], g[3]);
+    const float ef = pl_add32(g[4], g[5]), gh = pl_add32(g[6], g[7]);
+    za = pl_add16(ab, cd);
+    zb = pl_add16(ef, gh);
+    float e = g[8];
+    asm volatile(
+        "s_nop 1\n"
+        "v_add_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %2, %2, %2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %2, %2, %2 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %2, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %2, %2, %2 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "s_nop 1\n"
+        "v_add_f32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_add_f32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        : "+v"(za), "+v"(zb), "+v"(e));
+    g[8] = e;
+}
+
 }  // namespace gsamd

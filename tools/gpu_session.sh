@@ -21,6 +21,7 @@ run() {  # name limit cmd...
 for step in "$@"; do
   case "$step" in
     tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
+    parity) run pytest_parity 600 python -m pytest tests/test_gpu_parity.py tests/test_gpu_cull.py -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
     bench3) run bench_cfg3 600 python bench.py --config cfg3_amr_1080p_1M --steps 20 --warmup 3 ;;
@@ -34,7 +35,7 @@ for step in "$@"; do
     pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
     ab_fwd) run ab_fwd 400 python tools/ab_tuning.py --key fwd_variant --values 0 1 2 --stage render ;;
-    ab_bwd) run ab_bwd 400 python tools/ab_tuning.py --key bwd_variant --values 0 1 2 3 --stage render_bwd --backward ;;
+    ab_bwd) run ab_bwd 400 python tools/ab_tuning.py --key bwd_variant --values 0 3 0 3 --stage render_bwd --backward ;;
     ab_cull) run ab_cull_fwd 400 python tools/ab_tuning.py --key cull --values 0 1 --stage render &&
              run ab_cull_bwd 400 python tools/ab_tuning.py --key cull --values 0 1 --stage render_bwd --backward ;;
     ab_chunk) run ab_chunk_dup 400 python tools/ab_tuning.py --key bin_chunk --values 2048 4096 8192 16384 --stage duplicate &&
@@ -46,6 +47,8 @@ for step in "$@"; do
               run ab_split4 600 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_sq -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_sq2) run pmc_sq2 600 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
+    pmc_bwd_a) run pmc_bwd_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_bwd_a -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
+    pmc_bwd_b) run pmc_bwd_b 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_bwd_b -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     gputrain) run pytest_gpu_train 600 python -m pytest tests/test_gpu_training.py tests/test_loss.py -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     train) run bench_train 600 python tools/bench_train.py ;;
     proftrain) run rocprof_train 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python3 tools/bench_train.py --reps 10 ;;
