@@ -70,10 +70,10 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, 1);
     const size_t plane = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
-    // acc_rec . dL_dpix and last_colour . dL_dpix are all the reference's
-    // accum_rec / last_color recurrences (backward.cu:500-507) feed into
-    // dL_dalpha, so each pixel carries those two scalars instead of 2 x 3.
-    float T[kPPL], nbg[kPPL], dpx[kPPL][3], acc_dot[kPPL], last_dot[kPPL], last_alpha[kPPL];
+    // accum_rec . dL_dpix is all the reference's accum_rec / last_color
+    // recurrences (backward.cu:500-507) feed into dL_dalpha, so each pixel
+    // carries that one scalar instead of 2 x 3.
+    float T[kPPL], nbg[kPPL], dpx[kPPL][3], acc_dot[kPPL];
     uint32_t last[kPPL];
     uint32_t wave_last = 0;
 #pragma unroll
@@ -86,8 +86,6 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
 #pragma unroll
         for (int c = 0; c < 3; c++) dpx[k][c] = px.inside[k] ? dL_dpixels[c * plane + pid] : 0.f;
         acc_dot[k] = 0.f;
-        last_dot[k] = 0.f;
-        last_alpha[k] = 0.f;
         // (-T_final / (1 - alpha)) * bg.dL_dpix = nbg * 1/(1 - alpha)
         nbg[k] = -Tf * (bg0 * dpx[k][0] + bg1 * dpx[k][1] + bg2 * dpx[k][2]);
     }
@@ -205,10 +203,12 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 // sum_ch (c - accum_rec) dL_dpix, with accum_rec . dL_dpix
                 // advanced by the reference's recurrence (backward.cu:500-507)
                 const float c_dot = cf.x * dpx[k][0] + cf.y * dpx[k][1] + cf.z * dpx[k][2];
-                acc_dot[k] = __builtin_fmaf(last_alpha[k], last_dot[k] - acc_dot[k], acc_dot[k]);
-                last_dot[k] = c_dot;
-                last_alpha[k] = alpha;
-                const float dL_dalpha = (c_dot - acc_dot[k]) * T[k] + nbg[k] * rinv;
+                // The reference advances accum_rec at the NEXT contributor from the
+                // stored (last_alpha, last_color); advancing it here with the same
+                // operands gives the same bits and needs no per-pixel "last" state.
+                const float diff = c_dot - acc_dot[k];
+                const float dL_dalpha = diff * T[k] + nbg[k] * rinv;
+                acc_dot[k] = __builtin_fmaf(alpha, diff, acc_dot[k]);
                 c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
                 c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
                 c2 = __builtin_fmaf(dchannel_dcolor, dpx[k][2], c2);

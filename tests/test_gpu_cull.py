@@ -94,8 +94,10 @@ def test_cull_is_exact(P, W, H, seed, variant):
     np.testing.assert_array_equal(res[0][0], res[1][0])  # image, bit-exact
     for k in res[0][1]:
         np.testing.assert_array_equal(res[0][1][k], res[1][1][k], err_msg=k)
+    # float-atomic ordering noise only (variant 2 adds LDS atomics from 4 waves
+    # in arbitrary order on top of the global ones): observed up to ~1.5e-6
     for i in range(3):  # dL_dmeans2D, dL_dcolors, dL_dopacity
-        assert G.rel_err(res[1][2][i], res[0][2][i]) < 1e-6, i
+        assert G.rel_err(res[1][2][i], res[0][2][i]) < 5e-6, i
     for c in range(9):  # each accumulated term, column by column
         a, b = res[0][3][:, c], res[1][3][:, c]
         scale = np.abs(a).max() + 1e-30
