@@ -165,14 +165,13 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
               mk[k] = uniform_u64(s_bal[c * 4 + wave * kPPL + k]) & lo_cut & gcut;
               todo |= mk[k];
           }
-          while (todo) {
-            const int cbit = __builtin_ctzll(todo);
-            todo &= todo - 1;
+          // One Gaussian (batch slot j, record staged in LDS) against the
+          // wave's pixels.  (Reading the next set bit's record ahead, in two
+          // register sets used in turn, measured no faster: the 4 waves per
+          // SIMD already hide the LDS latency.)
+          auto visit = [&](const int cbit, const float2 xy, const float4 pc, const float4 cf) {
             const int j = 64 * c + cbit;
             const uint32_t contributor = (uint32_t)(top - 1 - j);
-            const float2 xy = s_xy[j];
-            const float4 pc = s_co[j];
-            const float4 cf = s_rgb[j];
             const float dx = xy.x - px.x;
             const float pa = (pc.x * dx) * dx, pb = pc.y * dx;  // the lane's pixels share x
             // Per pixel with t = G dL_dalpha the reference adds (backward.cu:
@@ -262,6 +261,12 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                     }
                 }
             }
+          };
+          while (todo) {
+            const int cbit = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const int j = 64 * c + cbit;
+            visit(cbit, s_xy[j], s_co[j], s_rgb[j]);
           }
         }
         __syncthreads();
@@ -305,7 +310,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
 }
 
 extern int g_cull;  // render.hip
-// 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave uncapped
+// 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave x 4 px with the
+// half-wave DPP-tree sums instead of the permlane transposition
 // (1 wave x 4 px capped at 5 or 6 waves per SIMD spills: measured slower)
 int g_bwd_variant = 0;
 
@@ -329,7 +335,6 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         case 1: GS_BWD_LAUNCH(2, 2, 4, true); break;
         case 2: GS_BWD_LAUNCH(1, 4, 4, true); break;
         case 3: GS_BWD_LAUNCH(4, 1, 4, false); break;
-        case 4: GS_BWD_LAUNCH(4, 1, 5, true); break;
         default: GS_BWD_LAUNCH(4, 1, 4, true); break;
     }
 #undef GS_BWD_LAUNCH

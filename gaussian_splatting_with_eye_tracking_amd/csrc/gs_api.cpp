@@ -56,6 +56,7 @@ enum Stage {
 };
 struct Profiler {
     bool on = false;
+    uint32_t mask = ~0u;  // stages that record events (bit = Stage)
     struct Pending { int stage; hipEvent_t a, b; };
     std::vector<Pending> pending;
     double total_ms[kStages] = {0};
@@ -82,7 +83,7 @@ std::mutex g_prof_mu;
 struct StageTimer {
     int stage; hipStream_t s; hipEvent_t a = nullptr, b = nullptr;
     StageTimer(int st, hipStream_t str) : stage(st), s(str) {
-        if (!g_prof.on) return;
+        if (!g_prof.on || !((g_prof.mask >> st) & 1u)) return;
         std::lock_guard<std::mutex> l(g_prof_mu);
         a = g_prof.get(); b = g_prof.get();
         hipEventRecord(a, s);
@@ -520,6 +521,11 @@ int gs_set_tuning(const char* key, int value) {
 void gs_profile_enable(int on) {
     std::lock_guard<std::mutex> l(g_prof_mu);
     g_prof.on = on != 0;
+}
+
+void gs_profile_set_mask(unsigned mask) {
+    std::lock_guard<std::mutex> l(g_prof_mu);
+    g_prof.mask = mask;
 }
 
 int gs_profile_stage_count(void) { return kStages; }

@@ -416,6 +416,18 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("activation_backward", &ActivationBackward);
     m.def("abi_version", []() { return gs_abi_version(); });
     m.def("profile_enable", [](bool on) { gs_profile_enable(on ? 1 : 0); });
+    m.def("profile_stages", [](const std::vector<std::string>& names) {
+        // [] = all stages
+        unsigned mask = names.empty() ? ~0u : 0u;
+        for (const auto& n : names) {
+            int i = 0;
+            for (; i < gs_profile_stage_count(); i++)
+                if (n == gs_profile_stage_name(i)) break;
+            if (i == gs_profile_stage_count()) throw std::invalid_argument("unknown stage " + n);
+            mask |= 1u << i;
+        }
+        gs_profile_set_mask(mask);
+    });
     m.def("profile_read", &ProfileRead, py::arg("reset") = true);
     m.def("set_tuning", [](const std::string& k, int v) { check(gs_set_tuning(k.c_str(), v), "set_tuning"); });
 }

@@ -211,6 +211,10 @@ int gs_reconstruct_keys(char* geom_buffer, char* binning_buffer, char* img_buffe
  * and launch counts per stage (names from gs_profile_stage_name).  Used by
  * bench.py for the live per-kernel roofline (cross-checked with rocprofv3). */
 void gs_profile_enable(int on);
+/* Restrict the timing to the stages whose bit (1 << stage index) is set
+ * (default: all).  Each timed stage adds two event records per launch, so
+ * the headline timing records only the kernel its roofline is quoted on. */
+void gs_profile_set_mask(unsigned mask);
 /* Kernel-geometry knobs for A/B measurements ("fwd_variant": 0 = one wave
  * per tile x 4 px/lane, 1 = 2 waves x 2 px/lane, 2 = 4 waves x
  * 1 px/lane, the default), "bwd_variant" (0 = 1 wave x 4 px/lane, the default; 1 = 2 x 2; 2 = 4 x 1; 3 = 1 x 4 uncapped registers), "cull" (1 =

@@ -28,6 +28,8 @@ for step in "$@"; do
     bench4) run bench_cfg4 600 python bench.py --config cfg4_bicycle_6M --steps 10 --warmup 3 --no-cpu-baseline ;;
     dist2) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 ;;
     dist2amr) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2amr 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 5 --warmup 2 --config cfg3_amr_1080p_1M ;;
+    benchnp) run bench_np 400 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-profile &&
+             run bench_p 400 python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
     benchq) run bench 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     prof4) run rocprof4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- python3 bench.py --config cfg4_bicycle_6M --steps 5 --warmup 2 --no-cpu-baseline --no-profile ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile ;;
@@ -35,7 +37,7 @@ for step in "$@"; do
     pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
     ab_fwd) run ab_fwd 400 python tools/ab_tuning.py --key fwd_variant --values 0 1 2 --stage render ;;
-    ab_bwd) run ab_bwd 400 python tools/ab_tuning.py --key bwd_variant --values 0 3 0 3 --stage render_bwd --backward ;;
+    ab_bwd) run ab_bwd 400 python tools/ab_tuning.py --key bwd_variant --values 0 4 0 4 --stage render_bwd --backward ;;
     ab_cull) run ab_cull_fwd 400 python tools/ab_tuning.py --key cull --values 0 1 --stage render &&
              run ab_cull_bwd 400 python tools/ab_tuning.py --key cull --values 0 1 --stage render_bwd --backward ;;
     ab_chunk) run ab_chunk_dup 400 python tools/ab_tuning.py --key bin_chunk --values 2048 4096 8192 16384 --stage duplicate &&
