@@ -5,10 +5,15 @@ config 2), N data-parallel ranks (config 5 at N = 8).
 
 One *step* = per rank: one forward + backward through the drop-in API
 (``diff_gaussian_rasterization.GaussianRasterizer``, autograd) of one
-1920x1080 view of the same 1M-Gaussian scene, with a fixed N(0,1) cotangent;
-for N > 1 the flattened parameter gradients (59 floats per Gaussian:
-means3D 3, SH 48, opacity 1, scales 3, rotations 4) are summed across ranks
-with one RCCL all-reduce.  Per-GPU work is fixed as N grows ("weak").
+1920x1080 view of the same 1M-Gaussian scene, with a fixed N(0,1) cotangent.
+For N > 1 every rank ends the step holding the parameter gradients (59
+floats per Gaussian: means3D 3, SH 48, opacity 1, scales 3, rotations 4)
+summed over all N views: by default (--exchange views) each rank runs the
+blend backward of its view, the 40-B/Gaussian view records are all-gathered
+over RCCL and every rank runs the multi-view parameter backward
+(data_parallel.py); --exchange params is the plain alternative, each rank's
+full backward + one RCCL all-reduce of the 59-float gradients.  Per-GPU work
+is fixed as N grows ("weak").
 
 Inputs are resident in HBM before the timed region.  The timed region is K
 steps bracketed by barrier + synchronize; the reported time is the max over
@@ -293,6 +298,9 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="disable the per-stage event timing")
+    ap.add_argument("--exchange", choices=("views", "params"), default="views",
+                    help="N > 1 gradient exchange: all-gather of per-view screen-space records (default) or "
+                         "all-reduce of the 59-float parameter gradients")
     ap.add_argument("--yaw-spread", type=float, default=0.0,
                     help="rank r renders the camera yawed by (r-(N-1)/2)*spread degrees (config 5 uses 5)")
     args = ap.parse_args()
@@ -342,11 +350,28 @@ def main():
     means2D = torch.zeros_like(params["means3D"], requires_grad=True)
     dpix = torch.from_numpy(S.make_cotangent(H, W, 100 + rank)).to(dev)
     rasterizer = GaussianRasterizer(settings)
-    # N > 1: parameter grads are views of one flat buffer (DDP's gradient-as-bucket-view):
-    # the backward accumulates straight into it and one RCCL all-reduce sums it.
-    flat = DP.FlatGrads(params) if distributed else None
+    # N > 1, --exchange params: parameter grads are views of one flat buffer (DDP's
+    # gradient-as-bucket-view): the backward accumulates straight into it and one
+    # RCCL all-reduce sums it.  --exchange views (default): each rank runs the
+    # blend backward of its view, one RCCL all-gather of the view records, then
+    # every rank forms the summed parameter gradients of all N views
+    # (data_parallel.py).
+    views_mode = distributed and args.exchange == "views"
+    flat = DP.FlatGrads(params) if (distributed and not views_mode) else None
+    e0 = torch.empty(0, device=dev)
+
+    def step_views():
+        with torch.no_grad():
+            fwd = _C.rasterize_gaussians(
+                settings.bg, params["means3D"], e0, params["opacities"], params["scales"], params["rotations"],
+                1.0, e0, settings.viewmatrix, settings.projmatrix, settings.tanfovx, settings.tanfovy, H, W,
+                params["shs"], 3, settings.campos, False, False)
+            return DP.exchange_view_grads(settings, fwd, dpix, params["means3D"], params["shs"], params["scales"],
+                                          params["rotations"])
 
     def step():
+        if views_mode:
+            return step_views()
         if flat is not None:
             flat.flat.zero_()
             flat.attach(params)
@@ -454,8 +479,12 @@ def main():
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "fp32", "data": "synthetic (SURVEY §8(d) generator, seed 0)",
             "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, 16x16 tiles, forward+backward, "
-                                   f"1 view per GPU per step" + (" + RCCL all-reduce of 59 f32/Gaussian grads"
-                                                                 if world > 1 else ""),
+                                   f"1 view per GPU per step" + (
+                                       ("" if world == 1 else
+                                        " + RCCL all-gather of the 40-B/Gaussian view records and the multi-view "
+                                        "parameter backward" if args.exchange == "views" else
+                                        " + RCCL all-reduce of 59 f32/Gaussian grads")),
+                       "exchange": None if world == 1 else args.exchange,
                        "P": P, "width": W, "height": H, "views_per_gpu_per_step": 1,
                        "parallelism": f"dp{world}", "K_instances": K, "V_visible": V, "K_bwd_entries": Kb},
             "roofline": roofline,

@@ -46,13 +46,14 @@ struct GsError : std::runtime_error {
 
 // ---- optional per-stage timing (gs_profile_*): hipEvents recorded on the
 // launch stream around each stage; elapsed times are harvested lazily.
-constexpr int kStages = 13;
+constexpr int kStages = 14;
 const char* kStageNames[kStages] = {"preprocess", "tile_scan",    "duplicate",   "sort_tiles",
                                     "render",     "render_bwd",   "bwd_gauss",   "amr_levels",
                                     "amr_render", "amr_interp",   "knn",         "zero_accum",
-                                    "count_tiles"};
+                                    "count_tiles", "multiview_bwd"};
 enum Stage {
-    kPre, kScan, kDup, kSort, kRender, kRenderBwd, kBwdGauss, kAmrLevels, kAmrRender, kAmrInterp, kKnn, kZero, kCount
+    kPre, kScan, kDup, kSort, kRender, kRenderBwd, kBwdGauss, kAmrLevels, kAmrRender, kAmrInterp, kKnn, kZero, kCount,
+    kMultiView
 };
 struct Profiler {
     bool on = false;
@@ -308,6 +309,71 @@ int gs_rasterizer_backward(int P, int D, int M, int R, const float* background, 
         a.dL_drot = dL_drot;
         { StageTimer _t(kBwdGauss, s); launch_backward_gaussians(a, g, s); }
         stage_check(debug != 0, s, "preprocess_backward");
+        return 0;
+    });
+}
+
+int gs_rasterizer_backward_view_grads(int P, int R, const float* background, int width, int height,
+                                      const float* colors_precomp, const float* viewmatrix, const float* projmatrix,
+                                      const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                                      char* geom_buffer, char* binning_buffer, char* img_buffer,
+                                      const float* dL_dpix, float* out_record, int debug, void* stream) {
+    return guarded([&]() -> int {
+        if (P < 0) throw GsError("gs_rasterizer_backward_view_grads: negative P");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        const int tile = 16;
+        const int T = ((width + tile - 1) / tile) * ((height + tile - 1) / tile);
+        GeomView g;
+        ImageView img;
+        BinningView b;
+        carve_geom(geom_buffer, P, &g);
+        carve_image(img_buffer, (size_t)width * height, T, &img);
+        carve_binning(binning_buffer, R, &b);
+        if (!radii) radii = g.radii;
+        { StageTimer _t(kZero, s); GS_HIP(hipMemsetAsync(g.grad_accum, 0, sizeof(float) * kGradRow * (size_t)P, s)); }
+        const float* colors = colors_precomp ? colors_precomp : g.rgb;
+        if (R > 0 && P > 0) { StageTimer _t(kRenderBwd, s); launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s); }
+        stage_check(debug != 0, s, "render_backward");
+        launch_pack_view_grads(P, g, radii, colors_precomp == nullptr, viewmatrix, projmatrix, campos, width, height,
+                               tan_fovx, tan_fovy, out_record, s);
+        stage_check(debug != 0, s, "pack_view_grads");
+        return 0;
+    });
+}
+
+int gs_backward_gaussians_multiview(int P, int D, int M, int V, const float* views, const float* means3D,
+                                    const float* shs, const float* scales, const float* rotations,
+                                    float scale_modifier, float* dL_dmeans3D, float* dL_dsh, float* dL_dopacity,
+                                    float* dL_dscales, float* dL_drotations, float* grad_norm_accum, float* denom,
+                                    float* max_radii, void* stream) {
+    return guarded([&]() -> int {
+        if (P <= 0) return 0;
+        if (V <= 0) throw GsError("gs_backward_gaussians_multiview: V must be positive");
+        if (!scales || !rotations)
+            throw GsError("gs_backward_gaussians_multiview: scales and rotations are required (no cov3D_precomp)");
+        if (shs && (M <= 0 || M > 16 || D < 0 || D > 3))
+            throw GsError("gs_backward_gaussians_multiview: SH with 1..16 coefficients, degree <= 3");
+        if (grad_norm_accum && (!denom || !max_radii))
+            throw GsError("gs_backward_gaussians_multiview: statistics need grad_norm_accum, denom and max_radii");
+        MultiViewArgs a;
+        a.P = P; a.D = D; a.M = M; a.V = V;
+        a.views = views;
+        a.means3D = means3D;
+        a.shs = shs;
+        a.scales = scales;
+        a.rotations = rotations;
+        a.scale_modifier = scale_modifier;
+        a.dL_dmean3D = dL_dmeans3D;
+        a.dL_dsh = dL_dsh;
+        a.dL_dopacity = dL_dopacity;
+        a.dL_dscale = dL_dscales;
+        a.dL_drot = dL_drotations;
+        a.grad_norm_accum = grad_norm_accum;
+        a.denom = denom;
+        a.max_radii = max_radii;
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        { StageTimer _t(kMultiView, s); launch_multiview_backward(a, s); }
+        stage_check(false, s, "multiview_backward");
         return 0;
     });
 }

@@ -77,6 +77,21 @@ __device__ __forceinline__ Mat3 quat_to_R(float r, float x, float y, float z) {
                      2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
 }
 
+// computeCov3D (base/cr/forward.cu:118-152): Sigma = (S R)^T (S R), upper
+// triangle.  Shared by the forward preprocess and the multi-view backward so
+// both see the same bits.
+__device__ __forceinline__ void compute_cov3d(const float (&sc)[3], float4 q, float mod, float (&cov3D)[6]) {
+    Mat3 S = mat3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    S.m[0][0] = mod * sc[0];
+    S.m[1][1] = mod * sc[1];
+    S.m[2][2] = mod * sc[2];
+    const Mat3 R = quat_to_R(q.x, q.y, q.z, q.w);
+    const Mat3 Mm = mat3_mul(S, R);
+    const Mat3 Sigma = mat3_mul(mat3_transpose(Mm), Mm);
+    cov3D[0] = Sigma.m[0][0]; cov3D[1] = Sigma.m[0][1]; cov3D[2] = Sigma.m[0][2];
+    cov3D[3] = Sigma.m[1][1]; cov3D[4] = Sigma.m[1][2]; cov3D[5] = Sigma.m[2][2];
+}
+
 // 4x4 matrices as 16 floats, column-major like the reference (auxiliary.h:58-77).
 struct Mat4 {
     float m[16];

@@ -101,6 +101,32 @@ struct BackwardGaussArgs {
 // base/cr/backward.cu:144-396 fused into one per-Gaussian pass.
 void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hipStream_t s);
 
+// Data-parallel view exchange (backward.hip): per-view screen-space rows and
+// the multi-view per-Gaussian backward.
+constexpr int kViewRow = 10;   // words per Gaussian per view
+constexpr int kCamWords = 40;  // view 16, proj 16, campos 3, W, H, tan_fovx, tan_fovy, pad
+struct MultiViewArgs {
+    int P, D, M, V;
+    const float* views;  // [V] view records: [P][kViewRow] rows, then [kCamWords] camera
+    const float* means3D;
+    const float* shs;  // nullable (colors precomputed: no SH gradient)
+    const float* scales;
+    const float* rotations;
+    float scale_modifier;
+    float* dL_dmean3D;
+    float* dL_dsh;
+    float* dL_dopacity;
+    float* dL_dscale;
+    float* dL_drot;
+    float* grad_norm_accum;  // nullable: densification statistics, accumulated
+    float* denom;
+    float* max_radii;
+};
+void launch_pack_view_grads(int P, const GeomView& g, const int* radii, bool has_sh, const float* viewmatrix,
+                            const float* projmatrix, const float* campos, int width, int height, float tan_fovx,
+                            float tan_fovy, float* out, hipStream_t s);
+void launch_multiview_backward(const MultiViewArgs& a, hipStream_t s);
+
 // AMR (amr/cr/rasterizer_impl.cu:181-243, amr/cr/forward.cu:261-648).
 void launch_amr_levels(int T, const ImageView& img, hipStream_t s);
 void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s);

@@ -130,15 +130,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
 
     // computeCov3D (forward.cu:118-152)
     if (!kCovPrecomp) {
-        Mat3 S = mat3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
-        S.m[0][0] = a.scale_modifier * sc[0];
-        S.m[1][1] = a.scale_modifier * sc[1];
-        S.m[2][2] = a.scale_modifier * sc[2];
-        const Mat3 R = quat_to_R(q.x, q.y, q.z, q.w);
-        const Mat3 Mm = mat3_mul(S, R);
-        const Mat3 Sigma = mat3_mul(mat3_transpose(Mm), Mm);
-        cov3D[0] = Sigma.m[0][0]; cov3D[1] = Sigma.m[0][1]; cov3D[2] = Sigma.m[0][2];
-        cov3D[3] = Sigma.m[1][1]; cov3D[4] = Sigma.m[1][2]; cov3D[5] = Sigma.m[2][2];
+        compute_cov3d(sc, q, a.scale_modifier, cov3D);
 #pragma unroll
         for (int i = 0; i < 6; i++) g.cov3D[6 * idx + i] = cov3D[i];
     }

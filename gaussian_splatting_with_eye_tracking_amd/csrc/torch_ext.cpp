@@ -196,6 +196,77 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> Raste
                            dL_drotations);
 }
 
+// Data-parallel stage 1 (gsplat_amd.h): blend backward of one view -> its
+// view record, [P * 10 + 40] floats (the record the ranks all-gather).
+Tensor RasterizeGaussiansBackwardViewGrads(const Tensor& background, const Tensor& radii_in,
+                                           const Tensor& colors_in, const Tensor& viewmatrix_in,
+                                           const Tensor& projmatrix_in, const float tan_fovx, const float tan_fovy,
+                                           const Tensor& campos_in, const Tensor& dL_dout_color_in,
+                                           const Tensor& geomBuffer, const int R, const Tensor& binningBuffer,
+                                           const Tensor& imageBuffer, const bool debug) {
+    const int P = (int)radii_in.size(0);
+    const int H = (int)dL_dout_color_in.size(1);
+    const int W = (int)dL_dout_color_in.size(2);
+    const at::OptionalDeviceGuard guard(device_of(dL_dout_color_in));
+    Tensor rec = torch::empty({(int64_t)P * 10 + 40}, dL_dout_color_in.options());
+    const Tensor bg = background.contiguous(), radii = radii_in.contiguous(), colors = colors_in.contiguous(),
+                 dL_dout = dL_dout_color_in.contiguous(), viewmatrix = viewmatrix_in.contiguous(),
+                 projmatrix = projmatrix_in.contiguous(), campos = campos_in.contiguous();
+    require_device(dL_dout, "dL_dout_color");
+    require_device(viewmatrix, "viewmatrix");
+    TORCH_CHECK(radii.is_cuda() && radii.scalar_type() == torch::kInt32, "radii must be an int32 device tensor");
+    check(gs_rasterizer_backward_view_grads(
+              P, R, fptr(bg), W, H, fptr(colors), fptr(viewmatrix), fptr(projmatrix), fptr(campos), tan_fovx,
+              tan_fovy, radii.data_ptr<int>(), reinterpret_cast<char*>(geomBuffer.data_ptr()),
+              reinterpret_cast<char*>(binningBuffer.data_ptr()), reinterpret_cast<char*>(imageBuffer.data_ptr()),
+              fptr(dL_dout), rec.data_ptr<float>(), debug, stream_of(dL_dout)),
+          "rasterize_gaussians_backward_view_grads");
+    return rec;
+}
+
+// Data-parallel stage 2: the per-Gaussian backward of V views at once (views
+// = [V, P * 10 + 40] records), summed over views; returns (dL_dmeans3D,
+// dL_dsh, dL_dopacity, dL_dscales, dL_drotations); densification statistics
+// accumulated in place when given (non-empty).
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> BackwardGaussiansMultiview(
+    const Tensor& views_in, const Tensor& means3D_in, const Tensor& sh_in, const int degree, const Tensor& scales_in,
+    const Tensor& rotations_in, const float scale_modifier, Tensor grad_norm_accum, Tensor denom,
+    Tensor max_radii) {
+    const int P = (int)means3D_in.size(0);
+    TORCH_CHECK(views_in.dim() == 2 && views_in.size(1) == (int64_t)P * 10 + 40,
+                "views must be [V, P * 10 + 40] view records");
+    const int V = (int)views_in.size(0);
+    const int M = sh_in.numel() != 0 ? (int)sh_in.size(1) : 0;
+    const at::OptionalDeviceGuard guard(device_of(means3D_in));
+    auto opts = means3D_in.options();
+    Tensor dL_dmeans3D = torch::empty({P, 3}, opts);
+    Tensor dL_dsh = torch::empty({P, M, 3}, opts);
+    Tensor dL_dopacity = torch::empty({P, 1}, opts);
+    Tensor dL_dscales = torch::empty({P, 3}, opts);
+    Tensor dL_drotations = torch::empty({P, 4}, opts);
+    const bool stats = grad_norm_accum.numel() != 0;
+    if (stats) {
+        for (const Tensor* t : {&grad_norm_accum, &denom, &max_radii}) {
+            TORCH_CHECK(t->numel() == P && t->is_contiguous() && t->is_cuda() && t->scalar_type() == torch::kFloat32,
+                        "statistics tensors must be contiguous float32 device tensors with P elements");
+        }
+    }
+    if (P != 0) {
+        const Tensor views = views_in.contiguous(), means3D = means3D_in.contiguous(), sh = sh_in.contiguous(),
+                     scales = scales_in.contiguous(), rotations = rotations_in.contiguous();
+        require_device(views, "views");
+        require_device(means3D, "means3D");
+        check(gs_backward_gaussians_multiview(
+                  P, degree, M, V, fptr(views), fptr(means3D), fptr(sh), fptr(scales), fptr(rotations),
+                  scale_modifier, fptr_mut(dL_dmeans3D), fptr_mut(dL_dsh), fptr_mut(dL_dopacity), fptr_mut(dL_dscales),
+                  fptr_mut(dL_drotations), stats ? grad_norm_accum.data_ptr<float>() : nullptr,
+                  stats ? denom.data_ptr<float>() : nullptr, stats ? max_radii.data_ptr<float>() : nullptr,
+                  stream_of(means3D)),
+              "backward_gaussians_multiview");
+    }
+    return std::make_tuple(dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations);
+}
+
 // base/rasterize_points.cu:198-217
 Tensor MarkVisible(Tensor& means3D_in, Tensor& viewmatrix_in, Tensor& projmatrix_in) {
     const int P = (int)means3D_in.size(0);
@@ -406,6 +477,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("rasterize_gaussians", &RasterizeGaussians);
     m.def("rasterize_gaussians_backward", &RasterizeGaussiansBackward);
     m.def("mark_visible", &MarkVisible);
+    m.def("rasterize_gaussians_backward_view_grads", &RasterizeGaussiansBackwardViewGrads);
+    m.def("backward_gaussians_multiview", &BackwardGaussiansMultiview);
     m.def("amr_rasterize_gaussians", &AMRRasterizeGaussians);
     m.def("distCUDA2", &DistCUDA2);
     m.def("parse_buffers", &ParseBuffers);

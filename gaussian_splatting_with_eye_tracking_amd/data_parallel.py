@@ -14,6 +14,19 @@ Gradients are written into one flat HBM buffer that is all-reduced in
 place: no per-tensor launches, no concatenation copy after the backward,
 and replicas stay bit-identical because the ring all-reduce hands every rank
 the same bits.  The same code runs on ``gloo`` for the CPU tests.
+
+The default exchange ("views") moves less: the per-Gaussian backward
+(base/cr/backward.cu:20-396) is linear in the 9 screen-space sums the blend
+backward produces, given the view's camera, radius and SH clamp bits.  Each
+rank therefore runs only the blend backward of its view and packs a VIEW
+RECORD (10 words per Gaussian + the 40-word camera, gsplat_amd.h); one
+all-gather hands every rank all N records, and one multi-view kernel forms
+the sum over the N views of the parameter gradients (and, for training,
+the per-view densification statistics), reading the parameters once.  Per
+rank that is (N-1) x 40 B per Gaussian received instead of a ring
+all-reduce's 2 (N-1)/N x 236 B -- 6x less at N = 2, 1.5x less at N = 8 --
+and every rank computes the same sum in the same view order, so replicas
+stay bit-identical.
 """
 from __future__ import annotations
 
@@ -23,6 +36,12 @@ import torch
 import torch.distributed as dist
 
 PARAM_ORDER: Tuple[str, ...] = ("means3D", "shs", "opacities", "scales", "rotations")
+VIEW_ROW = 10    # words per Gaussian in a view record
+CAM_WORDS = 40   # camera words closing a view record
+
+
+def view_record_numel(P: int) -> int:
+    return P * VIEW_ROW + CAM_WORDS
 
 
 class FlatGrads:
@@ -75,3 +94,55 @@ def grads_of(params: Dict[str, torch.Tensor], order: Iterable[str] = PARAM_ORDER
 
 def flat_numel_per_gaussian(sh_coeffs: int = 16) -> int:
     return 3 + 3 * sh_coeffs + 1 + 3 + 4  # 59 at SH degree 3
+
+
+# ------------------------------------------------------------ view exchange ---
+def gather_view_records(record: torch.Tensor, group=None) -> torch.Tensor:
+    """All ranks' view records, [world, P * 10 + 40], in rank order (one
+    RCCL all-gather; on gloo the list form)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return record.unsqueeze(0)
+    world = dist.get_world_size(group)
+    out = torch.empty((world, record.numel()), dtype=record.dtype, device=record.device)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(out, record.contiguous(), group=group)
+    else:
+        dist.all_gather(list(out.unbind(0)), record.contiguous(), group=group)
+    return out
+
+
+def view_record(settings, radii: torch.Tensor, geom: torch.Tensor, num_rendered: int, binning: torch.Tensor,
+                img: torch.Tensor, dL_dpix: torch.Tensor, colors_precomp: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Stage 1: the blend backward of one rendered view -> its view record."""
+    from . import _C
+    e = torch.empty(0, device=dL_dpix.device) if colors_precomp is None else colors_precomp
+    return _C.rasterize_gaussians_backward_view_grads(
+        settings.bg, radii, e, settings.viewmatrix, settings.projmatrix, settings.tanfovx, settings.tanfovy,
+        settings.campos, dL_dpix, geom, num_rendered, binning, img, settings.debug)
+
+
+def multiview_param_grads(views: torch.Tensor, means3D: torch.Tensor, shs: torch.Tensor, sh_degree: int,
+                          scales: torch.Tensor, rotations: torch.Tensor, scale_modifier: float = 1.0,
+                          stats: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None):
+    """Stage 2: sum over the gathered views of the parameter gradients:
+    (dL_dmeans3D, dL_dshs, dL_dopacities, dL_dscales, dL_drotations).  With
+    stats = (xyz_gradient_accum, denom, max_radii2D) the densification
+    statistics of every view are accumulated in place (train.py:111-113)."""
+    from . import _C
+    e = torch.empty(0, device=means3D.device)
+    st = stats if stats is not None else (e, e, e)
+    return _C.backward_gaussians_multiview(views, means3D, shs if shs is not None else e, int(sh_degree), scales,
+                                           rotations, float(scale_modifier), st[0], st[1], st[2])
+
+
+def exchange_view_grads(settings, fwd, dL_dpix: torch.Tensor, means3D: torch.Tensor, shs: torch.Tensor,
+                        scales: torch.Tensor, rotations: torch.Tensor, group=None, stats=None):
+    """The data-parallel backward of one step: this rank's view record,
+    all-gathered, then the multi-view parameter gradients (identical bits on
+    every rank).  fwd = (num_rendered, color, radii, geom, binning, img) as
+    returned by _C.rasterize_gaussians."""
+    num_rendered, _color, radii, geom, binning, img = fwd
+    rec = view_record(settings, radii, geom, num_rendered, binning, img, dL_dpix)
+    views = gather_view_records(rec, group)
+    return multiview_param_grads(views, means3D, shs, settings.sh_degree, scales, rotations, settings.scale_modifier,
+                                 stats)

@@ -68,6 +68,36 @@ int gs_rasterizer_backward(int P, int D, int M, int R, const float* background, 
                            float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
                            float* dL_dsh, float* dL_dscale, float* dL_drot, int debug, void* stream);
 
+/* Data-parallel training (no reference counterpart: the
+ * reference trains one view per step on one GPU, train.py:67-125).
+ *
+ * Stage 1 of the backward of one view: the blend backward only
+ * (base/cr/backward.cu:399-557), written as a VIEW RECORD of P * 10 + 40
+ * floats: per Gaussian dL_dcolor[3], dL_dmean2D.xy[2], dL_dconic (x, y,
+ * w)[3], dL_dopacity, and word 9 = radius | clamped_bits << 24 (bit
+ * pattern; 0 = not visible in this view); then the camera: viewmatrix[16],
+ * projmatrix[16], campos[3], width, height, tan_fovx, tan_fovy, 0.  The
+ * ranks exchange (all-gather) these records instead of parameter
+ * gradients. */
+int gs_rasterizer_backward_view_grads(int P, int R, const float* background, int width, int height,
+                                      const float* colors_precomp, const float* viewmatrix, const float* projmatrix,
+                                      const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                                      char* geom_buffer, char* binning_buffer, char* img_buffer,
+                                      const float* dL_dpix, float* out_record, int debug, void* stream);
+
+/* Stage 2: the per-Gaussian backward (base/cr/backward.cu:20-396) of V views
+ * at once, summed over the views in view order; views = V stage-1 records
+ * back to back (device).  Writes every element of dL_dmeans3D[P][3],
+ * dL_dsh[P][M][3] (if shs), dL_dopacity[P], dL_dscales[P][3],
+ * dL_drotations[P][4].  If grad_norm_accum is non-null, the densification
+ * statistics of every view (train.py:111-113) are accumulated into
+ * grad_norm_accum[P], denom[P], max_radii[P] (float), view by view. */
+int gs_backward_gaussians_multiview(int P, int D, int M, int V, const float* views, const float* means3D,
+                                    const float* shs, const float* scales, const float* rotations,
+                                    float scale_modifier, float* dL_dmeans3D, float* dL_dsh, float* dL_dopacity,
+                                    float* dL_dscales, float* dL_drotations, float* grad_norm_accum, float* denom,
+                                    float* max_radii, void* stream);
+
 /* Replaces CudaRasterizer::Rasterizer::markVisible
  * (base/cr/rasterizer.h:24-29, base/cr/rasterizer_impl.cu:141-153). */
 int gs_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -102,3 +102,47 @@ def test_two_rank_gradient_allreduce():
     np.testing.assert_allclose(outs[0][1], accs[0] + accs[1], rtol=1e-6)
     np.testing.assert_array_equal(outs[0][2], dens[0] + dens[1])
     np.testing.assert_array_equal(outs[0][3], np.maximum(rads[0], rads[1]))
+
+
+def _gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+        P = 1000
+        rec = torch.arange(DP.view_record_numel(P), dtype=torch.float32) * (rank + 1) + 0.25 * rank
+        views = DP.gather_view_records(rec)
+        q.put((rank, views.numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_view_record_all_gather_rank_order():
+    """The "views" exchange: every rank receives all ranks' view records, in
+    rank order, bit-identically (the multi-view backward then sums the views
+    in that order on every rank, test_gpu_multiview.py)."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = {}
+    for _ in range(world):
+        rank, views = q.get(timeout=240)
+        outs[rank] = views
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import sys
+    sys.path.insert(0, ROOT)
+    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+    n = DP.view_record_numel(1000)
+    exp = np.stack([np.arange(n, dtype=np.float32) * (r + 1) + np.float32(0.25 * r) for r in range(world)])
+    for r in range(world):
+        assert outs[r].shape == (world, n)
+        np.testing.assert_array_equal(outs[r], exp)

@@ -1,0 +1,110 @@
+"""Data-parallel view exchange (data_parallel.py, gsplat_amd.h stages 1-2).
+
+The multi-view per-Gaussian backward over V gathered view records must equal
+the sum over the V views of the reference-API backward
+(_C.rasterize_gaussians_backward, itself pinned to the oracle in
+test_gpu_parity.py).  Both sides run the blend backward separately, whose
+float atomics add in a run-dependent order, so the bar is the atomic-order
+noise (1e-5 relative) far inside the north_star's 1e-4; the densification
+statistics must match the per-view densify_stats kernel applied view by view.
+"""
+import numpy as np
+import pytest
+
+import gs_helpers as G
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+REL = 1e-5
+
+
+def _views(P, W, H, yaws, seed=0):
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    cam0 = S.make_camera(W, H)
+    sc = S.make_scene(P, cam0, seed=seed)
+    cams = [S.make_orbit_camera(W, H, y) for y in yaws]
+    return sc, cams
+
+
+def _forward(C, s, t):
+    e = torch.Tensor([])
+    return C.rasterize_gaussians(s.bg, t["means3D"], e, t["opacities"], t["scales"], t["rotations"], 1.0, e,
+                                 s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width,
+                                 t["shs"], 3, s.campos, False, False)
+
+
+def _full_backward(C, s, t, fwd, dpix):
+    K, color, radii, geom, binning, img = fwd
+    e = torch.Tensor([])
+    return C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, e, t["scales"], t["rotations"], 1.0, e,
+                                          s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, dpix, t["shs"], 3,
+                                          s.campos, geom, K, binning, img, False)
+
+
+@pytest.mark.parametrize("yaws", [(0.0,), (-5.0, 0.0, 5.0), (-12.0, -3.0, 4.0, 9.0, 15.0)])
+def test_multiview_equals_sum_of_view_backwards(yaws):
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    P, W, H = 20000, 256, 192
+    sc, cams = _views(P, W, H, yaws)
+    t = G.scene_tensors(sc)
+    want = None
+    records = []
+    stats_ref = [torch.zeros(P, device="cuda") for _ in range(3)]
+    for v, cam in enumerate(cams):
+        s = G.torch_settings(cam)
+        dpix = torch.from_numpy(S.make_cotangent(H, W, 10 + v)).cuda()
+        fwd = _forward(C, s, t)
+        g = _full_backward(C, s, t, fwd, dpix)
+        # (dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations) of this view
+        per = [g[3], g[5], g[2], g[6], g[7]]
+        want = [x.double().clone() for x in per] if want is None else [a + x.double() for a, x in zip(want, per)]
+        C.densify_stats(fwd[2].contiguous(), g[0], stats_ref[0], stats_ref[1], stats_ref[2])
+        records.append(DP.view_record(s, fwd[2], fwd[3], fwd[0], fwd[4], fwd[5], dpix))
+    views = torch.stack(records)
+    stats = [torch.zeros(P, device="cuda") for _ in range(3)]
+    got = DP.multiview_param_grads(views, t["means3D"], t["shs"], 3, t["scales"], t["rotations"], 1.0,
+                                   stats=tuple(stats))
+    torch.cuda.synchronize()
+    names = ("dL_dmeans3D", "dL_dsh", "dL_dopacity", "dL_dscales", "dL_drotations")
+    for name, a, b in zip(names, got, want):
+        assert a.shape == b.shape, name
+        assert np.isfinite(a.cpu().numpy()).all(), name
+        err = G.rel_err(a.cpu().numpy(), b.cpu().numpy())
+        assert err < REL, (name, err)
+    # statistics: the same per-view quantities, accumulated view by view
+    assert G.rel_err(stats[0].cpu().numpy(), stats_ref[0].cpu().numpy()) < REL
+    np.testing.assert_array_equal(stats[1].cpu().numpy(), stats_ref[1].cpu().numpy())
+    np.testing.assert_array_equal(stats[2].cpu().numpy(), stats_ref[2].cpu().numpy())
+
+
+def test_view_record_layout():
+    """Word 9 = radius | clamped << 24, zero rows for invisible Gaussians, and
+    the 40 camera words closing the record."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    P, W, H = 5000, 128, 96
+    sc, cams = _views(P, W, H, (7.0,))
+    s = G.torch_settings(cams[0])
+    t = G.scene_tensors(sc)
+    dpix = torch.from_numpy(S.make_cotangent(H, W, 3)).cuda()
+    fwd = _forward(C, s, t)
+    rec = DP.view_record(s, fwd[2], fwd[3], fwd[0], fwd[4], fwd[5], dpix).cpu().numpy()
+    rows = rec[:P * 10].reshape(P, 10)
+    w9 = rows[:, 9].view(np.uint32)
+    radii = fwd[2].cpu().numpy()
+    np.testing.assert_array_equal((w9 & 0xFFFFFF).astype(np.int64), np.maximum(radii, 0).astype(np.int64))
+    assert (rows[radii <= 0] == 0).all()
+    bufs = C.parse_buffers(fwd[3], fwd[4], fwd[5], P, fwd[0], W, H, 16)
+    cb = bufs["clamped_bits"].cpu().numpy().astype(np.uint32)
+    vis = radii > 0
+    np.testing.assert_array_equal(w9[vis] >> 24, cb[vis])
+    cam = rec[P * 10:]
+    np.testing.assert_array_equal(cam[:16], s.viewmatrix.cpu().numpy().ravel())
+    np.testing.assert_array_equal(cam[16:32], s.projmatrix.cpu().numpy().ravel())
+    np.testing.assert_array_equal(cam[32:35], s.campos.cpu().numpy())
+    assert cam[35] == W and cam[36] == H
+    assert cam[37] == np.float32(s.tanfovx) and cam[38] == np.float32(s.tanfovy)

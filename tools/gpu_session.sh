@@ -51,6 +51,8 @@ for step in "$@"; do
     pmc_sq2) run pmc_sq2 600 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_bwd_a) run pmc_bwd_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_bwd_a -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_bwd_b) run pmc_bwd_b 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_bwd_b -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
+    mv) run pytest_mv 400 python -m pytest tests/test_gpu_multiview.py -q -m gpu -p no:cacheprovider --timeout 300 -rf &&
+        run bench_exchange 400 python tools/bench_exchange.py ;;
     gputrain) run pytest_gpu_train 600 python -m pytest tests/test_gpu_training.py tests/test_loss.py -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     train) run bench_train 600 python tools/bench_train.py ;;
     proftrain) run rocprof_train 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python3 tools/bench_train.py --reps 10 ;;
