@@ -898,10 +898,11 @@ void launch_pack_view_grads(int P, const GeomView& g, const int* radii, bool has
 // max_radii = max(max_radii, radius) for every view that sees the Gaussian.
 template <bool kHasSH, bool kSH16>
 __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= a.P) return;
-    const float* rows = a.views + (size_t)idx * kViewRow;
-    const size_t vstride = (size_t)a.P * kViewRow + kCamWords;  // view records back to back
+    const int local = blockIdx.x * 256 + threadIdx.x;
+    if (local >= a.count) return;
+    const int idx = a.g0 + local;
+    const float* rows = a.rows + (size_t)local * kViewRow;
+    const size_t vstride = a.row_view_stride;
     bool any = false;
     for (int v = 0; v < a.V; v++) any |= __float_as_uint(rows[v * vstride + 9]) != 0u;
     const int ncoef_out = a.M;
@@ -969,7 +970,7 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
             acc[2 * q + 1] = t.y;
         }
         acc[8] = row[8];
-        const float* cam = a.views + v * vstride + (size_t)a.P * kViewRow;
+        const float* cam = a.cams + v * a.cam_stride;
         const Mat4 V = load_mat4(cam);
         const Mat4 Pm = load_mat4(cam + 16);
         const float tan_fovx = cam[37], tan_fovy = cam[38];
@@ -1035,8 +1036,8 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
 }
 
 void launch_multiview_backward(const MultiViewArgs& a, hipStream_t s) {
-    if (a.P == 0) return;
-    const dim3 grid((a.P + 255) / 256);
+    if (a.count <= 0) return;
+    const dim3 grid((a.count + 255) / 256);
     const bool sh = a.shs != nullptr;
     if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward_kernel<true, true>), grid, dim3(256), 0, s, a);
     else if (sh) hipLaunchKernelGGL((multiview_backward_kernel<true, false>), grid, dim3(256), 0, s, a);

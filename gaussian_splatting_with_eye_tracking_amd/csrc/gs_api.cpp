@@ -341,14 +341,16 @@ int gs_rasterizer_backward_view_grads(int P, int R, const float* background, int
     });
 }
 
-int gs_backward_gaussians_multiview(int P, int D, int M, int V, const float* views, const float* means3D,
-                                    const float* shs, const float* scales, const float* rotations,
-                                    float scale_modifier, float* dL_dmeans3D, float* dL_dsh, float* dL_dopacity,
-                                    float* dL_dscales, float* dL_drotations, float* grad_norm_accum, float* denom,
-                                    float* max_radii, void* stream) {
+namespace {
+int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* rows, size_t row_view_stride,
+                   const float* cams, size_t cam_stride, const float* means3D, const float* shs, const float* scales,
+                   const float* rotations, float scale_modifier, float* dL_dmeans3D, float* dL_dsh,
+                   float* dL_dopacity, float* dL_dscales, float* dL_drotations, float* grad_norm_accum, float* denom,
+                   float* max_radii, void* stream) {
     return guarded([&]() -> int {
-        if (P <= 0) return 0;
+        if (P <= 0 || count == 0) return 0;
         if (V <= 0) throw GsError("gs_backward_gaussians_multiview: V must be positive");
+        if (g0 < 0 || count < 0 || g0 + count > P) throw GsError("gs_backward_gaussians_multiview: bad range");
         if (!scales || !rotations)
             throw GsError("gs_backward_gaussians_multiview: scales and rotations are required (no cov3D_precomp)");
         if (shs && (M <= 0 || M > 16 || D < 0 || D > 3))
@@ -357,7 +359,12 @@ int gs_backward_gaussians_multiview(int P, int D, int M, int V, const float* vie
             throw GsError("gs_backward_gaussians_multiview: statistics need grad_norm_accum, denom and max_radii");
         MultiViewArgs a;
         a.P = P; a.D = D; a.M = M; a.V = V;
-        a.views = views;
+        a.g0 = g0;
+        a.count = count;
+        a.rows = rows;
+        a.row_view_stride = row_view_stride;
+        a.cams = cams;
+        a.cam_stride = cam_stride;
         a.means3D = means3D;
         a.shs = shs;
         a.scales = scales;
@@ -376,6 +383,30 @@ int gs_backward_gaussians_multiview(int P, int D, int M, int V, const float* vie
         stage_check(false, s, "multiview_backward");
         return 0;
     });
+}
+}  // namespace
+
+int gs_backward_gaussians_multiview(int P, int D, int M, int V, const float* views, const float* means3D,
+                                    const float* shs, const float* scales, const float* rotations,
+                                    float scale_modifier, float* dL_dmeans3D, float* dL_dsh, float* dL_dopacity,
+                                    float* dL_dscales, float* dL_drotations, float* grad_norm_accum, float* denom,
+                                    float* max_radii, void* stream) {
+    const size_t rec = (size_t)P * kViewRow + kCamWords;
+    return multiview_impl(P, 0, P, D, M, V, views, rec, views + (size_t)P * kViewRow, rec, means3D, shs, scales,
+                          rotations, scale_modifier, dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations,
+                          grad_norm_accum, denom, max_radii, stream);
+}
+
+int gs_backward_gaussians_multiview_range(int P, int g0, int count, int D, int M, int V, const float* rows,
+                                          size_t row_view_stride, const float* cams, size_t cam_stride,
+                                          const float* means3D, const float* shs, const float* scales,
+                                          const float* rotations, float scale_modifier, float* dL_dmeans3D,
+                                          float* dL_dsh, float* dL_dopacity, float* dL_dscales,
+                                          float* dL_drotations, float* grad_norm_accum, float* denom,
+                                          float* max_radii, void* stream) {
+    return multiview_impl(P, g0, count, D, M, V, rows, row_view_stride, cams, cam_stride, means3D, shs, scales,
+                          rotations, scale_modifier, dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations,
+                          grad_norm_accum, denom, max_radii, stream);
 }
 
 int gs_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

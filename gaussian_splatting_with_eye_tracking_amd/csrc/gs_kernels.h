@@ -107,7 +107,11 @@ constexpr int kViewRow = 10;   // words per Gaussian per view
 constexpr int kCamWords = 40;  // view 16, proj 16, campos 3, W, H, tan_fovx, tan_fovy, pad
 struct MultiViewArgs {
     int P, D, M, V;
-    const float* views;  // [V] view records: [P][kViewRow] rows, then [kCamWords] camera
+    int g0, count;           // this launch: Gaussians [g0, g0 + count)
+    const float* rows;       // view 0's row of Gaussian g0 ([kViewRow] words per Gaussian)
+    size_t row_view_stride;  // floats from one view's rows to the next view's
+    const float* cams;       // view 0's camera ([kCamWords])
+    size_t cam_stride;       // floats from one view's camera to the next
     const float* means3D;
     const float* shs;  // nullable (colors precomputed: no SH gradient)
     const float* scales;

@@ -267,6 +267,48 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> BackwardGaussiansMultiview(
     return std::make_tuple(dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations);
 }
 
+// Chunked stage 2: rows [V, count * 10] (view v's rows of Gaussians [g0,
+// g0 + count)), cams [V, 40]; writes that range of the caller's full-size
+// output tensors (and statistics, when non-empty).
+void BackwardGaussiansMultiviewRange(const Tensor& rows_in, const Tensor& cams_in, const int g0,
+                                     const Tensor& means3D_in, const Tensor& sh_in, const int degree,
+                                     const Tensor& scales_in, const Tensor& rotations_in, const float scale_modifier,
+                                     Tensor dL_dmeans3D, Tensor dL_dsh, Tensor dL_dopacity, Tensor dL_dscales,
+                                     Tensor dL_drotations, Tensor grad_norm_accum, Tensor denom, Tensor max_radii) {
+    const int P = (int)means3D_in.size(0);
+    TORCH_CHECK(rows_in.dim() == 2 && rows_in.size(1) % 10 == 0, "rows must be [V, count * 10]");
+    const int V = (int)rows_in.size(0);
+    const int count = (int)(rows_in.size(1) / 10);
+    TORCH_CHECK(cams_in.dim() == 2 && cams_in.size(0) == V && cams_in.size(1) == 40, "cams must be [V, 40]");
+    TORCH_CHECK(g0 >= 0 && g0 + count <= P, "Gaussian range out of bounds");
+    const int M = sh_in.numel() != 0 ? (int)sh_in.size(1) : 0;
+    for (const Tensor* t : {&dL_dmeans3D, &dL_dopacity, &dL_dscales, &dL_drotations})
+        TORCH_CHECK(t->is_contiguous() && t->size(0) == P && t->scalar_type() == torch::kFloat32,
+                    "outputs must be contiguous float32 [P, ...] tensors");
+    TORCH_CHECK(M == 0 || (dL_dsh.is_contiguous() && dL_dsh.numel() == (int64_t)P * M * 3), "dL_dsh must be [P, M, 3]");
+    const bool stats = grad_norm_accum.numel() != 0;
+    if (stats) {
+        for (const Tensor* t : {&grad_norm_accum, &denom, &max_radii}) {
+            TORCH_CHECK(t->numel() == P && t->is_contiguous() && t->is_cuda() && t->scalar_type() == torch::kFloat32,
+                        "statistics tensors must be contiguous float32 device tensors with P elements");
+        }
+    }
+    const at::OptionalDeviceGuard guard(device_of(means3D_in));
+    TORCH_CHECK(rows_in.stride(1) == 1 && cams_in.stride(1) == 1, "rows / cams rows must be contiguous");
+    const Tensor means3D = means3D_in.contiguous(), sh = sh_in.contiguous(), scales = scales_in.contiguous(),
+                 rotations = rotations_in.contiguous();
+    require_device(rows_in, "rows");
+    require_device(cams_in, "cams");
+    check(gs_backward_gaussians_multiview_range(
+              P, g0, count, degree, M, V, rows_in.data_ptr<float>(), (size_t)rows_in.stride(0), cams_in.data_ptr<float>(),
+              (size_t)cams_in.stride(0), fptr(means3D), fptr(sh), fptr(scales), fptr(rotations), scale_modifier,
+              fptr_mut(dL_dmeans3D), M ? fptr_mut(dL_dsh) : nullptr, fptr_mut(dL_dopacity), fptr_mut(dL_dscales),
+              fptr_mut(dL_drotations), stats ? grad_norm_accum.data_ptr<float>() : nullptr,
+              stats ? denom.data_ptr<float>() : nullptr, stats ? max_radii.data_ptr<float>() : nullptr,
+              stream_of(means3D)),
+          "backward_gaussians_multiview_range");
+}
+
 // base/rasterize_points.cu:198-217
 Tensor MarkVisible(Tensor& means3D_in, Tensor& viewmatrix_in, Tensor& projmatrix_in) {
     const int P = (int)means3D_in.size(0);
@@ -479,6 +521,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("mark_visible", &MarkVisible);
     m.def("rasterize_gaussians_backward_view_grads", &RasterizeGaussiansBackwardViewGrads);
     m.def("backward_gaussians_multiview", &BackwardGaussiansMultiview);
+    m.def("backward_gaussians_multiview_range", &BackwardGaussiansMultiviewRange);
     m.def("amr_rasterize_gaussians", &AMRRasterizeGaussians);
     m.def("distCUDA2", &DistCUDA2);
     m.def("parse_buffers", &ParseBuffers);

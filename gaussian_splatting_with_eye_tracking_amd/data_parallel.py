@@ -136,13 +136,57 @@ def multiview_param_grads(views: torch.Tensor, means3D: torch.Tensor, shs: torch
 
 
 def exchange_view_grads(settings, fwd, dL_dpix: torch.Tensor, means3D: torch.Tensor, shs: torch.Tensor,
-                        scales: torch.Tensor, rotations: torch.Tensor, group=None, stats=None):
+                        scales: torch.Tensor, rotations: torch.Tensor, group=None, stats=None, chunks: int = 4):
     """The data-parallel backward of one step: this rank's view record,
     all-gathered, then the multi-view parameter gradients (identical bits on
     every rank).  fwd = (num_rendered, color, radii, geom, binning, img) as
-    returned by _C.rasterize_gaussians."""
+    returned by _C.rasterize_gaussians.
+
+    With more than one rank the gather is split into `chunks` ranges of
+    Gaussians, all issued asynchronously up front: the RCCL stream moves
+    chunk c + 1 while the compute stream runs the multi-view backward of
+    chunk c (each chunk's work waits only for its own collective), so at
+    most one chunk's backward is exposed after the last transfer."""
     num_rendered, _color, radii, geom, binning, img = fwd
     rec = view_record(settings, radii, geom, num_rendered, binning, img, dL_dpix)
-    views = gather_view_records(rec, group)
-    return multiview_param_grads(views, means3D, shs, settings.sh_degree, scales, rotations, settings.scale_modifier,
-                                 stats)
+    return exchange_view_records(rec, settings, means3D, shs, scales, rotations, group, stats, chunks)
+
+
+def exchange_view_records(rec: torch.Tensor, settings, means3D: torch.Tensor, shs: torch.Tensor,
+                          scales: torch.Tensor, rotations: torch.Tensor, group=None, stats=None, chunks: int = 4):
+    """exchange_view_grads from this rank's view record on: the (chunked)
+    all-gather and the multi-view parameter backward."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1 or chunks <= 1:
+        views = gather_view_records(rec, group)
+        return multiview_param_grads(views, means3D, shs, settings.sh_degree, scales, rotations,
+                                     settings.scale_modifier, stats)
+    from . import _C
+    world = dist.get_world_size(group)
+    P = means3D.shape[0]
+    nccl = dist.get_backend(group) == "nccl"
+
+    def gather_async(src: torch.Tensor) -> Tuple[torch.Tensor, object]:
+        out = torch.empty((world, src.numel()), dtype=src.dtype, device=src.device)
+        if nccl:
+            w = dist.all_gather_into_tensor(out, src, group=group, async_op=True)
+        else:
+            w = dist.all_gather(list(out.unbind(0)), src, group=group, async_op=True)
+        return out, w
+
+    cams, w_cam = gather_async(rec[P * VIEW_ROW:])
+    step = -(-P // chunks)
+    bounds = [(a, min(P, a + step)) for a in range(0, P, step)]
+    pending = [(a, b) + gather_async(rec[a * VIEW_ROW:b * VIEW_ROW]) for a, b in bounds]
+    dev = means3D.device
+    M = shs.shape[1] if shs is not None and shs.numel() else 0
+    outs = (torch.empty((P, 3), device=dev), torch.empty((P, M, 3), device=dev), torch.empty((P, 1), device=dev),
+            torch.empty((P, 3), device=dev), torch.empty((P, 4), device=dev))
+    e = torch.empty(0, device=dev)
+    st = stats if stats is not None else (e, e, e)
+    w_cam.wait()
+    for a, b, rows, w in pending:
+        w.wait()
+        _C.backward_gaussians_multiview_range(rows, cams, a, means3D, shs if shs is not None else e,
+                                              int(settings.sh_degree), scales, rotations,
+                                              float(settings.scale_modifier), *outs, st[0], st[1], st[2])
+    return outs

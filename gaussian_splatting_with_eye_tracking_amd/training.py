@@ -385,6 +385,47 @@ class FlatGaussianModel:
         return pkg, {"loss": out3[0], "l1": out3[1], "ssim": out3[2]}
 
 
+def render_and_backward_views(model: FlatGaussianModel, settings: GaussianRasterizationSettings,
+                              gt_image: torch.Tensor, lambda_dssim: float, stats: bool, group=None):
+    """The data-parallel fused iteration with the "views" exchange
+    (data_parallel.py): activate -> forward -> fused loss -> blend backward
+    of this rank's view -> all-gather of the view records -> multi-view
+    parameter backward (the sum over all ranks' views, identical on every
+    rank) -> activation backward into the flat gradient buffer.  With stats
+    the densification statistics of every rank's view are accumulated too
+    (train.py:111-113), so no statistics all-reduce is needed afterwards."""
+    from . import data_parallel as DP
+    s = settings._replace(sh_degree=model.active_sh_degree)
+    raw = {g: model.group_view(model.params, g) for g in GROUPS}
+    a = model._act
+    _C.activate(raw["f_dc"], raw["f_rest"], raw["opacity"], raw["scaling"], raw["rotation"], a["shs"],
+                a["opacities"], a["scales"], a["rotations"])
+    e = torch.empty(0, device=model.device)
+    xyz = raw["xyz"]
+    fwd = _C.rasterize_gaussians(
+        s.bg, xyz, e, a["opacities"], a["scales"], a["rotations"], s.scale_modifier, e, s.viewmatrix,
+        s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, a["shs"], s.sh_degree, s.campos,
+        s.prefiltered, s.debug)
+    num_rendered, color, radii, geom, binning, img = fwd
+    out3, d_image = _C.l1_ssim_loss(color, gt_image, float(lambda_dssim))
+    st = (model.xyz_gradient_accum, model.denom, model.max_radii2D) if stats else None
+    d_means3D, d_shs, d_opac, d_scales, d_rot = DP.exchange_view_grads(
+        s, fwd, d_image, xyz, a["shs"], a["scales"], a["rotations"], group=group, stats=st)
+    gv = {g: model.group_view(model.grads, g) for g in GROUPS}
+    _C.activation_backward(d_shs, d_opac, d_scales, d_rot, d_means3D, raw["opacity"], raw["scaling"],
+                           raw["rotation"], gv["xyz"], gv["f_dc"], gv["f_rest"], gv["opacity"], gv["scaling"],
+                           gv["rotation"], False)
+    model._grads_stale = False
+    model.mark_backward()
+    pkg = {"render": color, "viewspace_grad": None, "visibility_filter": radii > 0, "radii": radii,
+           "stats_done": stats}
+    return pkg, {"loss": out3[0], "l1": out3[1], "ssim": out3[2]}
+
+
+def _world(group=None) -> int:
+    return dist.get_world_size(group) if (dist.is_available() and dist.is_initialized()) else 1
+
+
 def allreduce_training_grads(model: FlatGaussianModel, group=None) -> None:
     """the one data-path exchange -- the flat gradient buffer,
     summed over the ranks' views with one RCCL all-reduce."""
@@ -403,17 +444,22 @@ def reduce_densification_stats(model: FlatGaussianModel, group=None) -> None:
 
 
 def forward_backward(model: FlatGaussianModel, iteration: int, settings: GaussianRasterizationSettings,
-                     gt_image: torch.Tensor, group=None, fused: bool = True):
+                     gt_image: torch.Tensor, group=None, fused: bool = True, exchange: str = "views"):
     """train.py:76-93 + the backward: learning-rate schedule, SH degree step,
     render, fused L1 + D-SSIM loss, backward into the flat gradient buffer,
     all-reduce over the data-parallel ranks.  fused=True runs the
     autograd-free native sequence (render_and_backward); fused=False the
     reference-shaped one (torch activations + the drop-in autograd
     rasterizer + autograd).  Returns (render package, loss terms as device
-    tensors); pkg["viewspace_grad"] is dL/dmeans2D."""
+    tensors); pkg["viewspace_grad"] is dL/dmeans2D.  With more than one rank
+    and exchange="views" (fused only) the ranks exchange view records instead
+    of all-reducing the gradients (data_parallel.py)."""
     model.update_learning_rate(iteration)
     if iteration % 1000 == 0:
         model.oneupSHdegree()
+    if fused and exchange == "views" and _world(group) > 1:
+        return render_and_backward_views(model, settings, gt_image, model.opt.lambda_dssim,
+                                         stats=iteration < model.opt.densify_until_iter, group=group)
     if fused:
         pkg, terms = model.render_and_backward(settings, gt_image, model.opt.lambda_dssim)
     else:
@@ -433,10 +479,13 @@ def post_backward(model: FlatGaussianModel, iteration: int, pkg, scene_extent: f
     """train.py:108-125: densification statistics, densify / prune / opacity
     reset on the reference's schedule, Adam, zero_grad."""
     o = model.opt
+    views_stats = pkg.get("stats_done", False)  # every view's statistics already accumulated on every rank
     if iteration < o.densify_until_iter:
-        model.add_densification_stats(pkg["viewspace_grad"], pkg["radii"])
+        if not views_stats:
+            model.add_densification_stats(pkg["viewspace_grad"], pkg["radii"])
         if iteration > o.densify_from_iter and iteration % o.densification_interval == 0:
-            reduce_densification_stats(model, group)
+            if not views_stats:
+                reduce_densification_stats(model, group)
             size_threshold = 20 if iteration > o.opacity_reset_interval else None
             model.densify_and_prune(o.densify_grad_threshold, 0.005, scene_extent, size_threshold)
         if iteration % o.opacity_reset_interval == 0 or (white_background and iteration == o.densify_from_iter):
@@ -448,9 +497,9 @@ def post_backward(model: FlatGaussianModel, iteration: int, pkg, scene_extent: f
 
 def training_iteration(model: FlatGaussianModel, iteration: int, settings: GaussianRasterizationSettings,
                        gt_image: torch.Tensor, scene_extent: float, white_background: bool = False,
-                       group=None, fused: bool = True) -> Dict[str, torch.Tensor]:
+                       group=None, fused: bool = True, exchange: str = "views") -> Dict[str, torch.Tensor]:
     """One iteration of train.py:67-125 (minus logging / saving / the GUI).
     Returns the loss terms as device tensors (no host sync)."""
-    pkg, terms = forward_backward(model, iteration, settings, gt_image, group, fused)
+    pkg, terms = forward_backward(model, iteration, settings, gt_image, group, fused, exchange)
     post_backward(model, iteration, pkg, scene_extent, white_background, group, fused)
     return terms

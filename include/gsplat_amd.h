@@ -98,6 +98,20 @@ int gs_backward_gaussians_multiview(int P, int D, int M, int V, const float* vie
                                     float* dL_dscales, float* dL_drotations, float* grad_norm_accum, float* denom,
                                     float* max_radii, void* stream);
 
+/* The same for Gaussians [g0, g0 + count) with the rows and cameras of the V
+ * views anywhere in device memory: view v's row of Gaussian g0 + i at
+ * rows + v * row_view_stride + 10 i, its camera at cams + v * cam_stride.
+ * Lets the exchange run chunk by chunk (the all-gather of chunk c + 1
+ * overlapping the backward of chunk c). Outputs and statistics are indexed
+ * by the global Gaussian index. */
+int gs_backward_gaussians_multiview_range(int P, int g0, int count, int D, int M, int V, const float* rows,
+                                          size_t row_view_stride, const float* cams, size_t cam_stride,
+                                          const float* means3D, const float* shs, const float* scales,
+                                          const float* rotations, float scale_modifier, float* dL_dmeans3D,
+                                          float* dL_dsh, float* dL_dopacity, float* dL_dscales,
+                                          float* dL_drotations, float* grad_norm_accum, float* denom,
+                                          float* max_radii, void* stream);
+
 /* Replaces CudaRasterizer::Rasterizer::markVisible
  * (base/cr/rasterizer.h:24-29, base/cr/rasterizer_impl.cu:141-153). */
 int gs_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -27,6 +27,7 @@ for step in "$@"; do
     bench3) run bench_cfg3 600 python bench.py --config cfg3_amr_1080p_1M --steps 20 --warmup 3 ;;
     bench4) run bench_cfg4 600 python bench.py --config cfg4_bicycle_6M --steps 10 --warmup 3 --no-cpu-baseline ;;
     dist2) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 ;;
+    dist2p) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2p 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --steps 5 --warmup 2 --exchange params ;;
     dist2amr) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2amr 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 5 --warmup 2 --config cfg3_amr_1080p_1M ;;
     benchnp) run bench_np 400 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-profile &&
              run bench_p 400 python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
@@ -51,7 +52,7 @@ for step in "$@"; do
     pmc_sq2) run pmc_sq2 600 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_bwd_a) run pmc_bwd_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_bwd_a -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_bwd_b) run pmc_bwd_b 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_bwd_b -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
-    mv) run pytest_mv 400 python -m pytest tests/test_gpu_multiview.py -q -m gpu -p no:cacheprovider --timeout 300 -rf &&
+    mv) run pytest_mv 400 python -m pytest tests/test_gpu_multiview.py tests/test_gpu_dist_views.py -q -m gpu -p no:cacheprovider --timeout 300 -rf &&
         run bench_exchange 400 python tools/bench_exchange.py ;;
     gputrain) run pytest_gpu_train 600 python -m pytest tests/test_gpu_training.py tests/test_loss.py -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     train) run bench_train 600 python tools/bench_train.py ;;

@@ -36,6 +36,8 @@ STAGES = {
     "amr_render_kernel": "amr_render",
     "amr_levels_kernel": "amr_levels",
     "amr_interpolate_kernel": "amr_interp",
+    "multiview_backward_kernel": "multiview_bwd",
+    "pack_view_grads_kernel": "pack_view",
 }
 
 
