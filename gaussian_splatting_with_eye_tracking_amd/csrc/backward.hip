@@ -385,8 +385,15 @@ __device__ __forceinline__ void load_sh_rows(const BackwardGaussArgs& a, int idx
 // computeColorFromSH backward (backward.cu:20-139), shared part: the
 // per-coefficient factors dsh_c[k] (dL_dsh[k][c] = dsh_c[k] * dRGB[c])
 // and the view-direction term added to dmean (+=).
+// (SH: float[16][3] in registers, or ShRowPtr, a row of 48 coefficients in LDS.)
+struct ShRowPtr {
+    const float* p;
+    __device__ __forceinline__ const float* operator[](int k) const { return p + 3 * k; }
+};
+
+template <typename SH>
 __device__ __forceinline__ void sh_backward_terms(int deg, const float* campos, float mx, float my, float mz,
-                                                  const float (&s)[16][3], uint8_t cb, const float* acc,
+                                                  const SH& s, uint8_t cb, const float* acc,
                                                   float (&dsh_c)[16], float (&dRGB)[3], float (&dmean)[3]) {
     const float dox = mx - campos[0], doy = my - campos[1], doz = mz - campos[2];
     const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
@@ -898,140 +905,172 @@ void launch_pack_view_grads(int P, const GeomView& g, const int* radii, bool has
 // max_radii = max(max_radii, radius) for every view that sees the Gaussian.
 template <bool kHasSH, bool kSH16>
 __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a) {
-    const int local = blockIdx.x * 256 + threadIdx.x;
-    if (local >= a.count) return;
+    // SH16: the workgroup's 256 SH rows staged in LDS (coalesced in, and the
+    // gradient rows coalesced out, as backward_gaussians_kernel), and read
+    // from there by the per-view SH terms: the 48 coefficients do not occupy
+    // registers across the view loop.
+    constexpr bool kStage = kHasSH && kSH16;
+    __shared__ float s_sh[kStage ? 256 * kShRow : 1];
+    const int local0 = blockIdx.x * 256;
+    const int nblk = min(256, a.count - local0);
+    if constexpr (kStage) {
+        const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)(a.g0 + local0) * 12;
+        for (int f = threadIdx.x; f < nblk * 12; f += 256) {
+            const float4 v = in[f];
+            float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
+            r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+        }
+        __syncthreads();
+    }
+    const int local = local0 + threadIdx.x;
+    const bool live = local < a.count;
     const int idx = a.g0 + local;
+    float* lrow = kStage ? s_sh + threadIdx.x * kShRow : nullptr;
     const float* rows = a.rows + (size_t)local * kViewRow;
     const size_t vstride = a.row_view_stride;
     bool any = false;
-    for (int v = 0; v < a.V; v++) any |= __float_as_uint(rows[v * vstride + 9]) != 0u;
-    const int ncoef_out = a.M;
-    if (!any) {
+    if (live)
+        for (int v = 0; v < a.V; v++) any |= __float_as_uint(rows[v * vstride + 9]) != 0u;
+    if (live && !any) {
 #pragma unroll
         for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = 0.f;
-        if (kHasSH)
-            for (int i = 0; i < ncoef_out * 3; i++) a.dL_dsh[(size_t)idx * ncoef_out * 3 + i] = 0.f;
+        if (kStage) {
+#pragma unroll
+            for (int i = 0; i < 48; i++) lrow[i] = 0.f;
+        } else if (kHasSH) {
+            for (int i = 0; i < a.M * 3; i++) a.dL_dsh[(size_t)idx * a.M * 3 + i] = 0.f;
+        }
         a.dL_dopacity[idx] = 0.f;
         for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = 0.f;
         reinterpret_cast<float4*>(a.dL_drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
-        return;
     }
-    const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
-    const float4 qrot = reinterpret_cast<const float4*>(a.rotations)[idx];
-    const float scl[3] = {a.scales[3 * idx + 0], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
-    float cov3D[6];
-    compute_cov3d(scl, qrot, a.scale_modifier, cov3D);
-    float s[16][3];
-    if (kHasSH) {
-        const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
-        const float* sh = a.shs + (size_t)idx * a.M * 3;
-        if (kSH16) {
-            const float4* s4 = reinterpret_cast<const float4*>(sh);
-            float buf[48];
-#pragma unroll
-            for (int i = 0; i < 12; i++) {
-                const float4 v4 = (i * 4 < ncoef * 3) ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-                buf[4 * i + 0] = v4.x; buf[4 * i + 1] = v4.y; buf[4 * i + 2] = v4.z; buf[4 * i + 3] = v4.w;
+    if (live && any) {
+        const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
+        float dmean_t[3] = {0.f, 0.f, 0.f};
+        // ---- pass 1: cov2D + projection terms, opacity, statistics; then the
+        // cov3D backward once on the summed dL/dcov3D
+        {
+            const float4 qrot = reinterpret_cast<const float4*>(a.rotations)[idx];
+            const float scl[3] = {a.scales[3 * idx + 0], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
+            float cov3D[6];
+            compute_cov3d(scl, qrot, a.scale_modifier, cov3D);
+            float dcov_t[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dop = 0.f;
+            float st_acc = 0.f, st_den = 0.f, st_max = 0.f;
+            const bool stats = a.grad_norm_accum != nullptr;
+            if (stats) {
+                st_acc = a.grad_norm_accum[idx];
+                st_den = a.denom[idx];
+                st_max = a.max_radii[idx];
             }
+            for (int v = 0; v < a.V; v++) {
+                const float* row = rows + v * vstride;
+                const uint32_t w9 = __float_as_uint(row[9]);
+                if (w9 == 0u) continue;  // not visible in view v: no terms (the reference's radii > 0 filter)
+                // mean2D.y, conic x, y, w (rows are 40 B: 8-B aligned only)
+                const float2 r1a = *reinterpret_cast<const float2*>(row + 4);
+                const float2 r1b = *reinterpret_cast<const float2*>(row + 6);
+                const float4 r1 = make_float4(r1a.x, r1a.y, r1b.x, r1b.y);
+                const float gx = row[3], dop_v = row[8];
+                const float* cam = a.cams + v * a.cam_stride;
+                const Mat4 V = load_mat4(cam);
+                const Mat4 Pm = load_mat4(cam + 16);
+                const float tan_fovx = cam[37], tan_fovy = cam[38];
+                // rasterizer_impl.cu:222-223 / gs_api.cpp: focal from the image size
+                const float focal_x = cam[35] / (2.0f * tan_fovx);
+                const float focal_y = cam[36] / (2.0f * tan_fovy);
+                float dmean[3], dcov[6];
+                cov2d_backward(mx, my, mz, cov3D, r1.y, r1.z, r1.w, V, focal_x, focal_y, tan_fovx, tan_fovy, dmean,
+                               dcov);
+                proj_backward(mx, my, mz, Pm, gx, r1.x, dmean);
 #pragma unroll
-            for (int k = 0; k < 16; k++)
+                for (int i = 0; i < 3; i++) dmean_t[i] += dmean[i];
 #pragma unroll
-                for (int c = 0; c < 3; c++) s[k][c] = buf[3 * k + c];
-        } else {
+                for (int i = 0; i < 6; i++) dcov_t[i] += dcov[i];
+                dop += dop_v;
+                if (stats) {
+                    st_acc = st_acc + sqrtf(gx * gx + r1.x * r1.x);
+                    st_den = st_den + 1.f;
+                    st_max = fmaxf(st_max, (float)(w9 & 0xFFFFFFu));
+                }
+            }
+            a.dL_dopacity[idx] = dop;
+            float dscale[3];
+            float4 dq;
+            cov3d_backward(qrot, scl, a.scale_modifier, dcov_t, dscale, dq);
 #pragma unroll
-            for (int k = 0; k < 16; k++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) s[k][c] = (k < ncoef) ? sh[3 * k + c] : 0.f;
+            for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = dscale[i];
+            reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
+            if (stats) {
+                a.grad_norm_accum[idx] = st_acc;
+                a.denom[idx] = st_den;
+                a.max_radii[idx] = st_max;
+            }
         }
-    }
-    float dmean_t[3] = {0.f, 0.f, 0.f}, dcov_t[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dop = 0.f;
-    float dsh_t[48];
-#pragma unroll
-    for (int i = 0; i < 48; i++) dsh_t[i] = 0.f;
-    float st_acc = 0.f, st_den = 0.f, st_max = 0.f;
-    const bool stats = a.grad_norm_accum != nullptr;
-    if (stats) {
-        st_acc = a.grad_norm_accum[idx];
-        st_den = a.denom[idx];
-        st_max = a.max_radii[idx];
-    }
-    for (int v = 0; v < a.V; v++) {
-        const float* row = rows + v * vstride;
-        const uint32_t w9 = __float_as_uint(row[9]);
-        if (w9 == 0u) continue;  // not visible in view v: no terms (the reference's radii > 0 filter)
-        const int radius = (int)(w9 & 0xFFFFFFu);
-        const uint8_t cb = (uint8_t)(w9 >> 24);
-        float acc[9];
-        const float2* r2 = reinterpret_cast<const float2*>(row);
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const float2 t = r2[q];
-            acc[2 * q] = t.x;
-            acc[2 * q + 1] = t.y;
-        }
-        acc[8] = row[8];
-        const float* cam = a.cams + v * a.cam_stride;
-        const Mat4 V = load_mat4(cam);
-        const Mat4 Pm = load_mat4(cam + 16);
-        const float tan_fovx = cam[37], tan_fovy = cam[38];
-        // rasterizer_impl.cu:222-223 / gs_api.cpp: focal from the image size
-        const float focal_x = cam[35] / (2.0f * tan_fovx);
-        const float focal_y = cam[36] / (2.0f * tan_fovy);
-        float dmean[3], dcov[6];
-        cov2d_backward(mx, my, mz, cov3D, acc[5], acc[6], acc[7], V, focal_x, focal_y, tan_fovx, tan_fovy, dmean,
-                       dcov);
-        proj_backward(mx, my, mz, Pm, acc[3], acc[4], dmean);
+        // ---- pass 2: SH coefficient gradients and the view-direction term
         if (kHasSH) {
             const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
-            float dsh_c[16], dRGB[3];
-            sh_backward_terms(a.D, cam + 32, mx, my, mz, s, cb, acc, dsh_c, dRGB, dmean);
+            float dsh_t[48];
 #pragma unroll
-            for (int k = 0; k < 16; k++)
+            for (int i = 0; i < 48; i++) dsh_t[i] = 0.f;
+            float s_reg[kStage ? 1 : 16][3];
+            if (!kStage) {
+                const float* sh = a.shs + (size_t)idx * a.M * 3;
 #pragma unroll
-                for (int c = 0; c < 3; c++)
-                    if (k < ncoef) dsh_t[3 * k + c] += dsh_c[k] * dRGB[c];
-        }
+                for (int k = 0; k < (kStage ? 1 : 16); k++)
 #pragma unroll
-        for (int i = 0; i < 3; i++) dmean_t[i] += dmean[i];
+                    for (int c = 0; c < 3; c++) s_reg[k][c] = (k < ncoef) ? sh[3 * k + c] : 0.f;
+            }
+            float ddir[3] = {0.f, 0.f, 0.f};
+            for (int v = 0; v < a.V; v++) {
+                const float* row = rows + v * vstride;
+                const uint32_t w9 = __float_as_uint(row[9]);
+                if (w9 == 0u) continue;
+                const float acc[3] = {row[0], row[1], row[2]};
+                const uint8_t cb = (uint8_t)(w9 >> 24);
+                const float* cam = a.cams + v * a.cam_stride;
+                float dsh_c[16], dRGB[3];
+                if constexpr (kStage) {
+                    sh_backward_terms(a.D, cam + 32, mx, my, mz, ShRowPtr{lrow}, cb, acc, dsh_c, dRGB, ddir);
+                } else {
+                    float s16[16][3];
 #pragma unroll
-        for (int i = 0; i < 6; i++) dcov_t[i] += dcov[i];
-        dop += acc[8];
-        if (stats) {
-            st_acc = st_acc + sqrtf(acc[3] * acc[3] + acc[4] * acc[4]);
-            st_den = st_den + 1.f;
-            st_max = fmaxf(st_max, (float)radius);
-        }
-    }
+                    for (int k = 0; k < 16; k++)
 #pragma unroll
-    for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = dmean_t[i];
-    if (kHasSH) {
-        if (kSH16) {
-#pragma unroll
-            for (int i = 0; i < 12; i++)
-                reinterpret_cast<float4*>(a.dL_dsh)[(size_t)idx * 12 + i] =
-                    make_float4(dsh_t[4 * i], dsh_t[4 * i + 1], dsh_t[4 * i + 2], dsh_t[4 * i + 3]);
-        } else {
-            for (int k = 0; k < a.M; k++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    float val = 0.f;
-#pragma unroll
-                    for (int kk = 0; kk < 16; kk++) val = (kk == k) ? dsh_t[3 * kk + c] : val;
-                    a.dL_dsh[(size_t)idx * a.M * 3 + 3 * k + c] = val;
+                        for (int c = 0; c < 3; c++) s16[k][c] = s_reg[kStage ? 0 : k][c];
+                    sh_backward_terms(a.D, cam + 32, mx, my, mz, s16, cb, acc, dsh_c, dRGB, ddir);
                 }
-        }
-    }
-    a.dL_dopacity[idx] = dop;
-    float dscale[3];
-    float4 dq;
-    cov3d_backward(qrot, scl, a.scale_modifier, dcov_t, dscale, dq);
 #pragma unroll
-    for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = dscale[i];
-    reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
-    if (stats) {
-        a.grad_norm_accum[idx] = st_acc;
-        a.denom[idx] = st_den;
-        a.max_radii[idx] = st_max;
+                for (int k = 0; k < 16; k++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++)
+                        if (k < ncoef) dsh_t[3 * k + c] += dsh_c[k] * dRGB[c];
+            }
+#pragma unroll
+            for (int i = 0; i < 3; i++) dmean_t[i] += ddir[i];
+            if (kStage) {
+#pragma unroll
+                for (int i = 0; i < 48; i++) lrow[i] = dsh_t[i];
+            } else {
+                for (int k = 0; k < a.M; k++)
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        float val = 0.f;
+#pragma unroll
+                        for (int kk = 0; kk < 16; kk++) val = (kk == k) ? dsh_t[3 * kk + c] : val;
+                        a.dL_dsh[(size_t)idx * a.M * 3 + 3 * k + c] = val;
+                    }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = dmean_t[i];
+    }
+    if constexpr (kStage) {  // the workgroup's gradient rows out, wave-contiguous
+        __syncthreads();
+        float4* out = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)(a.g0 + local0) * 12;
+        for (int f = threadIdx.x; f < nblk * 12; f += 256) {
+            const float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
+            out[f] = make_float4(r[0], r[1], r[2], r[3]);
+        }
     }
 }
 
