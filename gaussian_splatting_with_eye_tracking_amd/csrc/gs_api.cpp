@@ -409,6 +409,54 @@ int gs_backward_gaussians_multiview_range(int P, int g0, int count, int D, int M
                           grad_norm_accum, denom, max_radii, stream);
 }
 
+int gs_ritnet_conv(int ksize, int nseg, const float* const* in, const int* in_channels, const int* in_upsample,
+                   int height, int width, const float* weight, const float* bias, int leaky_relu, const float* bn_scale,
+                   const float* bn_shift, float* out, void* stream) {
+    return guarded([&]() -> int {
+        if (ksize != 1 && ksize != 3) throw GsError("gs_ritnet_conv: kernel size must be 1 or 3");
+        if (nseg < 1 || nseg > 3) throw GsError("gs_ritnet_conv: 1 to 3 input segments");
+        if ((bn_scale == nullptr) != (bn_shift == nullptr)) throw GsError("gs_ritnet_conv: bn_scale and bn_shift");
+        for (int i = 0; i < nseg; i++)
+            if (in_channels[i] <= 0 || !in[i] || (in_upsample[i] && ((height | width) & 1)))
+                throw GsError("gs_ritnet_conv: bad input segment");
+        if (height <= 0 || width <= 0) return 0;
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_ritnet_conv(ksize, in, in_channels, in_upsample, nseg, height, width, weight, bias, leaky_relu,
+                           bn_scale, bn_shift, out, s);
+        stage_check(false, s, "ritnet_conv");
+        return 0;
+    });
+}
+
+int gs_avgpool2(const float* in, int channels, int height, int width, float* out, void* stream) {
+    return guarded([&]() -> int {
+        if ((height | width) & 1) throw GsError("gs_avgpool2: even height and width required");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_avgpool2(in, channels, height, width, out, s);
+        stage_check(false, s, "avgpool2");
+        return 0;
+    });
+}
+
+int gs_ritnet_head(const float* in, int height, int width, const float* weight, const float* bias, float* logits,
+                   uint8_t* labels, void* stream) {
+    return guarded([&]() -> int {
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_ritnet_head(in, height, width, weight, bias, logits, labels, s);
+        stage_check(false, s, "ritnet_head");
+        return 0;
+    });
+}
+
+int gs_label_moments(const uint8_t* labels, int height, int width, int label, double* out3, void* stream) {
+    return guarded([&]() -> int {
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_label_moments(labels, height, width, label, out3, s);
+        stage_check(false, s, "label_moments");
+        return 0;
+    });
+}
+
 int gs_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                                uint8_t* present, void* stream) {
     return guarded([&]() -> int {

@@ -131,6 +131,15 @@ void launch_pack_view_grads(int P, const GeomView& g, const int* radii, bool has
                             float tan_fovy, float* out, hipStream_t s);
 void launch_multiview_backward(const MultiViewArgs& a, hipStream_t s);
 
+// Eye-tracking front end (ritnet.hip): RITnet DenseNet2D building blocks.
+void launch_ritnet_conv(int k, const float* const* in_ptr, const int* in_c, const int* in_up, int nseg, int H, int W,
+                        const float* w, const float* bias, int lrelu, const float* bn_scale, const float* bn_shift,
+                        float* out, hipStream_t s);
+void launch_avgpool2(const float* in, int C, int H, int W, float* out, hipStream_t s);
+void launch_ritnet_head(const float* in, int H, int W, const float* w, const float* bias, float* logits,
+                        uint8_t* labels, hipStream_t s);
+void launch_label_moments(const uint8_t* labels, int H, int W, int cls, double* out, hipStream_t s);
+
 // AMR (amr/cr/rasterizer_impl.cu:181-243, amr/cr/forward.cu:261-648).
 void launch_amr_levels(int T, const ImageView& img, hipStream_t s);
 void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s);

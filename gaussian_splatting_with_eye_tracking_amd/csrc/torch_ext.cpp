@@ -309,6 +309,74 @@ void BackwardGaussiansMultiviewRange(const Tensor& rows_in, const Tensor& cams_i
           "backward_gaussians_multiview_range");
 }
 
+// ---- eye-tracking front end (ritnet.hip) ----
+// out [32, H, W] = conv over the virtual concatenation of `ins` (each
+// [C, h, w]; up[i] = 1: read through nearest 2x upsampling).
+void RitnetConv(int ksize, const std::vector<Tensor>& ins, const std::vector<int>& up, const Tensor& weight,
+                const Tensor& bias, bool leaky_relu, const Tensor& bn_scale, const Tensor& bn_shift, Tensor out) {
+    TORCH_CHECK(!ins.empty() && ins.size() <= 3 && up.size() == ins.size(), "1 to 3 inputs, one up flag each");
+    TORCH_CHECK(out.dim() == 3 && out.size(0) == 32 && out.is_contiguous(), "out must be a contiguous [32, H, W]");
+    const int H = (int)out.size(1), W = (int)out.size(2);
+    const float* p[3];
+    int c[3], u[3];
+    int Cin = 0;
+    for (size_t i = 0; i < ins.size(); i++) {
+        const Tensor& t = ins[i];
+        require_device(t, "input");
+        TORCH_CHECK(t.dim() == 3 && t.is_contiguous(), "inputs must be contiguous [C, h, w]");
+        TORCH_CHECK(t.size(1) == (up[i] ? H / 2 : H) && t.size(2) == (up[i] ? W / 2 : W), "input size mismatch");
+        p[i] = t.data_ptr<float>();
+        c[i] = (int)t.size(0);
+        u[i] = up[i];
+        Cin += c[i];
+    }
+    TORCH_CHECK(weight.numel() == (int64_t)Cin * ksize * ksize * 32 && weight.is_contiguous(),
+                "weight must be [Cin, k*k, 32]");
+    TORCH_CHECK(bias.numel() == 32, "bias must have 32 elements");
+    const at::OptionalDeviceGuard guard(device_of(out));
+    check(gs_ritnet_conv(ksize, (int)ins.size(), p, c, u, H, W, weight.data_ptr<float>(), bias.data_ptr<float>(),
+                         leaky_relu ? 1 : 0, bn_scale.numel() ? bn_scale.data_ptr<float>() : nullptr,
+                         bn_shift.numel() ? bn_shift.data_ptr<float>() : nullptr, out.data_ptr<float>(),
+                         stream_of(out)),
+          "ritnet_conv");
+}
+
+Tensor AvgPool2(const Tensor& in) {
+    require_device(in, "input");
+    TORCH_CHECK(in.dim() == 3 && in.is_contiguous(), "input must be a contiguous [C, H, W]");
+    const at::OptionalDeviceGuard guard(device_of(in));
+    Tensor out = torch::empty({in.size(0), in.size(1) / 2, in.size(2) / 2}, in.options());
+    check(gs_avgpool2(in.data_ptr<float>(), (int)in.size(0), (int)in.size(1), (int)in.size(2), out.data_ptr<float>(),
+                      stream_of(in)),
+          "avgpool2");
+    return out;
+}
+
+std::tuple<Tensor, Tensor> RitnetHead(const Tensor& in, const Tensor& weight, const Tensor& bias, bool want_logits) {
+    require_device(in, "input");
+    TORCH_CHECK(in.dim() == 3 && in.size(0) == 32 && in.is_contiguous(), "input must be a contiguous [32, H, W]");
+    TORCH_CHECK(weight.numel() == 128 && bias.numel() == 4, "head weight [32, 4], bias [4]");
+    const int H = (int)in.size(1), W = (int)in.size(2);
+    const at::OptionalDeviceGuard guard(device_of(in));
+    Tensor labels = torch::empty({H, W}, in.options().dtype(torch::kUInt8));
+    Tensor logits = want_logits ? torch::empty({4, H, W}, in.options()) : torch::empty({0}, in.options());
+    check(gs_ritnet_head(in.data_ptr<float>(), H, W, weight.data_ptr<float>(), bias.data_ptr<float>(),
+                         want_logits ? logits.data_ptr<float>() : nullptr, labels.data_ptr<uint8_t>(), stream_of(in)),
+          "ritnet_head");
+    return std::make_tuple(logits, labels);
+}
+
+Tensor LabelMoments(const Tensor& labels, int label) {
+    TORCH_CHECK(labels.is_cuda() && labels.scalar_type() == torch::kUInt8 && labels.dim() == 2 && labels.is_contiguous(),
+                "labels must be a contiguous uint8 [H, W] device tensor");
+    const at::OptionalDeviceGuard guard(device_of(labels));
+    Tensor out = torch::empty({3}, labels.options().dtype(torch::kFloat64));
+    check(gs_label_moments(labels.data_ptr<uint8_t>(), (int)labels.size(0), (int)labels.size(1), label,
+                           out.data_ptr<double>(), stream_of(labels)),
+          "label_moments");
+    return out;
+}
+
 // base/rasterize_points.cu:198-217
 Tensor MarkVisible(Tensor& means3D_in, Tensor& viewmatrix_in, Tensor& projmatrix_in) {
     const int P = (int)means3D_in.size(0);
@@ -522,6 +590,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("rasterize_gaussians_backward_view_grads", &RasterizeGaussiansBackwardViewGrads);
     m.def("backward_gaussians_multiview", &BackwardGaussiansMultiview);
     m.def("backward_gaussians_multiview_range", &BackwardGaussiansMultiviewRange);
+    m.def("ritnet_conv", &RitnetConv);
+    m.def("avgpool2", &AvgPool2);
+    m.def("ritnet_head", &RitnetHead);
+    m.def("label_moments", &LabelMoments);
     m.def("amr_rasterize_gaussians", &AMRRasterizeGaussians);
     m.def("distCUDA2", &DistCUDA2);
     m.def("parse_buffers", &ParseBuffers);

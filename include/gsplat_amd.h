@@ -112,6 +112,30 @@ int gs_backward_gaussians_multiview_range(int P, int g0, int count, int D, int M
                                           float* dL_drotations, float* grad_norm_accum, float* denom,
                                           float* max_radii, void* stream);
 
+/* Eye-tracking front end (RITnet/densenet.py:17-144,
+ * track_render.py:50-97).  Activations are [C][H][W] float32 planes.
+ *
+ * One RITnet convolution (3x3 padding 1, or 1x1) to 32 output channels over a
+ * virtual channel concatenation of nseg <= 3 inputs: in[i] holds
+ * in_channels[i] planes, read through nearest 2x upsampling when
+ * in_upsample[i] (then it is height/2 x width/2).  weight is [Cin][k*k][32]
+ * (the torch [32][Cin][k][k] tensor repacked), bias [32]; epilogue:
+ * LeakyReLU(0.01) if leaky_relu, then y * bn_scale + bn_shift if given
+ * (eval BatchNorm). Replaces nn.Conv2d / torch.cat / F.interpolate /
+ * nn.LeakyReLU / nn.BatchNorm2d of DenseNet2D_down_block and _up_block. */
+int gs_ritnet_conv(int ksize, int nseg, const float* const* in, const int* in_channels, const int* in_upsample,
+                   int height, int width, const float* weight, const float* bias, int leaky_relu, const float* bn_scale,
+                   const float* bn_shift, float* out, void* stream);
+/* nn.AvgPool2d(2) (densenet.py:26) over [channels][height][width]. */
+int gs_avgpool2(const float* in, int channels, int height, int width, float* out, void* stream);
+/* out_conv1 (32 -> 4, 1x1; weight [32][4]) + get_predictions' argmax
+ * (RITnet/utils.py:186-190): labels [H][W] uint8, logits [4][H][W] if non-null. */
+int gs_ritnet_head(const float* in, int height, int width, const float* weight, const float* bias, float* logits,
+                   uint8_t* labels, void* stream);
+/* out3 (device, f64) = {sum x, sum y, count} over the pixels labelled `label`
+ * (the pupil centroid of the segmentation). */
+int gs_label_moments(const uint8_t* labels, int height, int width, int label, double* out3, void* stream);
+
 /* Replaces CudaRasterizer::Rasterizer::markVisible
  * (base/cr/rasterizer.h:24-29, base/cr/rasterizer_impl.cu:141-153). */
 int gs_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -1,0 +1,115 @@
+"""Eye-tracking front end on the MI355X (csrc/ritnet.hip via eye_tracking.py)
+against the CPU oracle of the network (oracle/ritnet_oracle.py, itself
+pinned to the reference's saved prediction in test_eye_tracking_host.py).
+
+The checkpoint is not part of this repository, so the GPU parity uses a
+seeded random state dict of the reference's shapes, on the reference's own
+eye image through the build's preprocessing (tests/golden/eye_pins.npz).
+Bars: logits within 1e-5 relative (float32, different summation order),
+labels equal wherever the top-two logit margin exceeds twice the largest
+logit difference.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import gs_helpers as G
+import ritnet_oracle as R
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "eye_pins.npz")
+
+
+def _E():
+    from gaussian_splatting_with_eye_tracking_amd import eye_tracking as E
+    return E
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_ritnet_matches_oracle_full_frame(seed):
+    E = _E()
+    g = np.load(GOLD)
+    x = E.preprocess(g["eye"])                      # [640, 400], the network's orientation
+    sd = R.random_state_dict(seed)
+    net = E.RITnet(sd)
+    logits, labels = net(torch.from_numpy(x).cuda(), want_logits=True)
+    torch.cuda.synchronize()
+    want = R.forward(sd, x)
+    got = logits.cpu().numpy()
+    assert got.shape == want.shape == (4, 640, 400)
+    assert G.rel_err(got, want) < 1e-5
+    lab = labels.cpu().numpy()
+    np.testing.assert_array_equal(lab, np.argmax(got, axis=0))  # the head's argmax of its own logits
+    # labels agree wherever the oracle's top-two margin exceeds twice the
+    # largest logit difference (elsewhere f32 summation order may flip them)
+    srt = np.sort(want, axis=0)
+    clear = (srt[-1] - srt[-2]) > 2.0 * float(np.abs(got - want).max())
+    assert clear.mean() > 0.999
+    np.testing.assert_array_equal(lab[clear], R.labels(want)[clear])
+
+
+def test_ritnet_small_odd_batchnorm_values():
+    """A small frame (64 x 48) with large BatchNorm statistics."""
+    E = _E()
+    sd = R.random_state_dict(7)
+    for k in sd:
+        if k.endswith("running_var"):
+            sd[k] = sd[k] * 5.0
+    x = np.random.default_rng(3).normal(0, 1, (64, 48)).astype(np.float32)
+    logits, _ = E.RITnet(sd)(torch.from_numpy(x).cuda(), want_logits=True)
+    assert G.rel_err(logits.cpu().numpy(), R.forward(sd, x)) < 1e-5
+
+
+def test_conv_virtual_concat_and_upsample():
+    """One _C.ritnet_conv over three segments, the first read through the
+    nearest 2x upsampling, against torch.cat + F.interpolate + F.conv2d."""
+    import torch.nn.functional as F
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    gen = torch.Generator().manual_seed(5)
+    H, W = 24, 40
+    a = torch.randn(32, H // 2, W // 2, generator=gen)
+    b = torch.randn(32, H, W, generator=gen)
+    c = torch.randn(7, H, W, generator=gen)
+    for k in (1, 3):
+        w = torch.randn(32, 71, k, k, generator=gen) * 0.1
+        bias = torch.randn(32, generator=gen)
+        scale, shift = torch.rand(32, generator=gen) + 0.5, torch.randn(32, generator=gen)
+        cat = torch.cat((F.interpolate(a[None], scale_factor=2, mode="nearest")[0], b, c), 0)
+        ref = F.leaky_relu(F.conv2d(cat[None], w, bias, padding=k // 2))[0] * scale[:, None, None] + shift[:, None, None]
+        out = torch.empty(32, H, W, device="cuda")
+        packed = w.permute(1, 2, 3, 0).reshape(71, k * k, 32).contiguous().cuda()
+        _C.ritnet_conv(k, [a.cuda(), b.cuda(), c.cuda()], [1, 0, 0], packed, bias.cuda(), True, scale.cuda(),
+                       shift.cuda(), out)
+        assert G.rel_err(out.cpu().numpy(), ref.numpy()) < 1e-5, k
+
+
+def test_avgpool_and_label_moments():
+    import torch.nn.functional as F
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    x = torch.randn(5, 16, 22, generator=torch.Generator().manual_seed(2))
+    np.testing.assert_array_equal(_C.avgpool2(x.cuda()).cpu().numpy(), F.avg_pool2d(x[None], 2)[0].numpy())
+    lab = torch.from_numpy(np.random.default_rng(4).integers(0, 4, (640, 400)).astype(np.uint8))
+    m = _C.label_moments(lab.cuda(), 3).cpu().numpy()
+    ys, xs = np.nonzero(lab.numpy() == 3)
+    np.testing.assert_array_equal(m, [xs.sum(), ys.sum(), len(xs)])
+
+
+def test_track_end_to_end():
+    """eye image -> labels (eye orientation) -> pupil centroid -> fovea."""
+    E = _E()
+    g = np.load(GOLD)
+    net = E.RITnet(R.random_state_dict(0))
+    labels, pxy, fovea = E.track(net, g["eye"], (1920, 1080))
+    lab = labels.cpu().numpy()
+    assert lab.shape == (400, 640)
+    want = R.labels(R.forward(R.random_state_dict(0), E.preprocess(g["eye"]))).T
+    assert (lab == want).mean() > 0.999
+    ys, xs = np.nonzero(lab == 3)
+    if len(xs):
+        assert abs(pxy[0] - xs.mean()) < 1e-6 and abs(pxy[1] - ys.mean()) < 1e-6
+        assert abs(fovea[0] - pxy[0] / 640 * 1920) < 1e-6 and abs(fovea[1] - pxy[1] / 400 * 1080) < 1e-6
+    else:
+        assert pxy is None and fovea is None

@@ -38,7 +38,7 @@ for step in "$@"; do
     pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
     pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
     ab_fwd) run ab_fwd 400 python tools/ab_tuning.py --key fwd_variant --values 0 1 2 --stage render ;;
-    ab_bwd) run ab_bwd 400 python tools/ab_tuning.py --key bwd_variant --values 0 4 0 4 --stage render_bwd --backward ;;
+    ab_bwd) run ab_bwd 400 python tools/ab_tuning.py --key bwd_variant --values 0 1 2 0 1 2 --stage render_bwd --backward ;;
     ab_cull) run ab_cull_fwd 400 python tools/ab_tuning.py --key cull --values 0 1 --stage render &&
              run ab_cull_bwd 400 python tools/ab_tuning.py --key cull --values 0 1 --stage render_bwd --backward ;;
     ab_chunk) run ab_chunk_dup 400 python tools/ab_tuning.py --key bin_chunk --values 2048 4096 8192 16384 --stage duplicate &&
@@ -54,6 +54,8 @@ for step in "$@"; do
     pmc_bwd_b) run pmc_bwd_b 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_bwd_b -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     mv) run pytest_mv 400 python -m pytest tests/test_gpu_multiview.py tests/test_gpu_dist_views.py -q -m gpu -p no:cacheprovider --timeout 300 -rf &&
         run bench_exchange 400 python tools/bench_exchange.py ;;
+    eye) run pytest_eye 400 python -m pytest tests/test_gpu_eye_tracking.py -q -m gpu -p no:cacheprovider --timeout 300 -rf &&
+         run bench_eye 300 python tools/bench_eye.py ;;
     gputrain) run pytest_gpu_train 600 python -m pytest tests/test_gpu_training.py tests/test_loss.py -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     train) run bench_train 600 python tools/bench_train.py ;;
     proftrain) run rocprof_train 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python3 tools/bench_train.py --reps 10 ;;
