@@ -67,6 +67,7 @@ void launch_render_forward(int W, int H, const ImageView& img, const BinningView
 void set_forward_variant(int v);
 void set_cull(int v);
 void set_amr_variant(int v);
+void set_ritnet_mfma(int v);
 void set_bwd_gauss_split(int v);  // 1: SH backward as its own kernel  // AMR blend geometry (as fwd_variant)  // row-group cull in the blend kernels (default on)
 void set_backward_variant(int v);
 // Blend backward (base/cr/backward.cu:399-557) into g.grad_accum.

@@ -21,7 +21,7 @@
 // head_kernel: the final 1x1 convolution to 4 classes fused with the
 // argmax (RITnet/utils.py:186-190, first maximum wins) into uint8 labels.
 // avgpool2_kernel: nn.AvgPool2d(2) (sum of the 4 inputs in window order,
-// then / 4).  pupil_kernel: sum of x, y and count over label-3 pixels.
+// then / 4).  label_moments_kernel: sum of x, y and count over label-3 pixels.
 #include <cmath>
 
 #include "gs_device.cuh"
@@ -90,6 +90,82 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvIn in, int Cin, int H, in
         if (lrelu) v = v > 0.f ? v : 0.01f * v;
         if (bn_scale) v = v * bn_scale[co] + bn_shift[co];
         out[co * plane + pix] = v;
+    }
+}
+
+// Implicit-GEMM convolution on the f32 matrix cores
+// (v_mfma_f32_32x32x2_f32: exact f32, a k-ordered fma chain per output).
+// Per wave: D[co][px] (32 output channels x 32 pixels of one row) += W^T x
+// im2col, two rows per wave, so a workgroup of 4 waves covers a 32 x 8
+// pixel block.  Per chunk of kCK input channels the block's input tile (with
+// the kK - 1 halo, zero padding, the virtual concatenation and the 2x
+// upsampling resolved while staging) and the chunk's weights go to LDS; each
+// MFMA then reads one A value (a weight: lane l -> co = l & 31, k = l >> 5)
+// and one B value (an input: k = l >> 5, pixel l & 31) from LDS.  The
+// accumulator layout (col = pixel = lane & 31, row = channel = (r & 3) +
+// 8 (r >> 2) + 4 (lane >> 5)) makes every epilogue store a coalesced
+// 128-B row segment of one output channel.
+template <int kK>
+__global__ void __launch_bounds__(256) conv_mfma_kernel(ConvIn in, int Cin, int H, int W, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, int lrelu,
+                                                        const float* __restrict__ bn_scale,
+                                                        const float* __restrict__ bn_shift, float* __restrict__ out) {
+    constexpr int kT = kK * kK;              // taps
+    constexpr int kCK = kK == 3 ? 16 : 32;   // input channels per LDS chunk (kCK * kT is even)
+    constexpr int kBW = 32, kBH = 8;         // output block: 32 x 8 pixels
+    constexpr int kIW = kBW + kK - 1, kIH = kBH + kK - 1;
+    __shared__ float s_in[kCK * kIH * kIW];
+    __shared__ float s_w[kCK * kT * kCo];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int x0 = blockIdx.x * kBW, y0 = blockIdx.y * kBH;
+    typedef float f32x16 __attribute__((ext_vector_type(16)));
+    f32x16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc[t][r] = 0.f;
+    const int half = lane >> 5, col = lane & 31;
+    for (int c0 = 0; c0 < Cin; c0 += kCK) {
+        __syncthreads();
+        for (int i = tid; i < kCK * kIH * kIW; i += 256) {
+            const int cc = i / (kIH * kIW), rem = i % (kIH * kIW);
+            const int ry = rem / kIW, rx = rem % kIW;
+            const int ci = c0 + cc, gy = y0 + ry - kK / 2, gx = x0 + rx - kK / 2;
+            const bool ok = ci < Cin && gy >= 0 && gy < H && gx >= 0 && gx < W;
+            s_in[i] = ok ? read_in(in, ci, gy, gx, H, W) : 0.f;
+        }
+        for (int i = tid; i < kCK * kT * kCo; i += 256) {
+            const int ci = c0 + i / (kT * kCo);
+            s_w[i] = ci < Cin ? w[(size_t)c0 * kT * kCo + i] : 0.f;
+        }
+        __syncthreads();
+#pragma unroll 2
+        for (int kp = 0; kp < kCK * kT / 2; kp++) {
+            const int k = 2 * kp + half;
+            const int cc = k / kT, tap = k % kT;
+            const float a = s_w[k * kCo + col];
+#pragma unroll
+            for (int t = 0; t < 2; t++) {
+                const int ry = 2 * wave + t + tap / kK, rx = col + tap % kK;
+                const float b = s_in[(cc * kIH + ry) * kIW + rx];
+                acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
+            }
+        }
+    }
+    const size_t plane = (size_t)H * W;
+    const int x = x0 + col;
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        const int y = y0 + 2 * wave + t;
+        if (x >= W || y >= H) continue;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            const int co = (r & 3) + 8 * (r >> 2) + 4 * half;
+            float v = acc[t][r] + bias[co];
+            if (lrelu) v = v > 0.f ? v : 0.01f * v;
+            if (bn_scale) v = v * bn_scale[co] + bn_shift[co];
+            out[co * plane + (size_t)y * W + x] = v;
+        }
     }
 }
 
@@ -169,6 +245,9 @@ __global__ void __launch_bounds__(256) label_moments_kernel(const uint8_t* __res
     }
 }
 
+int g_ritnet_mfma = 1;  // 1: conv_mfma_kernel (default), 0: the SGPR-weight FMA kernel
+void set_ritnet_mfma(int v) { g_ritnet_mfma = v; }
+
 void launch_ritnet_conv(int k, const float* const* in_ptr, const int* in_c, const int* in_up, int nseg, int H, int W,
                         const float* w, const float* bias, int lrelu, const float* bn_scale, const float* bn_shift,
                         float* out, hipStream_t s) {
@@ -179,6 +258,16 @@ void launch_ritnet_conv(int k, const float* const* in_ptr, const int* in_c, cons
         in.C[i] = i < nseg ? in_c[i] : 0;
         in.up[i] = i < nseg ? in_up[i] : 0;
         Cin += in.C[i];
+    }
+    if (g_ritnet_mfma) {
+        const dim3 grid((W + 31) / 32, (H + 7) / 8);
+        if (k == 3)
+            hipLaunchKernelGGL(conv_mfma_kernel<3>, grid, dim3(256), 0, s, in, Cin, H, W, w, bias, lrelu, bn_scale,
+                               bn_shift, out);
+        else
+            hipLaunchKernelGGL(conv_mfma_kernel<1>, grid, dim3(256), 0, s, in, Cin, H, W, w, bias, lrelu, bn_scale,
+                               bn_shift, out);
+        return;
     }
     const dim3 grid((W + 63) / 64, (H + 3) / 4);
     if (k == 3)

@@ -63,13 +63,17 @@ def test_ritnet_small_odd_batchnorm_values():
     assert G.rel_err(logits.cpu().numpy(), R.forward(sd, x)) < 1e-5
 
 
-def test_conv_virtual_concat_and_upsample():
+@pytest.mark.parametrize("mfma", [1, 0])
+@pytest.mark.parametrize("HW", [(24, 40), (10, 70)])
+def test_conv_virtual_concat_and_upsample(mfma, HW):
     """One _C.ritnet_conv over three segments, the first read through the
-    nearest 2x upsampling, against torch.cat + F.interpolate + F.conv2d."""
+    nearest 2x upsampling, against torch.cat + F.interpolate + F.conv2d, on
+    the matrix-core kernel (default) and the SGPR-weight FMA kernel."""
     import torch.nn.functional as F
     from gaussian_splatting_with_eye_tracking_amd import _C
     gen = torch.Generator().manual_seed(5)
-    H, W = 24, 40
+    H, W = HW
+    _C.set_tuning("ritnet_mfma", mfma)
     a = torch.randn(32, H // 2, W // 2, generator=gen)
     b = torch.randn(32, H, W, generator=gen)
     c = torch.randn(7, H, W, generator=gen)
@@ -81,8 +85,12 @@ def test_conv_virtual_concat_and_upsample():
         ref = F.leaky_relu(F.conv2d(cat[None], w, bias, padding=k // 2))[0] * scale[:, None, None] + shift[:, None, None]
         out = torch.empty(32, H, W, device="cuda")
         packed = w.permute(1, 2, 3, 0).reshape(71, k * k, 32).contiguous().cuda()
-        _C.ritnet_conv(k, [a.cuda(), b.cuda(), c.cuda()], [1, 0, 0], packed, bias.cuda(), True, scale.cuda(),
-                       shift.cuda(), out)
+        try:
+            _C.ritnet_conv(k, [a.cuda(), b.cuda(), c.cuda()], [1, 0, 0], packed, bias.cuda(), True, scale.cuda(),
+                           shift.cuda(), out)
+            torch.cuda.synchronize()
+        finally:
+            _C.set_tuning("ritnet_mfma", 1)
         assert G.rel_err(out.cpu().numpy(), ref.numpy()) < 1e-5, k
 
 

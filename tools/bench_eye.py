@@ -53,7 +53,20 @@ def main():
             n = int(lvl[-1]) if lvl.startswith("down_block") else (5 - int(lvl[-1])) if lvl.startswith("up_block") else 1
             px = (640 >> (n - 1)) * (400 >> (n - 1)) if lvl != "out_conv1" else 640 * 400
             flops += 2 * w.numel() * px
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    _C.set_tuning("ritnet_mfma", 0)
+    for _ in range(2):
+        net(x)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(10):
+        net(x)
+    b.record()
+    torch.cuda.synchronize()
+    fma_ms = a.elapsed_time(b) / 10
+    _C.set_tuning("ritnet_mfma", 1)
     print(json.dumps({"metric": "RITnet eye frames/s (640x400, fp32)", "ritnet_ms": round(net_ms, 4),
+                      "ritnet_ms_vector_fma_kernel": round(fma_ms, 4),
                       "frames_per_s": round(1e3 / net_ms, 1), "gflop_per_frame": round(flops / 1e9, 2),
                       "achieved_tflops": round(flops / (net_ms * 1e-3) / 1e12, 2),
                       "track_ms_incl_host_preprocess": round(track_ms, 3), "host_preprocess_ms": round(pre_ms, 3),
