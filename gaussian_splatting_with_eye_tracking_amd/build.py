@@ -24,7 +24,7 @@ INCLUDE = os.path.join(ROOT, "include")
 BUILD = os.path.join(PKG, "_build")
 LIB = os.path.join(PKG, "libgsplat_amd.so")
 HIP_SOURCES = ["preprocess.hip", "binning.hip", "render.hip", "backward.hip", "amr.hip", "knn.hip", "loss.hip",
-               "train.hip", "ritnet.hip", "gs_api.cpp"]
+               "train.hip", "ritnet.hip", "eye_preprocess.hip", "gs_api.cpp"]
 ARCH = os.environ.get("GSAMD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off is part of the parity contract (see gs_device.cuh).

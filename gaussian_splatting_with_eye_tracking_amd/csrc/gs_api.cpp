@@ -457,6 +457,26 @@ int gs_label_moments(const uint8_t* labels, int height, int width, int label, do
     });
 }
 
+int gs_eye_preprocess(const uint8_t* gray, int height, int width, const uint8_t* gamma_lut, double clip_limit,
+                      int tiles_x, int tiles_y, float* luts, float* out, void* stream) {
+    return guarded([&]() -> int {
+        if (tiles_x <= 0 || tiles_y <= 0 || height % tiles_y || width % tiles_x)
+            throw GsError("gs_eye_preprocess: image size must be divisible by the tile grid");
+        if (height <= 0 || width <= 0) return 0;
+        // OpenCV CLAHE_Impl::apply: int(clip * tile area / 256), at least 1; 0 disables clipping
+        const int area = (width / tiles_x) * (height / tiles_y);
+        int limit = 0;
+        if (clip_limit > 0.0) {
+            limit = static_cast<int>(clip_limit * area / 256);
+            if (limit < 1) limit = 1;
+        }
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_eye_preprocess(gray, height, width, gamma_lut, tiles_x, tiles_y, limit, luts, out, s);
+        stage_check(false, s, "eye_preprocess");
+        return 0;
+    });
+}
+
 int gs_rasterizer_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                                uint8_t* present, void* stream) {
     return guarded([&]() -> int {

@@ -377,6 +377,22 @@ Tensor LabelMoments(const Tensor& labels, int label) {
     return out;
 }
 
+// gray [H, W] uint8 -> RITnet input [W, H] float32 (gamma, CLAHE, normalise, transpose).
+Tensor EyePreprocess(const Tensor& gray, const Tensor& gamma_lut, double clip_limit, int tiles_x, int tiles_y) {
+    TORCH_CHECK(gray.is_cuda() && gray.scalar_type() == torch::kUInt8 && gray.dim() == 2 && gray.is_contiguous(),
+                "gray must be a contiguous uint8 [H, W] device tensor");
+    TORCH_CHECK(gamma_lut.is_cuda() && gamma_lut.scalar_type() == torch::kUInt8 && gamma_lut.numel() == 256,
+                "gamma_lut must be 256 uint8 on the device");
+    const at::OptionalDeviceGuard guard(device_of(gray));
+    const int H = (int)gray.size(0), W = (int)gray.size(1);
+    Tensor out = torch::empty({W, H}, gray.options().dtype(torch::kFloat32));
+    Tensor luts = torch::empty({(int64_t)tiles_x * tiles_y * 256}, gray.options().dtype(torch::kFloat32));
+    check(gs_eye_preprocess(gray.data_ptr<uint8_t>(), H, W, gamma_lut.data_ptr<uint8_t>(), clip_limit, tiles_x,
+                            tiles_y, luts.data_ptr<float>(), out.data_ptr<float>(), stream_of(gray)),
+          "eye_preprocess");
+    return out;
+}
+
 // base/rasterize_points.cu:198-217
 Tensor MarkVisible(Tensor& means3D_in, Tensor& viewmatrix_in, Tensor& projmatrix_in) {
     const int P = (int)means3D_in.size(0);
@@ -594,6 +610,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("avgpool2", &AvgPool2);
     m.def("ritnet_head", &RitnetHead);
     m.def("label_moments", &LabelMoments);
+    m.def("eye_preprocess", &EyePreprocess);
     m.def("amr_rasterize_gaussians", &AMRRasterizeGaussians);
     m.def("distCUDA2", &DistCUDA2);
     m.def("parse_buffers", &ParseBuffers);

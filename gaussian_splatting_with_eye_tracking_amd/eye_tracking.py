@@ -11,8 +11,11 @@ so the pupil centroid is the fovea signal, as SURVEY §8(d) config 3 uses it):
   the TRANSPOSED image.  OpenCV is not a dependency here: ``clahe`` restates
   its 8-bit CLAHE (per-tile histogram, clip limit int(1.5 * tile area / 256),
   batch + stepped-residual redistribution, rounded LUT, bilinear blend of
-  the four surrounding tile LUTs).  The preprocessing is a few hundred
-  kilobytes of 8-bit host work per frame; it stays on the host.
+  the four surrounding tile LUTs).  ``preprocess`` is that host
+  restatement (pinned by the reference's saved segmentation); the tracking
+  path runs the same arithmetic on the MI355X (``preprocess_device``,
+  csrc/eye_preprocess.hip, bit-identical), so a frame crosses PCIe as
+  256 KB of bytes and never takes a host pass.
 * DenseNet2D (RITnet/densenet.py:17-144, eval mode: dropout off, BatchNorm
   on running statistics) on the MI355X: every convolution, the fused
   LeakyReLU / BatchNorm epilogues, the pooling, the virtual concatenations /
@@ -127,6 +130,22 @@ def preprocess(gray: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(normalize(clahe(apply_gamma(gray))).T)
 
 
+_GAMMA_DEV: Dict[torch.device, torch.Tensor] = {}
+
+
+def preprocess_device(gray: torch.Tensor) -> torch.Tensor:
+    """``preprocess`` on the device: uint8 [h, w] device tensor -> float32
+    [w, h] (gamma table, CLAHE, ToTensor + Normalize, transpose) by the HIP
+    kernels of csrc/eye_preprocess.hip; bit-identical to ``preprocess``."""
+    if gray.dtype != torch.uint8 or gray.dim() != 2 or not gray.is_cuda:
+        raise ValueError("preprocess_device: uint8 [H, W] device tensor required")
+    lut = _GAMMA_DEV.get(gray.device)
+    if lut is None:
+        lut = torch.from_numpy(gamma_table().astype(np.uint8)).to(gray.device)
+        _GAMMA_DEV[gray.device] = lut
+    return _C.eye_preprocess(gray.contiguous(), lut, CLAHE_CLIP, CLAHE_GRID[0], CLAHE_GRID[1])
+
+
 # ----------------------------------------------------------------- network ---
 _DOWN = ("down_block1", "down_block2", "down_block3", "down_block4", "down_block5")
 _UP = ("up_block1", "up_block2", "up_block3", "up_block4")
@@ -228,7 +247,8 @@ def fovea_center(pupil_xy: Tuple[float, float], eye_size: Tuple[int, int], scree
 def track(model: RITnet, gray: np.ndarray, screen_size: Tuple[int, int]):
     """One frame of the front end: 8-bit eye image [h, w] -> (labels in the
     eye image's orientation [h, w], pupil (x, y), fovea centre on the screen)."""
-    x = torch.from_numpy(preprocess(gray)).to(model.device)
+    g = torch.from_numpy(np.ascontiguousarray(gray, np.uint8)).to(model.device, non_blocking=True)
+    x = preprocess_device(g)
     _, labels_t = model(x)            # transposed image in, transposed labels out
     labels = labels_t.t().contiguous()
     pxy = pupil_centroid(labels)

@@ -135,6 +135,16 @@ int gs_ritnet_head(const float* in, int height, int width, const float* weight, 
 /* out3 (device, f64) = {sum x, sum y, count} over the pixels labelled `label`
  * (the pupil centroid of the segmentation). */
 int gs_label_moments(const uint8_t* labels, int height, int width, int label, double* out3, void* stream);
+/* Eye-image preprocessing (track_render.py:69-80): gray [height][width]
+ * uint8 -> gamma_lut (256 bytes: uint8(255 * (i/255)^0.8), track_render.py:72)
+ * -> OpenCV 8-bit CLAHE (clip_limit, tiles_x x tiles_y grid;
+ * cv2.createCLAHE(1.5, (8, 8)).apply, track_render.py:75-76) -> ToTensor +
+ * Normalize([0.5], [0.5]) (RITnet/dataset.py:35-37) -> out [width][height]
+ * float32, the transposed image RITnet is fed (track_render.py:80).
+ * luts: scratch of tiles_x * tiles_y * 256 floats.  height and width must be
+ * multiples of the grid (error otherwise). */
+int gs_eye_preprocess(const uint8_t* gray, int height, int width, const uint8_t* gamma_lut, double clip_limit,
+                      int tiles_x, int tiles_y, float* luts, float* out, void* stream);
 
 /* Replaces CudaRasterizer::Rasterizer::markVisible
  * (base/cr/rasterizer.h:24-29, base/cr/rasterizer_impl.cu:141-153). */

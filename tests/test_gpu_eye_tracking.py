@@ -121,3 +121,33 @@ def test_track_end_to_end():
         assert abs(fovea[0] - pxy[0] / 640 * 1920) < 1e-6 and abs(fovea[1] - pxy[1] / 400 * 1080) < 1e-6
     else:
         assert pxy is None and fovea is None
+
+
+def _gray_cases():
+    g = np.load(GOLD)
+    rng = np.random.default_rng(11)
+    yield "reference eye.png", g["eye"]
+    yield "uniform noise", rng.integers(0, 256, (400, 640)).astype(np.uint8)
+    yield "flat (all excess redistributed)", np.full((400, 640), 97, np.uint8)
+    yield "dark ramp, small frame", (np.add.outer(np.arange(48), np.arange(80)) // 3).astype(np.uint8)
+    yield "sparse spikes (residual steps)", np.where(rng.random((160, 96)) < 0.02, 255, 3).astype(np.uint8)
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_preprocess_device_bit_identical(case):
+    """csrc/eye_preprocess.hip == eye_tracking.preprocess (the host
+    restatement pinned by the reference's saved segmentation), bit for bit:
+    gamma table, CLAHE histograms/clip/redistribution/LUTs, bilinear blend,
+    normalisation and the transpose."""
+    E = _E()
+    name, gray = list(_gray_cases())[case]
+    want = E.preprocess(gray)
+    got = E.preprocess_device(torch.from_numpy(gray).cuda()).cpu().numpy()
+    assert got.shape == want.shape == gray.shape[::-1], name
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32), err_msg=name)
+
+
+def test_preprocess_device_rejects_ragged_grid():
+    E = _E()
+    with pytest.raises(RuntimeError, match="divisible"):
+        E.preprocess_device(torch.zeros((401, 640), dtype=torch.uint8, device="cuda"))

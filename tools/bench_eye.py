@@ -35,14 +35,28 @@ def main():
     b.record()
     torch.cuda.synchronize()
     net_ms = a.elapsed_time(b) / reps
+    E.track(net, g["eye"], (1920, 1080))
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(reps):
+    for _ in range(reps):  # host image in, fovea on the host out (upload, preprocess, network, centroid)
         labels, pxy, fovea = E.track(net, g["eye"], (1920, 1080))
     torch.cuda.synchronize()
     track_ms = (time.perf_counter() - t0) * 1e3 / reps
-    t0 = time.perf_counter()
     E.preprocess(g["eye"])
-    pre_ms = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    for _ in range(5):
+        E.preprocess(g["eye"])
+    pre_ms = (time.perf_counter() - t0) * 1e3 / 5
+    gray = torch.from_numpy(g["eye"]).cuda()
+    for _ in range(3):
+        E.preprocess_device(gray)
+    torch.cuda.synchronize()
+    a.record()
+    for _ in range(reps):
+        E.preprocess_device(gray)
+    b.record()
+    torch.cuda.synchronize()
+    pre_dev_ms = a.elapsed_time(b) / reps
     t0 = time.perf_counter()
     R.forward(sd, E.preprocess(g["eye"]))
     cpu_ms = (time.perf_counter() - t0) * 1e3
@@ -69,7 +83,8 @@ def main():
                       "ritnet_ms_vector_fma_kernel": round(fma_ms, 4),
                       "frames_per_s": round(1e3 / net_ms, 1), "gflop_per_frame": round(flops / 1e9, 2),
                       "achieved_tflops": round(flops / (net_ms * 1e-3) / 1e12, 2),
-                      "track_ms_incl_host_preprocess": round(track_ms, 3), "host_preprocess_ms": round(pre_ms, 3),
+                      "track_ms": round(track_ms, 3), "device_preprocess_ms": round(pre_dev_ms, 4),
+                      "host_preprocess_ms_numpy_restatement": round(pre_ms, 3),
                       "cpu_oracle_ms": round(cpu_ms, 1), "cpu_threads": torch.get_num_threads()}))
 
 
