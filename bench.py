@@ -191,10 +191,18 @@ def run_amr(args, world, rank, local_rank, distributed, dev):
     a = (t["means3D"], means2D, t["shs"], e, t["opacities"], t["scales"], t["rotations"], e)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
 
-    def frame_5step(record=False):
+    from gaussian_splatting_with_eye_tracking_amd import rasterization_amr as RA
+    # extension: the tracked fovea centre of config 3
+    # (pupil (361.74, 248.19) in the 640x400 eye image -> screen) with the
+    # reference's unused fovea radii W/2 .. W/16 restricting the AMR levels
+    fov_centres, fov_radii = RA.reference_foveae(W, H, (361.74 / 640 * W, 248.19 / 400 * H))
+
+    def frame_5step(record=False, fovea=False):
         if record:
             ev[0].record()
         c, radii, gb, bb, ib = _RasterizeGaussians.apply(*a, 0, e, u8, u8, u8, False, st)
+        if fovea:
+            RA.apply_fovea_levels(ib, W, H, fov_centres, fov_radii)
         acc = c
         if record:
             ev[1].record()
@@ -244,10 +252,17 @@ def run_amr(args, world, rank, local_rank, distributed, dev):
         el1 = time.perf_counter() - t0
         if not args.no_profile:
             _C.profile_enable(False)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            frame_5step(fovea=True)
+        torch.cuda.synchronize()
         if distributed:
-            tt = torch.tensor([el5, el1], device=dev, dtype=torch.float64)
+            dist.barrier()
+        elf = time.perf_counter() - t0
+        if distributed:
+            tt = torch.tensor([el5, el1, elf], device=dev, dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el5, el1 = float(tt[0].item()), float(tt[1].item())
+            el5, el1, elf = float(tt[0].item()), float(tt[1].item()), float(tt[2].item())
         result = None
         if rank == 0:
             acc, gb, bb, ib = frame_5step()
@@ -256,6 +271,9 @@ def run_amr(args, world, rank, local_rank, distributed, dev):
             d = _C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
             rng = d["ranges"].cpu().numpy().astype(np.int64)
             lv = d["levels"].cpu().numpy().astype(np.int64)
+            _, _, _, ibf = frame_5step(fovea=True)
+            lvf = _C.parse_buffers(gb, bb, ibf, P, K, W, H, 32)["levels"].cpu().numpy().astype(np.int64)
+            fovea_hist = np.bincount(lvf, minlength=5)[1:].tolist()
             stages = {n: {"avg_ms": ms / c, "launches": c, "ms_per_frame": ms / args.steps}
                       for n, (ms, c) in prof.items() if c}
             roofline = None
@@ -280,6 +298,9 @@ def run_amr(args, world, rank, local_rank, distributed, dev):
                            "P": P, "width": W, "height": H, "K_instances": K, "parallelism": f"replicas{world}",
                            "levels_hist": np.bincount(lv, minlength=5)[1:].tolist()},
                 "render_once_fps": world * args.steps / el1,
+                "fovea_levels_ext": {"fps": world * args.steps / elf, "centre": [round(v, 2) for v in fov_centres[0]],
+                                     "radii": fov_radii, "levels_hist": fovea_hist,
+                                     "note": "extension beyond parity: tracked fovea discs clamp the AMR levels"},
                 "per_step_ms": [round(x / args.steps, 4) for x in step_ms],
                 "roofline": roofline,
                 "cpu_baseline": cpu,

@@ -125,4 +125,58 @@ void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s) {
                        img.levels_current, img.levels);
 }
 
+// Fovea-driven levels (an extension beyond parity).
+// The reference defines per-step fovea centres and radii
+// (gaussian_renderer_amr/__init__.py:98-106: centre = image centre, radii
+// W/2, W/4, W/8, W/16) but never passes them to the rasterizer, and leaves
+// "if outside the current fovea, set to same as last step" as a TODO
+// (:244).  This kernel implements that TODO on the step-0 levels: fovea k
+// (k = 1..nf) is the disc (centre_k, radius_k); a tile is inside it when the
+// disc meets the tile's pixel rectangle [x0, x1] x [y0, y1] (the squared
+// distance from the centre to the rectangle <= radius^2).  F(t) = the
+// largest k such that the tile is inside foveae 1..k (0 if not inside the
+// first), floored at min_level; then
+//   clamp   (replace = 0): L'(t) = min(L(t), max(F(t), min_level))
+//   replace (replace = 1): L'(t) = max(F(t), min_level)
+// so the steps k >= 1 that follow (setFoveaAMRLevelsKernel: current = L >= k
+// ? k : last) keep a tile outside fovea k at its last round.  Integer
+// output; float math only in the rectangle distance (no contraction).
+struct FoveaDiscs {
+    float cx[4], cy[4], r2[4];
+};
+
+__global__ void __launch_bounds__(256) fovea_override_kernel(int T, int grid_x, int W, int H, int tile, FoveaDiscs d,
+                                                             int nf, uint32_t min_level, int replace,
+                                                             uint32_t* __restrict__ levels) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const int tx = t % grid_x, ty = t / grid_x;
+    const float x0 = (float)(tx * tile), y0 = (float)(ty * tile);
+    const float x1 = (float)min(tx * tile + tile, W) - 1.0f, y1 = (float)min(ty * tile + tile, H) - 1.0f;
+    uint32_t F = 0;
+    for (int k = 0; k < nf; k++) {
+        const float dx = fmaxf(fmaxf(x0 - d.cx[k], d.cx[k] - x1), 0.0f);
+        const float dy = fmaxf(fmaxf(y0 - d.cy[k], d.cy[k] - y1), 0.0f);
+        if (dx * dx + dy * dy > d.r2[k]) break;
+        F = (uint32_t)(k + 1);
+    }
+    const uint32_t f = F > min_level ? F : min_level;
+    const uint32_t L = levels[t];
+    levels[t] = replace ? f : (L < f ? L : f);
+}
+
+void launch_fovea_override(int W, int H, const ImageView& img, int nf, const float* cx, const float* cy,
+                           const float* radius, int min_level, int replace, hipStream_t s) {
+    const int tile = 32, grid_x = (W + tile - 1) / tile, T = grid_x * ((H + tile - 1) / tile);
+    if (T == 0) return;
+    FoveaDiscs d{};
+    for (int k = 0; k < nf; k++) {
+        d.cx[k] = cx[k];
+        d.cy[k] = cy[k];
+        d.r2[k] = radius[k] * radius[k];
+    }
+    hipLaunchKernelGGL(fovea_override_kernel, dim3((T + 255) / 256), dim3(256), 0, s, T, grid_x, W, H, tile, d, nf,
+                       (uint32_t)min_level, replace, img.levels);
+}
+
 }  // namespace gsamd

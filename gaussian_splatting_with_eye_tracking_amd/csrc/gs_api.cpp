@@ -573,6 +573,33 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
     });
 }
 
+int gs_amr_fovea_levels(char* image_buffer, size_t image_buffer_bytes, int width, int height, int nfovea, const float* centres_xy,
+                        const float* radii, int min_level, int replace, void* stream) {
+    return guarded([&]() -> int {
+        if (nfovea < 0 || nfovea > 4) throw GsError("gs_amr_fovea_levels: 0 to 4 foveae");
+        if (min_level < 0 || min_level > 4) throw GsError("gs_amr_fovea_levels: min_level in 0..4");
+        if (width <= 0 || height <= 0) return 0;
+        if (!image_buffer) throw GsError("gs_amr_fovea_levels: needs the image buffer of foveaStep 0");
+        float cx[4], cy[4], r[4];
+        for (int k = 0; k < nfovea; k++) {
+            cx[k] = centres_xy[2 * k];
+            cy[k] = centres_xy[2 * k + 1];
+            r[k] = radii[k];
+            if (!(r[k] >= 0.f)) throw GsError("gs_amr_fovea_levels: radii must be >= 0");
+        }
+        const int tile = 32;
+        const size_t T = (size_t)((width + tile - 1) / tile) * ((height + tile - 1) / tile);
+        if (image_buffer_bytes < carve_image(nullptr, (size_t)width * height, T, nullptr))
+            throw GsError("gs_amr_fovea_levels: image buffer too small for width x height");
+        ImageView img;
+        carve_image(image_buffer, (size_t)width * height, T, &img);
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_fovea_override(width, height, img, nfovea, cx, cy, r, min_level, replace, s);
+        stage_check(false, s, "amr_fovea_levels");
+        return 0;
+    });
+}
+
 int gs_simple_knn(int P, const float* points, float* mean_dists, gs_buffer scratch, void* stream) {
     return guarded([&]() -> int {
         if (P <= 0) return 0;

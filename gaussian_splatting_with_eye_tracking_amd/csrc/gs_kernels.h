@@ -140,6 +140,9 @@ void launch_avgpool2(const float* in, int C, int H, int W, float* out, hipStream
 void launch_ritnet_head(const float* in, int H, int W, const float* w, const float* bias, float* logits,
                         uint8_t* labels, hipStream_t s);
 void launch_label_moments(const uint8_t* labels, int H, int W, int cls, double* out, hipStream_t s);
+// Fovea-driven AMR levels (amr.hip), applied to the step-0 levels in place.
+void launch_fovea_override(int W, int H, const ImageView& img, int nf, const float* cx, const float* cy,
+                           const float* radius, int min_level, int replace, hipStream_t s);
 // Eye-image preprocessing (eye_preprocess.hip): gamma table, CLAHE, normalise, transpose.
 void launch_eye_preprocess(const uint8_t* gray, int H, int W, const uint8_t* gamma, int tiles_x, int tiles_y,
                            int limit, float* luts, float* out, hipStream_t s);

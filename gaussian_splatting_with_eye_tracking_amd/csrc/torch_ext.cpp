@@ -377,6 +377,25 @@ Tensor LabelMoments(const Tensor& labels, int label) {
     return out;
 }
 
+// Fovea-driven AMR levels on the image buffer of foveaStep 0 (in place).
+void AmrFoveaLevels(Tensor imageBuffer, int width, int height, const std::vector<double>& centres_xy,
+                    const std::vector<double>& radii, int min_level, bool replace) {
+    TORCH_CHECK(imageBuffer.is_cuda() && imageBuffer.scalar_type() == torch::kUInt8 && imageBuffer.numel() > 0,
+                "imageBuffer must be the uint8 device buffer returned by foveaStep 0");
+    TORCH_CHECK(centres_xy.size() == 2 * radii.size() && radii.size() <= 4, "up to 4 foveae: centres [n][2], radii [n]");
+    float c[8], r[4];
+    for (size_t i = 0; i < radii.size(); i++) {
+        c[2 * i] = (float)centres_xy[2 * i];
+        c[2 * i + 1] = (float)centres_xy[2 * i + 1];
+        r[i] = (float)radii[i];
+    }
+    const at::OptionalDeviceGuard guard(device_of(imageBuffer));
+    check(gs_amr_fovea_levels(reinterpret_cast<char*>(imageBuffer.data_ptr<uint8_t>()), (size_t)imageBuffer.numel(),
+                              width, height,
+                              (int)radii.size(), c, r, min_level, replace ? 1 : 0, stream_of(imageBuffer)),
+          "amr_fovea_levels");
+}
+
 // gray [H, W] uint8 -> RITnet input [W, H] float32 (gamma, CLAHE, normalise, transpose).
 Tensor EyePreprocess(const Tensor& gray, const Tensor& gamma_lut, double clip_limit, int tiles_x, int tiles_y) {
     TORCH_CHECK(gray.is_cuda() && gray.scalar_type() == torch::kUInt8 && gray.dim() == 2 && gray.is_contiguous(),
@@ -611,6 +630,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("ritnet_head", &RitnetHead);
     m.def("label_moments", &LabelMoments);
     m.def("eye_preprocess", &EyePreprocess);
+    m.def("amr_fovea_levels", &AmrFoveaLevels);
     m.def("amr_rasterize_gaussians", &AMRRasterizeGaussians);
     m.def("distCUDA2", &DistCUDA2);
     m.def("parse_buffers", &ParseBuffers);

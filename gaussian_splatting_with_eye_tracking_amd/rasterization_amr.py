@@ -28,7 +28,7 @@ that says so.
 """
 from __future__ import annotations
 
-from typing import NamedTuple
+from typing import NamedTuple, Optional, Sequence, Tuple
 
 import torch
 import torch.nn as nn
@@ -92,3 +92,27 @@ class GaussianRasterizer(nn.Module):
             _empty_u8() if binningBuffer_precomp is None else binningBuffer_precomp,
             _empty_u8() if imageBuffer_precomp is None else imageBuffer_precomp, interpolate_image,
             self.raster_settings)
+
+
+# ------------------------------------------------ fovea-driven levels (ext.) ---
+def reference_foveae(width: int, height: int, centre: Optional[Tuple[float, float]] = None):
+    """The fovea discs the reference builds and leaves unused
+    (gaussian_renderer_amr/__init__.py:98-106): four centres (the image
+    centre there; the tracked fovea centre here when given) and radii
+    W/2, W/4, W/8, W/16."""
+    c = (width / 2, height / 2) if centre is None else (float(centre[0]), float(centre[1]))
+    return [c] * 4, [width / 2, width / 4, width / 8, width / 16]
+
+
+def apply_fovea_levels(imageBuffer: torch.Tensor, width: int, height: int, centres: Sequence[Tuple[float, float]],
+                       radii: Sequence[float], min_level: int = 1, replace: bool = False) -> None:
+    """Extension beyond parity: implement the
+    reference's TODO "if outside the current fovea, set to same as last step"
+    (gaussian_renderer_amr/__init__.py:244) on the tile levels foveaStep 0
+    left in ``imageBuffer`` (mutated in place, on the device): a tile keeps
+    round k only while its rectangle meets foveae 1..k; ``replace`` makes the
+    fovea alone decide the level (pure eccentricity foveation).  Call it
+    between step 0 and steps 1..4; see csrc/amr.hip fovea_override_kernel."""
+    flat = [float(v) for c in centres for v in c]
+    _C.amr_fovea_levels(imageBuffer, int(width), int(height), flat, [float(r) for r in radii], int(min_level),
+                        bool(replace))

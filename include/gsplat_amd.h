@@ -186,6 +186,19 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
 /* Replaces SimpleKNN::knn (knn/simple_knn.h:16-19, knn/simple_knn.cu:185-221)
  * behind simple_knn._C.distCUDA2.  `scratch` is resized to the workspace
  * size; no host synchronisation. */
+/* Fovea-driven AMR levels -- an extension beyond parity.
+ * The reference builds foveaCenters [4][2] / foveaRadii [4]
+ * (gaussian_renderer_amr/__init__.py:98-106) but never passes them on, and
+ * leaves "if outside the current fovea, set to same as last step" as a TODO
+ * (:244).  Called between foveaStep 0 and the steps 1..4 on the image
+ * buffer foveaStep 0 returned (levels mutated in place): F(t) = the largest
+ * k <= nfovea such that tile t's pixel rectangle meets the discs
+ * (centres_xy[2j], centres_xy[2j+1], radii[j]) for all j < k;
+ * replace = 0: level = min(level, max(F, min_level)); replace = 1: level =
+ * max(F, min_level).  centres_xy / radii are host arrays; image_buffer_bytes
+ * is checked against the layout of width x height. */
+int gs_amr_fovea_levels(char* image_buffer, size_t image_buffer_bytes, int width, int height, int nfovea, const float* centres_xy,
+                        const float* radii, int min_level, int replace, void* stream);
 int gs_simple_knn(int P, const float* points, float* mean_dists, gs_buffer scratch, void* stream);
 
 /* Training loss of the reference (train.py:91-93, utils/loss_utils.py:17-63):

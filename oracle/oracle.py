@@ -299,9 +299,41 @@ def orc_fovea(L, step, T, st: AMRState):
                            _p(st.levels))
 
 
-def amr_render_foveated(s: Settings, scene_kwargs: dict, interpolate_image: bool = False):
-    """gaussian_renderer_amr/__init__.py:24-608: steps 0..4, summing the partial images."""
+def fovea_levels(levels, W: int, H: int, centres, radii, min_level: int = 1, replace: bool = False):
+    """Extension beyond parity (no reference implementation exists): the
+    fovea-driven level rule of csrc/amr.hip fovea_override_kernel, restated.
+    It implements the reference's TODO (gaussian_renderer_amr/__init__.py:244)
+    with its unused fovea discs (:98-106).  Tile rectangle [x0, x1] x [y0, y1]
+    in pixel coordinates; inside disc k when the float32 squared distance from
+    the centre to the rectangle is <= radius^2 (float32)."""
+    tile = 32
+    gx = (W + tile - 1) // tile
+    out = np.asarray(levels, np.uint32).copy()
+    f32 = np.float32
+    for t in range(out.shape[0]):
+        tx, ty = t % gx, t // gx
+        x0, y0 = f32(tx * tile), f32(ty * tile)
+        x1, y1 = f32(min(tx * tile + tile, W)) - f32(1), f32(min(ty * tile + tile, H)) - f32(1)
+        F = 0
+        for k, (c, r) in enumerate(zip(centres, radii)):
+            cx, cy, rr = f32(c[0]), f32(c[1]), f32(r)
+            dx = max(x0 - cx, cx - x1, f32(0))
+            dy = max(y0 - cy, cy - y1, f32(0))
+            if f32(dx * dx) + f32(dy * dy) > f32(rr * rr):
+                break
+            F = k + 1
+        f = max(F, min_level)
+        out[t] = f if replace else min(int(out[t]), f)
+    return out
+
+
+def amr_render_foveated(s: Settings, scene_kwargs: dict, interpolate_image: bool = False, levels_hook=None):
+    """gaussian_renderer_amr/__init__.py:24-608: steps 0..4, summing the partial
+    images.  ``levels_hook(levels) -> levels`` (extension) rewrites the step-0
+    tile levels before the progressive steps."""
     c0, radii, st = amr_forward(s, foveaStep=0, **scene_kwargs)
+    if levels_hook is not None:
+        st.levels[:] = levels_hook(st.levels)
     acc = c0.copy()
     steps = [c0]
     for k in range(1, 5):

@@ -226,7 +226,7 @@ def test_prefiltered_violation_raises():
 
 
 # ---------------------------------------------------------------- AMR ----
-def _amr_gpu_steps(sc, cam, interpolate_last=False, bg=(0.0, 0.0, 0.0)):
+def _amr_gpu_steps(sc, cam, interpolate_last=False, bg=(0.0, 0.0, 0.0), after_step0=None):
     from diff_gaussian_rasterization_amr import _RasterizeGaussians
     s = G.torch_settings(cam, amr=True, bg=bg)
     t = G.scene_tensors(sc)
@@ -235,6 +235,8 @@ def _amr_gpu_steps(sc, cam, interpolate_last=False, bg=(0.0, 0.0, 0.0)):
     means2D = torch.zeros_like(t["means3D"])
     args = (t["means3D"], means2D, t["shs"], e, t["opacities"], t["scales"], t["rotations"], e)
     c0, radii, gb, bb, ib = _RasterizeGaussians.apply(*args, 0, e, u8, u8, u8, False, s)
+    if after_step0 is not None:
+        after_step0(ib)
     acc = c0
     steps = [c0]
     for k in range(1, 5):
@@ -313,6 +315,46 @@ def test_amr_step4_interpolate():
         interpolate_image=True)
     assert G.image_l1(steps[4].cpu().numpy(), rsteps[4]) < G.IMAGE_L1_TOL
     assert G.image_l1(acc.cpu().numpy(), racc) < G.IMAGE_L1_TOL
+
+
+@pytest.mark.parametrize("W,H,centre,min_level,replace", [
+    (256, 256, None, 1, False),                 # the reference's discs: image centre, W/2 .. W/16
+    (256, 160, (181.0, 99.0), 1, False),        # a tracked fovea off centre
+    (200, 120, (20.5, 110.0), 0, False),        # periphery left blank (the TODO read literally)
+    (256, 160, (181.0, 99.0), 1, True),         # eccentricity alone decides the level
+])
+def test_amr_fovea_levels_extension(W, H, centre, min_level, replace):
+    """Extension beyond parity: fovea-driven tile
+    levels between step 0 and steps 1..4.  Levels bit-exact against the
+    oracle's restatement of the rule; every step's image and the sum against
+    the oracle's AMR render with the same levels."""
+    import oracle as O
+    from gaussian_splatting_with_eye_tracking_amd import rasterization_amr as RA
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(6000, W, H, 4)
+    centres, radii = RA.reference_foveae(W, H, centre)
+    hook = lambda ib: RA.apply_fovea_levels(ib, W, H, centres, radii, min_level, replace)  # noqa: E731
+    acc, radii_g, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, after_step0=hook)
+    s = O.settings_from_camera(cam)
+    kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+    racc, _, st, rsteps = O.amr_render_foveated(
+        s, kw, levels_hook=lambda lv: O.fovea_levels(lv, W, H, centres, radii, min_level, replace))
+    d = C.parse_buffers(gb, bb, ib, 6000, st.fwd.num_rendered, W, H, 32)
+    got = d["levels"].cpu().numpy().astype(np.uint32)
+    np.testing.assert_array_equal(got, st.levels)
+    assert got.min() >= min_level and got.max() <= 4
+    if not replace:
+        assert (got <= O.amr_render_foveated(s, kw)[2].levels).all()
+    for k in range(5):
+        assert G.image_l1(steps[k].cpu().numpy(), rsteps[k]) < G.IMAGE_L1_TOL, k
+    assert G.image_l1(acc.cpu().numpy(), racc) < G.IMAGE_L1_TOL
+
+
+def test_amr_fovea_levels_rejects_bad_buffer():
+    from gaussian_splatting_with_eye_tracking_amd import rasterization_amr as RA
+    small = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(RuntimeError, match="too small"):
+        RA.apply_fovea_levels(small, 256, 256, *RA.reference_foveae(256, 256))
 
 
 def test_amr_backward_is_forward_only():

@@ -160,3 +160,29 @@ def test_knn_bbox_zero_init_quirk():
     q = np.floor((pts - 0.0) / (pts.max(0) - 0.0) * 1023).astype(np.uint32)
     assert q.min() > 900  # all codes are near the top of the [0, max] box
     assert np.all(np.isfinite(d)) and np.all(d > 0)
+
+
+def test_fovea_levels_rule():
+    """The extension's fovea rule (oracle.fovea_levels) on hand-checked tiles:
+    a 4 x 3 grid of 32-px tiles (128 x 96), one disc set centred in tile
+    (1, 1)."""
+    import oracle as O
+    W, H = 128, 96
+    lv = np.full(12, 4, np.uint32)
+    centres = [(48.0, 48.0)] * 4
+    radii = [100.0, 20.0, 1.0, 0.0]   # fovea 4 (radius 0) still contains its own tile
+    got = O.fovea_levels(lv, W, H, centres, radii).reshape(3, 4)
+    # tile (1,1) holds the centre -> inside all 4; tiles with the rectangle
+    # within 20 px -> 2; everything within 100 px -> 1
+    # column x-ranges [0,31] dx = 17, [64,95] dx = 16, [96,127] dx = 48 (> 20);
+    # row y-ranges [0,31] dy = 17, [64,95] dy = 16.  Edge neighbours are within
+    # 20 px (level 2); diagonal ones are sqrt(17^2 + 17^2) ~ 24 > 20 (level 1)
+    want = np.array([[1, 2, 1, 1], [2, 4, 2, 1], [1, 2, 1, 1]], np.uint32)
+    np.testing.assert_array_equal(got, want)
+    # clamp never raises a level; replace ignores the count-based level
+    low = np.ones(12, np.uint32)
+    assert (O.fovea_levels(low, W, H, centres, radii) == 1).all()
+    np.testing.assert_array_equal(O.fovea_levels(low, W, H, centres, radii, replace=True).reshape(3, 4), want)
+    # min_level 0 leaves tiles outside the first fovea blank
+    far = O.fovea_levels(lv, W, H, [(500.0, 500.0)] * 4, radii, min_level=0)
+    assert (far == 0).all()
