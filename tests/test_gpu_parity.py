@@ -126,6 +126,51 @@ def test_backward_parity(name, P, W, H, seed, variant):
         assert G.rel_err(gg, rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(gg, rg[n]))
 
 
+def _psnr(img, gt):
+    """utils/image_utils.py:19-21 (per leading row, then the mean as
+    metrics.py / train.py report it), on images clamped to [0, 1] as saved."""
+    img = np.clip(img, 0.0, 1.0).astype(np.float64)
+    gt = np.clip(gt, 0.0, 1.0).astype(np.float64)
+    mse = ((img - gt) ** 2).reshape(img.shape[0], -1).mean(1)
+    return float(np.mean(20.0 * np.log10(1.0 / np.sqrt(mse))))
+
+
+def test_config2_full_size_parity_and_psnr():
+    """BASELINE config 2 at full size (1M Gaussians, 1920x1080, seed 0):
+    the tile keys / point_list / ranges bit-exact, the image within the L1
+    bar, PSNR against a target within 0.01 dB of the oracle's (the
+    north_star's PSNR bar), and every gradient within 1e-4 relative."""
+    import oracle as O
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    P, W, H = 1_000_000, 1920, 1080
+    sc, cam = G.scene_and_camera(P, W, H, 0)
+    s, t, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
+    os_, ref, kw = _oracle_forward(sc, cam)
+    assert K == ref.num_rendered
+    d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
+    np.testing.assert_array_equal(radii.cpu().numpy(), ref.radii)
+    np.testing.assert_array_equal(d["ranges"].cpu().numpy().astype(np.uint32), ref.ranges)
+    np.testing.assert_array_equal(d["point_list"].cpu().numpy().astype(np.uint32), ref.point_list)
+    np.testing.assert_array_equal(d["point_list_keys"].cpu().numpy().view(np.uint64), ref.point_list_keys)
+    got = color.cpu().numpy()
+    assert G.image_l1(got, ref.color) < G.IMAGE_L1_TOL
+    gt = np.clip(ref.color + np.random.default_rng(3).normal(0, 0.05, ref.color.shape), 0, 1).astype(np.float32)
+    assert abs(_psnr(got, gt) - _psnr(ref.color, gt)) < 0.01
+    assert _psnr(got, ref.color) > 80.0
+    dpix = S.make_cotangent(H, W, 1)
+    e = torch.Tensor([])
+    grads = C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, e, t["scales"], t["rotations"],
+                                           s.scale_modifier, e, s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy,
+                                           torch.from_numpy(dpix).cuda(), t["shs"], s.sh_degree, s.campos, geom, K,
+                                           binning, img, False)
+    rg = O.backward(os_, ref, sc.means3D, dpix, **kw)
+    names = ["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    for n, g in zip(names, grads):
+        assert G.rel_err(g.cpu().numpy(), rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(g.cpu().numpy(), rg[n]))
+
+
 @pytest.mark.parametrize("bwd_variant", [0, 1, 2, 3])
 @pytest.mark.parametrize("fwd_variant", [0, 1, 2])
 def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
