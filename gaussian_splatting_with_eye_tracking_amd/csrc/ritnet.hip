@@ -105,6 +105,18 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvIn in, int Cin, int H, in
 // accumulator layout (col = pixel = lane & 31, row = channel = (r & 3) +
 // 8 (r >> 2) + 4 (lane >> 5)) makes every epilogue store a coalesced
 // 128-B row segment of one output channel.
+//
+// Staging is software-pipelined: every thread issues all of its global loads
+// for chunk c + 1 (a compile-time count, unrolled, so they are all in flight
+// at once) into registers before the MFMAs of chunk c and writes them to LDS
+// after them.  A thread owns fixed positions of the input tile and walks the
+// chunk's channels: the channel is wave-uniform, so the segment choice of the
+// virtual concatenation is scalar and each load is a scalar base + the
+// lane's precomputed spatial offset (one for direct, one for upsampled
+// segments; out-of-image positions load a safe address and are zeroed when
+// written to LDS).  Weights are 16-B loads.  (A load-then-store loop
+// serialises one memory latency per element: ~25 us per chunk at the small
+// deep levels.)
 template <int kK>
 __global__ void __launch_bounds__(256) conv_mfma_kernel(ConvIn in, int Cin, int H, int W, const float* __restrict__ w,
                                                         const float* __restrict__ bias, int lrelu,
@@ -114,8 +126,14 @@ __global__ void __launch_bounds__(256) conv_mfma_kernel(ConvIn in, int Cin, int 
     constexpr int kCK = kK == 3 ? 16 : 32;   // input channels per LDS chunk (kCK * kT is even)
     constexpr int kBW = 32, kBH = 8;         // output block: 32 x 8 pixels
     constexpr int kIW = kBW + kK - 1, kIH = kBH + kK - 1;
-    __shared__ float s_in[kCK * kIH * kIW];
-    __shared__ float s_w[kCK * kT * kCo];
+    constexpr int kPos = kIH * kIW;          // input tile positions
+    constexpr int kNP = (kPos + 255) / 256;  // positions per thread
+    constexpr int kNW4 = kCK * kT * kCo / 4; // staged weight float4s per chunk
+    constexpr int kRW = (kNW4 + 255) / 256;
+    __shared__ float s_in[kCK * kPos];
+    __shared__ float4 s_w4[kNW4];
+    const float* s_w = reinterpret_cast<const float*>(s_w4);
+    const float4* __restrict__ w4 = reinterpret_cast<const float4*>(w);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int x0 = blockIdx.x * kBW, y0 = blockIdx.y * kBH;
     typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -125,20 +143,65 @@ __global__ void __launch_bounds__(256) conv_mfma_kernel(ConvIn in, int Cin, int 
 #pragma unroll
         for (int r = 0; r < 16; r++) acc[t][r] = 0.f;
     const int half = lane >> 5, col = lane & 31;
+    // the lane's tile positions: validity and spatial offsets (direct / 2x upsampled)
+    bool pv[kNP];
+    int off0[kNP], off1[kNP];
+#pragma unroll
+    for (int q = 0; q < kNP; q++) {
+        const int pos = tid + 256 * q;
+        const int gy = y0 + pos / kIW - kK / 2, gx = x0 + pos % kIW - kK / 2;
+        pv[q] = pos < kPos && gy >= 0 && gy < H && gx >= 0 && gx < W;
+        off0[q] = pv[q] ? gy * W + gx : 0;
+        off1[q] = pv[q] ? (gy >> 1) * (W >> 1) + (gx >> 1) : 0;
+    }
+    float rin[kCK][kNP];
+    float4 rw[kRW];
+    auto fetch = [&](int c0) {
+#pragma unroll
+        for (int cc = 0; cc < kCK; cc++) {
+            int ci = c0 + cc;  // wave-uniform: scalar segment choice
+            if (ci >= Cin) {
+#pragma unroll
+                for (int q = 0; q < kNP; q++) rin[cc][q] = 0.f;
+                continue;
+            }
+            int sg = 0;
+            if (ci >= in.C[0]) {
+                ci -= in.C[0];
+                sg = 1;
+                if (ci >= in.C[1]) {
+                    ci -= in.C[1];
+                    sg = 2;
+                }
+            }
+            const int u = sg == 0 ? in.up[0] : sg == 1 ? in.up[1] : in.up[2];
+            const float* base = (sg == 0 ? in.p[0] : sg == 1 ? in.p[1] : in.p[2]) +
+                                (size_t)ci * (size_t)(H >> u) * (size_t)(W >> u);
+#pragma unroll
+            for (int q = 0; q < kNP; q++) rin[cc][q] = base[u ? off1[q] : off0[q]];
+        }
+#pragma unroll
+        for (int v = 0; v < kRW; v++) {
+            const int i = tid + 256 * v;
+            float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+            // kT * kCo is a multiple of 4: one float4 never spans two input channels
+            if (i < kNW4 && c0 + (4 * i) / (kT * kCo) < Cin) x = w4[(size_t)c0 * (kT * kCo / 4) + i];
+            rw[v] = x;
+        }
+    };
+    fetch(0);
     for (int c0 = 0; c0 < Cin; c0 += kCK) {
+        __syncthreads();  // the previous chunk's MFMAs are done with the LDS tiles
+#pragma unroll
+        for (int cc = 0; cc < kCK; cc++)
+#pragma unroll
+            for (int q = 0; q < kNP; q++)
+                if (tid + 256 * q < kPos) s_in[cc * kPos + tid + 256 * q] = pv[q] ? rin[cc][q] : 0.f;
+#pragma unroll
+        for (int v = 0; v < kRW; v++)
+            if (tid + 256 * v < kNW4) s_w4[tid + 256 * v] = rw[v];
         __syncthreads();
-        for (int i = tid; i < kCK * kIH * kIW; i += 256) {
-            const int cc = i / (kIH * kIW), rem = i % (kIH * kIW);
-            const int ry = rem / kIW, rx = rem % kIW;
-            const int ci = c0 + cc, gy = y0 + ry - kK / 2, gx = x0 + rx - kK / 2;
-            const bool ok = ci < Cin && gy >= 0 && gy < H && gx >= 0 && gx < W;
-            s_in[i] = ok ? read_in(in, ci, gy, gx, H, W) : 0.f;
-        }
-        for (int i = tid; i < kCK * kT * kCo; i += 256) {
-            const int ci = c0 + i / (kT * kCo);
-            s_w[i] = ci < Cin ? w[(size_t)c0 * kT * kCo + i] : 0.f;
-        }
-        __syncthreads();
+        if (c0 + kCK < Cin) fetch(c0 + kCK);  // in flight during this chunk's MFMAs
 #pragma unroll 2
         for (int kp = 0; kp < kCK * kT / 2; kp++) {
             const int k = 2 * kp + half;
