@@ -43,7 +43,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
     const float4* __restrict__ conic_opacity, const float* __restrict__ colors, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ bg,
-    float* __restrict__ grad_accum, int cull, const uint32_t* __restrict__ order, int gx) {
+    float* __restrict__ grad_accum, int cull, const uint32_t* __restrict__ order, int gx, int xcd) {
 #pragma clang fp contract(fast)
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
@@ -60,7 +60,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int tile = order ? (int)order[blockIdx.x] : (int)blockIdx.x;
+    const int tile = order ? (int)order[blockIdx.x]
+                           : xcd ? xcd_block_tile((int)blockIdx.x, gx, (int)(gridDim.x / gx)) : (int)blockIdx.x;
     const uint32_t ox = (uint32_t)(tile % gx) * 16, oy = (uint32_t)(tile / gx) * 16;
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const int n = (int)(range.y - range.x);
@@ -323,14 +324,14 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
     if (gx == 0 || gy == 0) return;
     const uint32_t* order = nullptr;
     if (tile_order_enabled()) {
-        launch_order_tiles(gx * gy, img, true, s);
+        launch_order_tiles(gx * gy, img, true, s, gx, gy);
         order = img.tile_order;
     }
 #define GS_BWD_LAUNCH(PPL, WAVES, OCC, SWAP)                                                                    \
     hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H,      \
                        img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
-                       dL_dpix, bg, g.grad_accum, g_cull, order, gx)
+                       dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1)
     switch (g_bwd_variant) {
         case 1: GS_BWD_LAUNCH(2, 2, 4, true); break;
         case 2: GS_BWD_LAUNCH(1, 4, 4, true); break;

@@ -20,6 +20,7 @@
 //      larger ones use an LDS chunk sort + in-block merge-path passes.
 // Per instance this moves ~20 B instead of the ~200 B of a 6-pass 64-bit
 // radix sort.
+#include "gs_blend.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
 
@@ -291,8 +292,52 @@ __global__ void __launch_bounds__(kOrderThreads) order_tiles_kernel(int T, const
     for (int t = tid; t < T; t += kOrderThreads) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
 }
 
-void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s) {
+// XCD-aware variant (gs_blend.cuh placement): the tiles of XCD chunk x
+// (a compact region) go to the blocks b = 8 k + x, heaviest first within
+// the chunk.  One workgroup, 8 counting sorts (one per chunk) in LDS.
+__global__ void __launch_bounds__(kOrderThreads) order_tiles_xcd_kernel(int T, int gx, int gy,
+                                                                        const uint32_t* __restrict__ ranges,
+                                                                        const uint32_t* __restrict__ max_contrib,
+                                                                        uint32_t* __restrict__ order) {
+    constexpr int kXB = kOrderBuckets / 4;  // 256 buckets per chunk: 8 x 256 counters
+    __shared__ uint32_t hist[8 * kXB];
+    __shared__ uint32_t s_wave[kOrderThreads / 64 + 1];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 8 * kXB; i += kOrderThreads) hist[i] = 0;
+    __syncthreads();
+    auto key = [&](int t) -> uint32_t {
+        uint32_t w = ranges[2 * t + 1] - ranges[2 * t];
+        if (max_contrib) w = min(w, max_contrib[t]);
+        const uint32_t b = min((uint32_t)(16.0f * __log2f((float)w + 1.0f)), (uint32_t)(kXB - 1));
+        const int x = xcd_chunk_of_pos(xcd_strip_pos_of_tile(t, gx, gy), T);
+        return (uint32_t)x * kXB + (uint32_t)(kXB - 1) - b;  // chunk-major, heaviest first
+    };
+    for (int t = tid; t < T; t += kOrderThreads) atomicAdd(&hist[key(t)], 1u);
+    __syncthreads();
+    // exclusive scan of the 2048 counters, 2 per thread; the chunk starts
+    // (xcd_chunk_start) fall out of it because chunk x holds exactly its tiles
+    const uint32_t a0 = hist[2 * tid], a1 = hist[2 * tid + 1];
+    uint32_t total;
+    const uint32_t base = block_exclusive_scan<kOrderThreads>(a0 + a1, s_wave, total);
+    __syncthreads();
+    hist[2 * tid] = base;
+    hist[2 * tid + 1] = base + a0;
+    __syncthreads();
+    for (int t = tid; t < T; t += kOrderThreads) {
+        const uint32_t k = key(t);
+        const int x = (int)(k / kXB);
+        const int rank = (int)atomicAdd(&hist[k], 1u) - xcd_chunk_start(x, T);
+        order[8 * rank + x] = (uint32_t)t;
+    }
+}
+
+void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s, int gx, int gy) {
     if (T <= 0) return;
+    if ((g_xcd_map & 2) && gx > 0 && T >= 8) {
+        hipLaunchKernelGGL(order_tiles_xcd_kernel, dim3(1), dim3(kOrderThreads), 0, s, T, gx, gy, img.ranges,
+                           use_max_contrib ? img.max_contrib : nullptr, img.tile_order);
+        return;
+    }
     hipLaunchKernelGGL(order_tiles_kernel, dim3(1), dim3(kOrderThreads), 0, s, T, img.ranges,
                        use_max_contrib ? img.max_contrib : nullptr, img.tile_order);
 }

@@ -698,6 +698,10 @@ int gs_set_tuning(const char* key, int value) {
         set_amr_variant(value);
         return 0;
     }
+    if (std::strcmp(key, "xcd_map") == 0) {
+        set_xcd_map(value);
+        return 0;
+    }
     if (std::strcmp(key, "tile_order") == 0) {
         set_tile_order(value);
         return 0;

@@ -83,6 +83,49 @@ __device__ __forceinline__ PixelSet make_pixels(int W, int H, uint32_t ox, uint3
 }
 
 
+// ------------------------------------------------------ XCD-aware placement
+// Blocks b and b + 8 run on one XCD (round-robin dispatch; MI355X_MICROARCH.md
+// §Workgroup dispatch -- observed, speed only), and each XCD has its own 4 MiB
+// L2.  With row-major tiles, neighbouring tiles -- which share most of their
+// Gaussians -- land on 8 different L2s and every gather of a shared record
+// misses 8 times.  Instead the tiles are laid out in a 2-D-compact order
+// (strips of kXcdStrip tile rows, walked column by column) and that order is
+// cut into 8 contiguous chunks, chunk x going to the blocks b = 8 k + x: each
+// XCD renders one compact region, in order.
+constexpr int kXcdStrip = 4;
+
+// position p of the strip order -> tile index
+__host__ __device__ __forceinline__ int xcd_strip_tile_of_pos(int p, int gx, int gy) {
+    const int s = p / (kXcdStrip * gx), q = p - s * kXcdStrip * gx;
+    const int rows = min(kXcdStrip, gy - s * kXcdStrip);
+    const int col = q / rows, r = q - col * rows;
+    return (s * kXcdStrip + r) * gx + col;
+}
+
+// tile index -> position p of the strip order
+__host__ __device__ __forceinline__ int xcd_strip_pos_of_tile(int t, int gx, int gy) {
+    const int row = t / gx, col = t - row * gx;
+    const int s = row / kXcdStrip, r = row - s * kXcdStrip;
+    const int rows = min(kXcdStrip, gy - s * kXcdStrip);
+    return s * kXcdStrip * gx + col * rows + r;
+}
+
+// chunk x of the NB positions: start(x) = x q + min(x, NB % 8), q = NB / 8
+__host__ __device__ __forceinline__ int xcd_chunk_start(int x, int NB) { return x * (NB / 8) + min(x, NB % 8); }
+
+__host__ __device__ __forceinline__ int xcd_chunk_of_pos(int p, int NB) {
+    const int q = NB / 8, rem = NB % 8;
+    if (p < rem * (q + 1)) return p / (q + 1);
+    return rem + (p - rem * (q + 1)) / q;
+}
+
+// block b -> tile (b = 8 k + x takes position start(x) + k)
+__device__ __forceinline__ int xcd_block_tile(int b, int gx, int gy) {
+    const int NB = gx * gy;
+    if (NB < 8) return b;
+    return xcd_strip_tile_of_pos(xcd_chunk_start(b & 7, NB) + (b >> 3), gx, gy);
+}
+
 // ------------------------------------------------------------ row-group cull
 // A (pixel, Gaussian) pair is blended only if alpha = min(0.99, o*exp(power))
 // >= 1/255 with power = -Q/2, Q = d^T C d (C = conic, d = mean - pixel), i.e.

@@ -51,7 +51,7 @@ void set_bin_chunk(int gaussians_per_workgroup);
 // long tiles of a blend launch start early instead of forming its tail.
 // Work = range length, or min(range length, max_contrib) if use_max_contrib.
 // Used by the backward blend (render_bwd 1.15 -> 1.06 ms at config 2).
-void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s);
+void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s, int gx = 0, int gy = 0);
 bool tile_order_enabled();
 void set_tile_order(int v);
 void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int max_count_host, int num_large_host,
@@ -65,6 +65,8 @@ void launch_render_forward(int W, int H, const ImageView& img, const BinningView
                            const float* features, const float* bg, float* out_color, hipStream_t s);
 // Tuning knob for A/B runs (gs_set_tuning("fwd_variant", v)).
 void set_forward_variant(int v);
+void set_xcd_map(int v);
+extern int g_xcd_map;
 void set_cull(int v);
 void set_amr_variant(int v);
 void set_ritnet_mfma(int v);

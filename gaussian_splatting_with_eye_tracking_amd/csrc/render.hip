@@ -54,14 +54,16 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
                                                                  uint32_t* __restrict__ max_contrib,
                                                                  const float* __restrict__ bg,
                                                                  float* __restrict__ out_color, int cull,
-                                                                 const uint32_t* __restrict__ order, int gx) {
+                                                                 const uint32_t* __restrict__ order, int gx,
+                                                                 int xcd) {
     __shared__ float2 s_xy[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
     __shared__ float4 s_rgb[64 * kWaves];
     __shared__ uint64_t s_bal[4 * kWaves];
     __shared__ uint32_t s_max;
     if (kWaves > 1 && threadIdx.x == 0) s_max = 0;
-    const int tile = order ? (int)order[blockIdx.x] : (int)blockIdx.x;
+    const int tile = order ? (int)order[blockIdx.x]
+                           : xcd ? xcd_block_tile((int)blockIdx.x, gx, (int)(gridDim.x / gx)) : (int)blockIdx.x;
     const uint32_t ox = (uint32_t)(tile % gx) * 16, oy = (uint32_t)(tile / gx) * 16;
     const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, 1);
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
@@ -85,6 +87,15 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
 int g_cull = 1;         // row-group cull on (gs_blend.cuh); 0 only for the exactness A/B test
 void set_cull(int v) { g_cull = v; }
 
+// XCD-aware tile placement (gs_blend.cuh): bit 0 the forward blend, bit 1 the
+// backward blend.  Measured at config 2 (profiles/r01g_xcd_ab.log): it halves
+// the blend kernels' L2 -> fabric fetches (forward 770 -> 395 MB, backward
+// 1100 -> 602 MB per launch) at the same forward time; the backward keeps the
+// global heaviest-first order, 1.7 % faster than per-XCD heaviest-first
+// (its XCD regions carry unequal work).  Default: forward only.
+int g_xcd_map = 1;
+void set_xcd_map(int v) { g_xcd_map = v; }
+
 int g_fwd_variant = 2;  // 0: 1 wave x 4 px/lane, 1: 2 waves x 2 px/lane, 2: 4 waves x 1 px/lane
 
 void set_forward_variant(int v) { g_fwd_variant = v; }
@@ -101,7 +112,7 @@ void launch_render_forward(int W, int H, const ImageView& img, const BinningView
     hipLaunchKernelGGL((render_fwd_kernel<PPL, WAVES>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H, img.ranges, \
                        b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
-                       img.max_contrib, bg, out_color, g_cull, order, gx)
+                       img.max_contrib, bg, out_color, g_cull, order, gx, g_xcd_map & 1)
     switch (g_fwd_variant) {
         case 0: GS_FWD_LAUNCH(4, 1); break;
         case 1: GS_FWD_LAUNCH(2, 2); break;

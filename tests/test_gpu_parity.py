@@ -126,6 +126,37 @@ def test_backward_parity(name, P, W, H, seed, variant):
         assert G.rel_err(gg, rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(gg, rg[n]))
 
 
+@pytest.mark.parametrize("xcd_map", [0, 1, 2, 3])
+def test_xcd_placement_is_result_invariant(xcd_map):
+    """XCD-aware tile placement (gs_blend.cuh; bit 0 forward, bit 1
+    backward) only changes which workgroup renders which tile: forward
+    buffers bit-identical, image and gradients within the bars, on a grid
+    whose tile count is not a multiple of 8 (ragged XCD chunks)."""
+    import oracle as O
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    P, W, H, seed = 6000, 250, 130, 7  # 16 x 9 = 144 tiles
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    C.set_tuning("xcd_map", xcd_map)
+    try:
+        s, t, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
+        dpix = S.make_cotangent(H, W, seed + 1)
+        e = torch.Tensor([])
+        grads = C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, e, t["scales"], t["rotations"],
+                                               s.scale_modifier, e, s.viewmatrix, s.projmatrix, s.tanfovx,
+                                               s.tanfovy, torch.from_numpy(dpix).cuda(), t["shs"], s.sh_degree,
+                                               s.campos, geom, K, binning, img, False)
+        torch.cuda.synchronize()
+    finally:
+        C.set_tuning("xcd_map", 1)
+    os_, ref, kw = _oracle_forward(sc, cam)
+    assert G.image_l1(color.cpu().numpy(), ref.color) < G.IMAGE_L1_TOL
+    rg = O.backward(os_, ref, sc.means3D, dpix, **kw)
+    for n, g in zip(["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
+                     "dL_dscales", "dL_drotations"], grads):
+        assert G.rel_err(g.cpu().numpy(), rg[n]) < G.GRAD_REL_TOL, n
+
+
 def _psnr(img, gt):
     """utils/image_utils.py:19-21 (per leading row, then the mean as
     metrics.py / train.py report it), on images clamped to [0, 1] as saved."""
