@@ -690,6 +690,10 @@ int gs_set_tuning(const char* key, int value) {
         set_bwd_gauss_split(value);
         return 0;
     }
+    if (std::strcmp(key, "ritnet_small_wgs") == 0) {
+        set_ritnet_small_wgs(value);
+        return 0;
+    }
     if (std::strcmp(key, "ritnet_mfma") == 0) {
         set_ritnet_mfma(value);
         return 0;

@@ -117,14 +117,14 @@ __global__ void __launch_bounds__(256) conv_kernel(ConvIn in, int Cin, int H, in
 // written to LDS).  Weights are 16-B loads.  (A load-then-store loop
 // serialises one memory latency per element: ~25 us per chunk at the small
 // deep levels.)
-template <int kK>
+template <int kK, int kR>
 __global__ void __launch_bounds__(256) conv_mfma_kernel(ConvIn in, int Cin, int H, int W, const float* __restrict__ w,
                                                         const float* __restrict__ bias, int lrelu,
                                                         const float* __restrict__ bn_scale,
                                                         const float* __restrict__ bn_shift, float* __restrict__ out) {
     constexpr int kT = kK * kK;              // taps
     constexpr int kCK = kK == 3 ? 16 : 32;   // input channels per LDS chunk (kCK * kT is even)
-    constexpr int kBW = 32, kBH = 8;         // output block: 32 x 8 pixels
+    constexpr int kBW = 32, kBH = 4 * kR;    // output block: 32 x 4 kR pixels (kR rows per wave)
     constexpr int kIW = kBW + kK - 1, kIH = kBH + kK - 1;
     constexpr int kPos = kIH * kIW;          // input tile positions
     constexpr int kNP = (kPos + 255) / 256;  // positions per thread
@@ -137,9 +137,9 @@ __global__ void __launch_bounds__(256) conv_mfma_kernel(ConvIn in, int Cin, int 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int x0 = blockIdx.x * kBW, y0 = blockIdx.y * kBH;
     typedef float f32x16 __attribute__((ext_vector_type(16)));
-    f32x16 acc[2];
+    f32x16 acc[kR];
 #pragma unroll
-    for (int t = 0; t < 2; t++)
+    for (int t = 0; t < kR; t++)
 #pragma unroll
         for (int r = 0; r < 16; r++) acc[t][r] = 0.f;
     const int half = lane >> 5, col = lane & 31;
@@ -208,8 +208,8 @@ __global__ void __launch_bounds__(256) conv_mfma_kernel(ConvIn in, int Cin, int 
             const int cc = k / kT, tap = k % kT;
             const float a = s_w[k * kCo + col];
 #pragma unroll
-            for (int t = 0; t < 2; t++) {
-                const int ry = 2 * wave + t + tap / kK, rx = col + tap % kK;
+            for (int t = 0; t < kR; t++) {
+                const int ry = kR * wave + t + tap / kK, rx = col + tap % kK;
                 const float b = s_in[(cc * kIH + ry) * kIW + rx];
                 acc[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[t], 0, 0, 0);
             }
@@ -218,8 +218,8 @@ __global__ void __launch_bounds__(256) conv_mfma_kernel(ConvIn in, int Cin, int 
     const size_t plane = (size_t)H * W;
     const int x = x0 + col;
 #pragma unroll
-    for (int t = 0; t < 2; t++) {
-        const int y = y0 + 2 * wave + t;
+    for (int t = 0; t < kR; t++) {
+        const int y = y0 + kR * wave + t;
         if (x >= W || y >= H) continue;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
@@ -310,6 +310,8 @@ __global__ void __launch_bounds__(256) label_moments_kernel(const uint8_t* __res
 
 int g_ritnet_mfma = 1;  // 1: conv_mfma_kernel (default), 0: the SGPR-weight FMA kernel
 void set_ritnet_mfma(int v) { g_ritnet_mfma = v; }
+int g_ritnet_small_wgs = 512;  // below this many 32 x 8 blocks: 32 x 4 blocks (one row per wave)
+void set_ritnet_small_wgs(int v) { g_ritnet_small_wgs = v; }
 
 void launch_ritnet_conv(int k, const float* const* in_ptr, const int* in_c, const int* in_up, int nseg, int H, int W,
                         const float* w, const float* bias, int lrelu, const float* bn_scale, const float* bn_shift,
@@ -323,13 +325,18 @@ void launch_ritnet_conv(int k, const float* const* in_ptr, const int* in_c, cons
         Cin += in.C[i];
     }
     if (g_ritnet_mfma) {
-        const dim3 grid((W + 31) / 32, (H + 7) / 8);
-        if (k == 3)
-            hipLaunchKernelGGL(conv_mfma_kernel<3>, grid, dim3(256), 0, s, in, Cin, H, W, w, bias, lrelu, bn_scale,
-                               bn_shift, out);
-        else
-            hipLaunchKernelGGL(conv_mfma_kernel<1>, grid, dim3(256), 0, s, in, Cin, H, W, w, bias, lrelu, bn_scale,
-                               bn_shift, out);
+        // small planes (the deep levels) are latency-bound: one row per wave
+        // doubles the workgroups and halves each wave's MFMA chain
+        const bool small = ((W + 31) / 32) * ((H + 7) / 8) < g_ritnet_small_wgs;
+        const dim3 grid((W + 31) / 32, small ? (H + 3) / 4 : (H + 7) / 8);
+#define GS_CONV_MFMA(K, R) \
+    hipLaunchKernelGGL((conv_mfma_kernel<K, R>), grid, dim3(256), 0, s, in, Cin, H, W, w, bias, lrelu, bn_scale, bn_shift, out)
+        if (k == 3) {
+            if (small) GS_CONV_MFMA(3, 1); else GS_CONV_MFMA(3, 2);
+        } else {
+            if (small) GS_CONV_MFMA(1, 1); else GS_CONV_MFMA(1, 2);
+        }
+#undef GS_CONV_MFMA
         return;
     }
     const dim3 grid((W + 63) / 64, (H + 3) / 4);
