@@ -372,10 +372,36 @@ __device__ __forceinline__ void bitonic_lds(uint64_t* s, int S) {
 //   j >= 64 E      partner in another wave: one LDS exchange + 2 barriers.
 // Only log2(S/64E)... the last few stages of each merge touch LDS, so a
 // 1024-key tile does 3 LDS stages instead of 55 LDS round trips.
+// v of lane ^ m for m in {1, 2, 4, 8, 16, 32}.  m is a constant once the
+// sort network is unrolled, so the chain folds to one cross-lane op: DPP
+// quad_perm (m = 1, 2: a VALU modifier), ds_swizzle bit mode (m = 4, 8: the
+// LDS crossbar without an address VGPR), v_permlane16/32_swap (m = 16, 32:
+// VALU) -- instead of ds_bpermute for every stage.
+__device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int m) {
+    if (m == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+    if (m == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+    if (m == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F);               // and 0x1f, xor 4
+    if (m == 8) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x201F);               // and 0x1f, xor 8
+    const int lane = (int)__lane_id();
+    if (m == 16) {
+        // with vdst = vsrc = v: r0 = [row0, row0, row2, row2], r1 = [row1, row1, row3, row3]
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        const uint32_t r0 = r[0], r1 = r[1];
+        return (lane & 16) ? r0 : r1;
+    }
+    if (m == 32) {
+        // r0 = [lo, lo], r1 = [hi, hi] (32-lane halves)
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        const uint32_t r0 = r[0], r1 = r[1];
+        return (lane & 32) ? r0 : r1;
+    }
+    return (uint32_t)__shfl_xor((int)v, m, 64);
+}
+
 __device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-    const int lo = __shfl_xor((int)(uint32_t)v, m, 64);
-    const int hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+    const uint32_t lo = shfl_xor_u32((uint32_t)v, m);
+    const uint32_t hi = shfl_xor_u32((uint32_t)(v >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
 }
 
 template <int E, int kWavesUsed>
