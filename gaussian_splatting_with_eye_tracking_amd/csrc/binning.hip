@@ -372,36 +372,46 @@ __device__ __forceinline__ void bitonic_lds(uint64_t* s, int S) {
 //   j >= 64 E      partner in another wave: one LDS exchange + 2 barriers.
 // Only log2(S/64E)... the last few stages of each merge touch LDS, so a
 // 1024-key tile does 3 LDS stages instead of 55 LDS round trips.
-// v of lane ^ m for m in {1, 2, 4, 8, 16, 32}.  m is a constant once the
-// sort network is unrolled, so the chain folds to one cross-lane op: DPP
-// quad_perm (m = 1, 2: a VALU modifier), ds_swizzle bit mode (m = 4, 8: the
-// LDS crossbar without an address VGPR), v_permlane16/32_swap (m = 16, 32:
-// VALU) -- instead of ds_bpermute for every stage.
-__device__ __forceinline__ uint32_t shfl_xor_u32(uint32_t v, int m) {
-    if (m == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
-    if (m == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
-    if (m == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F);               // and 0x1f, xor 4
-    if (m == 8) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x201F);               // and 0x1f, xor 8
-    const int lane = (int)__lane_id();
-    if (m == 16) {
+// v of lane ^ M for M in {1, 2, 4, 8, 16, 32}, one cross-lane op each: DPP
+// quad_perm (M = 1, 2: a VALU modifier), ds_swizzle bit mode (M = 4, 8: the
+// LDS crossbar without an address VGPR), v_permlane16/32_swap (M = 16, 32:
+// VALU) -- instead of ds_bpermute.
+template <int M>
+__device__ __forceinline__ uint32_t shfl_xor_c(uint32_t v) {
+    static_assert(M == 1 || M == 2 || M == 4 || M == 8 || M == 16 || M == 32, "xor distance");
+    if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);  // [1,0,3,2]
+    if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);  // [2,3,0,1]
+    if constexpr (M == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x101F);              // and 0x1f, xor 4
+    if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x201F);              // and 0x1f, xor 8
+    if constexpr (M == 16) {
         // with vdst = vsrc = v: r0 = [row0, row0, row2, row2], r1 = [row1, row1, row3, row3]
         const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
         const uint32_t r0 = r[0], r1 = r[1];
-        return (lane & 16) ? r0 : r1;
+        return (__lane_id() & 16) ? r0 : r1;
     }
-    if (m == 32) {
+    if constexpr (M == 32) {
         // r0 = [lo, lo], r1 = [hi, hi] (32-lane halves)
         const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
         const uint32_t r0 = r[0], r1 = r[1];
-        return (lane & 32) ? r0 : r1;
+        return (__lane_id() & 32) ? r0 : r1;
     }
-    return (uint32_t)__shfl_xor((int)v, m, 64);
+    return v;
 }
 
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-    const uint32_t lo = shfl_xor_u32((uint32_t)v, m);
-    const uint32_t hi = shfl_xor_u32((uint32_t)(v >> 32), m);
-    return ((uint64_t)hi << 32) | lo;
+// One cross-lane compare-exchange stage (k, j) with partner distance
+// M = j / E lanes.
+template <int M, int E>
+__device__ __forceinline__ void bitonic_cross_stage(uint64_t (&v)[E], int k, int j) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = tid * E + e;
+        const uint32_t lo = shfl_xor_c<M>((uint32_t)v[e]);
+        const uint32_t hi = shfl_xor_c<M>((uint32_t)(v[e] >> 32));
+        const uint64_t p = ((uint64_t)hi << 32) | lo;
+        const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+        v[e] = keep_min ? (v[e] < p ? v[e] : p) : (v[e] < p ? p : v[e]);
+    }
 }
 
 template <int E, int kWavesUsed>
@@ -424,12 +434,27 @@ __device__ __forceinline__ void bitonic_regs(uint64_t (&v)[E], uint64_t* lds) {
                     v[e | j] = sw ? a : b;
                 }
             } else if (j < 64 * E) {
+                if constexpr (E > 4) {
+                    // E = 8, 16: the network is not fully unrolled; measured, a
+                    // per-stage switch over the specialised moves ran 2.3x slower
+                    // at config 4 than ds_bpermute (1.06 vs 0.46 ms)
 #pragma unroll
-                for (int e = 0; e < E; e++) {
-                    const int i = tid * E + e;
-                    const uint64_t p = shfl_xor_u64(v[e], j / E);
-                    const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
-                    v[e] = keep_min ? (v[e] < p ? v[e] : p) : (v[e] < p ? p : v[e]);
+                    for (int e = 0; e < E; e++) {
+                        const int i = tid * E + e;
+                        const int m = j / E;
+                        const int lo = __shfl_xor((int)(uint32_t)v[e], m, 64);
+                        const int hi = __shfl_xor((int)(uint32_t)(v[e] >> 32), m, 64);
+                        const uint64_t p = ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+                        const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+                        v[e] = keep_min ? (v[e] < p ? v[e] : p) : (v[e] < p ? p : v[e]);
+                    }
+                } else switch (j / E) {  // folded: the E <= 4 networks are fully unrolled
+                    case 1: bitonic_cross_stage<1, E>(v, k, j); break;
+                    case 2: bitonic_cross_stage<2, E>(v, k, j); break;
+                    case 4: bitonic_cross_stage<4, E>(v, k, j); break;
+                    case 8: bitonic_cross_stage<8, E>(v, k, j); break;
+                    case 16: bitonic_cross_stage<16, E>(v, k, j); break;
+                    default: bitonic_cross_stage<32, E>(v, k, j); break;
                 }
             } else {
 #pragma unroll
