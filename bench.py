@@ -259,10 +259,30 @@ def run_amr(args, world, rank, local_rank, distributed, dev):
         if distributed:
             dist.barrier()
         elf = time.perf_counter() - t0
+    # extension: the foveated backward -- render_once (interpolated) forward +
+    # backward through the drop-in autograd API with a fixed cotangent
+    tg = {k: v.detach().clone().requires_grad_(True) for k, v in t.items()}
+    m2 = torch.zeros_like(tg["means3D"], requires_grad=True)
+    cot = torch.from_numpy(S.make_cotangent(H, W, 1)).to(dev)
+
+    def frame_once_fwd_bwd():
+        img = rast(means3D=tg["means3D"], means2D=m2, opacities=tg["opacities"], shs=tg["shs"],
+                   scales=tg["scales"], rotations=tg["rotations"], foveaStep=-2, interpolate_image=True)[0]
+        torch.autograd.backward(img, cot)
+
+    for _ in range(max(1, args.warmup)):
+        frame_once_fwd_bwd()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame_once_fwd_bwd()
+    torch.cuda.synchronize()
+    elb = time.perf_counter() - t0
+    with torch.no_grad():
         if distributed:
-            tt = torch.tensor([el5, el1, elf], device=dev, dtype=torch.float64)
+            tt = torch.tensor([el5, el1, elf, elb], device=dev, dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el5, el1, elf = float(tt[0].item()), float(tt[1].item()), float(tt[2].item())
+            el5, el1, elf, elb = (float(v) for v in tt.tolist())
         result = None
         if rank == 0:
             acc, gb, bb, ib = frame_5step()
@@ -298,6 +318,9 @@ def run_amr(args, world, rank, local_rank, distributed, dev):
                            "P": P, "width": W, "height": H, "K_instances": K, "parallelism": f"replicas{world}",
                            "levels_hist": np.bincount(lv, minlength=5)[1:].tolist()},
                 "render_once_fps": world * args.steps / el1,
+                "amr_backward_ext": {"render_once_fwd_bwd_fps": world * args.steps / elb,
+                                     "note": "extension beyond parity: interpolated render_once forward + "
+                                             "backward through the autograd API"},
                 "fovea_levels_ext": {"fps": world * args.steps / elf, "centre": [round(v, 2) for v in fov_centres[0]],
                                      "radii": fov_radii, "levels_hist": fovea_hist,
                                      "note": "extension beyond parity: tracked fovea discs clamp the AMR levels"},

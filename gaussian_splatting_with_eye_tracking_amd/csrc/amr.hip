@@ -125,6 +125,51 @@ void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s) {
                        img.levels_current, img.levels);
 }
 
+// Backward of render_once's interpolation (amr/cr/forward.cu:520-648, the
+// foveaStep < 0 branch): a pixel whose round exceeds its tile's level is a
+// copy of its 2x2 cell's (0, 0) (levels 1, 2) or (1, 1) (level 3) pixel, so
+// its cotangent is added to that source's.  One thread per cell, copies
+// summed in round order; rendered pixels keep their own cotangent, copies
+// get 0 (the blend backward reads only rendered pixels).
+__global__ void __launch_bounds__(256) amr_interp_fold_kernel(int W, int H, int tgx, const uint32_t* __restrict__ levels,
+                                                              const float* __restrict__ g_in,
+                                                              float* __restrict__ g_out) {
+    const int cw = (W + 1) / 2, ch = (H + 1) / 2;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= cw * ch) return;
+    const int cx = c % cw, cy = c / cw;
+    const int x0 = 2 * cx, y0 = 2 * cy;
+    const uint32_t L = min(levels[(y0 / 32) * tgx + x0 / 32], 4u);
+    const int o = (L == 3 || L == 4) ? 1 : 0;
+    const int sxp = x0 + o, syp = y0 + o;
+    const bool src_in = sxp < W && syp < H;
+    const size_t plane = (size_t)W * H;
+    // the cell's pixels in round order 1..4: (0,0), (1,1), (1,0), (0,1)
+    const int dxs[4] = {0, 1, 1, 0}, dys[4] = {0, 1, 0, 1};
+    for (int ch3 = 0; ch3 < 3; ch3++) {
+        float fold = 0.f;
+        for (int r = 0; r < 4; r++) {
+            const int px = x0 + dxs[r], py = y0 + dys[r];
+            if (px >= W || py >= H) continue;
+            const size_t pid = (size_t)py * W + px;
+            if ((uint32_t)(r + 1) <= L) {
+                g_out[ch3 * plane + pid] = g_in[ch3 * plane + pid];
+            } else {
+                g_out[ch3 * plane + pid] = 0.f;
+                if (src_in) fold += g_in[ch3 * plane + pid];
+            }
+        }
+        if (src_in && L < 4) g_out[ch3 * plane + (size_t)syp * W + sxp] += fold;
+    }
+}
+
+void launch_amr_interp_fold(int W, int H, const ImageView& img, const float* g_in, float* g_out, hipStream_t s) {
+    const int cells = ((W + 1) / 2) * ((H + 1) / 2);
+    if (cells == 0) return;
+    hipLaunchKernelGGL(amr_interp_fold_kernel, dim3((cells + 255) / 256), dim3(256), 0, s, W, H, (W + 31) / 32,
+                       img.levels, g_in, g_out);
+}
+
 // Fovea-driven levels (an extension beyond parity).
 // The reference defines per-step fovea centres and radii
 // (gaussian_renderer_amr/__init__.py:98-106: centre = image centre, radii

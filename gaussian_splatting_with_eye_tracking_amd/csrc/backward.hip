@@ -43,7 +43,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
     const float4* __restrict__ conic_opacity, const float* __restrict__ colors, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ bg,
-    float* __restrict__ grad_accum, int cull, const uint32_t* __restrict__ order, int gx, int xcd) {
+    float* __restrict__ grad_accum, int cull, const uint32_t* __restrict__ order, int gx, int xcd,
+    int amr_mode, const uint32_t* __restrict__ levels) {
 #pragma clang fp contract(fast)
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
@@ -60,15 +61,35 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const int tile = order ? (int)order[blockIdx.x]
-                           : xcd ? xcd_block_tile((int)blockIdx.x, gx, (int)(gridDim.x / gx)) : (int)blockIdx.x;
-    const uint32_t ox = (uint32_t)(tile % gx) * 16, oy = (uint32_t)(tile / gx) * 16;
+    // AMR mode (amr_mode != 0; the foveated backward, an extension beyond
+    // parity): block b = (32-px tile b / 4, sub-lattice (b & 1, (b >> 1) & 1)),
+    // its 16 x 16 pixels at stride 2 -- the pixels amr_render_kernel blended
+    // for that AMR round.  amr_mode = k > 0: foveaStep k's image (round k of
+    // tiles with level >= k); < 0: render_once (rounds <= level).
+    int tile;
+    uint32_t ox, oy;
+    uint32_t pstride = 1;
+    if (amr_mode != 0) {
+        tile = (int)(blockIdx.x >> 2);
+        const uint32_t sx = blockIdx.x & 1u, sy = (blockIdx.x >> 1) & 1u;
+        const uint32_t round = sx == 0 ? (sy == 0 ? 1u : 4u) : (sy == 0 ? 3u : 2u);  // amr/cr/forward.cu:313-339
+        const uint32_t L = min(levels[tile], 4u);
+        if (amr_mode > 0 ? (round != (uint32_t)amr_mode || L < round) : round > L) return;
+        ox = (uint32_t)(tile % gx) * 32 + sx;
+        oy = (uint32_t)(tile / gx) * 32 + sy;
+        pstride = 2;
+    } else {
+        tile = order ? (int)order[blockIdx.x]
+                     : xcd ? xcd_block_tile((int)blockIdx.x, gx, (int)(gridDim.x / gx)) : (int)blockIdx.x;
+        ox = (uint32_t)(tile % gx) * 16;
+        oy = (uint32_t)(tile / gx) * 16;
+    }
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const int n = (int)(range.y - range.x);
-    const int m = min(n, (int)max_contrib[tile]);
+    int m = amr_mode != 0 ? n : min(n, (int)max_contrib[tile]);
     if (m == 0) return;  // block-uniform
 
-    const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, 1);
+    const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, pstride);
     const size_t plane = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
     // accum_rec . dL_dpix is all the reference's accum_rec / last_color
@@ -102,6 +123,12 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) g = max(g, (uint32_t)__shfl_xor((int)g, off, 64));
         group_last[k] = __builtin_amdgcn_readfirstlane((int)g);
+    }
+    // AMR: no per-tile max_contrib was recorded for the sub-lattice; with one
+    // wave per block (the only AMR instantiation) the wave max is the block's
+    if (amr_mode != 0) {
+        m = min(n, (int)wave_last);
+        if (m == 0) return;
     }
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
@@ -137,7 +164,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             s_xy[tid] = xy;
             s_co[tid] = splat_coef(co);
             s_rgb[tid] = make_float4(nrgb[0], nrgb[1], nrgb[2], 0.f);
-            gm = cull ? splat_group_mask(xy, co, (float)ox, (float)oy, 1.0f) : 0xfu;
+            gm = cull ? splat_group_mask(xy, co, (float)ox, (float)oy, (float)pstride) : 0xfu;
         }
         const int ntop = top - kB;  // the next batch: entries [ntop - ncnt, ntop)
         const bool has_next = ntop > 0 && tid < min(kB, ntop);
@@ -331,7 +358,7 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
     hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H,      \
                        img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
-                       dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1)
+                       dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1, 0, nullptr)
     switch (g_bwd_variant) {
         case 1: GS_BWD_LAUNCH(2, 2, 4, true); break;
         case 2: GS_BWD_LAUNCH(1, 4, 4, true); break;
@@ -339,6 +366,21 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         default: GS_BWD_LAUNCH(4, 1, 4, true); break;
     }
 #undef GS_BWD_LAUNCH
+}
+
+// The foveated (AMR) blend backward: 32-px tile ranges, one wave per
+// (tile, sub-lattice) block of 16 x 16 pixels at stride 2, only the blocks
+// whose round the forward rendered (mode: foveaStep k > 0, or < 0 for
+// render_once).  The 1 wave x 4 px geometry (gs_blend.cuh) only.
+void launch_amr_render_backward(int W, int H, int mode, const ImageView& img, const BinningView& b,
+                                const GeomView& g, const float* colors, const float* bg, const float* dL_dpix,
+                                hipStream_t s) {
+    const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
+    if (tgx == 0 || tgy == 0 || mode == 0) return;
+    hipLaunchKernelGGL((render_bwd_kernel<4, 1, 4, true>), dim3(4 * tgx * tgy), dim3(64), 0, s, W, H, img.ranges,
+                       img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),
+                       reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,
+                       dL_dpix, bg, g.grad_accum, g_cull, nullptr, tgx, 0, mode, img.levels);
 }
 
 // ------------------------------------------------------ per-Gaussian bwd ---

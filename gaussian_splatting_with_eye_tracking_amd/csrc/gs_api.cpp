@@ -255,18 +255,23 @@ int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image
     });
 }
 
-int gs_rasterizer_backward(int P, int D, int M, int R, const float* background, int width, int height,
-                           const float* means3D, const float* shs, const float* colors_precomp, const float* scales,
-                           float scale_modifier, const float* rotations, const float* cov3D_precomp,
-                           const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
-                           float tan_fovy, const int* radii, char* geom_buffer, char* binning_buffer,
-                           char* img_buffer, const float* dL_dpix, float* dL_dmean2D, float* dL_dconic,
-                           float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
-                           float* dL_dsh, float* dL_dscale, float* dL_drot, int debug, void* stream) {
-    return guarded([&]() -> int {
+namespace {
+// Shared by the base and the AMR backward.  amr_mode 0: base 16-px tiles;
+// != 0: AMR 32-px tiles, the rendered sub-lattices of foveaStep amr_mode
+// (> 0) or of render_once (< 0; dL_dpix already folded through the
+// interpolation when it was applied).
+int rasterizer_backward_impl(int amr_mode, int P, int D, int M, int R, const float* background, int width,
+                             int height, const float* means3D, const float* shs, const float* colors_precomp,
+                             const float* scales, float scale_modifier, const float* rotations,
+                             const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                             const float* campos, float tan_fovx, float tan_fovy, const int* radii, char* geom_buffer,
+                             char* binning_buffer, char* img_buffer, const float* dL_dpix, float* dL_dmean2D,
+                             float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D,
+                             float* dL_dcov3D, float* dL_dsh, float* dL_dscale, float* dL_drot, int debug,
+                             hipStream_t s) {
+    {
         if (P <= 0) return 0;
-        hipStream_t s = static_cast<hipStream_t>(stream);
-        const int tile = 16;
+        const int tile = amr_mode != 0 ? 32 : 16;
         const int T = ((width + tile - 1) / tile) * ((height + tile - 1) / tile);
         GeomView g;
         ImageView img;
@@ -277,7 +282,11 @@ int gs_rasterizer_backward(int P, int D, int M, int R, const float* background, 
         if (!radii) radii = g.radii;
         { StageTimer _t(kZero, s); GS_HIP(hipMemsetAsync(g.grad_accum, 0, sizeof(float) * kGradRow * (size_t)P, s)); }
         const float* colors = colors_precomp ? colors_precomp : g.rgb;
-        if (R > 0) { StageTimer _t(kRenderBwd, s); launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s); }
+        if (R > 0) {
+            StageTimer _t(kRenderBwd, s);
+            if (amr_mode != 0) launch_amr_render_backward(width, height, amr_mode, img, b, g, colors, background, dL_dpix, s);
+            else launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s);
+        }
         stage_check(debug != 0, s, "render_backward");
         BackwardGaussArgs a;
         a.P = P;
@@ -310,6 +319,58 @@ int gs_rasterizer_backward(int P, int D, int M, int R, const float* background, 
         { StageTimer _t(kBwdGauss, s); launch_backward_gaussians(a, g, s); }
         stage_check(debug != 0, s, "preprocess_backward");
         return 0;
+    }
+}
+}  // namespace
+
+int gs_rasterizer_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                           const float* means3D, const float* shs, const float* colors_precomp, const float* scales,
+                           float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                           const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                           float tan_fovy, const int* radii, char* geom_buffer, char* binning_buffer,
+                           char* img_buffer, const float* dL_dpix, float* dL_dmean2D, float* dL_dconic,
+                           float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
+                           float* dL_dsh, float* dL_dscale, float* dL_drot, int debug, void* stream) {
+    return guarded([&]() -> int {
+        return rasterizer_backward_impl(0, P, D, M, R, background, width, height, means3D, shs, colors_precomp,
+                                        scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix,
+                                        campos, tan_fovx, tan_fovy, radii, geom_buffer, binning_buffer, img_buffer,
+                                        dL_dpix, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dmean3D, dL_dcov3D,
+                                        dL_dsh, dL_dscale, dL_drot, debug, static_cast<hipStream_t>(stream));
+    });
+}
+
+int gs_amr_rasterizer_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                               const float* means3D, const float* shs, const float* colors_precomp,
+                               const float* scales, float scale_modifier, const float* rotations,
+                               const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                               const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                               char* geom_buffer, char* binning_buffer, char* img_buffer, int foveaStep,
+                               int interpolate_image, const float* dL_dpix, float* dL_dpix_scratch,
+                               float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
+                               float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale, float* dL_drot,
+                               int debug, void* stream) {
+    return guarded([&]() -> int {
+        if (foveaStep == 0) throw GsError("gs_amr_rasterizer_backward: foveaStep 0 renders nothing");
+        if (foveaStep > 4) throw GsError("gs_amr_rasterizer_backward: foveaStep 1..4 or < 0 (render_once)");
+        if (interpolate_image && foveaStep > 0)
+            throw GsError("gs_amr_rasterizer_backward: interpolate_image is supported for render_once only");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        const float* g = dL_dpix;
+        if (interpolate_image && P > 0) {
+            if (!dL_dpix_scratch) throw GsError("gs_amr_rasterizer_backward: interpolation needs dL_dpix_scratch");
+            const int T = ((width + 31) / 32) * ((height + 31) / 32);
+            ImageView img;
+            carve_image(img_buffer, (size_t)width * height, T, &img);
+            launch_amr_interp_fold(width, height, img, dL_dpix, dL_dpix_scratch, s);
+            stage_check(debug != 0, s, "amr_interp_fold");
+            g = dL_dpix_scratch;
+        }
+        return rasterizer_backward_impl(foveaStep, P, D, M, R, background, width, height, means3D, shs,
+                                        colors_precomp, scales, scale_modifier, rotations, cov3D_precomp, viewmatrix,
+                                        projmatrix, campos, tan_fovx, tan_fovy, radii, geom_buffer, binning_buffer,
+                                        img_buffer, g, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dmean3D,
+                                        dL_dcov3D, dL_dsh, dL_dscale, dL_drot, debug, s);
     });
 }
 
@@ -555,6 +616,11 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
         ForwardIn in{P, D, M, background, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
                      viewmatrix, projmatrix, cam_pos, width, height, scale_modifier, tan_fovx, tan_fovy, prefiltered};
         Binned r = preprocess_and_bin(in, geometry, binning, image, radii, tile, dbg, s);
+        // the geometry buffer keeps its own copy of the radii: the progressive
+        // steps return zero radii (as the reference), and the AMR backward of a
+        // step reads the step-0 radii from here
+        if (radii && radii != r.g.radii)
+            GS_HIP(hipMemcpyAsync(r.g.radii, radii, sizeof(int) * (size_t)P, hipMemcpyDeviceToDevice, s));
         { StageTimer _t(kAmrLevels, s); launch_amr_levels(r.T, r.img, s); }
         stage_check(dbg, s, "amr_levels");
         if (foveaStep == 0) return r.K;  // step 0: buffers only (amr/cr/rasterizer_impl.cu:651)

@@ -143,6 +143,12 @@ void launch_avgpool2(const float* in, int C, int H, int W, float* out, hipStream
 void launch_ritnet_head(const float* in, int H, int W, const float* w, const float* bias, float* logits,
                         uint8_t* labels, hipStream_t s);
 void launch_label_moments(const uint8_t* labels, int H, int W, int cls, double* out, hipStream_t s);
+// AMR backward (extension): blend backward over the rendered sub-lattices,
+// and the backward of render_once's interpolation.
+void launch_amr_render_backward(int W, int H, int mode, const ImageView& img, const BinningView& b,
+                                const GeomView& g, const float* colors, const float* bg, const float* dL_dpix,
+                                hipStream_t s);
+void launch_amr_interp_fold(int W, int H, const ImageView& img, const float* g_in, float* g_out, hipStream_t s);
 // Fovea-driven AMR levels (amr.hip), applied to the step-0 levels in place.
 void launch_fovea_override(int W, int H, const ImageView& img, int nf, const float* cx, const float* cy,
                            const float* radius, int min_level, int replace, hipStream_t s);

@@ -152,12 +152,17 @@ std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> AMRRasterizeGaussians(
 }
 
 // base/rasterize_points.cu:117-196
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> RasterizeGaussiansBackward(
-    const Tensor& background, const Tensor& means3D_in, const Tensor& radii_in, const Tensor& colors_in,
-    const Tensor& scales_in, const Tensor& rotations_in, const float scale_modifier, const Tensor& cov3D_precomp_in,
-    const Tensor& viewmatrix_in, const Tensor& projmatrix_in, const float tan_fovx, const float tan_fovy,
-    const Tensor& dL_dout_color_in, const Tensor& sh_in, const int degree, const Tensor& campos_in,
-    const Tensor& geomBuffer, const int R, const Tensor& binningBuffer, const Tensor& imageBuffer, const bool debug) {
+using Grads8 = std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor>;
+
+// amr_step 0: the base backward; != 0: the AMR (foveated) backward of
+// foveaStep amr_step (< 0: render_once, with `interpolate`).
+Grads8 BackwardImpl(int amr_step, bool interpolate, const Tensor& background, const Tensor& means3D_in,
+                    const Tensor& radii_in, const Tensor& colors_in, const Tensor& scales_in,
+                    const Tensor& rotations_in, const float scale_modifier, const Tensor& cov3D_precomp_in,
+                    const Tensor& viewmatrix_in, const Tensor& projmatrix_in, const float tan_fovx,
+                    const float tan_fovy, const Tensor& dL_dout_color_in, const Tensor& sh_in, const int degree,
+                    const Tensor& campos_in, const Tensor& geomBuffer, const int R, const Tensor& binningBuffer,
+                    const Tensor& imageBuffer, const bool debug) {
     const int P = (int)means3D_in.size(0);
     const int H = (int)dL_dout_color_in.size(1);
     const int W = (int)dL_dout_color_in.size(2);
@@ -182,18 +187,63 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> Raste
         require_device(means3D, "means3D");
         require_device(dL_dout, "dL_dout_color");
         TORCH_CHECK(radii.scalar_type() == torch::kInt32, "radii must be int32");
-        const int rc = gs_rasterizer_backward(
-            P, degree, M, R, fptr(bg), W, H, fptr(means3D), fptr(sh), fptr(colors), fptr(scales), scale_modifier,
-            fptr(rotations), fptr(cov3D_precomp), fptr(viewmatrix), fptr(projmatrix), fptr(campos), tan_fovx,
-            tan_fovy, radii.data_ptr<int>(), reinterpret_cast<char*>(geomBuffer.data_ptr()),
-            reinterpret_cast<char*>(binningBuffer.data_ptr()), reinterpret_cast<char*>(imageBuffer.data_ptr()),
-            fptr(dL_dout), fptr_mut(dL_dmeans2D), fptr_mut(dL_dconic), fptr_mut(dL_dopacity), fptr_mut(dL_dcolors),
-            fptr_mut(dL_dmeans3D), fptr_mut(dL_dcov3D), fptr_mut(dL_dsh), fptr_mut(dL_dscales),
-            fptr_mut(dL_drotations), debug, stream_of(means3D));
-        check(rc, "rasterize_gaussians_backward");
+        int rc;
+        if (amr_step == 0) {
+            rc = gs_rasterizer_backward(
+                P, degree, M, R, fptr(bg), W, H, fptr(means3D), fptr(sh), fptr(colors), fptr(scales), scale_modifier,
+                fptr(rotations), fptr(cov3D_precomp), fptr(viewmatrix), fptr(projmatrix), fptr(campos), tan_fovx,
+                tan_fovy, radii.data_ptr<int>(), reinterpret_cast<char*>(geomBuffer.data_ptr()),
+                reinterpret_cast<char*>(binningBuffer.data_ptr()), reinterpret_cast<char*>(imageBuffer.data_ptr()),
+                fptr(dL_dout), fptr_mut(dL_dmeans2D), fptr_mut(dL_dconic), fptr_mut(dL_dopacity),
+                fptr_mut(dL_dcolors), fptr_mut(dL_dmeans3D), fptr_mut(dL_dcov3D), fptr_mut(dL_dsh),
+                fptr_mut(dL_dscales), fptr_mut(dL_drotations), debug, stream_of(means3D));
+        } else {
+            TORCH_CHECK(imageBuffer.numel() > 0, "the AMR backward needs the image buffer of the forward");
+            Tensor scratch = interpolate ? torch::empty_like(dL_dout) : torch::empty({0}, opts);
+            rc = gs_amr_rasterizer_backward(
+                P, degree, M, R, fptr(bg), W, H, fptr(means3D), fptr(sh), fptr(colors), fptr(scales), scale_modifier,
+                fptr(rotations), fptr(cov3D_precomp), fptr(viewmatrix), fptr(projmatrix), fptr(campos), tan_fovx,
+                tan_fovy, radii.data_ptr<int>(), reinterpret_cast<char*>(geomBuffer.data_ptr()),
+                reinterpret_cast<char*>(binningBuffer.data_ptr()), reinterpret_cast<char*>(imageBuffer.data_ptr()),
+                amr_step, interpolate ? 1 : 0, fptr(dL_dout), interpolate ? fptr_mut(scratch) : nullptr,
+                fptr_mut(dL_dmeans2D), fptr_mut(dL_dconic), fptr_mut(dL_dopacity), fptr_mut(dL_dcolors),
+                fptr_mut(dL_dmeans3D), fptr_mut(dL_dcov3D), fptr_mut(dL_dsh), fptr_mut(dL_dscales),
+                fptr_mut(dL_drotations), debug, stream_of(means3D));
+        }
+        check(rc, amr_step ? "amr_rasterize_gaussians_backward" : "rasterize_gaussians_backward");
     }
     return std::make_tuple(dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
                            dL_drotations);
+}
+
+// base/rasterize_points.cu:117-196
+Grads8 RasterizeGaussiansBackward(const Tensor& background, const Tensor& means3D, const Tensor& radii,
+                                  const Tensor& colors, const Tensor& scales, const Tensor& rotations,
+                                  const float scale_modifier, const Tensor& cov3D_precomp, const Tensor& viewmatrix,
+                                  const Tensor& projmatrix, const float tan_fovx, const float tan_fovy,
+                                  const Tensor& dL_dout_color, const Tensor& sh, const int degree,
+                                  const Tensor& campos, const Tensor& geomBuffer, const int R,
+                                  const Tensor& binningBuffer, const Tensor& imageBuffer, const bool debug) {
+    return BackwardImpl(0, false, background, means3D, radii, colors, scales, rotations, scale_modifier,
+                        cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
+                        geomBuffer, R, binningBuffer, imageBuffer, debug);
+}
+
+// The AMR backward (an extension: the reference's is unreachable): the
+// image of foveaStep k (1..4) or of render_once (foveaStep < 0, optionally
+// interpolated) -> the same 8 gradients as the base backward.
+Grads8 AmrRasterizeGaussiansBackward(const Tensor& background, const Tensor& means3D, const Tensor& radii,
+                                     const Tensor& colors, const Tensor& scales, const Tensor& rotations,
+                                     const float scale_modifier, const Tensor& cov3D_precomp,
+                                     const Tensor& viewmatrix, const Tensor& projmatrix, const float tan_fovx,
+                                     const float tan_fovy, const Tensor& dL_dout_color, const Tensor& sh,
+                                     const int degree, const Tensor& campos, const Tensor& geomBuffer, const int R,
+                                     const Tensor& binningBuffer, const Tensor& imageBuffer, const int foveaStep,
+                                     const bool interpolate_image, const bool debug) {
+    TORCH_CHECK(foveaStep != 0, "foveaStep 0 renders nothing: its gradient is zero");
+    return BackwardImpl(foveaStep, interpolate_image, background, means3D, radii, colors, scales, rotations,
+                        scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh,
+                        degree, campos, geomBuffer, R, binningBuffer, imageBuffer, debug);
 }
 
 // Data-parallel stage 1 (gsplat_amd.h): blend backward of one view -> its
@@ -621,6 +671,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "MI355X (gfx950) Gaussian rasterizer -- PyTorch binding over include/gsplat_amd.h";
     m.def("rasterize_gaussians", &RasterizeGaussians);
     m.def("rasterize_gaussians_backward", &RasterizeGaussiansBackward);
+    m.def("amr_rasterize_gaussians_backward", &AmrRasterizeGaussiansBackward);
     m.def("mark_visible", &MarkVisible);
     m.def("rasterize_gaussians_backward_view_grads", &RasterizeGaussiansBackwardViewGrads);
     m.def("backward_gaussians_multiview", &BackwardGaussiansMultiview);

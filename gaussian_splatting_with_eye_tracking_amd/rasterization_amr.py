@@ -22,9 +22,11 @@ in one call (``render_once``).
 
 The reference's AMR backward is unreachable (its autograd forward has 15
 inputs/5 outputs while its backward takes 2 grads and returns 9, and its
-kernel misindexes the 2x render grid -- SURVEY §8(a) row B-AMR).  The AMR
-path is forward-only here as well; calling backward raises a RuntimeError
-that says so.
+kernel misindexes the 2x render grid -- SURVEY §8(a) row B-AMR).  Here the
+backward works (an extension): each call's image is
+differentiated through the pixels it rendered (see
+_RasterizeGaussians.backward), so a 5-step foveated frame or a render_once
+frame can be trained on.
 """
 from __future__ import annotations
 
@@ -57,13 +59,47 @@ class _RasterizeGaussians(torch.autograd.Function):
             s.campos, s.prefiltered, int(foveaStep), out_color_precomp, geomBuffer_precomp, binningBuffer_precomp,
             imageBuffer_precomp, bool(interpolate_image), s.debug)
         ctx.num_rendered = num_rendered
+        ctx.raster_settings = s
+        ctx.fovea_step = int(foveaStep)
+        ctx.interpolate = bool(interpolate_image)
+        # steps >= 1 return zero radii (as the reference); the backward then
+        # reads the radii the step-0 preprocess left in the geometry buffer
+        ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp,
+                              radii if int(foveaStep) < 0 else torch.empty(0, dtype=torch.int32, device=radii.device),
+                              sh, geomBuffer, binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii, geomBuffer, binningBuffer, imgBuffer)
         return color, radii, geomBuffer, binningBuffer, imgBuffer
 
     @staticmethod
-    def backward(ctx, *grads):
-        raise RuntimeError("diff_gaussian_rasterization_amr is forward-only (as in the reference, whose AMR "
-                           "backward is unreachable); use diff_gaussian_rasterization for training.")
+    def backward(ctx, grad_color, *_):
+        """Extension beyond parity: the reference's AMR
+        backward is unreachable (15 inputs / 2 grads in, 9 out), and its kernel
+        misindexes the 2x render grid (SURVEY §8(a) B-AMR bwd).  Here the
+        image of one AMR call is differentiated exactly: foveaStep k in 1..4
+        renders round k of the tiles with level >= k, render_once (k < 0)
+        every round <= level, through the interpolation copies when
+        interpolate_image; the gradient flows only through the rendered
+        pixels, with the 32-px tile lists the forward blended (same 8 outputs
+        as diff_gaussian_rasterization's backward).  foveaStep 0 renders a
+        blank image: no gradient.  Interpolation at foveaStep >= 1 (the
+        reference's racy precomp-copy path) is not differentiated."""
+        step = ctx.fovea_step
+        nones = (None,) * 7
+        if step == 0:
+            return (None,) * 8 + nones
+        if ctx.interpolate and step > 0:
+            raise RuntimeError("the AMR backward differentiates interpolate_image only for render_once "
+                               "(foveaStep < 0)")
+        s = ctx.raster_settings
+        (colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geomBuffer, binningBuffer,
+         imgBuffer) = ctx.saved_tensors
+        (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
+         grad_scales, grad_rotations) = _C.amr_rasterize_gaussians_backward(
+            s.bg, means3D, radii, colors_precomp, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_color, sh, s.sh_degree, s.campos, geomBuffer,
+            ctx.num_rendered, binningBuffer, imgBuffer, step, ctx.interpolate, s.debug)
+        return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
+                grad_rotations, grad_cov3Ds_precomp) + nones
 
 
 def _empty_u8():

@@ -186,6 +186,25 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
 /* Replaces SimpleKNN::knn (knn/simple_knn.h:16-19, knn/simple_knn.cu:185-221)
  * behind simple_knn._C.distCUDA2.  `scratch` is resized to the workspace
  * size; no host synchronisation. */
+/* The AMR (foveated) backward -- an extension: the reference's
+ * amr/cr/rasterizer.h:69-98 / rasterizer_impl.cu:698-796 is unreachable
+ * (SURVEY §8(a) B-AMR bwd).
+ * Gradients of the image one AMR forward call produced, on the buffers it
+ * returned: foveaStep k in 1..4 -> round k of the tiles whose level >= k;
+ * foveaStep < 0 -> render_once (rounds <= level), through the interpolation
+ * when interpolate_image (then dL_dpix_scratch: 3 * width * height floats).
+ * Outputs and their layout as gs_rasterizer_backward (all written). */
+int gs_amr_rasterizer_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                               const float* means3D, const float* shs, const float* colors_precomp,
+                               const float* scales, float scale_modifier, const float* rotations,
+                               const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix,
+                               const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                               char* geom_buffer, char* binning_buffer, char* img_buffer, int foveaStep,
+                               int interpolate_image, const float* dL_dpix, float* dL_dpix_scratch,
+                               float* dL_dmean2D, float* dL_dconic, float* dL_dopacity, float* dL_dcolor,
+                               float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale, float* dL_drot,
+                               int debug, void* stream);
+
 /* Fovea-driven AMR levels -- an extension beyond parity.
  * The reference builds foveaCenters [4][2] / foveaRadii [4]
  * (gaussian_renderer_amr/__init__.py:98-106) but never passes them on, and

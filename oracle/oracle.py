@@ -171,19 +171,21 @@ def preprocess_and_bin(s: Settings, means3D, opacities, shs=None, colors_precomp
 
 
 def forward(s: Settings, means3D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
-            cov3D_precomp=None) -> ForwardResult:
-    """Base forward (rasterizer_impl.cu:198-336)."""
-    r = preprocess_and_bin(s, means3D, opacities, shs, colors_precomp, scales, rotations, cov3D_precomp, 16)
+            cov3D_precomp=None, block: int = 16) -> ForwardResult:
+    """Base forward (rasterizer_impl.cu:198-336); block = 32 blends every
+    pixel with the AMR path's 32-px tile lists (the state the AMR render
+    leaves at every pixel it renders)."""
+    r = preprocess_and_bin(s, means3D, opacities, shs, colors_precomp, scales, rotations, cov3D_precomp, block)
     W, H = int(s.image_width), int(s.image_height)
     feats = r.extra["colors_precomp"] if r.extra["colors_precomp"] is not None else r.rgb
-    lib().orc_render_forward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(16), ctypes.c_int(16),
+    lib().orc_render_forward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(block), ctypes.c_int(block),
                              _p(r.ranges), _p(r.point_list), _p(r.means2D), _p(np.ascontiguousarray(feats)),
                              _p(r.conic_opacity), _p(r.final_T), _p(r.n_contrib), _p(_f32(s.bg)), _p(r.color))
     return r
 
 
 def backward(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors_precomp=None, scales=None,
-             rotations=None, cov3D_precomp=None) -> dict:
+             rotations=None, cov3D_precomp=None, block: int = 16) -> dict:
     """Base backward (rasterize_points.cu:117-196 + rasterizer_impl.cu:340-434).
     Returns the 8 gradients of _C.rasterize_gaussians_backward plus dL_dconic."""
     L = lib()
@@ -207,7 +209,7 @@ def backward(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors
     g_scale = np.zeros((P, 3), np.float32)
     g_rot = np.zeros((P, 4), np.float32)
     colors = colors_precomp if colors_precomp is not None else fwd.rgb
-    L.orc_render_backward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(16), ctypes.c_int(16), _p(fwd.ranges),
+    L.orc_render_backward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(block), ctypes.c_int(block), _p(fwd.ranges),
                           _p(fwd.point_list), _p(_f32(s.bg)), _p(fwd.means2D), _p(fwd.conic_opacity),
                           _p(np.ascontiguousarray(colors)), _p(fwd.final_T), _p(fwd.n_contrib), _p(dL_dpix),
                           ctypes.c_int(P), _p(g_mean2D), _p(g_conic), _p(g_opac), _p(g_col))
@@ -348,6 +350,74 @@ def amr_render_foveated(s: Settings, scene_kwargs: dict, interpolate_image: bool
 def amr_render_once(s: Settings, scene_kwargs: dict):
     """gaussian_renderer_amr/__init__.py:612-749: one call with foveaStep=-2, interpolate=True."""
     return amr_forward(s, foveaStep=-2, interpolate_image=True, **scene_kwargs)
+
+
+def amr_pixel_rounds(W: int, H: int) -> np.ndarray:
+    """amr/cr/forward.cu:313-339: the AMR round of every pixel, [H, W]."""
+    ys, xs = np.mgrid[0:H, 0:W]
+    ox, oy = xs & 1, ys & 1
+    return np.where(ox == 0, np.where(oy == 0, 1, 4), np.where(oy == 0, 3, 2)).astype(np.uint32)
+
+
+def amr_tile_levels_per_pixel(levels, W: int, H: int) -> np.ndarray:
+    tgx = (W + 31) // 32
+    ys, xs = np.mgrid[0:H, 0:W]
+    return np.minimum(np.asarray(levels, np.uint32)[(ys // 32) * tgx + xs // 32], 4)
+
+
+def amr_interp_fold(dL_dpix, levels, W: int, H: int) -> np.ndarray:
+    """Adjoint of render_once's interpolation (amr/cr/forward.cu:520-648): a
+    pixel with round > level copies its 2x2 cell's (0,0) (levels 1, 2) or
+    (1,1) (level 3) pixel, so its cotangent moves there (copies summed in
+    round order, as csrc/amr.hip amr_interp_fold_kernel)."""
+    g = np.asarray(dL_dpix, np.float32)
+    out = np.zeros_like(g)
+    rnd = amr_pixel_rounds(W, H)
+    lvl = amr_tile_levels_per_pixel(levels, W, H)
+    order = [(0, 0), (1, 1), (1, 0), (0, 1)]  # (dx, dy) of rounds 1..4
+    for cy in range(0, H, 2):
+        for cx in range(0, W, 2):
+            L = int(lvl[cy, cx])
+            o = 1 if L in (3, 4) else 0
+            sx, sy = cx + o, cy + o
+            src_in = sx < W and sy < H
+            fold = np.zeros(3, np.float32)
+            for r, (dx, dy) in enumerate(order):
+                px, py = cx + dx, cy + dy
+                if px >= W or py >= H:
+                    continue
+                if r + 1 <= L:
+                    out[:, py, px] = g[:, py, px]
+                elif src_in:
+                    fold = (fold + g[:, py, px]).astype(np.float32)
+            if src_in and L < 4:
+                out[:, sy, sx] = (out[:, sy, sx] + fold).astype(np.float32)
+    return out
+
+
+def amr_backward(s: Settings, scene_kwargs: dict, dL_dpix, foveaStep: int, levels,
+                 interpolate_image: bool = False) -> dict:
+    """Extension beyond parity (the reference's AMR backward is unreachable):
+    the gradients of one AMR call's image.  Every pixel the AMR render blends
+    gets the state of a 32-px-tile base blend, so the backward is the base
+    backward on the 32-px binning with the cotangent kept on the rendered
+    pixels only -- foveaStep k > 0: round k where level >= k; < 0
+    (render_once): round <= level, after folding the interpolation copies."""
+    W, H = int(s.image_width), int(s.image_height)
+    kw = dict(scene_kwargs)
+    means3D = kw.pop("means3D")
+    opacities = kw.pop("opacities")
+    fwd = forward(s, means3D, opacities, block=32, **kw)
+    g = np.asarray(dL_dpix, np.float32)
+    if interpolate_image:
+        if foveaStep > 0:
+            raise ValueError("interpolate_image is differentiated for render_once only")
+        g = amr_interp_fold(g, levels, W, H)
+    rnd = amr_pixel_rounds(W, H)
+    lvl = amr_tile_levels_per_pixel(levels, W, H)
+    keep = (rnd == foveaStep) & (lvl >= foveaStep) if foveaStep > 0 else rnd <= lvl
+    g = np.where(keep[None], g, np.float32(0)).astype(np.float32)
+    return backward(s, fwd, means3D, g, block=32, **kw)
 
 
 # ------------------------------------------------------------- simple-knn ---

@@ -433,16 +433,87 @@ def test_amr_fovea_levels_rejects_bad_buffer():
         RA.apply_fovea_levels(small, 256, 256, *RA.reference_foveae(256, 256))
 
 
-def test_amr_backward_is_forward_only():
+def _amr_grads_vs_oracle(t, means2D, cam, levels, dpix, mode, interpolate):
+    import oracle as O
+    sc_np = {k: v.detach().cpu().numpy() for k, v in t.items()}
+    s = O.settings_from_camera(cam)
+    rg = O.amr_backward(s, dict(means3D=sc_np["means3D"], opacities=sc_np["opacities"], shs=sc_np["shs"],
+                                scales=sc_np["scales"], rotations=sc_np["rotations"]), dpix, mode, levels,
+                        interpolate_image=interpolate)
+    pairs = [(means2D.grad, rg["dL_dmeans2D"]), (t["means3D"].grad, rg["dL_dmeans3D"]),
+             (t["shs"].grad, rg["dL_dsh"]), (t["opacities"].grad, rg["dL_dopacity"]),
+             (t["scales"].grad, rg["dL_dscales"]), (t["rotations"].grad, rg["dL_drotations"])]
+    assert np.abs(rg["dL_dopacity"]).sum() > 0  # the case has gradient at all
+    for i, (g, r) in enumerate(pairs):
+        assert G.rel_err(g.cpu().numpy(), r) < G.GRAD_REL_TOL, (i, G.rel_err(g.cpu().numpy(), r))
+
+
+@pytest.mark.parametrize("interpolate", [False, True])
+@pytest.mark.parametrize("W,H,seed", [(224, 160, 5), (200, 120, 3)])
+def test_amr_backward_render_once(interpolate, W, H, seed):
+    """Extension: render_once's image differentiated
+    through the pixels it rendered (and the interpolation copies) against
+    the oracle's restatement (base backward on the 32-px binning with the
+    cotangent kept on the rendered pixels)."""
     from diff_gaussian_rasterization_amr import GaussianRasterizer
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(5000, W, H, seed)
+    s = G.torch_settings(cam, amr=True)
+    t = G.scene_tensors(sc, requires_grad=True)
+    means2D = torch.zeros_like(t["means3D"], requires_grad=True)
+    color, radii, gb, bb, ib = GaussianRasterizer(s)(
+        means3D=t["means3D"], means2D=means2D, opacities=t["opacities"], shs=t["shs"], scales=t["scales"],
+        rotations=t["rotations"], foveaStep=-2, interpolate_image=interpolate)
+    dpix = S.make_cotangent(H, W, seed + 1)
+    (color * torch.from_numpy(dpix).cuda()).sum().backward()
+    torch.cuda.synchronize()
+    K = int(C.parse_buffers(gb, bb, ib, 5000, 0, W, H, 32)["hdr"][0].item())
+    levels = C.parse_buffers(gb, bb, ib, 5000, K, W, H, 32)["levels"].cpu().numpy().astype(np.uint32)
+    _amr_grads_vs_oracle(t, means2D, cam, levels, dpix, -2, interpolate)
+
+
+def test_amr_backward_five_steps_sum():
+    """The 5-step foveated frame (gaussian_renderer_amr.render's sum of the
+    step images) back-propagated through autograd: every step's backward
+    covers its own round, so the sum equals render_once's (no interpolation)
+    -- checked against the oracle; step 0 contributes nothing."""
+    from diff_gaussian_rasterization_amr import _RasterizeGaussians
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    W, H, seed = 224, 160, 6
+    sc, cam = G.scene_and_camera(5000, W, H, seed)
+    s = G.torch_settings(cam, amr=True)
+    t = G.scene_tensors(sc, requires_grad=True)
+    means2D = torch.zeros_like(t["means3D"], requires_grad=True)
+    e = torch.Tensor([])
+    u8 = torch.Tensor([]).to(torch.uint8)
+    args = (t["means3D"], means2D, t["shs"], e, t["opacities"], t["scales"], t["rotations"], e)
+    acc, radii, gb, bb, ib = _RasterizeGaussians.apply(*args, 0, e, u8, u8, u8, False, s)
+    for k in range(1, 5):
+        ck, _, gb, bb, ib = _RasterizeGaussians.apply(*args, k, acc, gb, bb, ib, False, s)
+        acc = acc + ck
+    dpix = S.make_cotangent(H, W, seed + 1)
+    (acc * torch.from_numpy(dpix).cuda()).sum().backward()
+    torch.cuda.synchronize()
+    K = int(C.parse_buffers(gb, bb, ib, 5000, 0, W, H, 32)["hdr"][0].item())
+    levels = C.parse_buffers(gb, bb, ib, 5000, K, W, H, 32)["levels"].cpu().numpy().astype(np.uint32)
+    _amr_grads_vs_oracle(t, means2D, cam, levels, dpix, -2, False)
+
+
+def test_amr_backward_rejects_interpolated_steps():
+    from diff_gaussian_rasterization_amr import _RasterizeGaussians
     sc, cam = G.scene_and_camera(500, 64, 64, 1)
     s = G.torch_settings(cam, amr=True)
     t = G.scene_tensors(sc, requires_grad=True)
-    color, *_ = GaussianRasterizer(s)(means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]),
-                                      opacities=t["opacities"], shs=t["shs"], scales=t["scales"],
-                                      rotations=t["rotations"], foveaStep=-1)
-    with pytest.raises(RuntimeError, match="forward-only"):
-        color.sum().backward()
+    e = torch.Tensor([])
+    u8 = torch.Tensor([]).to(torch.uint8)
+    args = (t["means3D"], torch.zeros_like(t["means3D"]), t["shs"], e, t["opacities"], t["scales"],
+            t["rotations"], e)
+    c0, _, gb, bb, ib = _RasterizeGaussians.apply(*args, 0, e, u8, u8, u8, False, s)
+    c4, *_ = _RasterizeGaussians.apply(*args, 1, c0, gb, bb, ib, True, s)
+    with pytest.raises(RuntimeError, match="render_once"):
+        c4.sum().backward()
 
 
 # ---------------------------------------------------------- simple-knn ----
