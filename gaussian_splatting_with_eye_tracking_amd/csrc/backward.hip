@@ -37,7 +37,7 @@ constexpr int kAccRow = 9;   // LDS accumulator row (floats; odd stride: 9 scala
 // One 16x16 tile per workgroup of kWaves wave64s, kPPL pixels per lane
 // (kWaves * 64 * kPPL = 256; gs_blend.cuh mapping).  kMinWaves: waves per
 // SIMD the register allocation must allow.
-template <int kPPL, int kWaves, int kMinWaves, bool kSwap>
+template <int kPPL, int kWaves, int kMinWaves, bool kSwap, bool kAMR = false>
 __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     int W, int H, const uint32_t* __restrict__ ranges, const uint32_t* __restrict__ max_contrib,
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
@@ -61,15 +61,16 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    // AMR mode (amr_mode != 0; the foveated backward, an extension beyond
+    // AMR mode (kAMR, amr_mode != 0; the foveated backward, an extension beyond
     // parity): block b = (32-px tile b / 4, sub-lattice (b & 1, (b >> 1) & 1)),
     // its 16 x 16 pixels at stride 2 -- the pixels amr_render_kernel blended
     // for that AMR round.  amr_mode = k > 0: foveaStep k's image (round k of
     // tiles with level >= k); < 0: render_once (rounds <= level).
     int tile;
     uint32_t ox, oy;
-    uint32_t pstride = 1;
-    if (amr_mode != 0) {
+    // (a template parameter: run-time AMR branches cost the base kernel 12 %)
+    constexpr uint32_t pstride = kAMR ? 2 : 1;
+    if constexpr (kAMR) {
         tile = (int)(blockIdx.x >> 2);
         const uint32_t sx = blockIdx.x & 1u, sy = (blockIdx.x >> 1) & 1u;
         const uint32_t round = sx == 0 ? (sy == 0 ? 1u : 4u) : (sy == 0 ? 3u : 2u);  // amr/cr/forward.cu:313-339
@@ -77,7 +78,6 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         if (amr_mode > 0 ? (round != (uint32_t)amr_mode || L < round) : round > L) return;
         ox = (uint32_t)(tile % gx) * 32 + sx;
         oy = (uint32_t)(tile / gx) * 32 + sy;
-        pstride = 2;
     } else {
         tile = order ? (int)order[blockIdx.x]
                      : xcd ? xcd_block_tile((int)blockIdx.x, gx, (int)(gridDim.x / gx)) : (int)blockIdx.x;
@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     }
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const int n = (int)(range.y - range.x);
-    int m = amr_mode != 0 ? n : min(n, (int)max_contrib[tile]);
+    int m = kAMR ? n : min(n, (int)max_contrib[tile]);
     if (m == 0) return;  // block-uniform
 
     const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, pstride);
@@ -126,7 +126,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     }
     // AMR: no per-tile max_contrib was recorded for the sub-lattice; with one
     // wave per block (the only AMR instantiation) the wave max is the block's
-    if (amr_mode != 0) {
+    if constexpr (kAMR) {
         m = min(n, (int)wave_last);
         if (m == 0) return;
     }
@@ -377,7 +377,7 @@ void launch_amr_render_backward(int W, int H, int mode, const ImageView& img, co
                                 hipStream_t s) {
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0 || mode == 0) return;
-    hipLaunchKernelGGL((render_bwd_kernel<4, 1, 4, true>), dim3(4 * tgx * tgy), dim3(64), 0, s, W, H, img.ranges,
+    hipLaunchKernelGGL((render_bwd_kernel<4, 1, 4, true, true>), dim3(4 * tgx * tgy), dim3(64), 0, s, W, H, img.ranges,
                        img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,
                        dL_dpix, bg, g.grad_accum, g_cull, nullptr, tgx, 0, mode, img.levels);
