@@ -18,13 +18,18 @@
 namespace gsamd {
 
 constexpr int kLvlThreads = 1024;
+constexpr int kLvlSortMax = 2048;  // tile grids up to this size sort their counts in LDS
 
 // k-th smallest (0-based) of v[0..n) -- MSD radix select, one workgroup.
 // Counts are read straight from ranges (count = y - x) so no global value is
-// read back after being written inside this launch.
+// read back after being written inside this launch.  Each 8-bit digit pass:
+// LDS histogram of the candidates, then the 256 bins are scanned by the
+// first four waves (wave prefix sums + a 4-entry carry) and the one bin whose
+// [start, start + count) holds k names the digit -- no serial 256-step loop.
 __device__ uint32_t block_select_kth(const uint32_t* __restrict__ ranges, int n, uint32_t k, uint32_t* hist,
                                      uint32_t* shared_word) {
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ uint32_t s_carry[4];
     uint32_t prefix = 0, mask = 0;
     for (int d = 3; d >= 0; d--) {
         for (int i = tid; i < 256; i += kLvlThreads) hist[i] = 0;
@@ -35,18 +40,25 @@ __device__ uint32_t block_select_kth(const uint32_t* __restrict__ ranges, int n,
             if ((x & mask) == prefix) atomicAdd(&hist[(x >> sh) & 0xFF], 1u);
         }
         __syncthreads();
-        if (tid == 0) {
-            uint32_t acc = 0, dig = 255;
-            for (int b = 0; b < 256; b++) {
-                if (acc + hist[b] > k) {
-                    dig = (uint32_t)b;
-                    break;
-                }
-                acc += hist[b];
+        uint32_t h = 0, inc = 0;
+        if (tid < 256) {
+            h = hist[tid];
+            inc = h;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)inc, off, 64);
+                if (lane >= off) inc += t;
             }
-            k -= acc;
-            shared_word[0] = dig;
-            shared_word[1] = k;
+            if (lane == 63) s_carry[wave] = inc;
+        }
+        __syncthreads();
+        if (tid < 256) {
+            uint32_t start = inc - h;
+            for (int w = 0; w < wave; w++) start += s_carry[w];
+            if (h > 0 && start <= k && k < start + h) {  // exactly one bin
+                shared_word[0] = (uint32_t)tid;
+                shared_word[1] = k - start;
+            }
         }
         __syncthreads();
         const uint32_t dig = shared_word[0];
@@ -69,10 +81,35 @@ __global__ void __launch_bounds__(kLvlThreads) amr_levels_kernel(int T, const ui
     // calculateIntersections (amr/cr/rasterizer_impl.cu:181-188)
     for (int t = tid; t < T; t += kLvlThreads) n_inter[t] = ranges[2 * t + 1] - ranges[2 * t];
     const float percentiles[3] = {0.25f, 0.5f, 0.9f};
-    for (int i = 0; i < 3; i++) {
-        const uint32_t k = (uint32_t)(int)(percentiles[i] * (float)T);  // float32 index, :630
-        const uint32_t val = T > 0 ? block_select_kth(ranges, T, k, hist, word) : 0u;
-        if (tid == 0) s_pv[i] = val;
+    if (T <= kLvlSortMax) {
+        // small grids (1080p: 2040 tiles): one LDS bitonic sort of the counts
+        // (padded with UINT32_MAX), then the three order statistics directly --
+        // 66 barrier-separated stages instead of 12 radix-select passes
+        __shared__ uint32_t s_sorted[kLvlSortMax];
+        for (int i = tid; i < kLvlSortMax; i += kLvlThreads)
+            s_sorted[i] = i < T ? ranges[2 * i + 1] - ranges[2 * i] : 0xFFFFFFFFu;
+        __syncthreads();
+        for (int kk = 2; kk <= kLvlSortMax; kk <<= 1) {
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                for (int p = tid; p < kLvlSortMax / 2; p += kLvlThreads) {
+                    const int i = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+                    const bool up = (i & kk) == 0;
+                    const uint32_t a = s_sorted[i], b = s_sorted[i + j];
+                    if ((a > b) == up) {
+                        s_sorted[i] = b;
+                        s_sorted[i + j] = a;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        if (tid < 3) s_pv[tid] = s_sorted[(int)(percentiles[tid] * (float)T)];  // float32 index, :630
+    } else {
+        for (int i = 0; i < 3; i++) {
+            const uint32_t k = (uint32_t)(int)(percentiles[i] * (float)T);  // float32 index, :630
+            const uint32_t val = block_select_kth(ranges, T, k, hist, word);
+            if (tid == 0) s_pv[i] = val;
+        }
     }
     __syncthreads();
     if (tid < 3) pv[tid] = s_pv[tid];

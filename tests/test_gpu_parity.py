@@ -323,7 +323,9 @@ def _amr_gpu_steps(sc, cam, interpolate_last=False, bg=(0.0, 0.0, 0.0), after_st
     return acc, radii, steps, (gb, bb, ib)
 
 
-@pytest.mark.parametrize("name,P,W,H,seed", [("amr_10k_256", 10000, 256, 256, 0), ("amr_ragged", 4000, 200, 120, 3)])
+@pytest.mark.parametrize("name,P,W,H,seed", [("amr_10k_256", 10000, 256, 256, 0), ("amr_ragged", 4000, 200, 120, 3),
+                                             # 66 x 33 = 2178 tiles > 2048: the radix-select percentile path
+                                             ("amr_big_grid", 3000, 2112, 1056, 8)])
 def test_amr_foveated_steps(name, P, W, H, seed):
     import oracle as O
     import gaussian_splatting_with_eye_tracking_amd._C as C
