@@ -156,3 +156,42 @@ def test_amr_wrapper_defaults_match_reference():
     assert sig.parameters["interpolate_image"].default is True
     for n in ("out_color_precomp", "geomBuffer_precomp", "binningBuffer_precomp", "imageBuffer_precomp"):
         assert sig.parameters[n].default is None
+
+
+def test_new_entry_points_validate_before_any_device_call():
+    """Argument errors of the extension entry points come back as negative
+    codes with a gs_last_error message, raised on the host before any HIP
+    call (so this runs without a GPU)."""
+    lib = ctypes.CDLL(LIB)
+    lib.gs_last_error.restype = ctypes.c_char_p
+    null = ctypes.c_void_p(0)
+    # gamma/CLAHE preprocessing: the image must tile into the grid
+    rc = lib.gs_eye_preprocess(null, ctypes.c_int(401), ctypes.c_int(640), null, ctypes.c_double(1.5),
+                               ctypes.c_int(8), ctypes.c_int(8), null, null, null)
+    assert rc < 0 and b"divisible" in lib.gs_last_error()
+    # fovea levels: at most 4 discs; the image buffer must hold width x height
+    buf = ctypes.create_string_buffer(64)
+    c = (ctypes.c_float * 8)()
+    r = (ctypes.c_float * 4)(100.0, 50.0, 25.0, 12.0)
+    rc = lib.gs_amr_fovea_levels(buf, ctypes.c_size_t(64), ctypes.c_int(256), ctypes.c_int(256), ctypes.c_int(5), c,
+                                 r, ctypes.c_int(1), ctypes.c_int(0), null)
+    assert rc < 0 and b"0 to 4" in lib.gs_last_error()
+    rc = lib.gs_amr_fovea_levels(buf, ctypes.c_size_t(64), ctypes.c_int(256), ctypes.c_int(256), ctypes.c_int(4), c,
+                                 r, ctypes.c_int(1), ctypes.c_int(0), null)
+    assert rc < 0 and b"too small" in lib.gs_last_error()
+    # AMR backward: foveaStep 0 has no image; interpolation only for render_once
+    def amr_bwd(step, interp):
+        args = [ctypes.c_int(10), ctypes.c_int(3), ctypes.c_int(16), ctypes.c_int(0), null, ctypes.c_int(64),
+                ctypes.c_int(64)] + [null] * 4 + [ctypes.c_float(1.0)] + [null] * 5 + [ctypes.c_float(0.5)] * 2 + \
+               [null] * 4 + [ctypes.c_int(step), ctypes.c_int(interp)] + [null] * 11 + [ctypes.c_int(0), null]
+        return lib.gs_amr_rasterizer_backward(*args)
+    assert amr_bwd(0, 0) < 0 and b"renders nothing" in lib.gs_last_error()
+    assert amr_bwd(2, 1) < 0 and b"render_once only" in lib.gs_last_error()
+    assert amr_bwd(5, 0) < 0 and b"1..4" in lib.gs_last_error()
+
+
+def test_extension_entry_points_in_torch_module():
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    for n in ("amr_rasterize_gaussians_backward", "amr_fovea_levels", "eye_preprocess", "ritnet_conv", "avgpool2",
+              "ritnet_head", "label_moments"):
+        assert hasattr(_C, n), n
