@@ -39,7 +39,8 @@ def sh_eval(sh, d):  # sh [P,16,3], d [P,3] unit
     return r
 
 
-def torch_forward(cam, fwd, means, scales, rots, opac, shs=None, colors=None, cov6=None, m2d=None, bg=(0, 0, 0)):
+def torch_forward(cam, fwd, means, scales, rots, opac, shs=None, colors=None, cov6=None, m2d=None, bg=(0, 0, 0),
+                  block=16):
     W, H = cam.image_width, cam.image_height
     V = torch.tensor(cam.world_view_transform, dtype=torch.float64)
     Pm = torch.tensor(cam.full_proj_transform, dtype=torch.float64)
@@ -83,14 +84,14 @@ def torch_forward(cam, fwd, means, scales, rots, opac, shs=None, colors=None, co
     else:
         rgb = colors
     out = torch.zeros(3, H, W, dtype=torch.float64)
-    gx = (W + 15) // 16
+    gx = (W + block - 1) // block
     ncontrib = fwd.n_contrib.reshape(H, W)
     bgt = torch.tensor(bg, dtype=torch.float64)
     for t in range(fwd.ranges.shape[0]):
         ty_, tx_ = divmod(t, gx)
         beg, end = fwd.ranges[t]
-        ys = torch.arange(ty_ * 16, min(ty_ * 16 + 16, H))
-        xs = torch.arange(tx_ * 16, min(tx_ * 16 + 16, W))
+        ys = torch.arange(ty_ * block, min(ty_ * block + block, H))
+        xs = torch.arange(tx_ * block, min(tx_ * block + block, W))
         if len(ys) == 0 or len(xs) == 0:
             continue
         PY, PX = torch.meshgrid(ys, xs, indexing="ij")
@@ -174,3 +175,55 @@ def test_backward_matches_autograd(variant, P, W, H, seed):
     else:
         assert _rel(g["dL_dscales"][vis], t["scales"].grad.numpy()[vis]) < tol
         assert _rel(g["dL_drotations"][vis], t["rotations"].grad.numpy()[vis]) < tol
+
+
+def amr_render_once_torch(img_full, levels, W, H, interpolate):
+    """render_once's image (amr/cr/forward.cu:261-648, foveaStep < 0) from the
+    32-px-tile blend of every pixel: pixels of rounds <= their tile's level
+    keep it, the others are 0 or, with interpolation, copies of their 2x2
+    cell's (0,0) (levels 1, 2) / (1,1) (level 3) pixel."""
+    rnd = O.amr_pixel_rounds(W, H)
+    lvl = O.amr_tile_levels_per_pixel(levels, W, H)
+    ys, xs = np.mgrid[0:H, 0:W]
+    o = np.where((lvl == 3) | (lvl == 4), 1, 0)
+    sx, sy = (xs & ~1) + o, (ys & ~1) + o
+    keep = rnd <= lvl
+    src_ok = (sx < W) & (sy < H)
+    idx = np.where(keep, ys * W + xs, np.where(src_ok, sy * W + sx, 0))
+    mask = keep | (src_ok & interpolate)
+    flat = img_full.reshape(3, -1)[:, torch.from_numpy(idx.reshape(-1))]
+    return flat.reshape(3, H, W) * torch.from_numpy(mask.astype(np.float64))
+
+
+@pytest.mark.parametrize("interpolate", [False, True])
+@pytest.mark.parametrize("P,W,H,seed", [(300, 96, 64, 4), (500, 80, 70, 6)])
+def test_amr_backward_matches_autograd(interpolate, P, W, H, seed):
+    """The AMR-backward extension (oracle.amr_backward: base backward on the
+    32-px binning, cotangent on the rendered pixels, interpolation folded)
+    against autodiff of a float64 torch restatement of render_once."""
+    cam = S.make_camera(W, H)
+    sc = S.make_scene(P, cam, seed=seed, spread=0.9, opacity_std=1.0, log_scale_mean=np.log(0.03))
+    sc.opacities = np.minimum(sc.opacities, 0.97).astype(np.float32)
+    bg = (0.3, 0.2, 0.1)
+    s = O.settings_from_camera(cam, bg=bg)
+    kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+    color, _, st = O.amr_forward(s, foveaStep=-2, interpolate_image=interpolate, **kw)
+    assert len(set(np.minimum(st.levels, 4).tolist())) > 1  # several levels in play
+    dpix = S.make_cotangent(H, W, seed + 1)
+    g = O.amr_backward(s, kw, dpix, -2, st.levels, interpolate_image=interpolate)
+    fwd32 = O.forward(s, sc.means3D, sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations, block=32)
+    t64 = lambda a: torch.tensor(a, dtype=torch.float64, requires_grad=True)  # noqa: E731
+    m, sca, rot, op, shs = t64(sc.means3D), t64(sc.scales), t64(sc.rotations), t64(sc.opacities), t64(sc.shs)
+    m2d = torch.zeros(P, 3, dtype=torch.float64, requires_grad=True)
+    full = torch_forward(cam, fwd32, m, sca, rot, op, shs=shs, m2d=m2d, bg=bg, block=32)
+    img = amr_render_once_torch(full, st.levels, W, H, interpolate)
+    assert float((img.detach() - torch.from_numpy(color).double()).abs().max()) < 1e-4
+    (img * torch.from_numpy(dpix).double()).sum().backward()
+    vis = fwd32.radii > 0
+    tol = 5e-5
+    assert _rel(g["dL_dopacity"][vis], op.grad.numpy()[vis]) < tol
+    assert _rel(g["dL_dmeans3D"][vis], m.grad.numpy()[vis]) < tol
+    assert _rel(g["dL_dmeans2D"][vis, :2], m2d.grad.numpy()[vis, :2]) < tol
+    assert _rel(g["dL_dsh"][vis], shs.grad.numpy()[vis]) < tol
+    assert _rel(g["dL_dscales"][vis], sca.grad.numpy()[vis]) < tol
+    assert _rel(g["dL_drotations"][vis], rot.grad.numpy()[vis]) < tol
