@@ -28,6 +28,16 @@
 
 #define NUM_CHANNELS 3
 
+/* Host threads for the per-Gaussian and per-pixel loops (OpenMP).  1 (the
+ * default) runs every loop serially, in the order the frozen golden fixtures
+ * were made with; n > 1 parallelises the loops whose iterations are
+ * independent, and the blend backward sums its per-Gaussian terms per band
+ * of tile rows, in band order (deterministic for a given n; differs from the
+ * serial sum only in double-precision rounding). */
+static int g_threads = 1;
+void orc_set_threads(int n) { g_threads = n < 1 ? 1 : n; }
+int orc_get_threads(void) { return g_threads; }
+
 /* ---------------------------------------------------------------- constants */
 /* base/cr/auxiliary.h:22-39 */
 static const float SH_C0 = 0.28209479177387814f;
@@ -302,6 +312,7 @@ void orc_preprocess(int P, int D, int M, const float* orig_points, const float* 
     (void)prefiltered;
     const unsigned gx = (unsigned)((W + block_x - 1) / block_x);
     const unsigned gy = (unsigned)((H + block_y - 1) / block_y);
+#pragma omp parallel for schedule(static, 4096) num_threads(g_threads) if (g_threads > 1)
     for (int idx = 0; idx < P; idx++) {
         radii[idx] = 0;
         tiles_touched[idx] = 0;
@@ -364,6 +375,7 @@ void orc_duplicate_with_keys(int P, const float* points_xy, const float* depths,
                              int block_y, uint64_t* keys, uint32_t* values) {
     const unsigned gx = (unsigned)((W + block_x - 1) / block_x);
     const unsigned gy = (unsigned)((H + block_y - 1) / block_y);
+#pragma omp parallel for schedule(dynamic, 4096) num_threads(g_threads) if (g_threads > 1)
     for (int idx = 0; idx < P; idx++) {
         if (radii[idx] > 0) {
             uint32_t off = (idx == 0) ? 0 : offsets[idx - 1];
@@ -466,6 +478,7 @@ void orc_render_forward(int W, int H, int block_x, int block_y, const uint32_t* 
                         const float* conic_opacity, float* final_T, uint32_t* n_contrib,
                         const float* bg_color, float* out_color) {
     const int gx = (W + block_x - 1) / block_x;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(g_threads) if (g_threads > 1)
     for (int py = 0; py < H; py++)
         for (int px = 0; px < W; px++) {
             int tile = (py / block_y) * gx + (px / block_x);
@@ -481,8 +494,72 @@ void orc_render_forward(int W, int H, int block_x, int block_y, const uint32_t* 
         }
 }
 
+/* base/cr/backward.cu:399-557 (renderCUDA<3> backward), one pixel: adds its
+ * nine per-Gaussian terms to acc[gid * stride + 0..8] in double (the exact
+ * sum of the reference's float atomics). */
+static void bwd_pixel(int W, int H, int px, int py, uint32_t rx, uint32_t ry,
+                      const uint32_t* point_list, const float* bg_color, const float* points_xy,
+                      const float* conic_opacity, const float* colors, const float* final_Ts,
+                      const uint32_t* n_contrib, const float* dL_dpixels, double* acc, int stride) {
+    const float ddelx_dx = (float)(0.5 * W);
+    const float ddely_dy = (float)(0.5 * H);
+    size_t pid = (size_t)W * py + px;
+    const float T_final = final_Ts[pid];
+    float T = T_final;
+    uint32_t contributor = ry - rx;
+    const uint32_t last_contributor = n_contrib[pid];
+    float accum_rec[3] = {0, 0, 0}, dL_dpixel[3], last_color[3] = {0, 0, 0};
+    float last_alpha = 0;
+    for (int i = 0; i < 3; i++) dL_dpixel[i] = dL_dpixels[(size_t)i * H * W + pid];
+    const float pixx = (float)px, pixy = (float)py;
+    for (uint32_t q = ry; q > rx; q--) {
+        uint32_t p = q - 1;
+        contributor--;
+        if (contributor >= last_contributor) continue;
+        uint32_t gid = point_list[p];
+        double* a = acc + (size_t)gid * stride;
+        float dx = points_xy[2 * gid] - pixx, dy = points_xy[2 * gid + 1] - pixy;
+        const float* co = conic_opacity + 4 * gid;
+        float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+        if (power > 0.0f) continue;
+        const float G = expf(power);
+        const float alpha = fminf(0.99f, co[3] * G);
+        if (alpha < 1.0f / 255.0f) continue;
+        T = T / (1.f - alpha);
+        const float dchannel_dcolor = alpha * T;
+        float dL_dalpha = 0.0f;
+        for (int ch = 0; ch < 3; ch++) {
+            const float c = colors[gid * 3 + ch];
+            accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
+            last_color[ch] = c;
+            const float dL_dchannel = dL_dpixel[ch];
+            dL_dalpha += (c - accum_rec[ch]) * dL_dchannel;
+            a[0 + ch] += (double)(dchannel_dcolor * dL_dchannel);
+        }
+        dL_dalpha *= T;
+        last_alpha = alpha;
+        float bg_dot_dpixel = 0;
+        for (int i = 0; i < 3; i++) bg_dot_dpixel += bg_color[i] * dL_dpixel[i];
+        dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
+        const float dL_dG = co[3] * dL_dalpha;
+        const float gdx = G * dx;
+        const float gdy = G * dy;
+        const float dG_ddelx = -gdx * co[0] - gdy * co[1];
+        const float dG_ddely = -gdy * co[2] - gdx * co[1];
+        a[3] += (double)(dL_dG * dG_ddelx * ddelx_dx);
+        a[4] += (double)(dL_dG * dG_ddely * ddely_dy);
+        a[5] += (double)(-0.5f * gdx * dx * dL_dG);
+        a[6] += (double)(-0.5f * gdx * dy * dL_dG);
+        a[7] += (double)(-0.5f * gdy * dy * dL_dG);
+        a[8] += (double)(G * dL_dalpha);
+    }
+}
+
 /* base/cr/backward.cu:399-557 (renderCUDA<3> backward).  Accumulates in double
- * (the exact sum of the reference's float atomics). dL_dconic is [P,4] (2x2). */
+ * (the exact sum of the reference's float atomics). dL_dconic is [P,4] (2x2).
+ * With g_threads > 1 the image is cut into g_threads bands of tile rows, each
+ * summed into its own accumulator (pixel order within a band as the serial
+ * loop), and the bands are added in band order. */
 void orc_render_backward(int W, int H, int block_x, int block_y, const uint32_t* ranges,
                          const uint32_t* point_list, const float* bg_color, const float* points_xy,
                          const float* conic_opacity, const float* colors, const float* final_Ts,
@@ -490,76 +567,39 @@ void orc_render_backward(int W, int H, int block_x, int block_y, const uint32_t*
                          float* dL_dmean2D, float* dL_dconic2D, float* dL_dopacity,
                          float* dL_dcolors) {
     const int gx = (W + block_x - 1) / block_x;
-    double* acc = (double*)calloc((size_t)P * 12, sizeof(double));
-    const float ddelx_dx = (float)(0.5 * W);
-    const float ddely_dy = (float)(0.5 * H);
-    for (int py = 0; py < H; py++)
-        for (int px = 0; px < W; px++) {
-            int tile = (py / block_y) * gx + (px / block_x);
-            uint32_t rx = ranges[2 * tile], ry = ranges[2 * tile + 1];
-            size_t pid = (size_t)W * py + px;
-            const float T_final = final_Ts[pid];
-            float T = T_final;
-            uint32_t contributor = ry - rx;
-            const uint32_t last_contributor = n_contrib[pid];
-            float accum_rec[3] = {0, 0, 0}, dL_dpixel[3], last_color[3] = {0, 0, 0};
-            float last_alpha = 0;
-            for (int i = 0; i < 3; i++) dL_dpixel[i] = dL_dpixels[(size_t)i * H * W + pid];
-            const float pixx = (float)px, pixy = (float)py;
-            for (uint32_t q = ry; q > rx; q--) {
-                uint32_t p = q - 1;
-                contributor--;
-                if (contributor >= last_contributor) continue;
-                uint32_t gid = point_list[p];
-                float dx = points_xy[2 * gid] - pixx, dy = points_xy[2 * gid + 1] - pixy;
-                const float* co = conic_opacity + 4 * gid;
-                float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
-                if (power > 0.0f) continue;
-                const float G = expf(power);
-                const float alpha = fminf(0.99f, co[3] * G);
-                if (alpha < 1.0f / 255.0f) continue;
-                T = T / (1.f - alpha);
-                const float dchannel_dcolor = alpha * T;
-                float dL_dalpha = 0.0f;
-                for (int ch = 0; ch < 3; ch++) {
-                    const float c = colors[gid * 3 + ch];
-                    accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
-                    last_color[ch] = c;
-                    const float dL_dchannel = dL_dpixel[ch];
-                    dL_dalpha += (c - accum_rec[ch]) * dL_dchannel;
-                    acc[(size_t)gid * 12 + 0 + ch] += (double)(dchannel_dcolor * dL_dchannel);
-                }
-                dL_dalpha *= T;
-                last_alpha = alpha;
-                float bg_dot_dpixel = 0;
-                for (int i = 0; i < 3; i++) bg_dot_dpixel += bg_color[i] * dL_dpixel[i];
-                dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
-                const float dL_dG = co[3] * dL_dalpha;
-                const float gdx = G * dx;
-                const float gdy = G * dy;
-                const float dG_ddelx = -gdx * co[0] - gdy * co[1];
-                const float dG_ddely = -gdy * co[2] - gdx * co[1];
-                acc[(size_t)gid * 12 + 3] += (double)(dL_dG * dG_ddelx * ddelx_dx);
-                acc[(size_t)gid * 12 + 4] += (double)(dL_dG * dG_ddely * ddely_dy);
-                acc[(size_t)gid * 12 + 5] += (double)(-0.5f * gdx * dx * dL_dG);
-                acc[(size_t)gid * 12 + 6] += (double)(-0.5f * gdx * dy * dL_dG);
-                acc[(size_t)gid * 12 + 7] += (double)(-0.5f * gdy * dy * dL_dG);
-                acc[(size_t)gid * 12 + 8] += (double)(G * dL_dalpha);
+    const int gy = (H + block_y - 1) / block_y;
+    const int nb = g_threads > 1 ? (g_threads < gy ? g_threads : (gy > 0 ? gy : 1)) : 1;
+    const int stride = 9;
+    double* acc = (double*)calloc((size_t)P * stride * (size_t)nb, sizeof(double));
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nb) if (nb > 1)
+    for (int b = 0; b < nb; b++) {
+        const int ty0 = (int)((long)gy * b / nb), ty1 = (int)((long)gy * (b + 1) / nb);
+        const int py0 = ty0 * block_y, py1 = ty1 * block_y < H ? ty1 * block_y : H;
+        double* a = acc + (size_t)P * stride * (size_t)b;
+        for (int py = py0; py < py1; py++)
+            for (int px = 0; px < W; px++) {
+                int tile = (py / block_y) * gx + (px / block_x);
+                bwd_pixel(W, H, px, py, ranges[2 * tile], ranges[2 * tile + 1], point_list, bg_color,
+                          points_xy, conic_opacity, colors, final_Ts, n_contrib, dL_dpixels, a, stride);
             }
-        }
+    }
+#pragma omp parallel for schedule(static, 4096) num_threads(g_threads) if (g_threads > 1)
     for (int g = 0; g < P; g++) {
-        const double* a = acc + (size_t)g * 12;
-        dL_dcolors[3 * g + 0] = (float)a[0];
-        dL_dcolors[3 * g + 1] = (float)a[1];
-        dL_dcolors[3 * g + 2] = (float)a[2];
-        dL_dmean2D[3 * g + 0] = (float)a[3];
-        dL_dmean2D[3 * g + 1] = (float)a[4];
+        double s[9];
+        for (int q = 0; q < 9; q++) s[q] = acc[(size_t)g * stride + q];
+        for (int b = 1; b < nb; b++)
+            for (int q = 0; q < 9; q++) s[q] += acc[((size_t)P * b + g) * stride + q];
+        dL_dcolors[3 * g + 0] = (float)s[0];
+        dL_dcolors[3 * g + 1] = (float)s[1];
+        dL_dcolors[3 * g + 2] = (float)s[2];
+        dL_dmean2D[3 * g + 0] = (float)s[3];
+        dL_dmean2D[3 * g + 1] = (float)s[4];
         dL_dmean2D[3 * g + 2] = 0.0f;
-        dL_dconic2D[4 * g + 0] = (float)a[5];
-        dL_dconic2D[4 * g + 1] = (float)a[6];
+        dL_dconic2D[4 * g + 0] = (float)s[5];
+        dL_dconic2D[4 * g + 1] = (float)s[6];
         dL_dconic2D[4 * g + 2] = 0.0f;
-        dL_dconic2D[4 * g + 3] = (float)a[7];
-        dL_dopacity[g] = (float)a[8];
+        dL_dconic2D[4 * g + 3] = (float)s[7];
+        dL_dopacity[g] = (float)s[8];
     }
     free(acc);
 }
@@ -569,6 +609,7 @@ void orc_cov2d_backward(int P, const float* means, const int* radii, const float
                         float h_x, float h_y, float tan_fovx, float tan_fovy,
                         const float* view_matrix, const float* dL_dconics, float* dL_dmeans,
                         float* dL_dcov) {
+#pragma omp parallel for schedule(static, 4096) num_threads(g_threads) if (g_threads > 1)
     for (int idx = 0; idx < P; idx++) {
         if (!(radii[idx] > 0)) continue;
         const float* cov3D = cov3Ds + 6 * idx;
@@ -776,6 +817,7 @@ void orc_preprocess_backward(int P, int D, int M, const float* means, const int*
                              const float* campos, const float* dL_dmean2D, float* dL_dmeans,
                              const float* dL_dcolor, const float* dL_dcov3D, float* dL_dsh,
                              float* dL_dscale, float* dL_drot) {
+#pragma omp parallel for schedule(static, 4096) num_threads(g_threads) if (g_threads > 1)
     for (int idx = 0; idx < P; idx++) {
         if (!(radii[idx] > 0)) continue;
         const float* m = means + 3 * idx;
@@ -857,6 +899,7 @@ void orc_amr_render(int W, int H, const uint32_t* ranges, const uint32_t* levels
                     int foveaStep) {
     const int BX = 32, R = 2;
     const int tgx = (W + BX - 1) / BX, tgy = (H + BX - 1) / BX;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(g_threads) if (g_threads > 1)
     for (int gy = 0; gy < tgy * R; gy++)
         for (int gx = 0; gx < tgx * R; gx++) {
             int tile = (gy / R) * tgx + (gx / R);

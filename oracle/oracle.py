@@ -41,6 +41,30 @@ def lib():
     return _lib
 
 
+def set_threads(n: int) -> None:
+    """Host threads of the C loops (OpenMP).  1 = serial, the order the golden
+    fixtures were frozen with; n > 1 parallelises the independent loops and
+    sums the blend backward per band of tile rows (gs_oracle.c)."""
+    lib().orc_set_threads(ctypes.c_int(int(n)))
+
+
+def get_threads() -> int:
+    return int(lib().orc_get_threads())
+
+
+def host_threads(cap: int = 16) -> int:
+    """Threads this process may use: its CPU affinity (the GPU box's share,
+    not the whole machine's os.cpu_count()), capped."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit():
+        n = min(n, int(env))
+    return max(1, min(cap, n))
+
+
 def _p(a):
     if a is None:
         return None
