@@ -1,30 +1,36 @@
 #!/usr/bin/env python3
 """Headline benchmark: rendered views/sec (forward + backward) of the MI355X
 Gaussian rasterizer at 1080p with 1M synthetic Gaussians (BASELINE.json
-config 2), N data-parallel ranks (config 5 at N = 8).
+config 2), and the 1 -> 8 GPU data-parallel curve (config 5).
 
-One *step* = per rank: one forward + backward through the drop-in API
+N = 1 (default): one *step* = one forward + backward through the drop-in API
 (``diff_gaussian_rasterization.GaussianRasterizer``, autograd) of one
-1920x1080 view of the same 1M-Gaussian scene, with a fixed N(0,1) cotangent.
-For N > 1 every rank ends the step holding the parameter gradients (59
-floats per Gaussian: means3D 3, SH 48, opacity 1, scales 3, rotations 4)
-summed over all N views: by default (--exchange views) each rank runs the
-blend backward of its view, the 40-B/Gaussian view records are all-gathered
-over RCCL and every rank runs the multi-view parameter backward
-(data_parallel.py); --exchange params is the plain alternative, each rank's
-full backward + one RCCL all-reduce of the 59-float gradients.  Per-GPU work
-is fixed as N grows ("weak").
+1920x1080 view of the 1M-Gaussian scene with a fixed N(0,1) cotangent
+(config 2).  Rank 0 then adds the other single-GPU configurations as
+``sub_results`` (config 3: foveated AMR 5-step frame; config 4: 6.1M
+Gaussians at 1600x1063; config 5 on one GPU: the 8-view step), each with its
+own roofline, and the CPU baselines.
 
-Inputs are resident in HBM before the timed region.  The timed region is K
-steps bracketed by barrier + synchronize; the reported time is the max over
-ranks.  ``roofline`` is computed from the HIP events the library records on
-its launch stream (gs_profile_*) around the dominant kernel (render_bwd)
-inside the timed region -- only that kernel is timed there, since every
-event pair adds queue time -- with the algorithmic bytes of DESIGN.md; the
-per-stage breakdown (``stages``) comes from a second pass of the same K
-steps with every stage timed.
-``cpu_baseline`` times the CPU oracle (a scalar port of the reference path)
-on one full view on rank 0.
+N > 1 (config 5): a fixed global batch of 8 views per step
+(cameras yawed -17.5 .. +17.5 degrees in 5-degree steps, cotangent seeds
+100 + v), 8 / N views per rank; every rank ends the step holding the
+parameter gradients (59 floats per Gaussian) summed over all 8 views.
+Headline exchange ("views"): each rank runs the blend backward of its views,
+the 40-B/Gaussian view records are all-gathered over RCCL and every rank
+runs the multi-view parameter backward (data_parallel.py).  The line also
+carries the north_star's exchange ("params": each rank's full backward +
+one RCCL all-reduce of the 59-float gradients) and both collectives timed
+alone (ms, bus GB/s, the world size RCCL reports).  views/s = 8 / step time
+("strong": the global batch is fixed).
+
+Launch: ``python bench.py --gpus N`` starts N ranks itself when WORLD_SIZE
+is unset (before any GPU call); under torchrun WORLD_SIZE must equal N.
+Inputs are resident in HBM before the timed region; K steps are bracketed by
+barrier + synchronize, the time is the max over ranks.  ``roofline``: HIP
+events the library records on its launch stream (gs_profile_*) around the
+dominant kernel inside the timed region, with the algorithmic bytes of
+DESIGN.md §4; ``traffic`` comes only from a committed PMC summary of the
+SAME configuration (profiles/*pmc_summary.json, keyed by P, W, H, tile).
 """
 from __future__ import annotations
 
@@ -32,6 +38,8 @@ import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -39,22 +47,59 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-ROOFLINE_STAGE = "render_bwd"  # the dominant kernel of the fwd+bwd step
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
+# instruction (MI355X_MICROARCH.md, execution model).
+VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2
+METRIC = "rendered views/sec (fwd+bwd) at 1080p, 1M Gaussians; achieved HBM GB/s %"
 
 CONFIGS = {
-    # name: (P, W, H)
-    "cfg2_1080p_1M": (1_000_000, 1920, 1080),
-    "cfg3_amr_1080p_1M": (1_000_000, 1920, 1080),   # forward-only foveated AMR (32-px tiles)
-    "cfg4_bicycle_6M": (6_100_000, 1600, 1063),
-    "small": (100_000, 640, 360),
+    # name: P, W, H, tile size, kind
+    "cfg2_1080p_1M": dict(P=1_000_000, W=1920, H=1080, tile=16, kind="fwd_bwd"),
+    "cfg3_amr_1080p_1M": dict(P=1_000_000, W=1920, H=1080, tile=32, kind="amr"),
+    "cfg4_bicycle_6M": dict(P=6_100_000, W=1600, H=1063, tile=16, kind="fwd_bwd"),
+    "cfg5_8view_1080p_1M": dict(P=1_000_000, W=1920, H=1080, tile=16, kind="multiview", views=8),
+    "small": dict(P=100_000, W=640, H=360, tile=16, kind="fwd_bwd"),
 }
 
 
-def algorithmic_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: int) -> float:
+# ------------------------------------------------------------------ launch ---
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` without a launcher: start N ranks of this script
+    as child processes (one per GPU, LOCAL_RANK = rank) and return the first
+    failing exit code (0 if all succeed).  Runs before anything touches the
+    GPU; a rank that fails ends the others (their exact PIDs)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:
+                    q.kill()
+        time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc
+
+
+# ------------------------------------------------------------- roofline ---
+def algorithmic_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: int, views: int = 1) -> float:
     """Compulsory HBM bytes of one launch of `stage`: the bytes
     the reference algorithm must read or write once, whatever the kernel.
     P Gaussians, V visible, K instances, Kb instances up to each tile's last
@@ -77,63 +122,93 @@ def algorithmic_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: in
         return 64.0 * P
     if stage == "tile_scan":    # count in, range + cursor + max_contrib out
         return 28.0 * T
+    if stage == "multiview_bwd":  # per view 40-B records; params in (means 12, SH 192, scales 12, rot 16),
+        return 40.0 * views * P + 232.0 * P + 236.0 * P  # 59 gradient floats out
     return 0.0
 
 
-def load_traffic(stage: str):
-    """HBM bytes per launch of `stage` from a committed rocprofv3 PMC summary
-    (profiles/*pmc*.json written by tools/pmc_summary.py), or None."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
-    for f in reversed(files):
+def config_key(P: int, W: int, H: int, tile: int) -> dict:
+    return {"P": int(P), "W": int(W), "H": int(H), "tile": int(tile)}
+
+
+def _pmc_files():
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
+
+
+def load_pmc(stage: str, key: dict, field: str):
+    """`field` ("per_launch_hbm_bytes" or "per_launch_valu_instructions") of
+    `stage` from the newest committed PMC summary of THIS configuration
+    (its "config" equals `key`), or None.  Summaries of another configuration
+    -- or with no recorded configuration -- are never used."""
+    for f in reversed(_pmc_files()):
         try:
             d = json.load(open(f))
-            if stage in d.get("per_launch_hbm_bytes", {}):
-                return float(d["per_launch_hbm_bytes"][stage])
-        except Exception:
+        except (OSError, ValueError):
             continue
+        if d.get("config") != key:
+            continue
+        v = d.get(field, {}).get(stage)
+        if v is not None:
+            return float(v), os.path.relpath(f, ROOT)
     return None
 
 
-# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU
-# instruction (MI355X_MICROARCH.md, execution model).
-VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2
+def make_roofline(stage: str, by: float, avg_ms: float, key: dict, src: str) -> dict:
+    ach = by / (avg_ms * 1e-3) / 1e9
+    tr = load_pmc(stage, key, "per_launch_hbm_bytes")
+    r = {"kernel": stage, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
+         "traffic_source": tr[1] if tr else None, "algorithmic_bytes": by, "avg_ms": round(avg_ms, 4), "events": src}
+    vi = load_pmc(stage, key, "per_launch_valu_instructions")
+    if vi is not None:  # the blend kernels' real bound (DESIGN.md §4)
+        a_ = vi[0] / (avg_ms * 1e-3)
+        r["valu_issue"] = {"instructions_per_launch": vi[0], "achieved": round(a_, 1),
+                           "peak": VALU_PEAK_WAVE_INSTR_PER_S, "unit": "wave-instr/s",
+                           "frac": round(a_ / VALU_PEAK_WAVE_INSTR_PER_S, 4)}
+    return r
 
 
-def load_valu_instructions(stage: str):
-    """SQ_INSTS_VALU per launch of `stage` from a committed PMC summary, or None."""
-    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))):
-        try:
-            d = json.load(open(f))
-            if stage in d.get("per_launch_valu_instructions", {}):
-                return float(d["per_launch_valu_instructions"][stage])
-        except Exception:
-            continue
-    return None
-
-
-def cpu_baseline_views_per_s(P: int, W: int, H: int, seed: int = 0):
-    """The CPU oracle (scalar C port of the reference path) timed on one full
-    view, forward + backward, single thread."""
+# ------------------------------------------------------------ CPU baselines ---
+def cpu_baseline_views_per_s(sc, cam, threads: int):
+    """The CPU oracle (a scalar C port of the reference path, OpenMP over
+    Gaussians / pixel rows / tile-row bands) on one full view, fwd + bwd."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from gaussian_splatting_with_eye_tracking_amd import synthetic as S
     O.lib()
-    cam = S.make_camera(W, H)
-    sc = S.make_scene(P, cam, seed=seed)
+    O.set_threads(threads)
     s = O.settings_from_camera(cam)
-    dpix = S.make_cotangent(H, W, 1)
+    dpix = S.make_cotangent(cam.image_height, cam.image_width, 1)
     kw = dict(shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
-    t0 = time.perf_counter()
-    r = O.forward(s, sc.means3D, sc.opacities, **kw)
-    O.backward(s, r, sc.means3D, dpix, **kw)
-    dt = time.perf_counter() - t0
+    try:
+        t0 = time.perf_counter()
+        r = O.forward(s, sc.means3D, sc.opacities, **kw)
+        O.backward(s, r, sc.means3D, dpix, **kw)
+        dt = time.perf_counter() - t0
+    finally:
+        O.set_threads(1)
     return 1.0 / dt, dt
+
+
+def cpu_baselines(sc, cam) -> dict:
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    n = O.host_threads(16)
+    v1, dt1 = cpu_baseline_views_per_s(sc, cam, 1)
+    vn, dtn = cpu_baseline_views_per_s(sc, cam, n)
+    W, H, P = cam.image_width, cam.image_height, sc.P
+    return {"value": vn, "unit": "views/s", "cores": n, "kind": "port",
+            "sample": f"one full {W}x{H} view, {P} Gaussians, fwd+bwd, CPU oracle (C, OpenMP, {n} threads): "
+                      f"{dtn:.2f} s",
+            "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "single_thread": {"value": v1, "cores": 1, "seconds": round(dt1, 2)}}
 
 
 def cpu_amr_test_path(seed: int = 0):
     """BASELINE.json north_star: the reference's CPU path, AMR_test.py, timed
     on the host (oracle/amr_test_path.py restates it) on config 1: 10k
-    Gaussians at 256x256; its input image is the CPU oracle's forward render."""
+    Gaussians at 256x256; its input image is the CPU oracle's forward render.
+    Single-threaded by construction (Python loops + Qhull)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import amr_test_path as A
     import oracle as O
@@ -155,6 +230,290 @@ def cpu_amr_test_path(seed: int = 0):
             "seconds": sec}
 
 
+# --------------------------------------------------------------- context ---
+class Ctx:
+    def __init__(self, world, rank, local_rank, distributed, dev, args):
+        self.world, self.rank, self.local_rank, self.distributed, self.dev, self.args = (
+            world, rank, local_rank, distributed, dev, args)
+        self._scenes = {}
+
+    def scene(self, P: int, W: int, H: int):
+        """The SURVEY §8(d) scene (seed args.seed) and the identity camera it is
+        generated in (cached: configs 2, 3 and 5 share the 1M scene)."""
+        from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+        k = (P, W, H)
+        if k not in self._scenes:
+            cam = S.make_camera(W, H)
+            self._scenes[k] = (S.make_scene(P, cam, seed=self.args.seed), cam)
+        return self._scenes[k]
+
+    def barrier(self):
+        import torch.distributed as dist
+        if self.distributed:
+            dist.barrier()
+
+    def max_over_ranks(self, *vals):
+        import torch
+        import torch.distributed as dist
+        if not self.distributed:
+            return vals
+        t = torch.tensor(list(vals), device=self.dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return tuple(float(v) for v in t.tolist())
+
+
+def raster_settings(cam, dev, module="diff_gaussian_rasterization"):
+    import importlib
+
+    import torch
+    GRS = importlib.import_module(module).GaussianRasterizationSettings
+    return GRS(image_height=cam.image_height, image_width=cam.image_width, tanfovx=cam.tanfovx,
+               tanfovy=cam.tanfovy, bg=torch.zeros(3, device=dev), scale_modifier=1.0,
+               viewmatrix=torch.from_numpy(cam.world_view_transform).to(dev),
+               projmatrix=torch.from_numpy(cam.full_proj_transform).to(dev), sh_degree=3,
+               campos=torch.from_numpy(cam.camera_center).to(dev), prefiltered=False, debug=False)
+
+
+def device_params(sc, dev, requires_grad: bool):
+    import torch
+    return {k: torch.from_numpy(np.ascontiguousarray(getattr(sc, k))).to(dev).requires_grad_(requires_grad)
+            for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+
+
+def workload_stats(settings, params, P: int, W: int, H: int, tile: int = 16):
+    """K, V, Kb and the tile ranges of one forward (outside any timed region)."""
+    import torch
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    with torch.no_grad():
+        K, color, radii, geom, binning, img = _C.rasterize_gaussians(
+            settings.bg, params["means3D"], torch.Tensor([]), params["opacities"], params["scales"],
+            params["rotations"], 1.0, torch.Tensor([]), settings.viewmatrix, settings.projmatrix,
+            settings.tanfovx, settings.tanfovy, H, W, params["shs"], 3, settings.campos, False, False)
+        bufs = _C.parse_buffers(geom, binning, img, P, K, W, H, tile)
+    V = int((radii > 0).sum().item())
+    rng = bufs["ranges"].cpu().numpy().astype(np.int64)
+    n_t = rng[:, 1] - rng[:, 0]
+    Kb = int(np.minimum(n_t, bufs["max_contrib"].cpu().numpy().astype(np.int64)).sum())
+    T = ((W + tile - 1) // tile) * ((H + tile - 1) // tile)
+    return dict(K=int(K), V=V, Kb=Kb, N=W * H, T=T)
+
+
+def stage_table(prof: dict, steps: int, P, ws, views=1) -> dict:
+    out = {}
+    for name, (ms, cnt) in prof.items():
+        if cnt:
+            st = {"avg_ms": ms / cnt, "launches": cnt, "ms_per_step": ms / steps}
+            b = algorithmic_bytes(name, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"], views)
+            st["algorithmic_GBps"] = round(b / (st["avg_ms"] * 1e-3) / 1e9, 1) if b else None
+            out[name] = st
+    return out
+
+
+# --------------------------------------------------------- config 2 / 4 ---
+def run_fwd_bwd(cfg_name: str, ctx: Ctx, steps: int, warmup: int) -> dict:
+    """One view forward + backward through the drop-in autograd API per step."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    c = CONFIGS[cfg_name]
+    P, W, H = c["P"], c["W"], c["H"]
+    sc, cam = ctx.scene(P, W, H)
+    settings = raster_settings(cam, ctx.dev)
+    params = device_params(sc, ctx.dev, True)
+    means2D = torch.zeros_like(params["means3D"], requires_grad=True)
+    dpix = torch.from_numpy(S.make_cotangent(H, W, 100 + ctx.rank)).to(ctx.dev)
+    rasterizer = GaussianRasterizer(settings)
+
+    def step():
+        for p in params.values():
+            p.grad = None
+        means2D.grad = None
+        color, _radii = rasterizer(means3D=params["means3D"], means2D=means2D, opacities=params["opacities"],
+                                   shs=params["shs"], scales=params["scales"], rotations=params["rotations"])
+        torch.autograd.backward(color, dpix)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    # Inside the timed region only the roofline kernel (render_bwd, the
+    # dominant stage at configs 2 and 4) records its event pair: each timed
+    # stage costs two event records per launch (~4 us of queue time).
+    prof_stage = "render_bwd"
+    if not ctx.args.no_profile:
+        _C.profile_enable(True)
+        _C.profile_stages([prof_stage])
+        _C.profile_read(True)
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    prof_timed, prof = {}, {}
+    if not ctx.args.no_profile:
+        prof_timed = _C.profile_read(True)
+        _C.profile_stages([])  # per-stage breakdown: the same K steps again, every stage timed
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        prof = _C.profile_read(True)
+        _C.profile_enable(False)
+    (elapsed,) = ctx.max_over_ranks(elapsed)
+    res = {"value": ctx.world * steps / elapsed, "unit": "views/s", "ms_per_step": 1000.0 * elapsed / steps}
+    if ctx.rank != 0:
+        return res
+    ws = workload_stats(settings, params, P, W, H)
+    stages = stage_table(prof, steps, P, ws)
+    roofline = None
+    if stages:
+        dom = max(stages, key=lambda n: stages[n]["ms_per_step"])
+        ms_t, cnt_t = prof_timed.get(dom, (0.0, 0))
+        avg_ms, src = (ms_t / cnt_t, "timed region") if cnt_t else (stages[dom]["avg_ms"], "stage-profile pass")
+        by = algorithmic_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"])
+        roofline = make_roofline(dom, by, avg_ms, config_key(P, W, H, 16), src)
+    res.update({
+        "config": {"workload": f"{cfg_name}: {P} Gaussians, {W}x{H}, 16x16 tiles, forward+backward, 1 view per "
+                               f"GPU per step", "P": P, "width": W, "height": H, "views_per_gpu_per_step": 1,
+                   "parallelism": f"dp{ctx.world}", "K_instances": ws["K"], "V_visible": ws["V"],
+                   "K_bwd_entries": ws["Kb"]},
+        "roofline": roofline, "stages": stages})
+    return res
+
+
+# ------------------------------------------------------------- config 5 ---
+def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange_alt: bool = True) -> dict:
+    """a fixed global batch of `global_views` yawed views per
+    step, global_views / N per rank; every rank ends the step with the summed
+    parameter gradients of all views."""
+    import torch
+    import torch.distributed as dist
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from gaussian_splatting_with_eye_tracking_amd import _C
+    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    c = CONFIGS["cfg5_8view_1080p_1M"]
+    P, W, H = c["P"], c["W"], c["H"]
+    G = global_views
+    if G % ctx.world:
+        raise SystemExit(f"--views {G} is not a multiple of the world size {ctx.world}")
+    vl = G // ctx.world
+    sc, _cam0 = ctx.scene(P, W, H)
+    params = device_params(sc, ctx.dev, True)
+    yaws = [(v - (G - 1) / 2.0) * 5.0 for v in range(G)]  # config 5: -17.5 .. +17.5 at G = 8
+    mine = list(range(ctx.rank * vl, (ctx.rank + 1) * vl))
+    views = []
+    for v in mine:
+        cam = S.make_orbit_camera(W, H, yaws[v])
+        st = raster_settings(cam, ctx.dev)
+        views.append({"v": v, "st": st, "rast": GaussianRasterizer(st),
+                      "dpix": torch.from_numpy(S.make_cotangent(H, W, 100 + v)).to(ctx.dev)})
+    st0 = views[0]["st"]
+    e0 = torch.empty(0, device=ctx.dev)
+    pg = params
+
+    def step_views():
+        with torch.no_grad():
+            recs = []
+            for vw in views:
+                st = vw["st"]
+                K, _color, radii, geom, binning, img = _C.rasterize_gaussians(
+                    st.bg, pg["means3D"], e0, pg["opacities"], pg["scales"], pg["rotations"], 1.0, e0,
+                    st.viewmatrix, st.projmatrix, st.tanfovx, st.tanfovy, H, W, pg["shs"], 3, st.campos, False, False)
+                recs.append(DP.view_record(st, radii, geom, K, binning, img, vw["dpix"]))
+            rec = recs[0] if vl == 1 else torch.stack(recs)
+            return DP.exchange_view_records(rec, st0, pg["means3D"], pg["shs"], pg["scales"], pg["rotations"])
+
+    flat = DP.FlatGrads(params)
+    m2 = torch.zeros_like(params["means3D"], requires_grad=True)
+
+    def step_params():
+        flat.flat.zero_()
+        flat.attach(params)
+        for vw in views:
+            color, _ = vw["rast"](means3D=pg["means3D"], means2D=m2, opacities=pg["opacities"], shs=pg["shs"],
+                                  scales=pg["scales"], rotations=pg["rotations"])
+            torch.autograd.backward(color, vw["dpix"])
+        DP.allreduce_(flat.flat)
+
+    def timed(fn, k):
+        ctx.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        (el,) = ctx.max_over_ranks(time.perf_counter() - t0)
+        return el
+
+    for _ in range(warmup):
+        step_views()
+    torch.cuda.synchronize()
+    el_views = timed(step_views, steps)
+    prof = {}
+    if not ctx.args.no_profile:
+        _C.profile_enable(True)
+        _C.profile_stages([])
+        _C.profile_read(True)
+        timed(step_views, steps)
+        prof = _C.profile_read(True)
+        _C.profile_enable(False)
+    res = {"value": G * steps / el_views, "unit": "views/s", "ms_per_step": 1000.0 * el_views / steps}
+    extra = {}
+    if exchange_alt:
+        for _ in range(max(1, warmup // 2)):
+            step_params()
+        torch.cuda.synchronize()
+        el_params = timed(step_params, steps)
+        extra["exchange_params"] = {
+            "value": G * steps / el_params, "unit": "views/s", "ms_per_step": 1000.0 * el_params / steps,
+            "note": "north_star exchange: full per-view backward into one flat buffer + one RCCL all-reduce "
+                    "(sum) of the 59 f32/Gaussian gradients" if ctx.world > 1 else
+                    "full per-view backward accumulated into one flat buffer (no collective at N = 1)"}
+    if ctx.distributed:
+        # the two collectives alone (nccl-tests bus-bandwidth conventions)
+        rec = torch.zeros((vl, DP.view_record_numel(P)), device=ctx.dev)
+        for _ in range(3):
+            DP.gather_view_records(rec)
+        el_g = timed(lambda: DP.gather_view_records(rec), steps)
+        for _ in range(3):
+            DP.allreduce_(flat.flat)
+        el_a = timed(lambda: DP.allreduce_(flat.flat), steps)
+        n = ctx.world
+        g_bytes = rec.numel() * 4 * n
+        a_bytes = flat.flat.numel() * 4
+        tg, ta = el_g / steps, el_a / steps
+        extra["collectives"] = {
+            "backend": dist.get_backend(), "world_size": dist.get_world_size(),
+            "all_gather_view_records": {"bytes_out": g_bytes, "ms": round(1e3 * tg, 4),
+                                        "bus_GBps": round(g_bytes * (n - 1) / n / tg / 1e9, 1)},
+            "all_reduce_grads": {"bytes": a_bytes, "ms": round(1e3 * ta, 4),
+                                 "bus_GBps": round(a_bytes * 2 * (n - 1) / n / ta / 1e9, 1)}}
+    res.update(extra)
+    if ctx.rank != 0:
+        return res
+    ws = workload_stats(views[0]["st"], params, P, W, H)
+    stages = stage_table(prof, steps, P, ws, G)
+    roofline = None
+    if stages:
+        dom = max(stages, key=lambda n: stages[n]["ms_per_step"])
+        by = algorithmic_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"], G)
+        roofline = make_roofline(dom, by, stages[dom]["avg_ms"], config_key(P, W, H, 16), "stage-profile pass")
+    res.update({
+        "config": {"workload": f"cfg5_8view_1080p_1M: {P} Gaussians, {W}x{H}, 16x16 tiles, {G} views per step "
+                               f"(yaw -17.5..17.5 deg), {vl} per GPU, forward + blend backward + view-record "
+                               f"exchange + multi-view parameter backward",
+                   "P": P, "width": W, "height": H, "global_views_per_step": G, "views_per_gpu_per_step": vl,
+                   "exchange": "views", "parallelism": f"dp{ctx.world}", "K_instances_view0": ws["K"],
+                   "V_visible_view0": ws["V"]},
+        "roofline": roofline, "stages": stages})
+    return res
+
+
+# ------------------------------------------------------------- config 3 ---
 def amr_algorithmic_bytes(ranges: np.ndarray, levels: np.ndarray) -> float:
     """Compulsory bytes of one 5-step frame's amr_render launches (DESIGN.md
     §4): every rendered (tile, round) block reads its tile's entries (id 4 +
@@ -165,33 +524,27 @@ def amr_algorithmic_bytes(ranges: np.ndarray, levels: np.ndarray) -> float:
     return float((L * (40.0 * n + 20.0 * 256)).sum())
 
 
-def run_amr(args, world, rank, local_rank, distributed, dev):
+def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
     """Config 3: forward-only foveated rendering (gaussian_renderer_amr's
     render(): foveaStep 0..4 through _RasterizeGaussians, summing the step
     images; and render_once(): foveaStep -2 with interpolation).  Per-frame and
     single-GPU: for N > 1 every rank renders its own frames (replicas only)."""
-    from diff_gaussian_rasterization_amr import GaussianRasterizationSettings, GaussianRasterizer, _RasterizeGaussians
+    import torch
+    from diff_gaussian_rasterization_amr import GaussianRasterizer, _RasterizeGaussians
     from gaussian_splatting_with_eye_tracking_amd import _C
+    from gaussian_splatting_with_eye_tracking_amd import rasterization_amr as RA
     from gaussian_splatting_with_eye_tracking_amd import synthetic as S
-
-    P, W, H = CONFIGS[args.config]
-    cam = S.make_camera(W, H)
-    sc = S.make_scene(P, cam, seed=args.seed)
-    st = GaussianRasterizationSettings(
-        image_height=H, image_width=W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
-        bg=torch.zeros(3, device=dev), scale_modifier=1.0,
-        viewmatrix=torch.from_numpy(cam.world_view_transform).to(dev),
-        projmatrix=torch.from_numpy(cam.full_proj_transform).to(dev), sh_degree=3,
-        campos=torch.from_numpy(cam.camera_center).to(dev), prefiltered=False, debug=False)
-    t = {k: torch.from_numpy(np.ascontiguousarray(getattr(sc, k))).to(dev)
-         for k in ("means3D", "opacities", "shs", "scales", "rotations")}
+    c = CONFIGS["cfg3_amr_1080p_1M"]
+    P, W, H = c["P"], c["W"], c["H"]
+    dev = ctx.dev
+    sc, cam = ctx.scene(P, W, H)
+    st = raster_settings(cam, dev, "diff_gaussian_rasterization_amr")
+    t = device_params(sc, dev, False)
     e = torch.empty(0, device=dev)
     u8 = torch.empty(0, dtype=torch.uint8, device=dev)
     means2D = torch.zeros_like(t["means3D"])
     a = (t["means3D"], means2D, t["shs"], e, t["opacities"], t["scales"], t["rotations"], e)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-
-    from gaussian_splatting_with_eye_tracking_amd import rasterization_amr as RA
     # extension (SURVEY §8(f) rank 4): the tracked fovea centre of config 3
     # (pupil (361.74, 248.19) in the 640x400 eye image -> screen) with the
     # reference's unused fovea radii W/2 .. W/16 restricting the AMR levels
@@ -200,15 +553,15 @@ def run_amr(args, world, rank, local_rank, distributed, dev):
     def frame_5step(record=False, fovea=False):
         if record:
             ev[0].record()
-        c, radii, gb, bb, ib = _RasterizeGaussians.apply(*a, 0, e, u8, u8, u8, False, st)
+        c_, _radii, gb, bb, ib = _RasterizeGaussians.apply(*a, 0, e, u8, u8, u8, False, st)
         if fovea:
             RA.apply_fovea_levels(ib, W, H, fov_centres, fov_radii)
-        acc = c
+        acc = c_
         if record:
             ev[1].record()
         for k in range(1, 5):
-            c, _, gb, bb, ib = _RasterizeGaussians.apply(*a, k, acc, gb, bb, ib, False, st)
-            acc = acc + c
+            c_, _, gb, bb, ib = _RasterizeGaussians.apply(*a, k, acc, gb, bb, ib, False, st)
+            acc = acc + c_
             if record:
                 ev[k + 1].record()
         return acc, gb, bb, ib
@@ -220,138 +573,166 @@ def run_amr(args, world, rank, local_rank, distributed, dev):
                     scales=t["scales"], rotations=t["rotations"], foveaStep=-2, interpolate_image=True)[0]
 
     with torch.no_grad():
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             frame_5step()
             frame_once()
         torch.cuda.synchronize()
-        if not args.no_profile:
-            _C.profile_enable(True)
-            _C.profile_read(True)
-        if distributed:
-            dist.barrier()
+        ctx.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        for _ in range(steps):
+            frame_5step()
+        torch.cuda.synchronize()
+        ctx.barrier()
+        el5 = time.perf_counter() - t0
+        # per-stage and per-step times: a second pass with events
+        prof = {}
         step_ms = np.zeros(5)
-        for _ in range(args.steps):
+        if not ctx.args.no_profile:
+            _C.profile_enable(True)
+            _C.profile_stages([])
+            _C.profile_read(True)
+        for _ in range(steps):
             frame_5step(record=True)
             torch.cuda.synchronize()
             step_ms += np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(5)])
-        torch.cuda.synchronize()
-        if distributed:
-            dist.barrier()
-        el5 = time.perf_counter() - t0
-        prof = {}
-        if not args.no_profile:
+        if not ctx.args.no_profile:
             prof = _C.profile_read(True)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            frame_once()
-        torch.cuda.synchronize()
-        if distributed:
-            dist.barrier()
-        el1 = time.perf_counter() - t0
-        if not args.no_profile:
             _C.profile_enable(False)
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            frame_5step(fovea=True)
+        for _ in range(steps):
+            frame_once()
         torch.cuda.synchronize()
-        if distributed:
-            dist.barrier()
-        elf = time.perf_counter() - t0
-    # extension: the foveated backward -- render_once (interpolated) forward +
-    # backward through the drop-in autograd API with a fixed cotangent
-    tg = {k: v.detach().clone().requires_grad_(True) for k, v in t.items()}
-    m2 = torch.zeros_like(tg["means3D"], requires_grad=True)
-    cot = torch.from_numpy(S.make_cotangent(H, W, 1)).to(dev)
-
-    def frame_once_fwd_bwd():
-        img = rast(means3D=tg["means3D"], means2D=m2, opacities=tg["opacities"], shs=tg["shs"],
-                   scales=tg["scales"], rotations=tg["rotations"], foveaStep=-2, interpolate_image=True)[0]
-        torch.autograd.backward(img, cot)
-
-    for _ in range(max(1, args.warmup)):
-        frame_once_fwd_bwd()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        frame_once_fwd_bwd()
-    torch.cuda.synchronize()
-    elb = time.perf_counter() - t0
-    with torch.no_grad():
-        if distributed:
-            tt = torch.tensor([el5, el1, elf, elb], device=dev, dtype=torch.float64)
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el5, el1, elf, elb = (float(v) for v in tt.tolist())
-        result = None
-        if rank == 0:
-            acc, gb, bb, ib = frame_5step()
+        ctx.barrier()
+        el1 = time.perf_counter() - t0
+        elf = None
+        if extensions:
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                frame_5step(fovea=True)
             torch.cuda.synchronize()
-            K = int(_C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)["hdr"][0].item())
-            d = _C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
-            rng = d["ranges"].cpu().numpy().astype(np.int64)
-            lv = d["levels"].cpu().numpy().astype(np.int64)
+            ctx.barrier()
+            elf = time.perf_counter() - t0
+    elb = None
+    if extensions:
+        # the foveated backward (extension): render_once (interpolated) forward +
+        # backward through the drop-in autograd API with a fixed cotangent
+        tg = {k: v.detach().clone().requires_grad_(True) for k, v in t.items()}
+        m2 = torch.zeros_like(tg["means3D"], requires_grad=True)
+        cot = torch.from_numpy(S.make_cotangent(H, W, 1)).to(dev)
+
+        def frame_once_fwd_bwd():
+            img = rast(means3D=tg["means3D"], means2D=m2, opacities=tg["opacities"], shs=tg["shs"],
+                       scales=tg["scales"], rotations=tg["rotations"], foveaStep=-2, interpolate_image=True)[0]
+            torch.autograd.backward(img, cot)
+
+        for _ in range(max(1, warmup)):
+            frame_once_fwd_bwd()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            frame_once_fwd_bwd()
+        torch.cuda.synchronize()
+        elb = time.perf_counter() - t0
+    el5, el1 = ctx.max_over_ranks(el5, el1)
+    res = {"value": ctx.world * steps / el5, "unit": "frames/s", "ms_per_step": 1000.0 * el5 / steps,
+           "render_once_fps": ctx.world * steps / el1}
+    if ctx.rank != 0:
+        return res
+    with torch.no_grad():
+        acc, gb, bb, ib = frame_5step()
+        torch.cuda.synchronize()
+        K = int(_C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)["hdr"][0].item())
+        d = _C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
+        rng = d["ranges"].cpu().numpy().astype(np.int64)
+        lv = d["levels"].cpu().numpy().astype(np.int64)
+        fovea_hist = None
+        if extensions:
             _, _, _, ibf = frame_5step(fovea=True)
             lvf = _C.parse_buffers(gb, bb, ibf, P, K, W, H, 32)["levels"].cpu().numpy().astype(np.int64)
             fovea_hist = np.bincount(lvf, minlength=5)[1:].tolist()
-            stages = {n: {"avg_ms": ms / c, "launches": c, "ms_per_frame": ms / args.steps}
-                      for n, (ms, c) in prof.items() if c}
-            roofline = None
-            if "amr_render" in stages:
-                by = amr_algorithmic_bytes(rng, lv)
-                ms = stages["amr_render"]["ms_per_frame"]
-                ach = by / (ms * 1e-3) / 1e9
-                roofline = {"kernel": "amr_render", "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                            "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic("amr_render"),
-                            "algorithmic_bytes_per_frame": by, "ms_per_frame": round(ms, 4)}
-            cpu = None
-            if not args.no_cpu_baseline and world == 1:
-                cpu = cpu_amr_test_path(args.seed)
-            result = {
-                "metric": "foveated AMR frames/sec (forward-only render(), 5 fovea steps) at 1080p, 1M Gaussians",
-                "value": world * args.steps / el5, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-                "warmup": args.warmup, "ms_per_step": 1000.0 * el5 / args.steps, "higher_is_better": True,
-                "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-                "data": "synthetic (SURVEY §8(d) generator, seed 0)",
-                "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, 32x32 AMR tiles, 5-step foveated "
-                                       f"render() per frame" + (", replicas" if world > 1 else ""),
-                           "P": P, "width": W, "height": H, "K_instances": K, "parallelism": f"replicas{world}",
-                           "levels_hist": np.bincount(lv, minlength=5)[1:].tolist()},
-                "render_once_fps": world * args.steps / el1,
-                "amr_backward_ext": {"render_once_fwd_bwd_fps": world * args.steps / elb,
-                                     "note": "extension beyond parity: interpolated render_once forward + "
-                                             "backward through the autograd API"},
-                "fovea_levels_ext": {"fps": world * args.steps / elf, "centre": [round(v, 2) for v in fov_centres[0]],
-                                     "radii": fov_radii, "levels_hist": fovea_hist,
-                                     "note": "extension beyond parity: tracked fovea discs clamp the AMR levels"},
-                "per_step_ms": [round(x / args.steps, 4) for x in step_ms],
-                "roofline": roofline,
-                "cpu_baseline": cpu,
-                "stages": stages,
-            }
-            print(json.dumps(result), flush=True)
-    return result
+    stages = {n: {"avg_ms": ms / cnt, "launches": cnt, "ms_per_frame": ms / steps} for n, (ms, cnt) in prof.items()
+              if cnt}
+    roofline = None
+    if "amr_render" in stages:
+        by = amr_algorithmic_bytes(rng, lv)
+        ms = stages["amr_render"]["ms_per_frame"]
+        roofline = make_roofline("amr_render", by, ms, config_key(P, W, H, 32), "stage-profile pass")
+        roofline["per"] = "frame (the 4 amr_render launches of steps 1..4 summed; traffic per frame)"
+    res.update({
+        "metric": "foveated AMR frames/sec (forward-only render(), 5 fovea steps) at 1080p, 1M Gaussians",
+        "config": {"workload": f"cfg3_amr_1080p_1M: {P} Gaussians, {W}x{H}, 32x32 AMR tiles, 5-step foveated "
+                               f"render() per frame" + (", replicas" if ctx.world > 1 else ""),
+                   "P": P, "width": W, "height": H, "K_instances": K, "parallelism": f"replicas{ctx.world}",
+                   "levels_hist": np.bincount(lv, minlength=5)[1:].tolist()},
+        "per_step_ms": [round(x / steps, 4) for x in step_ms],
+        "roofline": roofline, "stages": stages})
+    if extensions:
+        res["amr_backward_ext"] = {"render_once_fwd_bwd_fps": steps / elb,
+                                   "note": "extension beyond parity: interpolated render_once forward + backward "
+                                           "through the autograd API"}
+        res["fovea_levels_ext"] = {"fps": steps / elf, "centre": [round(v, 2) for v in fov_centres[0]],
+                                   "radii": fov_radii, "levels_hist": fovea_hist,
+                                   "note": "extension beyond parity: tracked fovea discs clamp the AMR levels"}
+    return res
 
 
-def main():
+def summary(r: dict, keys=("value", "unit", "ms_per_step", "config", "roofline", "per_step_ms",
+                           "render_once_fps", "exchange_params")) -> dict:
+    return {k: r[k] for k in keys if k in r}
+
+
+# ------------------------------------------------------------------ main ---
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="cfg2_1080p_1M", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="default: cfg2_1080p_1M at N = 1, cfg5_8view_1080p_1M at N > 1")
+    ap.add_argument("--views", type=int, default=8, help="config 5: global views per step")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sub", action="store_true", help="N = 1: skip the config 3 / 4 / 5 sub-results")
     ap.add_argument("--no-profile", action="store_true", help="disable the per-stage event timing")
-    ap.add_argument("--exchange", choices=("views", "params"), default="views",
-                    help="N > 1 gradient exchange: all-gather of per-view screen-space records (default) or "
-                         "all-reduce of the 59-float parameter gradients")
-    ap.add_argument("--yaw-spread", type=float, default=0.0,
-                    help="rank r renders the camera yawed by (r-(N-1)/2)*spread degrees (config 5 uses 5)")
-    args = ap.parse_args()
+    ap.add_argument("--launcher-dry-run", action="store_true",
+                    help="test hook: rendezvous over gloo on the CPU and print the JSON skeleton (no GPU)")
+    return ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+
+def dry_run(world, rank):
+    """CPU test of the launcher: every rank joins a gloo group, rank 0 prints."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        ok = float(t.item()) == world * (world - 1) / 2
+        dist.destroy_process_group()
+    else:
+        ok = True
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "dry_run": True, "allreduce_ok": ok}), flush=True)
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: start the ranks here, before anything touches the GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:] if argv is None else list(argv)))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launcher_dry_run:
+        return dry_run(world, rank)
+
+    import torch
+    import torch.distributed as dist
     distributed = world > 1
     # GS_BENCH_SHARE_DEVICE=1 / GS_BENCH_BACKEND=gloo only rehearse the N>1 path
     # on a one-GPU box (every rank on device 0); real runs use one GPU per rank
@@ -366,181 +747,47 @@ def main():
         else:
             dist.init_process_group(backend)
     dev = torch.device("cuda", local_rank)
-    if args.config.startswith("cfg3"):
-        result = run_amr(args, world, rank, local_rank, distributed, dev)
-        if distributed:
-            dist.barrier()
-            dist.destroy_process_group()
-        return result
-
-    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
-    from gaussian_splatting_with_eye_tracking_amd import _C
-    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
-    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
-
-    P, W, H = CONFIGS[args.config]
-    cam0 = S.make_camera(W, H)
-    sc = S.make_scene(P, cam0, seed=args.seed)
-    yaw = (rank - (world - 1) / 2.0) * args.yaw_spread
-    cam = cam0 if yaw == 0.0 else S.make_orbit_camera(W, H, yaw)
-    settings = GaussianRasterizationSettings(
-        image_height=H, image_width=W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
-        bg=torch.zeros(3, device=dev), scale_modifier=1.0,
-        viewmatrix=torch.from_numpy(cam.world_view_transform).to(dev),
-        projmatrix=torch.from_numpy(cam.full_proj_transform).to(dev), sh_degree=3,
-        campos=torch.from_numpy(cam.camera_center).to(dev), prefiltered=False, debug=False)
-    params = {k: torch.from_numpy(np.ascontiguousarray(getattr(sc, k))).to(dev).requires_grad_(True)
-              for k in ("means3D", "opacities", "shs", "scales", "rotations")}
-    means2D = torch.zeros_like(params["means3D"], requires_grad=True)
-    dpix = torch.from_numpy(S.make_cotangent(H, W, 100 + rank)).to(dev)
-    rasterizer = GaussianRasterizer(settings)
-    # N > 1, --exchange params: parameter grads are views of one flat buffer (DDP's
-    # gradient-as-bucket-view): the backward accumulates straight into it and one
-    # RCCL all-reduce sums it.  --exchange views (default): each rank runs the
-    # blend backward of its view, one RCCL all-gather of the view records, then
-    # every rank forms the summed parameter gradients of all N views
-    # (data_parallel.py).
-    views_mode = distributed and args.exchange == "views"
-    flat = DP.FlatGrads(params) if (distributed and not views_mode) else None
-    e0 = torch.empty(0, device=dev)
-
-    def step_views():
-        with torch.no_grad():
-            fwd = _C.rasterize_gaussians(
-                settings.bg, params["means3D"], e0, params["opacities"], params["scales"], params["rotations"],
-                1.0, e0, settings.viewmatrix, settings.projmatrix, settings.tanfovx, settings.tanfovy, H, W,
-                params["shs"], 3, settings.campos, False, False)
-            return DP.exchange_view_grads(settings, fwd, dpix, params["means3D"], params["shs"], params["scales"],
-                                          params["rotations"])
-
-    def step():
-        if views_mode:
-            return step_views()
-        if flat is not None:
-            flat.flat.zero_()
-            flat.attach(params)
-        else:
-            for p in params.values():
-                p.grad = None
-        means2D.grad = None
-        color, radii = rasterizer(means3D=params["means3D"], means2D=means2D, opacities=params["opacities"],
-                                  shs=params["shs"], scales=params["scales"], rotations=params["rotations"])
-        torch.autograd.backward(color, dpix)
-        if flat is not None:
-            DP.allreduce_(flat.flat)
-        return color
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    # Inside the timed region only the roofline kernel (render_bwd, the
-    # dominant stage at every config measured) records its event pair: each
-    # timed stage costs two event records per launch (~4 us of queue time).
-    if not args.no_profile:
-        _C.profile_enable(True)
-        _C.profile_stages([ROOFLINE_STAGE])
-        _C.profile_read(True)
-    if distributed:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if distributed:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    prof_timed = {}
-    prof = {}
-    if not args.no_profile:
-        prof_timed = _C.profile_read(True)
-        # Per-stage breakdown: the same K steps again, every stage timed
-        # (outside the headline timing).
-        _C.profile_stages([])
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        prof = _C.profile_read(True)
-        _C.profile_enable(False)
-    if distributed:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    ms_per_step = 1000.0 * elapsed / args.steps
-    views = world * args.steps
-    value = views / elapsed
-
-    result = None
+    torch.cuda.set_device(dev)
+    ctx = Ctx(world, rank, local_rank, distributed, dev, args)
+    cfg = args.config or ("cfg2_1080p_1M" if world == 1 else "cfg5_8view_1080p_1M")
+    kind = CONFIGS[cfg]["kind"]
+    base = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "higher_is_better": True, "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (SURVEY §8(d) generator, seed 0)"}
+    if kind == "amr":
+        r = run_amr(ctx, args.steps, args.warmup)
+        out = dict(base, **r, scaling="weak")
+    elif kind == "multiview":
+        r = run_multiview(ctx, args.steps, args.warmup, args.views)
+        out = dict(base, **r, scaling="strong" if world > 1 else "weak")
+    else:
+        r = run_fwd_bwd(cfg, ctx, args.steps, args.warmup)
+        out = dict(base, **r, scaling="weak")
+    if rank == 0 and world == 1 and kind == "fwd_bwd" and cfg == "cfg2_1080p_1M" and not args.no_sub:
+        torch.cuda.empty_cache()
+        sub = {}
+        k3 = max(5, args.steps // 2)
+        sub["cfg3_amr_1080p_1M"] = summary(run_amr(ctx, k3, min(3, args.warmup), extensions=False))
+        sub["cfg3_amr_1080p_1M"]["metric"] = "foveated AMR frames/sec (forward-only 5-step render())"
+        sub["cfg5_8view_1080p_1M_1gpu"] = summary(run_multiview(ctx, max(5, args.steps // 4),
+                                                                min(3, args.warmup), args.views))
+        torch.cuda.empty_cache()
+        sub["cfg4_bicycle_6M"] = summary(run_fwd_bwd("cfg4_bicycle_6M", ctx, max(5, args.steps // 2),
+                                                     min(3, args.warmup)))
+        out["sub_results"] = sub
+        torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        c = CONFIGS[cfg]
+        sc, cam = ctx.scene(c["P"], c["W"], c["H"])
+        if kind in ("fwd_bwd", "multiview"):
+            out["cpu_baseline"] = cpu_baselines(sc, cam)
+        out["cpu_amr_test_path"] = cpu_amr_test_path(args.seed)
     if rank == 0:
-        # Workload statistics (K, V, ...) from one extra forward, outside the timed region.
-        with torch.no_grad():
-            K, color, radii, geom, binning, img = _C.rasterize_gaussians(
-                settings.bg, params["means3D"], torch.Tensor([]), params["opacities"], params["scales"],
-                params["rotations"], 1.0, torch.Tensor([]), settings.viewmatrix, settings.projmatrix,
-                settings.tanfovx, settings.tanfovy, H, W, params["shs"], 3, settings.campos, False, False)
-            bufs = _C.parse_buffers(geom, binning, img, P, K, W, H, 16)
-        V = int((radii > 0).sum().item())
-        rng = bufs["ranges"].cpu().numpy().astype(np.int64)
-        n_t = rng[:, 1] - rng[:, 0]
-        Kb = int(np.minimum(n_t, bufs["max_contrib"].cpu().numpy().astype(np.int64)).sum())
-        N = W * H
-        T = ((W + 15) // 16) * ((H + 15) // 16)
-        stages = {}
-        for name, (ms, cnt) in prof.items():
-            if cnt:
-                stages[name] = {"avg_ms": ms / cnt, "launches": cnt, "ms_per_step": ms / args.steps}
-        roofline = None
-        if stages:
-            dom = max(stages, key=lambda n: stages[n]["ms_per_step"])
-            ms_t, cnt_t = prof_timed.get(dom, (0.0, 0))
-            if cnt_t:  # events recorded inside the timed region
-                avg_ms, src = ms_t / cnt_t, "timed region"
-            else:
-                avg_ms, src = stages[dom]["avg_ms"], "stage-profile pass"
-            by = algorithmic_bytes(dom, P, V, K, Kb, N, T)
-            ach = by / (avg_ms * 1e-3) / 1e9
-            roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": load_traffic(dom),
-                        "algorithmic_bytes": by, "avg_ms": round(avg_ms, 4), "events": src}
-            vi = load_valu_instructions(dom)
-            if vi is not None:  # the blend kernels' real bound
-                a_ = vi / (avg_ms * 1e-3)
-                roofline["valu_issue"] = {"instructions_per_launch": vi, "achieved": round(a_, 1),
-                                          "peak": VALU_PEAK_WAVE_INSTR_PER_S, "unit": "wave-instr/s",
-                                          "frac": round(a_ / VALU_PEAK_WAVE_INSTR_PER_S, 4)}
-            for n, st in stages.items():
-                b = algorithmic_bytes(n, P, V, K, Kb, N, T)
-                st["algorithmic_GBps"] = round(b / (st["avg_ms"] * 1e-3) / 1e9, 1) if b else None
-        cpu = None
-        if not args.no_cpu_baseline and world == 1:
-            v, dt = cpu_baseline_views_per_s(P, W, H, args.seed)
-            cpu = {"value": v, "unit": "views/s", "cores": 1, "kind": "port",
-                   "sample": f"one full {W}x{H} view, {P} Gaussians, fwd+bwd, CPU oracle (C, 1 thread): {dt:.1f} s"}
-        result = {
-            "metric": "rendered views/sec (fwd+bwd) at 1080p, 1M Gaussians; achieved HBM GB/s %",
-            "value": value, "unit": "views/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32", "data": "synthetic (SURVEY §8(d) generator, seed 0)",
-            "config": {"workload": f"{args.config}: {P} Gaussians, {W}x{H}, 16x16 tiles, forward+backward, "
-                                   f"1 view per GPU per step" + (
-                                       ("" if world == 1 else
-                                        " + RCCL all-gather of the 40-B/Gaussian view records and the multi-view "
-                                        "parameter backward" if args.exchange == "views" else
-                                        " + RCCL all-reduce of 59 f32/Gaussian grads")),
-                       "exchange": None if world == 1 else args.exchange,
-                       "P": P, "width": W, "height": H, "views_per_gpu_per_step": 1,
-                       "parallelism": f"dp{world}", "K_instances": K, "V_visible": V, "K_bwd_entries": Kb},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            "cpu_amr_test_path": cpu_amr_test_path(args.seed) if (cpu is not None) else None,
-            "stages": stages,
-        }
-        print(json.dumps(result), flush=True)
+        print(json.dumps(out), flush=True)
     if distributed:
         dist.barrier()
         dist.destroy_process_group()
-    return result
+    return out
 
 
 if __name__ == "__main__":

@@ -44,7 +44,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const float4* __restrict__ conic_opacity, const float* __restrict__ colors, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ bg,
     float* __restrict__ grad_accum, int cull, const uint32_t* __restrict__ order, int gx, int xcd,
-    int amr_mode, const uint32_t* __restrict__ levels) {
+    int amr_mode, const uint32_t* __restrict__ levels, int flush_mode) {
 #pragma clang fp contract(fast)
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
@@ -331,7 +331,12 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                                : (comp >= 5 && comp <= 7) ? -0.5f * o : 1.0f;
                 const float kb = comp == 3 ? -o * cy * ddelx_dx : comp == 4 ? -o * cz * ddely_dy : 0.0f;
                 const float v = ka * qa + kb * qb;
-                if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[par][r] * kGradRow + comp], v);
+                float* dst = &grad_accum[(size_t)s_id[par][r] * kGradRow + comp];
+                if (flush_mode == 0) {
+                    if (v != 0.f) atomicAdd(dst, v);
+                } else if (flush_mode == 1) {  // diagnostic only (wrong sums): plain stores of the same shape
+                    *dst = v;
+                }
             }
         }
     }
@@ -342,6 +347,11 @@ extern int g_cull;  // render.hip
 // half-wave DPP-tree sums instead of the permlane transposition
 // (1 wave x 4 px capped at 5 or 6 waves per SIMD spills: measured slower)
 int g_bwd_variant = 0;
+// Flush of the per-(tile, Gaussian) sums: 0 = memory-side atomics (the only
+// correct mode); 1 = plain stores of the same shape, 2 = no flush -- timing
+// diagnostics for the A/B tool only (they produce wrong gradients).
+int g_bwd_flush = 0;
+void set_backward_flush(int v) { g_bwd_flush = v; }
 
 void set_backward_variant(int v) { g_bwd_variant = v; }
 
@@ -358,7 +368,7 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
     hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H,      \
                        img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
-                       dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1, 0, nullptr)
+                       dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1, 0, nullptr, g_bwd_flush)
     switch (g_bwd_variant) {
         case 1: GS_BWD_LAUNCH(2, 2, 4, true); break;
         case 2: GS_BWD_LAUNCH(1, 4, 4, true); break;
@@ -380,7 +390,7 @@ void launch_amr_render_backward(int W, int H, int mode, const ImageView& img, co
     hipLaunchKernelGGL((render_bwd_kernel<4, 1, 4, true, true>), dim3(4 * tgx * tgy), dim3(64), 0, s, W, H, img.ranges,
                        img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,
-                       dL_dpix, bg, g.grad_accum, g_cull, nullptr, tgx, 0, mode, img.levels);
+                       dL_dpix, bg, g.grad_accum, g_cull, nullptr, tgx, 0, mode, img.levels, 0);
 }
 
 // ------------------------------------------------------ per-Gaussian bwd ---

@@ -780,6 +780,10 @@ int gs_set_tuning(const char* key, int value) {
         set_bin_chunk(value);
         return 0;
     }
+    if (std::strcmp(key, "bwd_flush") == 0) {
+        set_backward_flush(value);
+        return 0;
+    }
     if (std::strcmp(key, "cull") == 0) {
         set_cull(value);
         return 0;

@@ -98,17 +98,21 @@ def flat_numel_per_gaussian(sh_coeffs: int = 16) -> int:
 
 # ------------------------------------------------------------ view exchange ---
 def gather_view_records(record: torch.Tensor, group=None) -> torch.Tensor:
-    """All ranks' view records, [world, P * 10 + 40], in rank order (one
-    RCCL all-gather; on gloo the list form)."""
+    """All ranks' view records in rank order: record is this rank's [P * 10 +
+    40] record or its [v, P * 10 + 40] records (v views per rank); returns
+    [world * v, P * 10 + 40] (one RCCL all-gather; on gloo the list form)."""
+    recs = record if record.dim() == 2 else record.unsqueeze(0)
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
-        return record.unsqueeze(0)
+        return recs
     world = dist.get_world_size(group)
-    out = torch.empty((world, record.numel()), dtype=record.dtype, device=record.device)
+    v, n = recs.shape
+    out = torch.empty((world, v * n), dtype=recs.dtype, device=recs.device)
+    src = recs.contiguous().view(-1)
     if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, record.contiguous(), group=group)
+        dist.all_gather_into_tensor(out, src, group=group)
     else:
-        dist.all_gather(list(out.unbind(0)), record.contiguous(), group=group)
-    return out
+        dist.all_gather(list(out.unbind(0)), src, group=group)
+    return out.view(world * v, n)
 
 
 def view_record(settings, radii: torch.Tensor, geom: torch.Tensor, num_rendered: int, binning: torch.Tensor,
@@ -152,31 +156,47 @@ def exchange_view_grads(settings, fwd, dL_dpix: torch.Tensor, means3D: torch.Ten
     return exchange_view_records(rec, settings, means3D, shs, scales, rotations, group, stats, chunks)
 
 
+def _empty_param_grads(means3D: torch.Tensor, shs: Optional[torch.Tensor]):
+    dev = means3D.device
+    P = means3D.shape[0]
+    M = shs.shape[1] if shs is not None and shs.dim() == 3 else 0
+    return (torch.zeros((P, 3), device=dev), torch.zeros((P, M, 3), device=dev), torch.zeros((P, 1), device=dev),
+            torch.zeros((P, 3), device=dev), torch.zeros((P, 4), device=dev))
+
+
 def exchange_view_records(rec: torch.Tensor, settings, means3D: torch.Tensor, shs: torch.Tensor,
                           scales: torch.Tensor, rotations: torch.Tensor, group=None, stats=None, chunks: int = 4):
-    """exchange_view_grads from this rank's view record on: the (chunked)
-    all-gather and the multi-view parameter backward."""
+    """exchange_view_grads from this rank's view record(s) on -- rec is one
+    [P * 10 + 40] record or [v, P * 10 + 40] (v views per rank, the same v on
+    every rank): the (chunked) all-gather and the multi-view parameter
+    backward over all world * v views, in rank-then-view order."""
+    recs = rec if rec.dim() == 2 else rec.unsqueeze(0)
+    P = means3D.shape[0]
+    if P == 0:  # every Gaussian pruned: nothing to exchange, empty gradients
+        return _empty_param_grads(means3D, shs)
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1 or chunks <= 1:
-        views = gather_view_records(rec, group)
+        views = gather_view_records(recs, group)
         return multiview_param_grads(views, means3D, shs, settings.sh_degree, scales, rotations,
                                      settings.scale_modifier, stats)
     from . import _C
     world = dist.get_world_size(group)
-    P = means3D.shape[0]
+    v = recs.shape[0]
     nccl = dist.get_backend(group) == "nccl"
 
-    def gather_async(src: torch.Tensor) -> Tuple[torch.Tensor, object]:
+    def gather_async(src: torch.Tensor, width: int) -> Tuple[torch.Tensor, object]:
+        # src: [v, width] -> [world * v, width] in rank-then-view order
+        src = src.contiguous().view(-1)
         out = torch.empty((world, src.numel()), dtype=src.dtype, device=src.device)
         if nccl:
             w = dist.all_gather_into_tensor(out, src, group=group, async_op=True)
         else:
             w = dist.all_gather(list(out.unbind(0)), src, group=group, async_op=True)
-        return out, w
+        return out.view(world * v, width), w
 
-    cams, w_cam = gather_async(rec[P * VIEW_ROW:])
-    step = -(-P // chunks)
+    cams, w_cam = gather_async(recs[:, P * VIEW_ROW:], CAM_WORDS)
+    step = max(1, -(-P // max(1, chunks)))
     bounds = [(a, min(P, a + step)) for a in range(0, P, step)]
-    pending = [(a, b) + gather_async(rec[a * VIEW_ROW:b * VIEW_ROW]) for a, b in bounds]
+    pending = [(a, b) + gather_async(recs[:, a * VIEW_ROW:b * VIEW_ROW], (b - a) * VIEW_ROW) for a, b in bounds]
     dev = means3D.device
     M = shs.shape[1] if shs is not None and shs.numel() else 0
     outs = (torch.empty((P, 3), device=dev), torch.empty((P, M, 3), device=dev), torch.empty((P, 1), device=dev),

@@ -146,3 +146,57 @@ def test_view_record_all_gather_rank_order():
     for r in range(world):
         assert outs[r].shape == (world, n)
         np.testing.assert_array_equal(outs[r], exp)
+
+
+def _multi_view_gather_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+        P = 700
+        n = DP.view_record_numel(P)
+        # two views per rank: view v = 2 * rank + i
+        rec = torch.stack([torch.arange(n, dtype=torch.float32) + 1000.0 * (2 * rank + i) for i in range(2)])
+        views = DP.gather_view_records(rec)
+        # zero Gaussians (everything pruned): empty gradients, no collective needed
+        z = torch.zeros((0, 3))
+
+        class _S:
+            sh_degree, scale_modifier = 3, 1.0
+
+        g = DP.exchange_view_records(torch.zeros(DP.view_record_numel(0)), _S, z, torch.zeros((0, 16, 3)),
+                                     z, torch.zeros((0, 4)))
+        q.put((rank, views.numpy().copy(), [tuple(t.shape) for t in g]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_view_record_gather_several_views_per_rank_and_empty_model():
+    """Config 5 at N < 8 ranks: each rank packs 8 / N view records; the
+    gather returns [world * v, record] in rank-then-view order on every rank.
+    A model with zero Gaussians yields empty gradients instead of failing."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_multi_view_gather_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = {}
+    for _ in range(world):
+        rank, views, shapes = q.get(timeout=240)
+        outs[rank] = (views, shapes)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import sys
+    sys.path.insert(0, ROOT)
+    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+    n = DP.view_record_numel(700)
+    exp = np.stack([np.arange(n, dtype=np.float32) + np.float32(1000.0 * v) for v in range(4)])
+    for r in range(world):
+        np.testing.assert_array_equal(outs[r][0], exp)
+        assert outs[r][1] == [(0, 3), (0, 16, 3), (0, 1), (0, 3), (0, 4)]

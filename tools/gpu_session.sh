@@ -27,6 +27,7 @@ for step in "$@"; do
     bench3) run bench_cfg3 600 python bench.py --config cfg3_amr_1080p_1M --steps 20 --warmup 3 ;;
     bench4) run bench_cfg4 600 python bench.py --config cfg4_bicycle_6M --steps 10 --warmup 3 --no-cpu-baseline ;;
     dist2) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 ;;
+    dist2l) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2_launcher 600 python bench.py --gpus 2 --steps 5 --warmup 2 ;;
     dist2p) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2p 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --steps 5 --warmup 2 --exchange params ;;
     dist2amr) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2amr 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 5 --warmup 2 --config cfg3_amr_1080p_1M ;;
     benchnp) run bench_np 400 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-profile &&
@@ -45,6 +46,7 @@ for step in "$@"; do
               run ab_chunk_cnt 400 python tools/ab_tuning.py --key bin_chunk --values 2048 4096 8192 16384 --stage count_tiles ;;
     ab_order) run ab_order_fwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render &&
               run ab_order_bwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render_bwd --backward ;;
+    ab_flush) run ab_flush 400 python tools/ab_tuning.py --key bwd_flush --values 0 1 2 --stage render_bwd --backward ;;
     ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 0 1 2 --stage amr_render --amr ;;
     ab_split) run ab_split2 400 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward &&
               run ab_split4 600 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
