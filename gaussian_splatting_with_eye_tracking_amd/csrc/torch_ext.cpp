@@ -50,6 +50,39 @@ void require_device(const Tensor& t, const char* name) {
     TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32");
 }
 
+// A non-empty operand must live on `ref`'s device with the given dtype and
+// hold `numel` elements (numel < 0: any): a host or other-GPU pointer, or a
+// short array, would otherwise reach a kernel as a raw pointer and fault the
+// GPU instead of raising here.
+void require_like(const Tensor& t, const Tensor& ref, const char* name, int64_t numel = -1,
+                  torch::ScalarType dt = torch::kFloat32) {
+    if (t.numel() == 0) return;
+    TORCH_CHECK(t.is_cuda() && t.device() == ref.device(), name, " must be on ", ref.device(),
+                " (the MI355X rasterizer has no CPU path)");
+    TORCH_CHECK(t.scalar_type() == dt, name, " must be ", c10::toString(dt));
+    TORCH_CHECK(numel < 0 || t.numel() == numel, name, " has ", t.numel(), " elements, expected ", numel);
+}
+
+// The per-Gaussian and camera operands of a forward / backward call.
+void check_operands(const Tensor& means3D, int P, const Tensor& bg, const Tensor& colors, const Tensor& opacity,
+                    const Tensor& scales, const Tensor& rotations, const Tensor& cov3D_precomp,
+                    const Tensor& viewmatrix, const Tensor& projmatrix, const Tensor& sh, const Tensor& campos) {
+    require_like(bg, means3D, "bg", 3);
+    require_like(colors, means3D, "colors_precomp", 3LL * P);
+    require_like(opacity, means3D, "opacities", P);
+    require_like(scales, means3D, "scales", 3LL * P);
+    require_like(rotations, means3D, "rotations", 4LL * P);
+    require_like(cov3D_precomp, means3D, "cov3D_precomp", 6LL * P);
+    require_like(viewmatrix, means3D, "viewmatrix", 16);
+    require_like(projmatrix, means3D, "projmatrix", 16);
+    require_like(campos, means3D, "campos", 3);
+    if (sh.numel()) {
+        TORCH_CHECK(sh.dim() == 3 && sh.size(0) == P && sh.size(2) == 3 && sh.size(1) >= 1 && sh.size(1) <= 16,
+                    "sh must be [P, M, 3] with 1 <= M <= 16");
+        require_like(sh, means3D, "sh");
+    }
+}
+
 // Empty tensor -> nullptr (rasterize_points.cu: `.contiguous().data<float>()` of an empty tensor).
 const float* fptr(const Tensor& t) { return t.numel() ? t.data_ptr<float>() : nullptr; }
 float* fptr_mut(Tensor& t) { return t.numel() ? t.data_ptr<float>() : nullptr; }
@@ -84,12 +117,8 @@ std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> rasterize_impl(
                      rotations = rotations_in.contiguous(), cov3D_precomp = cov3D_precomp_in.contiguous(),
                      viewmatrix = viewmatrix_in.contiguous(), projmatrix = projmatrix_in.contiguous(),
                      sh = sh_in.contiguous(), campos = campos_in.contiguous();
-        for (auto& pr : {std::make_pair(&bg, "bg"), std::make_pair(&colors, "colors_precomp"),
-                         std::make_pair(&opacity, "opacities"), std::make_pair(&scales, "scales"),
-                         std::make_pair(&rotations, "rotations"), std::make_pair(&cov3D_precomp, "cov3D_precomp"),
-                         std::make_pair(&viewmatrix, "viewmatrix"), std::make_pair(&projmatrix, "projmatrix"),
-                         std::make_pair(&sh, "sh"), std::make_pair(&campos, "campos")})
-            require_device(*pr.first, pr.second);
+        check_operands(means3D, P, bg, colors, opacity, scales, rotations, cov3D_precomp, viewmatrix, projmatrix, sh,
+                       campos);
         const int M = sh.size(0) != 0 ? (int)sh.size(1) : 0;
         void* stream = stream_of(means3D);
         if (!amr) {
@@ -102,7 +131,8 @@ std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> rasterize_impl(
             check(rendered, "rasterize_gaussians");
         } else {
             const Tensor pre = out_color_precomp_in.contiguous();
-            require_device(pre, "out_color_precomp");
+            require_like(pre, means3D, "out_color_precomp", 3LL * H * W);
+            for (const Tensor* bt : {&geom_pre, &bin_pre, &img_pre}) require_like(*bt, means3D, "precomp buffer", -1, torch::kByte);
             Tensor g = geom_pre, b = bin_pre, im = img_pre;
             // K of the precomputed buffers from the binning buffer's size (no sync)
             const int hint = foveaStep >= 1 ? gs_binning_count_of_bytes((size_t)b.numel()) : -1;
@@ -185,8 +215,16 @@ Grads8 BackwardImpl(int amr_step, bool interpolate, const Tensor& background, co
                      viewmatrix = viewmatrix_in.contiguous(), projmatrix = projmatrix_in.contiguous(),
                      dL_dout = dL_dout_color_in.contiguous(), sh = sh_in.contiguous(), campos = campos_in.contiguous();
         require_device(means3D, "means3D");
-        require_device(dL_dout, "dL_dout_color");
-        TORCH_CHECK(radii.scalar_type() == torch::kInt32, "radii must be int32");
+        require_like(dL_dout, means3D, "dL_dout_color", 3LL * H * W);
+        TORCH_CHECK(dL_dout.dim() == 3 && dL_dout.size(0) == 3, "dL_dout_color must be [3, H, W]");
+        // (AMR steps >= 1 pass no radii: the geometry buffer keeps step 0's)
+        TORCH_CHECK(radii.numel() == P || (amr_step != 0 && radii.numel() == 0), "radii must have P elements");
+        require_like(radii, means3D, "radii", P, torch::kInt32);
+        const Tensor no_opacity = torch::empty({0}, opts);
+        check_operands(means3D, P, bg, colors, no_opacity, scales, rotations, cov3D_precomp, viewmatrix,
+                       projmatrix, sh, campos);
+        for (const Tensor* bt : {&geomBuffer, &binningBuffer, &imageBuffer})
+            require_like(*bt, means3D, "geometry / binning / image buffer", -1, torch::kByte);
         int rc;
         if (amr_step == 0) {
             rc = gs_rasterizer_backward(
@@ -264,7 +302,16 @@ Tensor RasterizeGaussiansBackwardViewGrads(const Tensor& background, const Tenso
                  projmatrix = projmatrix_in.contiguous(), campos = campos_in.contiguous();
     require_device(dL_dout, "dL_dout_color");
     require_device(viewmatrix, "viewmatrix");
+    TORCH_CHECK(dL_dout.dim() == 3 && dL_dout.size(0) == 3, "dL_dout_color must be [3, H, W]");
+    require_like(viewmatrix, dL_dout, "viewmatrix", 16);
+    require_like(projmatrix, dL_dout, "projmatrix", 16);
+    require_like(campos, dL_dout, "campos", 3);
+    require_like(bg, dL_dout, "bg", 3);
+    require_like(colors, dL_dout, "colors_precomp", 3LL * P);
+    for (const Tensor* bt : {&geomBuffer, &binningBuffer, &imageBuffer})
+        require_like(*bt, dL_dout, "geometry / binning / image buffer", -1, torch::kByte);
     TORCH_CHECK(radii.is_cuda() && radii.scalar_type() == torch::kInt32, "radii must be an int32 device tensor");
+    require_like(radii, dL_dout, "radii", P, torch::kInt32);
     check(gs_rasterizer_backward_view_grads(
               P, R, fptr(bg), W, H, fptr(colors), fptr(viewmatrix), fptr(projmatrix), fptr(campos), tan_fovx,
               tan_fovy, radii.data_ptr<int>(), reinterpret_cast<char*>(geomBuffer.data_ptr()),
@@ -304,8 +351,11 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> BackwardGaussiansMultiview(
     if (P != 0) {
         const Tensor views = views_in.contiguous(), means3D = means3D_in.contiguous(), sh = sh_in.contiguous(),
                      scales = scales_in.contiguous(), rotations = rotations_in.contiguous();
-        require_device(views, "views");
         require_device(means3D, "means3D");
+        require_like(views, means3D, "views");
+        require_like(scales, means3D, "scales", 3LL * P);
+        require_like(rotations, means3D, "rotations", 4LL * P);
+        require_like(sh, means3D, "sh", (int64_t)P * M * 3);
         check(gs_backward_gaussians_multiview(
                   P, degree, M, V, fptr(views), fptr(means3D), fptr(sh), fptr(scales), fptr(rotations),
                   scale_modifier, fptr_mut(dL_dmeans3D), fptr_mut(dL_dsh), fptr_mut(dL_dopacity), fptr_mut(dL_dscales),
@@ -347,8 +397,12 @@ void BackwardGaussiansMultiviewRange(const Tensor& rows_in, const Tensor& cams_i
     TORCH_CHECK(rows_in.stride(1) == 1 && cams_in.stride(1) == 1, "rows / cams rows must be contiguous");
     const Tensor means3D = means3D_in.contiguous(), sh = sh_in.contiguous(), scales = scales_in.contiguous(),
                  rotations = rotations_in.contiguous();
-    require_device(rows_in, "rows");
-    require_device(cams_in, "cams");
+    require_device(means3D, "means3D");
+    require_like(rows_in, means3D, "rows");
+    require_like(cams_in, means3D, "cams");
+    require_like(scales, means3D, "scales", 3LL * P);
+    require_like(rotations, means3D, "rotations", 4LL * P);
+    require_like(sh, means3D, "sh", (int64_t)P * M * 3);
     check(gs_backward_gaussians_multiview_range(
               P, g0, count, degree, M, V, rows_in.data_ptr<float>(), (size_t)rows_in.stride(0), cams_in.data_ptr<float>(),
               (size_t)cams_in.stride(0), fptr(means3D), fptr(sh), fptr(scales), fptr(rotations), scale_modifier,

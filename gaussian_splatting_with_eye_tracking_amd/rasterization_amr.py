@@ -48,6 +48,19 @@ def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales,
 
 
 class _RasterizeGaussians(torch.autograd.Function):
+    @classmethod
+    def apply(cls, *args):
+        # the copies of the foveaStep >= 1 interpolation (the reference's racy
+        # precomp-copy path) have no backward here: refuse at the call that
+        # would record them (grad mode on, an input requiring grad), not at
+        # loss.backward()
+        if int(args[8]) > 0 and bool(args[13]) and torch.is_grad_enabled() and any(
+                isinstance(a, torch.Tensor) and a.requires_grad for a in args[:8]):
+            raise RuntimeError("the AMR backward differentiates interpolate_image only for render_once "
+                               "(foveaStep < 0); run foveaStep >= 1 with interpolate_image=False or under "
+                               "torch.no_grad()")
+        return super().apply(*args)
+
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, foveaStep,
                 out_color_precomp, geomBuffer_precomp, binningBuffer_precomp, imageBuffer_precomp,
@@ -152,3 +165,6 @@ def apply_fovea_levels(imageBuffer: torch.Tensor, width: int, height: int, centr
     flat = [float(v) for c in centres for v in c]
     _C.amr_fovea_levels(imageBuffer, int(width), int(height), flat, [float(r) for r in radii], int(min_level),
                         bool(replace))
+    # the levels changed in place: a backward that saved this buffer before
+    # the call must fail loudly rather than use the new levels
+    torch.autograd.graph.increment_version(imageBuffer)

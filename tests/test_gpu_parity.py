@@ -504,6 +504,9 @@ def test_amr_backward_five_steps_sum():
 
 
 def test_amr_backward_rejects_interpolated_steps():
+    """foveaStep >= 1 with interpolate_image=True has no backward: it is
+    refused in the forward when an input requires grad, and runs normally
+    under no_grad."""
     from diff_gaussian_rasterization_amr import _RasterizeGaussians
     sc, cam = G.scene_and_camera(500, 64, 64, 1)
     s = G.torch_settings(cam, amr=True)
@@ -513,9 +516,61 @@ def test_amr_backward_rejects_interpolated_steps():
     args = (t["means3D"], torch.zeros_like(t["means3D"]), t["shs"], e, t["opacities"], t["scales"],
             t["rotations"], e)
     c0, _, gb, bb, ib = _RasterizeGaussians.apply(*args, 0, e, u8, u8, u8, False, s)
-    c4, *_ = _RasterizeGaussians.apply(*args, 1, c0, gb, bb, ib, True, s)
     with pytest.raises(RuntimeError, match="render_once"):
-        c4.sum().backward()
+        _RasterizeGaussians.apply(*args, 1, c0, gb, bb, ib, True, s)
+    with torch.no_grad():
+        c1, *_ = _RasterizeGaussians.apply(*args, 1, c0, gb, bb, ib, True, s)
+    assert c1.shape == c0.shape
+
+
+def test_fovea_levels_after_forward_invalidates_saved_buffer():
+    """apply_fovea_levels rewrites the levels of an image buffer in place: a
+    pending backward that saved the buffer raises instead of using them."""
+    from diff_gaussian_rasterization_amr import GaussianRasterizer
+    from gaussian_splatting_with_eye_tracking_amd import rasterization_amr as RA
+    sc, cam = G.scene_and_camera(800, 96, 64, 2)
+    s = G.torch_settings(cam, amr=True)
+    t = G.scene_tensors(sc, requires_grad=True)
+    color, radii, gb, bb, ib = GaussianRasterizer(s)(
+        means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"], shs=t["shs"],
+        scales=t["scales"], rotations=t["rotations"], foveaStep=-2, interpolate_image=False)
+    RA.apply_fovea_levels(ib, 96, 64, *RA.reference_foveae(96, 64))
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        color.sum().backward()
+
+
+def test_bindings_reject_misplaced_operands():
+    """A host tensor, a short array or a wrong dtype raises a Python error in
+    the binding instead of reaching a kernel as a raw pointer."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(300, 64, 48, 3)
+    s = G.torch_settings(cam)
+    t = G.scene_tensors(sc)
+    e = torch.Tensor([])
+
+    def fwd(**over):
+        a = dict(bg=s.bg, means3D=t["means3D"], colors=e, opacity=t["opacities"], scales=t["scales"],
+                 rotations=t["rotations"], cov=e, sh=t["shs"])
+        a.update(over)
+        return C.rasterize_gaussians(a["bg"], a["means3D"], a["colors"], a["opacity"], a["scales"], a["rotations"],
+                                     1.0, a["cov"], s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, 48, 64,
+                                     a["sh"], 3, s.campos, False, False)
+    with pytest.raises(RuntimeError, match="opacities"):
+        fwd(opacity=t["opacities"].cpu())
+    with pytest.raises(RuntimeError, match="scales"):
+        fwd(scales=t["scales"][:100])
+    with pytest.raises(RuntimeError, match="rotations"):
+        fwd(rotations=t["rotations"].double())
+    K, color, radii, geom, binning, img = fwd()
+    dpix = torch.zeros_like(color)
+    with pytest.raises(RuntimeError, match="radii"):
+        C.rasterize_gaussians_backward(s.bg, t["means3D"], radii.cpu(), e, t["scales"], t["rotations"], 1.0, e,
+                                       s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, dpix, t["shs"], 3, s.campos,
+                                       geom, K, binning, img, False)
+    with pytest.raises(RuntimeError, match="sh"):
+        C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, e, t["scales"], t["rotations"], 1.0, e,
+                                       s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, dpix, t["shs"][:10], 3,
+                                       s.campos, geom, K, binning, img, False)
 
 
 # ---------------------------------------------------------- simple-knn ----

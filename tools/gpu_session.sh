@@ -21,6 +21,7 @@ run() {  # name limit cmd...
 for step in "$@"; do
   case "$step" in
     tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
+    configs) run pytest_configs 1100 python -u -m pytest tests/test_gpu_parity_configs.py tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf ;;
     parity) run pytest_parity 600 python -m pytest tests/test_gpu_parity.py tests/test_gpu_cull.py -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
