@@ -46,14 +46,14 @@ struct GsError : std::runtime_error {
 
 // ---- optional per-stage timing (gs_profile_*): hipEvents recorded on the
 // launch stream around each stage; elapsed times are harvested lazily.
-constexpr int kStages = 14;
+constexpr int kStages = 15;
 const char* kStageNames[kStages] = {"preprocess", "tile_scan",    "duplicate",   "sort_tiles",
                                     "render",     "render_bwd",   "bwd_gauss",   "amr_levels",
                                     "amr_render", "amr_interp",   "knn",         "zero_accum",
-                                    "count_tiles", "multiview_bwd"};
+                                    "count_tiles", "multiview_bwd", "amr_lists"};
 enum Stage {
     kPre, kScan, kDup, kSort, kRender, kRenderBwd, kBwdGauss, kAmrLevels, kAmrRender, kAmrInterp, kKnn, kZero, kCount,
-    kMultiView
+    kMultiView, kAmrLists
 };
 struct Profiler {
     bool on = false;
@@ -623,6 +623,15 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
             GS_HIP(hipMemcpyAsync(r.g.radii, radii, sizeof(int) * (size_t)P, hipMemcpyDeviceToDevice, s));
         { StageTimer _t(kAmrLevels, s); launch_amr_levels(r.T, r.img, s); }
         stage_check(dbg, s, "amr_levels");
+        if (g_amr_variant == 3) {
+            // the AMR blend's work units: tiles heaviest first (by list length;
+            // the levels follow the same counts) and the 16x16 quadrant
+            // sub-lists in the dead sort-key space of the binning buffer
+            { StageTimer _t(kAmrLists, s);
+              launch_order_tiles(r.T, r.img, false, s);
+              launch_amr_quad_lists(W, H, r.img, r.b, r.g, r.K, s); }
+            stage_check(dbg, s, "amr_quad_lists");
+        }
         if (foveaStep == 0) return r.K;  // step 0: buffers only (amr/cr/rasterizer_impl.cu:651)
         launch_fovea_levels(foveaStep, r.T, r.img, s);
         const float* feats = colors_precomp ? colors_precomp : r.g.rgb;

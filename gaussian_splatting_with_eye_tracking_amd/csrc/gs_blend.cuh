@@ -144,56 +144,80 @@ __device__ __forceinline__ int xcd_block_tile(int b, int gx, int gy) {
 //     any non-finite value the Gaussian is kept ("hit");
 //   * o*255 < 0.999 means alpha <= o < 1/255 for every pixel (exp(power) <= 1
 //     once power <= 0, and power > 0 is skipped anyway): never blended.
-// Returns bit r set when the box meets row group r of the 16x16 block at
+// The same test on any pixel rectangle culls the AMR quadrant lists.
+//
+// The per-Gaussian part of the test: threshold, box half-widths and the
+// edge-minimum slopes.  `never`: alpha < 1/255 at every pixel.
+struct SplatBox {
+    float2 xy;
+    float4 co;
+    float thr, hx, hy, kyx, kxy;
+    bool ok, never;
+};
+
+__device__ __forceinline__ SplatBox splat_box(float2 xy, float4 co) {
+    SplatBox b;
+    b.xy = xy;
+    b.co = co;
+    const float o = co.w;
+    b.never = o * 255.0f < 0.999f;  // false for NaN: kept
+    const float lt = fmaxf(__logf(255.0f * o), 0.0f);
+    b.thr = 2.04f * lt + 2e-3f;
+    const float cxz = co.x * co.z;
+    b.ok = co.x > 0.0f && co.z > 0.0f && co.y * co.y < 0.998f * cxz;
+    const float det = cxz - co.y * co.y;
+    b.hx = b.ok ? sqrtf(b.thr * co.z / det) * 1.001f + 0.02f : __builtin_inff();
+    b.hy = b.ok ? sqrtf(b.thr * co.x / det) * 1.001f + 0.02f : __builtin_inff();
+    b.kyx = -co.y / co.z;
+    b.kxy = -co.y / co.x;
+    return b;
+}
+
+// Does the Gaussian reach alpha >= 1/255 anywhere in the pixel-centre
+// rectangle [x0, x1] x [y0, y1]?  (Conservative: false only when no pixel of
+// the rectangle can pass the reference's alpha test.)  "misses" comparisons
+// are false for NaN / inf widths -> kept.
+__device__ __forceinline__ bool splat_rect_hit(const SplatBox& b, float x0, float x1, float y0, float y1) {
+    if (b.never) return false;
+    const float2 xy = b.xy;
+    if (xy.x + b.hx < x0 || xy.x - b.hx > x1) return false;
+    if (xy.y + b.hy < y0 || xy.y - b.hy > y1) return false;
+    if (!b.ok) return true;  // ill-conditioned or non-finite: box test only
+    // Exact second stage: the minimum of Q over the rectangle (grown by 0.02
+    // px) against the same threshold; a box that only grazes the rectangle
+    // with a corner the ellipse does not reach is culled too.  The minimum
+    // lies inside (Q = 0) or on an edge, where Q is a 1-D quadratic minimised
+    // at a clamped point; rounding of that point moves Q by O(c * (1e-4
+    // px)^2), far inside the margins above.
+    const float xa = x0 - 0.02f, xb = x1 + 0.02f, ya = y0 - 0.02f, yb = y1 + 0.02f;
+    if (xy.x >= xa && xy.x <= xb && xy.y >= ya && xy.y <= yb) return true;
+    const float4 co = b.co;
+    float q = __builtin_inff();
+#pragma unroll
+    for (int e = 0; e < 2; e++) {  // vertical edges x = xa, xb
+        const float dx = xy.x - (e ? xb : xa);
+        const float dy = fminf(fmaxf(b.kyx * dx, xy.y - yb), xy.y - ya);
+        q = fminf(q, co.x * dx * dx + 2.0f * co.y * dx * dy + co.z * dy * dy);
+    }
+#pragma unroll
+    for (int e = 0; e < 2; e++) {  // horizontal edges y = ya, yb
+        const float dy = xy.y - (e ? yb : ya);
+        const float dx = fminf(fmaxf(b.kxy * dy, xy.x - xb), xy.x - xa);
+        q = fminf(q, co.x * dx * dx + 2.0f * co.y * dx * dy + co.z * dy * dy);
+    }
+    return !(q > b.thr);  // NaN -> kept
+}
+
+// Bit r set when the Gaussian can reach row group r of the 16x16 block at
 // (ox, oy) with pixel stride st (1 = base, 2 = AMR sub-lattice).
 __device__ __forceinline__ uint32_t splat_group_mask(float2 xy, float4 co, float ox, float oy, float st) {
-    const float o = co.w;
-    if (o * 255.0f < 0.999f) return 0u;  // false for NaN: kept
-    const float lt = fmaxf(__logf(255.0f * o), 0.0f);
-    const float thr = 2.04f * lt + 2e-3f;
-    const float cxz = co.x * co.z;
-    const bool ok = co.x > 0.0f && co.z > 0.0f && co.y * co.y < 0.998f * cxz;
-    const float det = cxz - co.y * co.y;
-    const float hx = ok ? sqrtf(thr * co.z / det) * 1.001f + 0.02f : __builtin_inff();
-    const float hy = ok ? sqrtf(thr * co.x / det) * 1.001f + 0.02f : __builtin_inff();
-    // "misses" comparisons are false for NaN / inf widths -> kept
-    if (xy.x + hx < ox || xy.x - hx > ox + 15.0f * st) return 0u;
-    // Exact second stage: the minimum of Q over the group's rectangle (grown
-    // by 0.02 px) against the same threshold; a box that only grazes the
-    // group with a corner the ellipse does not reach is culled too.  The
-    // minimum lies inside (Q = 0) or on an edge, where Q is a 1-D quadratic
-    // minimised at a clamped point; rounding of that point moves Q by
-    // O(c * (1e-4 px)^2), far inside the margins above.
-    const float x0 = ox - 0.02f, x1 = ox + 15.0f * st + 0.02f;
-    const float kyx = -co.y / co.z, kxy = -co.y / co.x;
+    const SplatBox b = splat_box(xy, co);
+    const float x0 = ox, x1 = ox + 15.0f * st;
     uint32_t m = 0;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const float y0 = oy + st * (4.0f * r), y1 = oy + st * (4.0f * r + 3.0f);
-        if (xy.y + hy < y0 || xy.y - hy > y1) continue;
-        bool hit = !ok;  // ill-conditioned or non-finite: box test only
-        if (!hit) {
-            const float ya = y0 - 0.02f, yb = y1 + 0.02f;
-            if (xy.x >= x0 && xy.x <= x1 && xy.y >= ya && xy.y <= yb) {
-                hit = true;
-            } else {
-                float q = __builtin_inff();
-#pragma unroll
-                for (int e = 0; e < 2; e++) {  // vertical edges x = x0, x1
-                    const float dx = xy.x - (e ? x1 : x0);
-                    const float dy = fminf(fmaxf(kyx * dx, xy.y - yb), xy.y - ya);
-                    q = fminf(q, co.x * dx * dx + 2.0f * co.y * dx * dy + co.z * dy * dy);
-                }
-#pragma unroll
-                for (int e = 0; e < 2; e++) {  // horizontal edges y = ya, yb
-                    const float dy = xy.y - (e ? yb : ya);
-                    const float dx = fminf(fmaxf(kxy * dy, xy.x - x1), xy.x - x0);
-                    q = fminf(q, co.x * dx * dx + 2.0f * co.y * dx * dy + co.z * dy * dy);
-                }
-                hit = !(q > thr);  // NaN -> kept
-            }
-        }
-        if (hit) m |= 1u << r;
+        if (splat_rect_hit(b, x0, x1, y0, y1)) m |= 1u << r;
     }
     return m;
 }

@@ -159,6 +159,10 @@ void launch_eye_preprocess(const uint8_t* gray, int H, int W, const uint8_t* gam
 
 // AMR (amr/cr/rasterizer_impl.cu:181-243, amr/cr/forward.cu:261-648).
 void launch_amr_levels(int T, const ImageView& img, hipStream_t s);
+// The 16x16 quadrant sub-lists of the sorted 32-px tile lists (render.hip).
+void launch_amr_quad_lists(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g, int K,
+                           hipStream_t s);
+extern int g_amr_variant;
 void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s);
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const GeomView& g, const float* features, const float* bg,

@@ -90,6 +90,7 @@ struct ImageView {
     uint32_t* pv;              // [4] percentile values (AMR)
     uint32_t* large_tiles;     // [T] list of tiles needing the large sort
     uint32_t* tile_order;      // [T] tiles by descending blend work (launch order)
+    uint32_t* quad_count;      // [T][4] AMR: entries of each 16x16 quadrant's sub-list
 };
 
 inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
@@ -107,6 +108,7 @@ inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
     g.pv = carve<uint32_t>(base, off, 4);
     g.large_tiles = carve<uint32_t>(base, off, T);
     g.tile_order = carve<uint32_t>(base, off, T);
+    g.quad_count = carve<uint32_t>(base, off, 4 * T);
     if (v) *v = g;
     return align_up(off);
 }
@@ -116,6 +118,14 @@ struct BinningView {
     uint64_t* pair_keys;   // [K]  (depth_bits << 32 | gaussian idx), grouped by tile
     uint64_t* scratch;     // [K]  merge-sort ping-pong
 };
+
+// AMR (32-px tiles): once the tile lists are sorted, pair_keys and scratch
+// (>= 16 K bytes, contiguous up to alignment) are dead; they hold the
+// quadrant sub-lists instead: tile t with range [beg, beg + n) keeps the
+// list of its quadrant q (16x16 pixels) at quad_lists(b) + 4 beg + q n --
+// positions i in [0, n) of the tile's entries that can reach the quadrant,
+// ascending (render.hip amr_quad_lists_kernel).
+inline uint32_t* quad_lists(const BinningView& b) { return reinterpret_cast<uint32_t*>(b.pair_keys); }
 
 inline size_t carve_binning(char* base, size_t K, BinningView* v) {
     size_t off = 0;

@@ -167,7 +167,284 @@ __global__ void __launch_bounds__(64 * kWaves) amr_render_kernel(int W, int H, i
     write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
 }
 
-int g_amr_variant = 2;  // same geometries as the forward: 0 = 1 x 4 px, 1 = 2 x 2, 2 = 4 x 1
+// ------------------------------------------------- AMR quadrant sub-lists ---
+// A 32-px AMR tile renders its 1024 pixels as four interleaved sub-lattices
+// (rounds), each spread over the whole tile, so a (tile, round) block walks
+// the tile's whole list.  Splitting by space instead: each 16x16 quadrant of
+// the tile keeps the positions of the tile's entries whose alpha >= 1/255
+// ellipse can reach it (splat_rect_hit, exact and conservative like the
+// row-group cull), in list order.  Every skipped (pixel, entry) pair is one
+// the reference skips with its alpha < 1/255 `continue`
+// (amr/cr/forward.cu:470-472) while still counting it as a contributor, so a
+// pixel blending the sub-list with each entry's ORIGINAL position as its
+// contributor index gets the reference's colour, final T and n_contrib.
+// One 256-thread workgroup per tile; ordered compaction by ballots.
+constexpr int kQlThreads = 256;
+constexpr int kQlPer = 4;  // entries per thread per pass: 1024 per pass, loads issued together
+__global__ void __launch_bounds__(kQlThreads) amr_quad_lists_kernel(int tgx, const uint32_t* __restrict__ ranges,
+                                                                    const uint32_t* __restrict__ point_list,
+                                                                    const float2* __restrict__ means2D,
+                                                                    const float4* __restrict__ conic_opacity,
+                                                                    uint32_t* __restrict__ lists,
+                                                                    uint32_t* __restrict__ quad_count) {
+    constexpr int kW = kQlThreads / 64;
+    __shared__ uint32_t s_cnt[kQlPer][4][kW];  // [pass slot][quadrant][wave] hits
+    __shared__ uint32_t s_base[4];             // entries written per quadrant so far
+    const int tile = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t beg = ranges[2 * tile];
+    const int n = (int)(ranges[2 * tile + 1] - beg);
+    const float ox = (float)((tile % tgx) * 32), oy = (float)((tile / tgx) * 32);
+    uint32_t* out = lists + 4 * (size_t)beg;
+    if (tid < 4) s_base[tid] = 0;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int c0 = 0; c0 < n; c0 += kQlThreads * kQlPer) {
+        // slot e of thread t: entry c0 + e * 256 + t (slot-major keeps the
+        // list order = (slot, wave, lane) order)
+        float2 xy[kQlPer];
+        float4 co[kQlPer];
+#pragma unroll
+        for (int e = 0; e < kQlPer; e++) {
+            const int i = c0 + e * kQlThreads + tid;
+            const uint32_t id = i < n ? point_list[beg + i] : 0u;
+            xy[e] = i < n ? means2D[id] : make_float2(0.f, 0.f);
+            co[e] = i < n ? conic_opacity[id] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        uint32_t m[kQlPer];
+        uint64_t bal[kQlPer][4];
+#pragma unroll
+        for (int e = 0; e < kQlPer; e++) {
+            const int i = c0 + e * kQlThreads + tid;
+            m[e] = 0;
+            if (i < n) {
+                const SplatBox b = splat_box(xy[e], co[e]);
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const float x0 = ox + 16.0f * (float)(q & 1), y0 = oy + 16.0f * (float)(q >> 1);
+                    if (splat_rect_hit(b, x0, x0 + 15.0f, y0, y0 + 15.0f)) m[e] |= 1u << q;
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                bal[e][q] = __ballot((m[e] >> q) & 1u);
+                if (lane == 0) s_cnt[e][q][wave] = (uint32_t)__popcll(bal[e][q]);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint32_t off = s_base[q];
+#pragma unroll
+            for (int e = 0; e < kQlPer; e++) {
+                uint32_t mine = off + (uint32_t)__popcll(bal[e][q] & below);
+#pragma unroll
+                for (int w = 0; w < kW; w++) {
+                    const uint32_t c = s_cnt[e][q][w];
+                    mine += w < wave ? c : 0u;
+                    off += c;
+                }
+                if ((m[e] >> q) & 1u) out[(size_t)q * n + mine] = (uint32_t)(c0 + e * kQlThreads + tid);
+            }
+        }
+        __syncthreads();
+        if (tid < 4) {
+            uint32_t add = 0;
+#pragma unroll
+            for (int e = 0; e < kQlPer; e++)
+#pragma unroll
+                for (int w = 0; w < kW; w++) add += s_cnt[e][tid][w];
+            s_base[tid] += add;
+        }
+        __syncthreads();
+    }
+    if (tid < 4) quad_count[4 * tile + tid] = s_base[tid];
+}
+
+void launch_amr_quad_lists(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g, int K,
+                           hipStream_t s) {
+    const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
+    if (tgx == 0 || tgy == 0) return;
+    if (K == 0) {  // no lists to build; the counts must still read 0
+        (void)hipMemsetAsync(img.quad_count, 0, sizeof(uint32_t) * 4 * (size_t)tgx * tgy, s);  // checked by the caller's stage_check
+        return;
+    }
+    hipLaunchKernelGGL(amr_quad_lists_kernel, dim3(tgx * tgy), dim3(kQlThreads), 0, s, tgx, img.ranges, b.point_list,
+                       reinterpret_cast<const float2*>(g.means2D), reinterpret_cast<const float4*>(g.conic_opacity),
+                       quad_lists(b), img.quad_count);
+}
+
+// One wave per (tile, quadrant) unit, units in the tile order of the step-0
+// launch (heaviest tiles first).  The unit renders the rounds r with
+// lo < r <= L of its quadrant: the 8x8 points of sub-lattice r, one pixel
+// per lane (kRounds = 1, the progressive steps: one round each, blended two
+// entries per iteration), or all rounds of the unit at once, one pixel per
+// lane and round (kRounds = 4, render_once).  Per pixel the blend is
+// amr/cr/forward.cu:440-495 (base/cr/forward.cu:300-373) with contributor =
+// the entry's position in the tile list + 1.
+template <int kRounds>
+__global__ void __launch_bounds__(64) amr_quad_render_kernel(int W, int H, int tgx, const uint32_t* __restrict__ order,
+                                                             const uint32_t* __restrict__ ranges,
+                                                             const uint32_t* __restrict__ lists,
+                                                             const uint32_t* __restrict__ quad_count,
+                                                             const uint32_t* __restrict__ levels,
+                                                             const uint32_t* __restrict__ levels_last,
+                                                             const uint32_t* __restrict__ point_list,
+                                                             const float2* __restrict__ means2D,
+                                                             const float* __restrict__ features,
+                                                             const float4* __restrict__ conic_opacity,
+                                                             float* __restrict__ final_T,
+                                                             uint32_t* __restrict__ n_contrib,
+                                                             const float* __restrict__ bg,
+                                                             float* __restrict__ out_color, int foveaStep) {
+#pragma clang fp contract(fast)
+    __shared__ float2 s_xy[64];
+    __shared__ float4 s_co[64];
+    __shared__ float4 s_rgb[64];
+    __shared__ uint32_t s_pos[64];
+    const int tile = (int)order[blockIdx.x >> 2];
+    const int q = (int)(blockIdx.x & 3);
+    const uint32_t L_last = levels_last[tile];
+    uint32_t L = levels[tile];
+    // Block-uniform early exits (amr/cr/forward.cu:287-367).
+    if (L <= L_last) return;
+    if (L > 4) L = 4;
+    const uint32_t lo = foveaStep > 0 ? L_last : 0u;  // rounds (lo, L]
+    const uint32_t cnt = quad_count[4 * tile + q];
+    const uint32_t beg = ranges[2 * tile];
+    const uint32_t n = ranges[2 * tile + 1] - beg;
+    const uint32_t* list = lists + 4 * (size_t)beg + (size_t)q * n;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t ax = (uint32_t)(tile % tgx) * 32 + 16 * (q & 1) + 2 * (lane & 7);
+    const uint32_t ay = (uint32_t)(tile / tgx) * 32 + 16 * (q >> 1) + 2 * (lane >> 3);
+    const size_t plane = (size_t)H * W;
+    const float b0 = bg[0], b1 = bg[1], b2 = bg[2];
+    constexpr int kSlots = kRounds;
+    // the rounds this launch renders: kRounds = 4 -> slot k = round k + 1;
+    // kRounds = 1 -> one round per pass, passes over (lo, L]
+    for (uint32_t r1 = lo + 1; r1 <= L; r1 += kRounds) {
+        float pxx[kSlots], pxy[kSlots], T[kSlots], C[kSlots][3];
+        uint32_t last[kSlots], pid[kSlots];
+        bool done[kSlots], active[kSlots];
+#pragma unroll
+        for (int k = 0; k < kSlots; k++) {
+            const uint32_t r = kRounds == 1 ? r1 : (uint32_t)k + 1;
+            active[k] = r > lo && r <= L;  // wave-uniform
+            // round -> sub-lattice offset (amr/cr/forward.cu:313-339): 1 (0,0), 2 (1,1), 3 (1,0), 4 (0,1)
+            const uint32_t sx = (r == 2 || r == 3) ? 1u : 0u, sy = (r == 2 || r == 4) ? 1u : 0u;
+            const uint32_t x = ax + sx, y = ay + sy;
+            pxx[k] = (float)x;
+            pxy[k] = (float)y;
+            const bool in = active[k] && x < (uint32_t)W && y < (uint32_t)H;
+            pid[k] = in ? (uint32_t)W * y + x : 0u;
+            done[k] = !in;
+            T[k] = 1.0f;
+            C[k][0] = C[k][1] = C[k][2] = 0.f;
+            last[k] = 0;
+        }
+        for (uint32_t b0i = 0; b0i < cnt; b0i += 64) {
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < kSlots; k++) any |= !done[k];
+            if (__ballot(any) == 0ull) break;  // every pixel of the unit saturated
+            __syncthreads();                     // single-wave workgroup: LDS fence only
+            if (b0i + lane < cnt) {
+                const uint32_t pos = list[b0i + lane];
+                const uint32_t id = point_list[beg + pos];
+                s_pos[lane] = pos;
+                s_xy[lane] = means2D[id];
+                s_co[lane] = splat_coef(conic_opacity[id]);
+                s_rgb[lane] = make_float4(features[3 * id], features[3 * id + 1], features[3 * id + 2], 0.f);
+            }
+            __syncthreads();
+            const uint32_t m = min(64u, cnt - b0i);
+            if constexpr (kRounds == 1) {
+                // two entries per iteration: their LDS reads share one wait and
+                // their alpha chains interleave; the blend stays in list order
+                for (uint32_t j = 0; j < m; j += 2) {
+                    const bool two = j + 1 < m;  // wave-uniform
+                    const uint32_t jB = two ? j + 1 : j;
+                    const float2 xyA = s_xy[j], xyB = s_xy[jB];
+                    const float4 coA = s_co[j], coB = s_co[jB];
+                    const float4 fA = s_rgb[j], fB = s_rgb[jB];
+                    const uint32_t cA = s_pos[j] + 1, cB = s_pos[jB] + 1;
+                    const float pA = splat_p2(xyA.x - pxx[0], xyA.y - pxy[0], coA);
+                    const float pB = splat_p2(xyB.x - pxx[0], xyB.y - pxy[0], coB);
+                    const float aA = fminf(0.99f, coA.w * splat_exp(pA));
+                    const float aB = fminf(0.99f, coB.w * splat_exp(pB));
+                    {
+                        const float test_T = T[0] * (1 - aA);
+                        const bool hit = !done[0] && !(pA > 0.0f) && !(aA < 1.0f / 255.0f);
+                        const bool stop = hit && test_T < 0.0001f;
+                        done[0] = done[0] || stop;
+                        if (hit && !stop) {
+                            const float w = aA * T[0];
+                            C[0][0] = __builtin_fmaf(fA.x, w, C[0][0]);
+                            C[0][1] = __builtin_fmaf(fA.y, w, C[0][1]);
+                            C[0][2] = __builtin_fmaf(fA.z, w, C[0][2]);
+                            T[0] = test_T;
+                            last[0] = cA;
+                        }
+                    }
+                    if (two) {
+                        const float test_T = T[0] * (1 - aB);
+                        const bool hit = !done[0] && !(pB > 0.0f) && !(aB < 1.0f / 255.0f);
+                        const bool stop = hit && test_T < 0.0001f;
+                        done[0] = done[0] || stop;
+                        if (hit && !stop) {
+                            const float w = aB * T[0];
+                            C[0][0] = __builtin_fmaf(fB.x, w, C[0][0]);
+                            C[0][1] = __builtin_fmaf(fB.y, w, C[0][1]);
+                            C[0][2] = __builtin_fmaf(fB.z, w, C[0][2]);
+                            T[0] = test_T;
+                            last[0] = cB;
+                        }
+                    }
+                    if (__ballot(!done[0]) == 0ull) break;
+                }
+            } else {
+                for (uint32_t j = 0; j < m; j++) {
+                    const float2 xy = s_xy[j];
+                    const float4 co = s_co[j];
+                    const uint32_t contributor = s_pos[j] + 1;
+                    bool alive = false;
+#pragma unroll
+                    for (int k = 0; k < kSlots; k++) {
+                        alive |= !done[k];
+                        if (!active[k]) continue;  // wave-uniform
+                        const float p = splat_p2(xy.x - pxx[k], xy.y - pxy[k], co);
+                        const float alpha = fminf(0.99f, co.w * splat_exp(p));
+                        const float test_T = T[k] * (1 - alpha);
+                        const bool hit = !done[k] && !(p > 0.0f) && !(alpha < 1.0f / 255.0f);
+                        const bool stop = hit && test_T < 0.0001f;
+                        done[k] = done[k] || stop;
+                        if (!hit || stop) continue;
+                        const float4 f = s_rgb[j];
+                        const float w = alpha * T[k];
+                        C[k][0] = __builtin_fmaf(f.x, w, C[k][0]);
+                        C[k][1] = __builtin_fmaf(f.y, w, C[k][1]);
+                        C[k][2] = __builtin_fmaf(f.z, w, C[k][2]);
+                        T[k] = test_T;
+                        last[k] = contributor;
+                    }
+                    if (__ballot(alive) == 0ull) break;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kSlots; k++) {
+            const uint32_t x = (uint32_t)pxx[k], y = (uint32_t)pxy[k];
+            if (!active[k] || x >= (uint32_t)W || y >= (uint32_t)H) continue;
+            const uint32_t p = pid[k];
+            final_T[p] = T[k];
+            n_contrib[p] = last[k];
+            out_color[p] = C[k][0] + T[k] * b0;
+            out_color[plane + p] = C[k][1] + T[k] * b1;
+            out_color[2 * plane + p] = C[k][2] + T[k] * b2;
+        }
+    }
+}
+
+int g_amr_variant = 3;  // 3: quadrant sub-lists (default); 0 = 1 x 4 px, 1 = 2 x 2, 2 = 4 x 1 full-list blocks
 void set_amr_variant(int v) { g_amr_variant = v; }
 
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
@@ -175,6 +452,24 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
                        float* out_color, int foveaStep, hipStream_t s) {
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0) return;
+    if (g_amr_variant == 3) {
+        // the tile order and quadrant lists were built by foveaStep 0 (or this
+        // render_once call) right after the binning (gs_api.cpp)
+        const int T = tgx * tgy;
+        if (foveaStep > 0)
+            hipLaunchKernelGGL(amr_quad_render_kernel<1>, dim3(4 * T), dim3(64), 0, s, W, H, tgx, img.tile_order,
+                               img.ranges, quad_lists(b), img.quad_count, levels, levels_last, b.point_list,
+                               reinterpret_cast<const float2*>(g.means2D), features,
+                               reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib, bg,
+                               out_color, foveaStep);
+        else
+            hipLaunchKernelGGL(amr_quad_render_kernel<4>, dim3(4 * T), dim3(64), 0, s, W, H, tgx, img.tile_order,
+                               img.ranges, quad_lists(b), img.quad_count, levels, levels_last, b.point_list,
+                               reinterpret_cast<const float2*>(g.means2D), features,
+                               reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib, bg,
+                               out_color, foveaStep);
+        return;
+    }
 #define GS_AMR_LAUNCH(PPL, WAVES)                                                                                  \
     hipLaunchKernelGGL((amr_render_kernel<PPL, WAVES>), dim3(2 * tgx, 2 * tgy), dim3(64 * WAVES), 0, s, W, H, tgx, \
                        img.ranges, levels, levels_last, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \

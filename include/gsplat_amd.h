@@ -292,6 +292,7 @@ typedef struct {
     uint32_t* pv; /* [4] */
     uint32_t* large_tiles;
     uint32_t* tile_order; /* [T] blend launch order (descending work) */
+    uint32_t* quad_count; /* [T][4] AMR quadrant sub-list lengths */
 } gs_image_view;
 
 typedef struct {

@@ -22,6 +22,7 @@ for step in "$@"; do
   case "$step" in
     tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     configs) run pytest_configs 1100 python -u -m pytest tests/test_gpu_parity_configs.py tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf ;;
+    amrtests) run pytest_amr 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_parity_configs.py tests/test_gpu_cull.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf -k "amr or config3 or cull" ;;
     parity) run pytest_parity 600 python -m pytest tests/test_gpu_parity.py tests/test_gpu_cull.py -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
@@ -35,6 +36,7 @@ for step in "$@"; do
              run bench_p 400 python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
     benchq) run bench 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     prof4) run rocprof4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- python3 bench.py --config cfg4_bicycle_6M --steps 5 --warmup 2 --no-cpu-baseline --no-profile ;;
+    prof3) run rocprof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 10 --warmup 3 --no-profile ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
     pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
@@ -47,8 +49,10 @@ for step in "$@"; do
               run ab_chunk_cnt 400 python tools/ab_tuning.py --key bin_chunk --values 2048 4096 8192 16384 --stage count_tiles ;;
     ab_order) run ab_order_fwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render &&
               run ab_order_bwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render_bwd --backward ;;
+    ab_pair) run ab_pair 400 python tools/ab_tuning.py --key bwd_variant --values 0 4 --stage render_bwd --backward ;;
+    pmc_ql) run pmc_ql 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS --kernel-trace -d gpurun_out/pmc_ql -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 3 --warmup 1 --no-profile ;;
     ab_flush) run ab_flush 400 python tools/ab_tuning.py --key bwd_flush --values 0 1 2 --stage render_bwd --backward ;;
-    ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 0 1 2 --stage amr_render --amr ;;
+    ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 2 3 --stage amr_render --amr ;;
     ab_split) run ab_split2 400 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward &&
               run ab_split4 600 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_sq -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
