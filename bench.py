@@ -153,16 +153,17 @@ def load_pmc(stage: str, key: dict, field: str):
     return None
 
 
-def make_roofline(stage: str, by: float, avg_ms: float, key: dict, src: str) -> dict:
+def make_roofline(stage: str, by: float, avg_ms: float, key: dict, src: str, per: float = 1.0) -> dict:
+    """`by` bytes in `avg_ms`; `per` = launches those cover (PMC values are per launch)."""
     ach = by / (avg_ms * 1e-3) / 1e9
     tr = load_pmc(stage, key, "per_launch_hbm_bytes")
     r = {"kernel": stage, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr[0] if tr else None,
+         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr[0] * per if tr else None,
          "traffic_source": tr[1] if tr else None, "algorithmic_bytes": by, "avg_ms": round(avg_ms, 4), "events": src}
     vi = load_pmc(stage, key, "per_launch_valu_instructions")
     if vi is not None:  # the blend kernels' real bound (DESIGN.md §4)
-        a_ = vi[0] / (avg_ms * 1e-3)
-        r["valu_issue"] = {"instructions_per_launch": vi[0], "achieved": round(a_, 1),
+        a_ = vi[0] * per / (avg_ms * 1e-3)
+        r["valu_issue"] = {"instructions": vi[0] * per, "achieved": round(a_, 1),
                            "peak": VALU_PEAK_WAVE_INSTR_PER_S, "unit": "wave-instr/s",
                            "frac": round(a_ / VALU_PEAK_WAVE_INSTR_PER_S, 4)}
     return r
@@ -657,7 +658,9 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
     if "amr_render" in stages:
         by = amr_algorithmic_bytes(rng, lv)
         ms = stages["amr_render"]["ms_per_frame"]
-        roofline = make_roofline("amr_render", by, ms, config_key(P, W, H, 32), "stage-profile pass")
+        # the PMC summary holds means per launch; the roofline is per frame
+        roofline = make_roofline("amr_render", by, ms, config_key(P, W, H, 32), "stage-profile pass",
+                                 per=stages["amr_render"]["launches"] / steps)
         roofline["per"] = "frame (the 4 amr_render launches of steps 1..4 summed; traffic per frame)"
     res.update({
         "metric": "foveated AMR frames/sec (forward-only render(), 5 fovea steps) at 1080p, 1M Gaussians",
@@ -679,7 +682,11 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
 
 def summary(r: dict, keys=("value", "unit", "ms_per_step", "config", "roofline", "per_step_ms",
                            "render_once_fps", "exchange_params")) -> dict:
-    return {k: r[k] for k in keys if k in r}
+    out = {k: r[k] for k in keys if k in r}
+    if r.get("stages"):  # compact per-stage ms per step (or per frame)
+        out["stages_ms"] = {n: round(v.get("ms_per_step", v.get("ms_per_frame", 0.0)), 4)
+                            for n, v in r["stages"].items()}
+    return out
 
 
 # ------------------------------------------------------------------ main ---
@@ -695,6 +702,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="N = 1: skip the config 3 / 4 / 5 sub-results")
     ap.add_argument("--no-profile", action="store_true", help="disable the per-stage event timing")
+    ap.add_argument("--no-ext", action="store_true", help="config 3: skip the extension legs (fovea discs, "
+                    "AMR backward), e.g. for PMC passes")
     ap.add_argument("--launcher-dry-run", action="store_true",
                     help="test hook: rendezvous over gloo on the CPU and print the JSON skeleton (no GPU)")
     return ap.parse_args(argv)
@@ -755,7 +764,7 @@ def main(argv=None):
             "higher_is_better": True, "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (SURVEY §8(d) generator, seed 0)"}
     if kind == "amr":
-        r = run_amr(ctx, args.steps, args.warmup)
+        r = run_amr(ctx, args.steps, args.warmup, extensions=not args.no_ext)
         out = dict(base, **r, scaling="weak")
     elif kind == "multiview":
         r = run_multiview(ctx, args.steps, args.warmup, args.views)

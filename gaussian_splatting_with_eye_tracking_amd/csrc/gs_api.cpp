@@ -185,6 +185,7 @@ struct Binned {
     GeomView g;
     ImageView img;
     BinningView b;
+    AmrBinningView ab;  // tile == 32 only
     int K;
     int T;
     int* radii;
@@ -217,8 +218,9 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     if (hdr[kHdrError])
         throw GsError("Point is filtered although prefiltered is set. This shouldn't happen!");
     r.K = (int)hdr[kHdrNumRendered];
-    char* bbase = call_resize(binning, carve_binning(nullptr, r.K, nullptr), "binning");
-    carve_binning(bbase, r.K, &r.b);
+    const bool amr = tile == 32;  // the AMR layout appends records and region lists
+    char* bbase = call_resize(binning, carve_binning(nullptr, r.K, nullptr, nullptr, amr), "binning");
+    carve_binning(bbase, r.K, &r.b, amr ? &r.ab : nullptr);
     if (r.K > 0) {
         { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s); }
         stage_check(debug, s, "duplicate");
@@ -597,13 +599,16 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
             }
             if (K > 0 && !binning_buffer_precomp)
                 throw GsError("foveaStep >= 1 needs the binning buffer returned by foveaStep 0");
-            carve_binning(binning_buffer_precomp, K, &b);
+            AmrBinningView ab;
+            carve_binning(binning_buffer_precomp, K, &b, &ab);
             launch_fovea_levels(foveaStep, T, img, s);
             stage_check(dbg, s, "fovea_levels");
+            if (g_amr_variant != 4)  // variant 4 writes the zeros of the pixels it does not render itself
+                GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, s));
             const float* feats = colors_precomp ? colors_precomp : g.rgb;
             { StageTimer _t(kAmrRender, s);
-              launch_amr_render(W, H, img, img.levels_current, img.levels_last, b, g, feats, background, out_color,
-                                foveaStep, s); }
+              launch_amr_render(W, H, img, img.levels_current, img.levels_last, b, ab, g, feats, background,
+                                out_color, foveaStep, s); }
             stage_check(dbg, s, "amr_render");
             if (interpolate_image) {
                 if (!out_color_precomp) throw GsError("interpolate_image at foveaStep >= 1 needs out_color_precomp");
@@ -623,21 +628,28 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
             GS_HIP(hipMemcpyAsync(r.g.radii, radii, sizeof(int) * (size_t)P, hipMemcpyDeviceToDevice, s));
         { StageTimer _t(kAmrLevels, s); launch_amr_levels(r.T, r.img, s); }
         stage_check(dbg, s, "amr_levels");
-        if (g_amr_variant == 3) {
+        const float* feats = colors_precomp ? colors_precomp : r.g.rgb;
+        if (g_amr_variant >= 3) {
             // the AMR blend's work units: tiles heaviest first (by list length;
-            // the levels follow the same counts) and the 16x16 quadrant
-            // sub-lists in the dead sort-key space of the binning buffer
+            // the levels follow the same counts) and their sub-lists: 16x16
+            // quadrants in the dead sort-key space (variant 3) or the 8x8
+            // regions + blend records of the AMR binning layout (4)
             { StageTimer _t(kAmrLists, s);
               launch_order_tiles(r.T, r.img, false, s);
-              launch_amr_quad_lists(W, H, r.img, r.b, r.g, r.K, s); }
-            stage_check(dbg, s, "amr_quad_lists");
+              if (g_amr_variant == 3) launch_amr_quad_lists(W, H, r.img, r.b, r.g, r.K, s);
+              else launch_amr_region_lists(W, H, r.img, r.b, r.ab, r.g, feats, r.K, s); }
+            stage_check(dbg, s, "amr_lists");
         }
-        if (foveaStep == 0) return r.K;  // step 0: buffers only (amr/cr/rasterizer_impl.cu:651)
+        if (foveaStep == 0) {  // step 0: buffers only, a zero image (amr/cr/rasterizer_impl.cu:651)
+            GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, s));
+            return r.K;
+        }
+        if (g_amr_variant != 4)  // variant 4 writes the zeros of the pixels it does not render itself
+            GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, s));
         launch_fovea_levels(foveaStep, r.T, r.img, s);
-        const float* feats = colors_precomp ? colors_precomp : r.g.rgb;
         { StageTimer _t(kAmrRender, s);
-          launch_amr_render(W, H, r.img, r.img.levels, r.img.levels_last, r.b, r.g, feats, background, out_color,
-                            foveaStep, s); }
+          launch_amr_render(W, H, r.img, r.img.levels, r.img.levels_last, r.b, r.ab, r.g, feats, background,
+                            out_color, foveaStep, s); }
         stage_check(dbg, s, "amr_render");
         if (interpolate_image) {
             launch_amr_interpolate(W, H, r.img, r.img.levels, r.img.levels_last, out_color, foveaStep,
@@ -777,6 +789,10 @@ int gs_set_tuning(const char* key, int value) {
         set_amr_variant(value);
         return 0;
     }
+    if (std::strcmp(key, "amr_batch") == 0) {
+        set_amr_batch(value);
+        return 0;
+    }
     if (std::strcmp(key, "xcd_map") == 0) {
         set_xcd_map(value);
         return 0;
@@ -837,15 +853,23 @@ size_t gs_image_bytes(int width, int height, int tile) {
 
 size_t gs_binning_bytes(int K) { return carve_binning(nullptr, (size_t)K, nullptr); }
 
-int gs_binning_count_of_bytes(size_t nbytes) {
+namespace {
+int binning_count_of_bytes(size_t nbytes, bool amr) {
     long lo = 0, hi = (long)std::min<size_t>(nbytes / 8 + 1, (size_t)INT32_MAX);
     while (lo < hi) {  // smallest K with bytes(K) >= nbytes (bytes() is strictly increasing)
         const long mid = (lo + hi) / 2;
-        if (carve_binning(nullptr, (size_t)mid, nullptr) < nbytes) lo = mid + 1;
+        if (carve_binning(nullptr, (size_t)mid, nullptr, nullptr, amr) < nbytes) lo = mid + 1;
         else hi = mid;
     }
-    return carve_binning(nullptr, (size_t)lo, nullptr) == nbytes ? (int)lo : -1;
+    return carve_binning(nullptr, (size_t)lo, nullptr, nullptr, amr) == nbytes ? (int)lo : -1;
 }
+}  // namespace
+
+int gs_binning_count_of_bytes(size_t nbytes) { return binning_count_of_bytes(nbytes, false); }
+
+size_t gs_amr_binning_bytes(int K) { return carve_binning(nullptr, (size_t)K, nullptr, nullptr, true); }
+
+int gs_amr_binning_count_of_bytes(size_t nbytes) { return binning_count_of_bytes(nbytes, true); }
 
 size_t gs_knn_workspace_bytes(int P) { return knn_workspace_bytes(P); }
 

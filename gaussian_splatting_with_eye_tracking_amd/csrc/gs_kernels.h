@@ -69,6 +69,7 @@ void set_xcd_map(int v);
 extern int g_xcd_map;
 void set_cull(int v);
 void set_amr_variant(int v);
+void set_amr_batch(int v);
 void set_ritnet_mfma(int v);
 void set_ritnet_small_wgs(int v);
 void set_bwd_gauss_split(int v);  // 1: SH backward as its own kernel  // AMR blend geometry (as fwd_variant)  // row-group cull in the blend kernels (default on)
@@ -162,11 +163,14 @@ void launch_amr_levels(int T, const ImageView& img, hipStream_t s);
 // The 16x16 quadrant sub-lists of the sorted 32-px tile lists (render.hip).
 void launch_amr_quad_lists(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g, int K,
                            hipStream_t s);
+// The 8x8-region sub-lists and per-instance blend records (variant 4).
+void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningView& b, const AmrBinningView& ab,
+                             const GeomView& g, const float* features, int K, hipStream_t s);
 extern int g_amr_variant;
 void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s);
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
-                       const BinningView& b, const GeomView& g, const float* features, const float* bg,
-                       float* out_color, int foveaStep, hipStream_t s);
+                       const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,
+                       const float* bg, float* out_color, int foveaStep, hipStream_t s);
 void launch_amr_interpolate(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                             float* out_color, int foveaStep, const float* out_color_precomp, hipStream_t s);
 

@@ -20,6 +20,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <hip/hip_runtime.h>  // float4
+
 namespace gsamd {
 
 constexpr size_t kAlign = 256;
@@ -91,6 +93,7 @@ struct ImageView {
     uint32_t* large_tiles;     // [T] list of tiles needing the large sort
     uint32_t* tile_order;      // [T] tiles by descending blend work (launch order)
     uint32_t* quad_count;      // [T][4] AMR: entries of each 16x16 quadrant's sub-list
+    uint32_t* region_count;    // [T][16] AMR: entries of each 8x8 region's sub-list
 };
 
 inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
@@ -109,6 +112,7 @@ inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
     g.large_tiles = carve<uint32_t>(base, off, T);
     g.tile_order = carve<uint32_t>(base, off, T);
     g.quad_count = carve<uint32_t>(base, off, 4 * T);
+    g.region_count = carve<uint32_t>(base, off, 16 * T);
     if (v) *v = g;
     return align_up(off);
 }
@@ -127,16 +131,44 @@ struct BinningView {
 // ascending (render.hip amr_quad_lists_kernel).
 inline uint32_t* quad_lists(const BinningView& b) { return reinterpret_cast<uint32_t*>(b.pair_keys); }
 
-inline size_t carve_binning(char* base, size_t K, BinningView* v) {
+// AMR binning extension (32-px tiles only; appended after the base arrays,
+// whose offsets it leaves unchanged).  Filled once per frame by foveaStep 0
+// (render.hip amr_region_lists_kernel), read by every progressive step:
+//   * the blend record of every instance in sorted tile-list order, so a
+//     step's loads are tile-local and coalesced instead of three random
+//     per-Gaussian gathers behind a point_list gather: rec_a = (mean x,
+//     mean y, r, g), rec_b = the log2(e)-scaled conic and opacity
+//     (gs_blend.cuh splat_coef), rec_c = b;
+//   * region lists: tile t with range [beg, beg + n) keeps, for each of its
+//     16 regions of 8x8 pixels (g = 4 row + col), the positions i in [0, n)
+//     of the entries that can reach the region, ascending, at
+//     region_lists + 16 beg + g n.
+struct AmrBinningView {
+    float4* rec_a;
+    float4* rec_b;
+    float* rec_c;
+    uint32_t* region_lists;
+};
+
+inline size_t carve_binning(char* base, size_t K, BinningView* v, AmrBinningView* amr = nullptr,
+                            bool with_amr = false) {
     size_t off = 0;
     BinningView g;
     g.point_list = carve<uint32_t>(base, off, K);
     g.pair_keys = carve<uint64_t>(base, off, K);
     g.scratch = carve<uint64_t>(base, off, K);
     if (v) *v = g;
+    if (amr || with_amr) {
+        AmrBinningView a;
+        a.rec_a = carve<float4>(base, off, K);
+        a.rec_b = carve<float4>(base, off, K);
+        a.rec_c = carve<float>(base, off, K);
+        a.region_lists = carve<uint32_t>(base, off, 16 * K);
+        if (amr) *amr = a;
+    }
     // Unpadded end: strictly increasing in K (>= 8 B per instance), so the
-    // caller can recover K from the buffer size (gs_binning_count_of_bytes)
-    // without a device read-back.
+    // caller can recover K from the buffer size (gs_binning_count_of_bytes,
+    // gs_amr_binning_count_of_bytes) without a device read-back.
     return off;
 }
 

@@ -13,6 +13,7 @@
 //   * no FMA contraction (file compiled with -ffp-contract=off): depth,
 //     means2D and radius are bit-identical to the oracle, which makes the
 //     tile keys bit-exact.
+#include "gs_blend.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
 
@@ -194,6 +195,23 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
     reinterpret_cast<float2*>(g.means2D)[idx] = make_float2(pix_x, pix_y);
     reinterpret_cast<float4*>(g.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     g.tiles_touched[idx] = area;
+    if (a.block == 32) {
+        // AMR: the blend record of this Gaussian as ONE 64-B row of the
+        // (forward-idle) grad_accum buffer, so foveaStep 0's region-list pass
+        // (render.hip) gathers one line per instance instead of three:
+        // (x, y, r, g), the log2(e)-scaled conic + opacity, (b, raw conic).
+        float r_, g_, b_;
+        if (kHasSH) {
+            r_ = g.rgb[3 * idx]; g_ = g.rgb[3 * idx + 1]; b_ = g.rgb[3 * idx + 2];
+        } else {
+            r_ = a.colors_precomp[3 * idx]; g_ = a.colors_precomp[3 * idx + 1]; b_ = a.colors_precomp[3 * idx + 2];
+        }
+        float4* row = reinterpret_cast<float4*>(g.grad_accum + (size_t)kGradRow * idx);
+        const float4 co = make_float4(conic_x, conic_y, conic_z, opacity);
+        row[0] = make_float4(pix_x, pix_y, r_, g_);
+        row[1] = splat_coef(co);
+        row[2] = make_float4(b_, conic_x, conic_y, conic_z);
+    }
 
     // Tile histogram with device atomics only when the tile grid is too large
     // for the LDS-privatised count_tiles kernel (binning.hip); wave-uniform.

@@ -444,14 +444,425 @@ __global__ void __launch_bounds__(64) amr_quad_render_kernel(int W, int H, int t
     }
 }
 
-int g_amr_variant = 3;  // 3: quadrant sub-lists (default); 0 = 1 x 4 px, 1 = 2 x 2, 2 = 4 x 1 full-list blocks
-void set_amr_variant(int v) { g_amr_variant = v; }
+// ------------------------------------------------- AMR 8x8 region lists ---
+// Variant 4.  The progressive steps are bound by their longest unit: a wave
+// walks its sub-list serially, one entry after the other for each of its
+// pixels, and a step ends when the heaviest unit ends (step 4 renders a tenth
+// of step 1's pixels in more than half its time).  So the unit's chain is
+// shortened twice:
+//   * finer lists: a (tile, quadrant) wave is four 16-lane groups, each the
+//     16 pixels of one 8x8 region (at the round's stride-2 offset) walking the
+//     region's own sub-list -- the entries whose alpha >= 1/255 ellipse can
+//     reach the region (splat_rect_hit, exact and conservative) keep their
+//     ORIGINAL tile-list positions, so contributor indices, n_contrib and
+//     final T are the reference's (amr/cr/forward.cu:440-495);
+//   * no pointer chase: foveaStep 0 writes each instance's blend record in
+//     tile-list order (AmrBinningView), so a batch is one coalesced position
+//     load and tile-local record loads, issued one batch ahead.
+// One 256-thread workgroup per tile builds the records and the 16 lists
+// (ordered compaction by ballots, 256 entries per round).
+constexpr int kRlThreads = 256;
+constexpr int kRlPer = 4;  // entries per thread per pass (loads issued together)
+// Region mask of one entry: the exact ellipse test (splat_rect_hit) on the
+// four 16x16 quadrants, refined to the 8x8 regions by the alpha >= 1/255
+// ellipse's bounding box (both conservative).  Bit g = 4 row + col.
+__device__ __forceinline__ uint32_t region_mask(float2 xy, float4 co, float ox, float oy) {
+    const SplatBox b = splat_box(xy, co);
+    uint32_t qm = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const float x0 = ox + 16.0f * (float)(q & 1), y0 = oy + 16.0f * (float)(q >> 1);
+        if (splat_rect_hit(b, x0, x0 + 15.0f, y0, y0 + 15.0f)) qm |= 1u << q;
+    }
+    // box columns / rows (comparisons false for NaN / inf widths -> kept)
+    uint32_t cm = 0, rm = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const float x0 = ox + 8.0f * (float)c, y0 = oy + 8.0f * (float)c;
+        if (!(xy.x + b.hx < x0 || xy.x - b.hx > x0 + 7.0f)) cm |= 1u << c;
+        if (!(xy.y + b.hy < y0 || xy.y - b.hy > y0 + 7.0f)) rm |= 1u << c;
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int g = 0; g < 16; g++) {
+        const int col = g & 3, row = g >> 2;
+        const bool in = ((cm >> col) & 1u) && ((rm >> row) & 1u) && ((qm >> (2 * (row >> 1) + (col >> 1))) & 1u);
+        m |= in ? 1u << g : 0u;
+    }
+    return m;
+}
 
-void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
-                       const BinningView& b, const GeomView& g, const float* features, const float* bg,
-                       float* out_color, int foveaStep, hipStream_t s) {
+// rows: the per-Gaussian 64-B blend rows the AMR preprocess wrote into
+// grad_accum (preprocess.hip): (x, y, r, g), splat_coef, (b, raw conic).
+__global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, const uint32_t* __restrict__ ranges,
+                                                                      const uint32_t* __restrict__ point_list,
+                                                                      const float4* __restrict__ rows,
+                                                                      float4* __restrict__ rec_a,
+                                                                      float4* __restrict__ rec_b,
+                                                                      float* __restrict__ rec_c,
+                                                                      uint32_t* __restrict__ lists,
+                                                                      uint32_t* __restrict__ region_count) {
+    constexpr int kW = kRlThreads / 64;
+    // per pass: hits of (slot e, region g, wave w), then their exclusive
+    // offsets in the pass's (e, w) order, per region
+    __shared__ uint32_t s_cnt[16][kRlPer * kW];
+    __shared__ uint32_t s_base[16];  // entries written per region by earlier passes
+    const int tile = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t beg = ranges[2 * tile];
+    const int n = (int)(ranges[2 * tile + 1] - beg);
+    const float ox = (float)((tile % tgx) * 32), oy = (float)((tile / tgx) * 32);
+    uint32_t* out = lists + 16 * (size_t)beg;
+    if (tid < 16) s_base[tid] = 0;
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int c0 = 0; c0 < n; c0 += kRlThreads * kRlPer) {
+        // slot e of thread t: entry c0 + e * 256 + t (slot-major keeps the
+        // list order = (slot, wave, lane) order)
+        uint32_t m[kRlPer];
+#pragma unroll
+        for (int e = 0; e < kRlPer; e++) {
+            const int i = c0 + e * kRlThreads + tid;
+            m[e] = 0;
+            if (i < n) {
+                const uint32_t id = point_list[beg + i];
+                const float4 ra = rows[4 * (size_t)id], rb = rows[4 * (size_t)id + 1], rc = rows[4 * (size_t)id + 2];
+                rec_a[beg + i] = ra;
+                rec_b[beg + i] = rb;
+                rec_c[beg + i] = rc.x;
+                m[e] = region_mask(make_float2(ra.x, ra.y), make_float4(rc.y, rc.z, rc.w, rb.w), ox, oy);
+            }
+#pragma unroll
+            for (int g = 0; g < 16; g++) {
+                const uint32_t c = (uint32_t)__popcll(__ballot((m[e] >> g) & 1u));
+                if (lane == 0) s_cnt[g][e * kW + wave] = c;
+            }
+        }
+        __syncthreads();
+        if (tid < 16) {  // exclusive scan of region tid's 16 counts, in list order
+            uint32_t acc = s_base[tid];
+#pragma unroll
+            for (int k = 0; k < kRlPer * kW; k++) {
+                const uint32_t c = s_cnt[tid][k];
+                s_cnt[tid][k] = acc;
+                acc += c;
+            }
+            s_base[tid] = acc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < kRlPer; e++) {
+            const int i = c0 + e * kRlThreads + tid;
+#pragma unroll
+            for (int g = 0; g < 16; g++) {
+                const uint64_t bal = __ballot((m[e] >> g) & 1u);
+                if ((m[e] >> g) & 1u)
+                    out[(size_t)g * n + s_cnt[g][e * kW + wave] + (uint32_t)__popcll(bal & below)] = (uint32_t)i;
+            }
+        }
+        __syncthreads();  // s_cnt is rewritten by the next pass
+    }
+    if (tid < 16) region_count[16 * tile + tid] = s_base[tid];
+}
+
+void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningView& b, const AmrBinningView& ab,
+                             const GeomView& g, const float* features, int K, hipStream_t s) {
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0) return;
+    if (K == 0) {  // no lists to build; the counts must still read 0
+        (void)hipMemsetAsync(img.region_count, 0, sizeof(uint32_t) * 16 * (size_t)tgx * tgy, s);  // checked by the caller's stage_check
+        return;
+    }
+    (void)features;  // in the rows (the preprocess saw colors_precomp / the SH colours)
+    hipLaunchKernelGGL(amr_region_lists_kernel, dim3(tgx * tgy), dim3(kRlThreads), 0, s, tgx, img.ranges,
+                       b.point_list, reinterpret_cast<const float4*>(g.grad_accum), ab.rec_a, ab.rec_b, ab.rec_c,
+                       ab.region_lists, img.region_count);
+}
+
+// One wave per (tile, quadrant): its four 16-lane groups are the quadrant's
+// four 8x8 regions, lane (i, j) of a group the region pixel (2i, 2j) + the
+// round's sub-lattice offset.  Waves b = 8 k + x (one XCD) take tile-order
+// positions 8 (k / 4) + x, quadrant k % 4: the four waves of a tile share one
+// XCD's L2 for its records, heaviest tiles first.  kRounds as in
+// amr_quad_render_kernel (1: the progressive steps, one round per pass; 4:
+// render_once, one pixel per lane and round).  feats_override (steps >= 1
+// given colors_precomp): colours from it through point_list instead of the
+// step-0 records.
+// kPer: entries each lane stages per batch (a group stages 16 kPer)
+template <int kRounds, int kPer>
+__global__ void __launch_bounds__(64) amr_region_render_kernel(
+    int W, int H, int tgx, int T, const uint32_t* __restrict__ order, const uint32_t* __restrict__ ranges,
+    const uint32_t* __restrict__ lists, const uint32_t* __restrict__ region_count,
+    const uint32_t* __restrict__ levels, const uint32_t* __restrict__ levels_last, const float4* __restrict__ rec_a,
+    const float4* __restrict__ rec_b, const float* __restrict__ rec_c, const uint32_t* __restrict__ point_list,
+    const float* __restrict__ feats_override, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
+    const float* __restrict__ bg, float* __restrict__ out_color, int foveaStep) {
+#pragma clang fp contract(fast)
+    constexpr int kRgBatch = 16 * kPer;
+    __shared__ float4 s_a[4][kRgBatch];
+    __shared__ float4 s_b[4][kRgBatch];
+    __shared__ float s_c[4][kRgBatch];
+    __shared__ uint32_t s_pos[4][kRgBatch];
+    const uint32_t bid = blockIdx.x, slot = bid >> 3;
+    const int p = (int)(8 * (slot >> 2) + (bid & 7));
+    if (p >= T) return;
+    const int tile = (int)order[p];
+    const int q = (int)(slot & 3);
+    const uint32_t lane = threadIdx.x, h = lane >> 4, l16 = lane & 15;
+    const uint32_t gcol = 2 * (q & 1) + (h & 1), grow = 2 * (q >> 1) + (h >> 1);
+    const uint32_t g = 4 * grow + gcol;
+    const uint32_t ax = (uint32_t)(tile % tgx) * 32 + 8 * gcol + 2 * (l16 & 3);
+    const uint32_t ay = (uint32_t)(tile / tgx) * 32 + 8 * grow + 2 * (l16 >> 2);
+    const size_t plane = (size_t)H * W;
+    // The call's image is zero wherever it renders nothing (the reference's
+    // zero-filled out_color, amr/rasterize_points.cu), so the unit writes its
+    // whole 16x16 quadrant: colours go to an LDS copy of the quadrant (zero
+    // where this call renders nothing), stored at the end as 64-B row
+    // segments (lane = row * 4 + 4-pixel chunk), so the caller needs no fill
+    // and the image stores are coalesced.
+    __shared__ float s_out[3][16][16];
+    const uint32_t qx0 = (uint32_t)(tile % tgx) * 32 + 16 * (q & 1), qy0 = (uint32_t)(tile / tgx) * 32 + 16 * (q >> 1);
+    const uint32_t orow = lane >> 2, ocol = 4 * (lane & 3);
+    auto store_quadrant = [&](bool zero) {
+        const uint32_t y = qy0 + orow, x = qx0 + ocol;
+        if (y >= (uint32_t)H) return;
+        const size_t pp = (size_t)W * y + x;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            const float4 v = zero ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                  : *reinterpret_cast<const float4*>(&s_out[ch][orow][ocol]);
+            float* dst = out_color + ch * plane + pp;
+            if ((W & 3) == 0 && x + 3 < (uint32_t)W) {
+                *reinterpret_cast<float4*>(dst) = v;
+            } else {
+                if (x < (uint32_t)W) dst[0] = v.x;
+                if (x + 1 < (uint32_t)W) dst[1] = v.y;
+                if (x + 2 < (uint32_t)W) dst[2] = v.z;
+                if (x + 3 < (uint32_t)W) dst[3] = v.w;
+            }
+        }
+    };
+    const uint32_t L_last = levels_last[tile];
+    uint32_t L = levels[tile];
+    // Block-uniform early exits (amr/cr/forward.cu:287-367).
+    if (L <= L_last) {
+        store_quadrant(true);
+        return;
+    }
+    if (L > 4) L = 4;
+    const uint32_t lo = foveaStep > 0 ? L_last : 0u;  // rounds (lo, L]
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++)
+        *reinterpret_cast<float4*>(&s_out[ch][orow][ocol]) = make_float4(0.f, 0.f, 0.f, 0.f);
+    const uint32_t beg = ranges[2 * tile];
+    const uint32_t n = ranges[2 * tile + 1] - beg;
+    const uint32_t cnt = region_count[16 * tile + g];  // uniform per group
+    // the wave's longest list (lanes 0, 16, 32, 48 hold the four counts)
+    const uint32_t cmax = max(max((uint32_t)__builtin_amdgcn_readlane((int)cnt, 0),
+                                  (uint32_t)__builtin_amdgcn_readlane((int)cnt, 16)),
+                              max((uint32_t)__builtin_amdgcn_readlane((int)cnt, 32),
+                                  (uint32_t)__builtin_amdgcn_readlane((int)cnt, 48)));
+    const uint32_t* list = lists + 16 * (size_t)beg + (size_t)g * n;
+    const float b0c = bg[0], b1c = bg[1], b2c = bg[2];
+    constexpr int kSlots = kRounds;
+    // staging: lane l16 of group h loads entries l16 + 16 u (u < kPer) of each batch
+    auto load_pos = [&](uint32_t b0, uint32_t (&pos)[kPer]) {
+#pragma unroll
+        for (int u = 0; u < kPer; u++) {
+            const uint32_t i = b0 + l16 + 16 * u;
+            pos[u] = i < cnt ? list[i] : 0xffffffffu;
+        }
+    };
+    auto load_rec = [&](const uint32_t (&pos)[kPer], float4 (&a)[kPer], float4 (&bb)[kPer], float (&c)[kPer]) {
+#pragma unroll
+        for (int u = 0; u < kPer; u++) {
+            if (pos[u] != 0xffffffffu) {
+                a[u] = rec_a[beg + pos[u]];
+                bb[u] = rec_b[beg + pos[u]];
+                c[u] = rec_c[beg + pos[u]];
+                if (feats_override) {
+                    const uint32_t id = point_list[beg + pos[u]];
+                    a[u].z = feats_override[3 * id];
+                    a[u].w = feats_override[3 * id + 1];
+                    c[u] = feats_override[3 * id + 2];
+                }
+            }
+        }
+    };
+    for (uint32_t r1 = lo + 1; r1 <= L; r1 += kRounds) {
+        float pxx[kSlots], pxy[kSlots], T_[kSlots], C[kSlots][3];
+        uint32_t last[kSlots], pid[kSlots];
+        bool done[kSlots], active[kSlots];
+#pragma unroll
+        for (int k = 0; k < kSlots; k++) {
+            const uint32_t r = kRounds == 1 ? r1 : (uint32_t)k + 1;
+            active[k] = r > lo && r <= L;  // wave-uniform
+            // round -> sub-lattice offset (amr/cr/forward.cu:313-339): 1 (0,0), 2 (1,1), 3 (1,0), 4 (0,1)
+            const uint32_t sx = (r == 2 || r == 3) ? 1u : 0u, sy = (r == 2 || r == 4) ? 1u : 0u;
+            const uint32_t x = ax + sx, y = ay + sy;
+            pxx[k] = (float)x;
+            pxy[k] = (float)y;
+            const bool in = active[k] && x < (uint32_t)W && y < (uint32_t)H;
+            pid[k] = in ? (uint32_t)W * y + x : 0u;
+            done[k] = !in;
+            T_[k] = 1.0f;
+            C[k][0] = C[k][1] = C[k][2] = 0.f;
+            last[k] = 0;
+        }
+        uint32_t pos[kPer], npos[kPer];
+        float4 ra[kPer], rb[kPer];
+        float rc[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; u++) {
+            ra[u] = rb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            rc[u] = 0.f;
+        }
+        load_pos(0, pos);
+        load_rec(pos, ra, rb, rc);
+        load_pos(kRgBatch, npos);
+        for (uint32_t b0 = 0; b0 < cmax; b0 += kRgBatch) {
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < kSlots; k++) any |= !done[k] && b0 < cnt;
+            if (__ballot(any) == 0ull) break;  // every pixel saturated or its list exhausted
+            __syncthreads();                     // single-wave workgroup: LDS fence only
+#pragma unroll
+            for (int u = 0; u < kPer; u++) {
+                s_a[h][l16 + 16 * u] = ra[u];
+                s_b[h][l16 + 16 * u] = rb[u];
+                s_c[h][l16 + 16 * u] = rc[u];
+                s_pos[h][l16 + 16 * u] = pos[u];
+            }
+            __syncthreads();
+            // the next batch's records and the one after's positions, in flight
+            // while this batch is blended
+#pragma unroll
+            for (int u = 0; u < kPer; u++) pos[u] = npos[u];
+            load_rec(pos, ra, rb, rc);
+            load_pos(b0 + 2 * kRgBatch, npos);
+            // entries of this batch: [0, m) for the group, [0, mw) for the wave
+            const int m = (int)min((uint32_t)kRgBatch, cnt > b0 ? cnt - b0 : 0u);
+            const int mw = (int)min((uint32_t)kRgBatch, cmax - b0);
+            if constexpr (kRounds == 1) {
+                // two entries per iteration: their LDS reads share one wait and
+                // their alpha chains interleave; the blend stays in list order
+                for (int j = 0; j < mw; j += 2) {
+                    const int jB = j + 1 < mw ? j + 1 : j;
+                    const bool okA = j < m, okB = j + 1 < m;
+                    const float4 aA = s_a[h][j], aB = s_a[h][jB];
+                    const float4 coA = s_b[h][j], coB = s_b[h][jB];
+                    const float cA_ = s_c[h][j], cB_ = s_c[h][jB];
+                    const uint32_t cA = s_pos[h][j] + 1, cB = s_pos[h][jB] + 1;
+                    const float pA = splat_p2(aA.x - pxx[0], aA.y - pxy[0], coA);
+                    const float pB = splat_p2(aB.x - pxx[0], aB.y - pxy[0], coB);
+                    const float alA = fminf(0.99f, coA.w * splat_exp(pA));
+                    const float alB = fminf(0.99f, coB.w * splat_exp(pB));
+                    {
+                        const float test_T = T_[0] * (1 - alA);
+                        const bool hit = okA && !done[0] && !(pA > 0.0f) && !(alA < 1.0f / 255.0f);
+                        const bool stop = hit && test_T < 0.0001f;
+                        done[0] = done[0] || stop;
+                        if (hit && !stop) {
+                            const float w = alA * T_[0];
+                            C[0][0] = __builtin_fmaf(aA.z, w, C[0][0]);
+                            C[0][1] = __builtin_fmaf(aA.w, w, C[0][1]);
+                            C[0][2] = __builtin_fmaf(cA_, w, C[0][2]);
+                            T_[0] = test_T;
+                            last[0] = cA;
+                        }
+                    }
+                    {
+                        const float test_T = T_[0] * (1 - alB);
+                        const bool hit = okB && !done[0] && !(pB > 0.0f) && !(alB < 1.0f / 255.0f);
+                        const bool stop = hit && test_T < 0.0001f;
+                        done[0] = done[0] || stop;
+                        if (hit && !stop) {
+                            const float w = alB * T_[0];
+                            C[0][0] = __builtin_fmaf(aB.z, w, C[0][0]);
+                            C[0][1] = __builtin_fmaf(aB.w, w, C[0][1]);
+                            C[0][2] = __builtin_fmaf(cB_, w, C[0][2]);
+                            T_[0] = test_T;
+                            last[0] = cB;
+                        }
+                    }
+                    if (__ballot(!done[0] && j + 2 < m) == 0ull) break;
+                }
+            } else {
+                for (int j = 0; j < mw; j++) {
+                    const float4 a = s_a[h][j];
+                    const float4 co = s_b[h][j];
+                    const uint32_t contributor = s_pos[h][j] + 1;
+                    const bool okj = j < m;
+                    bool alive = false;
+#pragma unroll
+                    for (int k = 0; k < kSlots; k++) {
+                        if (!active[k]) continue;  // wave-uniform
+                        const float pw = splat_p2(a.x - pxx[k], a.y - pxy[k], co);
+                        const float alpha = fminf(0.99f, co.w * splat_exp(pw));
+                        const float test_T = T_[k] * (1 - alpha);
+                        const bool hit = okj && !done[k] && !(pw > 0.0f) && !(alpha < 1.0f / 255.0f);
+                        const bool stop = hit && test_T < 0.0001f;
+                        done[k] = done[k] || stop;
+                        alive |= !done[k] && j + 1 < m;
+                        if (!hit || stop) continue;
+                        const float w = alpha * T_[k];
+                        C[k][0] = __builtin_fmaf(a.z, w, C[k][0]);
+                        C[k][1] = __builtin_fmaf(a.w, w, C[k][1]);
+                        C[k][2] = __builtin_fmaf(s_c[h][j], w, C[k][2]);
+                        T_[k] = test_T;
+                        last[k] = contributor;
+                    }
+                    if (__ballot(alive) == 0ull) break;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kSlots; k++) {
+            const uint32_t x = (uint32_t)pxx[k], y = (uint32_t)pxy[k];
+            if (!active[k] || x >= (uint32_t)W || y >= (uint32_t)H) continue;
+            const uint32_t pp = pid[k];
+            final_T[pp] = T_[k];
+            n_contrib[pp] = last[k];
+            const uint32_t lx = x - qx0, ly = y - qy0;
+            s_out[0][ly][lx] = C[k][0] + T_[k] * b0c;
+            s_out[1][ly][lx] = C[k][1] + T_[k] * b1c;
+            s_out[2][ly][lx] = C[k][2] + T_[k] * b2c;
+        }
+    }
+    __syncthreads();  // single-wave workgroup: LDS fence only
+    store_quadrant(false);
+}
+
+int g_amr_variant = 4;  // 4: 8x8 region sub-lists + records (default); 3: quadrant sub-lists; 0 = 1 x 4 px, 1 = 2 x 2, 2 = 4 x 1 full-list blocks
+void set_amr_variant(int v) { g_amr_variant = v; }
+int g_amr_batch = 1;  // variant 4: entries staged per lane and batch (1 or 2)
+void set_amr_batch(int v) { g_amr_batch = v == 2 ? 2 : 1; }
+
+void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
+                       const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,
+                       const float* bg, float* out_color, int foveaStep, hipStream_t s) {
+    const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
+    if (tgx == 0 || tgy == 0) return;
+    if (g_amr_variant == 4) {
+        // lists, records and tile order from foveaStep 0 (or this render_once
+        // call); colours from the records unless this step brought its own
+        const int T = tgx * tgy;
+        const float* ov = (foveaStep > 0 && features != g.rgb) ? features : nullptr;
+        const int nb = 32 * ((T + 7) / 8);  // b = 8 (4 (p / 8) + q) + p % 8
+#define GS_AMR_REGION(R, PER)                                                                                     \
+        hipLaunchKernelGGL((amr_region_render_kernel<R, PER>), dim3(nb), dim3(64), 0, s, W, H, tgx, T,            \
+                           img.tile_order,                                                                          \
+                           img.ranges, ab.region_lists, img.region_count, levels, levels_last, ab.rec_a, ab.rec_b, \
+                           ab.rec_c, b.point_list, ov, img.accum_alpha, img.n_contrib, bg, out_color, foveaStep)
+        if (foveaStep > 0) {
+            if (g_amr_batch == 2) GS_AMR_REGION(1, 2);
+            else GS_AMR_REGION(1, 1);
+        } else {
+            if (g_amr_batch == 2) GS_AMR_REGION(4, 2);
+            else GS_AMR_REGION(4, 1);
+        }
+#undef GS_AMR_REGION
+        return;
+    }
     if (g_amr_variant == 3) {
         // the tile order and quadrant lists were built by foveaStep 0 (or this
         // render_once call) right after the binning (gs_api.cpp)

@@ -103,7 +103,8 @@ std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> rasterize_impl(
     const at::OptionalDeviceGuard guard(device_of(means3D_in));
     require_device(means3D_in, "means3D");
     auto float_opts = means3D_in.options().dtype(torch::kFloat32);
-    Tensor out_color = (amr || P == 0) ? torch::zeros({3, H, W}, float_opts) : torch::empty({3, H, W}, float_opts);
+    // both forwards write every pixel (the AMR one zeros where it renders nothing)
+    Tensor out_color = P == 0 ? torch::zeros({3, H, W}, float_opts) : torch::empty({3, H, W}, float_opts);
     Tensor radii = (amr && foveaStep >= 1) || P == 0 ? torch::zeros({P}, means3D_in.options().dtype(torch::kInt32))
                                                     : torch::empty({P}, means3D_in.options().dtype(torch::kInt32));
     auto byte_opts = means3D_in.options().dtype(torch::kByte);
@@ -135,7 +136,7 @@ std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> rasterize_impl(
             for (const Tensor* bt : {&geom_pre, &bin_pre, &img_pre}) require_like(*bt, means3D, "precomp buffer", -1, torch::kByte);
             Tensor g = geom_pre, b = bin_pre, im = img_pre;
             // K of the precomputed buffers from the binning buffer's size (no sync)
-            const int hint = foveaStep >= 1 ? gs_binning_count_of_bytes((size_t)b.numel()) : -1;
+            const int hint = foveaStep >= 1 ? gs_amr_binning_count_of_bytes((size_t)b.numel()) : -1;
             rendered = gs_amr_rasterizer_forward_ex(
                 buf_of(geomBuffer), buf_of(binningBuffer), buf_of(imgBuffer), P, degree, M, fptr(bg), W, H,
                 fptr(means3D), fptr(sh), fptr(colors), fptr(opacity), fptr(scales), scale_modifier, fptr(rotations),
@@ -586,6 +587,10 @@ py::dict ParseBuffers(const Tensor& geomBuffer, const Tensor& binningBuffer, con
     d["levels_last"] = view(im.levels_last, {T}, i32);
     d["levels_current"] = view(im.levels_current, {T}, i32);
     d["pv"] = view(im.pv, {4}, i32);
+    if (tile == 32) {
+        d["tile_order"] = view(im.tile_order, {T}, i32);
+        d["region_count"] = view(im.region_count, {T, 16}, i32);
+    }
     if (K > 0) {
         d["point_list"] = view(b.point_list, {K}, i32);
         Tensor keys = torch::empty({K}, o.dtype(torch::kInt64));

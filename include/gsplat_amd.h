@@ -157,6 +157,8 @@ int gs_rasterizer_mark_visible(int P, const float* means3D, const float* viewmat
  * 1..4: progressive step on the *_precomp buffers (image buffer mutated in
  * place), the geometry/binning/image callbacks are not called;
  * <0: one-shot render of every level (render_once).
+ * Every pixel of out_color is written (0 where the call renders nothing, as
+ * the reference's zero-filled output), so it need not be initialised.
  * Reads K back to the host once (both branches, as the reference does). */
 int gs_amr_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image, int P, int D, int M,
                               const float* background, int width, int height, const float* means3D,
@@ -170,7 +172,7 @@ int gs_amr_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer i
 
 /* gs_amr_rasterizer_forward with num_rendered_hint: for foveaStep >= 1, a
  * hint >= 0 is taken as K (the caller recovered it from the binning buffer's
- * size with gs_binning_count_of_bytes) and the device read-back of K is
+ * size with gs_amr_binning_count_of_bytes) and the device read-back of K is
  * skipped, so the progressive steps run without host synchronisation; -1
  * reads it back like the reference. */
 int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffer image, int P, int D, int M,
@@ -293,6 +295,7 @@ typedef struct {
     uint32_t* large_tiles;
     uint32_t* tile_order; /* [T] blend launch order (descending work) */
     uint32_t* quad_count; /* [T][4] AMR quadrant sub-list lengths */
+    uint32_t* region_count; /* [T][16] AMR 8x8-region sub-list lengths */
 } gs_image_view;
 
 typedef struct {
@@ -306,6 +309,11 @@ size_t gs_image_bytes(int width, int height, int tile);
 size_t gs_binning_bytes(int K);
 /* Inverse of gs_binning_bytes (exact; -1 if nbytes is not a binning size). */
 int gs_binning_count_of_bytes(size_t nbytes);
+/* The AMR (32-px tile) binning buffer: the base arrays at the same offsets,
+ * followed by the per-instance blend records and the 8x8-region sub-lists
+ * foveaStep 0 builds for the progressive steps (csrc/gs_layout.h). */
+size_t gs_amr_binning_bytes(int K);
+int gs_amr_binning_count_of_bytes(size_t nbytes);
 size_t gs_knn_workspace_bytes(int P);
 int gs_geom_view_of(char* base, int P, gs_geom_view* out);
 int gs_image_view_of(char* base, int width, int height, int tile, gs_image_view* out);

@@ -63,22 +63,29 @@ def test_host_layout_helpers():
     assert v.grad_accum + 1000 * 64 - base <= g1
 
 
-def test_binning_size_inverse_is_exact():
-    """gs_binning_count_of_bytes inverts gs_binning_bytes (the AMR steps >= 1
-    recover K from the binning buffer's size instead of a device read-back)."""
+@pytest.mark.parametrize("prefix", ["gs_binning", "gs_amr_binning"])
+def test_binning_size_inverse_is_exact(prefix):
+    """gs_(amr_)binning_count_of_bytes inverts gs_(amr_)binning_bytes (the AMR
+    steps >= 1 recover K from the binning buffer's size instead of a device
+    read-back); the AMR layout is larger and keeps the base arrays' offsets."""
     lib = ctypes.CDLL(LIB)
+    nbytes = getattr(lib, prefix + "_bytes")
+    count = getattr(lib, prefix + "_count_of_bytes")
+    nbytes.restype = ctypes.c_size_t
+    nbytes.argtypes = [ctypes.c_int]
+    count.restype = ctypes.c_int
+    count.argtypes = [ctypes.c_size_t]
     lib.gs_binning_bytes.restype = ctypes.c_size_t
     lib.gs_binning_bytes.argtypes = [ctypes.c_int]
-    lib.gs_binning_count_of_bytes.restype = ctypes.c_int
-    lib.gs_binning_count_of_bytes.argtypes = [ctypes.c_size_t]
     ks = list(range(0, 700)) + [4095, 4096, 4097, 123457, 2205067, 4437743, 22303484]
     prev = -1
     for k in ks:
-        b = lib.gs_binning_bytes(k)
+        b = nbytes(k)
         assert b > prev or k == 0
+        assert b >= lib.gs_binning_bytes(k)
         prev = b
-        assert lib.gs_binning_count_of_bytes(b) == k, k
-    assert lib.gs_binning_count_of_bytes(lib.gs_binning_bytes(1000) + 1) == -1
+        assert count(b) == k, k
+    assert count(nbytes(1000) + 1) == -1
 
 
 def test_torch_extension_surface():

@@ -323,14 +323,28 @@ def _amr_gpu_steps(sc, cam, interpolate_last=False, bg=(0.0, 0.0, 0.0), after_st
     return acc, radii, steps, (gb, bb, ib)
 
 
+@pytest.mark.parametrize("amr_variant,amr_batch", [(4, 1), (4, 2), (3, 1), (2, 1)])
 @pytest.mark.parametrize("name,P,W,H,seed", [("amr_10k_256", 10000, 256, 256, 0), ("amr_ragged", 4000, 200, 120, 3),
                                              # 66 x 33 = 2178 tiles > 2048: the radix-select percentile path
-                                             ("amr_big_grid", 3000, 2112, 1056, 8)])
-def test_amr_foveated_steps(name, P, W, H, seed):
+                                             ("amr_big_grid", 3000, 2112, 1056, 8),
+                                             # dense: long sub-lists (several 32-entry batches per region)
+                                             ("amr_dense", 60000, 160, 96, 4)])
+def test_amr_foveated_steps(name, P, W, H, seed, amr_variant, amr_batch):
+    """Every AMR blend variant (4: 8x8-region sub-lists + records, the
+    default; 3: 16x16 quadrant sub-lists; 2: full 32-px lists) against the
+    oracle: per-step images, and per pixel n_contrib / final T of the last
+    step that rendered it (the contributor indices of the sub-lists are the
+    positions in the tile list)."""
     import oracle as O
     import gaussian_splatting_with_eye_tracking_amd._C as C
     sc, cam = G.scene_and_camera(P, W, H, seed)
-    acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.1, 0.1))
+    C.set_tuning("amr_variant", amr_variant)
+    C.set_tuning("amr_batch", amr_batch)
+    try:
+        acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.1, 0.1))
+    finally:
+        C.set_tuning("amr_variant", 4)
+        C.set_tuning("amr_batch", 1)
     s = O.settings_from_camera(cam, bg=(0.1, 0.1, 0.1))
     kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
     racc, rradii, st, rsteps = O.amr_render_foveated(s, kw)
@@ -347,6 +361,14 @@ def test_amr_foveated_steps(name, P, W, H, seed):
     for k in range(5):
         assert G.image_l1(steps[k].cpu().numpy(), rsteps[k]) < G.IMAGE_L1_TOL, k
     assert G.image_l1(acc.cpu().numpy(), racc) < G.IMAGE_L1_TOL
+    # pixels some step rendered (round <= level); the others are never written
+    rendered = (O.amr_pixel_rounds(W, H) <= O.amr_tile_levels_per_pixel(st.levels, W, H)).reshape(-1)
+    nc = d["n_contrib"].cpu().numpy().astype(np.uint32)[rendered]
+    rnc = st.n_contrib[rendered]
+    assert np.mean(nc != rnc) < 1e-3  # exp is hardware v_exp_f32 vs libm expf
+    same = nc == rnc
+    np.testing.assert_allclose(d["accum_alpha"].cpu().numpy()[rendered][same], st.final_T[rendered][same],
+                               rtol=1e-5, atol=1e-7)
 
 
 def test_amr_steps_with_nothing_in_front():
@@ -366,15 +388,21 @@ def test_amr_steps_with_nothing_in_front():
     np.testing.assert_allclose(acc.cpu().numpy(), racc, atol=1e-6)
 
 
-def test_amr_render_once_interpolated():
+@pytest.mark.parametrize("amr_variant", [4, 3])
+def test_amr_render_once_interpolated(amr_variant):
     import oracle as O
+    import gaussian_splatting_with_eye_tracking_amd._C as C
     from diff_gaussian_rasterization_amr import GaussianRasterizer
     sc, cam = G.scene_and_camera(8000, 224, 160, 5)
     s = G.torch_settings(cam, amr=True)
     t = G.scene_tensors(sc)
-    color, radii, gb, bb, ib = GaussianRasterizer(s)(
-        means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"], shs=t["shs"],
-        scales=t["scales"], rotations=t["rotations"], foveaStep=-2, interpolate_image=True)
+    C.set_tuning("amr_variant", amr_variant)
+    try:
+        color, radii, gb, bb, ib = GaussianRasterizer(s)(
+            means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"], shs=t["shs"],
+            scales=t["scales"], rotations=t["rotations"], foveaStep=-2, interpolate_image=True)
+    finally:
+        C.set_tuning("amr_variant", 4)
     os_ = O.settings_from_camera(cam)
     rcol, rrad, st = O.amr_render_once(os_, dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs,
                                                   scales=sc.scales, rotations=sc.rotations))

@@ -18,6 +18,7 @@ run() {  # name limit cmd...
   if fault "$rc"; then echo "[gpu_session] stopping after fault-type exit $rc in $name"; exit "$rc"; fi
   return 0
 }
+cfg_of() { case "$1" in *2) echo cfg2_1080p_1M;; *3) echo cfg3_amr_1080p_1M;; *4) echo cfg4_bicycle_6M;; esac; }
 for step in "$@"; do
   case "$step" in
     tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
@@ -35,8 +36,6 @@ for step in "$@"; do
     benchnp) run bench_np 400 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-profile &&
              run bench_p 400 python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
     benchq) run bench 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
-    prof4) run rocprof4 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof4 -o run --output-format csv -- python3 bench.py --config cfg4_bicycle_6M --steps 5 --warmup 2 --no-cpu-baseline --no-profile ;;
-    prof3) run rocprof3 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof3 -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 10 --warmup 3 --no-profile ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile ;;
     pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
     pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
@@ -52,7 +51,8 @@ for step in "$@"; do
     ab_pair) run ab_pair 400 python tools/ab_tuning.py --key bwd_variant --values 0 4 --stage render_bwd --backward ;;
     pmc_ql) run pmc_ql 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS --kernel-trace -d gpurun_out/pmc_ql -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 3 --warmup 1 --no-profile ;;
     ab_flush) run ab_flush 400 python tools/ab_tuning.py --key bwd_flush --values 0 1 2 --stage render_bwd --backward ;;
-    ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 2 3 --stage amr_render --amr ;;
+    ab_amrb) run ab_amrb 400 python tools/ab_tuning.py --key amr_batch --values 1 2 1 2 --stage amr_render --amr ;;
+    ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 3 4 3 4 --stage amr_render --amr ;;
     ab_split) run ab_split2 400 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward &&
               run ab_split4 600 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
     pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_sq -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
@@ -66,6 +66,13 @@ for step in "$@"; do
     gputrain) run pytest_gpu_train 600 python -m pytest tests/test_gpu_training.py tests/test_loss.py -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     train) run bench_train 600 python tools/bench_train.py ;;
     proftrain) run rocprof_train 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python3 tools/bench_train.py --reps 10 ;;
+    prof2|prof3|prof4)
+      c=$(cfg_of "$step"); run "rocprof_$c" 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_$c" -o run --output-format csv -- python3 bench.py --config "$c" --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
+    pmc2|pmc3|pmc4)  # one counter per pass (separate runs), MI355X_MICROARCH.md HBM recipe
+      c=$(cfg_of "$step")
+      run "pmc_${c}_fetch" 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "gpurun_out/pmc_${c}_fetch" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext &&
+      run "pmc_${c}_write" 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "gpurun_out/pmc_${c}_write" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext &&
+      run "pmc_${c}_valu" 300 rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace -d "gpurun_out/pmc_${c}_valu" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
