@@ -522,6 +522,26 @@ __global__ void __launch_bounds__(kSortThreads) sort_tiles_small_kernel(int lo, 
     }
 }
 
+// Tiles with lo < n <= hi as ONE E = 4 register network over kThreads / 64
+// waves (n <= 4 kThreads): the fully unrolled E <= 4 networks move partners
+// with DPP / ds_swizzle / permlane swaps instead of the ds_bpermute of the
+// E = 8 / 16 networks, at the price of log2(kThreads / 64) more LDS stages
+// per merge.  n in (1024, 2048] -> 512 threads, (2048, 4096] -> 1024.
+int g_sort_wide = 1;
+void set_sort_wide(int v) { g_sort_wide = v; }
+
+template <int kThreads>
+__global__ void __launch_bounds__(kThreads) sort_tiles_wide_kernel(int lo, int hi, const uint32_t* __restrict__ ranges,
+                                                                   const uint64_t* __restrict__ pair_keys,
+                                                                   uint32_t* __restrict__ point_list) {
+    __shared__ uint64_t lds[4 * kThreads];
+    const int tile = blockIdx.x;
+    const uint32_t beg = ranges[2 * tile], end = ranges[2 * tile + 1];
+    const int n = (int)(end - beg);
+    if (n <= lo || n > hi) return;
+    sort_tile_regs<4, kThreads / 64>(pair_keys + beg, n, point_list + beg, lds);
+}
+
 // Merge-path split: number of elements taken from A for the first `diag`
 // outputs of merge(A[0..na), B[0..nb)); keys are unique.
 __device__ __forceinline__ int merge_path(const uint64_t* A, int na, const uint64_t* B, int nb, int diag) {
@@ -591,9 +611,19 @@ void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int ma
     // only if such a tile exists: the forward read back the maximum count)
     hipLaunchKernelGGL(sort_tiles_small_kernel<4>, dim3(T), dim3(kSortThreads), 0, s, 0, 1024, img.ranges,
                        b.pair_keys, b.point_list);
-    if (max_count_host > 1024)
+    // (1024, 2048]: the E = 4 network over 8 waves (AMR tiles: 0.078 -> 0.073 ms
+    // at config 3); (2048, 4096] stays on E = 16 over 4 waves (the 16-wave E = 4
+    // network measured 0.453 -> 0.467 ms at config 4; profiles/r02f_ab_sort*)
+    if (max_count_host > 1024 && g_sort_wide) {
+        hipLaunchKernelGGL(sort_tiles_wide_kernel<512>, dim3(T), dim3(512), 0, s, 1024, 2048, img.ranges,
+                           b.pair_keys, b.point_list);
+        if (max_count_host > 2048)
+            hipLaunchKernelGGL(sort_tiles_small_kernel<16>, dim3(T), dim3(kSortThreads), 0, s, 2048, kSmallCap,
+                               img.ranges, b.pair_keys, b.point_list);
+    } else if (max_count_host > 1024) {
         hipLaunchKernelGGL(sort_tiles_small_kernel<16>, dim3(T), dim3(kSortThreads), 0, s, 1024, kSmallCap,
                            img.ranges, b.pair_keys, b.point_list);
+    }
     if (num_large_host > 0)
         hipLaunchKernelGGL(sort_tiles_large_kernel, dim3(num_large_host), dim3(kLargeThreads), 0, s,
                            img.large_tiles, img.ranges, b.pair_keys, b.scratch, b.point_list);

@@ -621,11 +621,9 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
         ForwardIn in{P, D, M, background, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
                      viewmatrix, projmatrix, cam_pos, width, height, scale_modifier, tan_fovx, tan_fovy, prefiltered};
         Binned r = preprocess_and_bin(in, geometry, binning, image, radii, tile, dbg, s);
-        // the geometry buffer keeps its own copy of the radii: the progressive
-        // steps return zero radii (as the reference), and the AMR backward of a
-        // step reads the step-0 radii from here
-        if (radii && radii != r.g.radii)
-            GS_HIP(hipMemcpyAsync(r.g.radii, radii, sizeof(int) * (size_t)P, hipMemcpyDeviceToDevice, s));
+        // (the geometry buffer's own copy of the radii -- the progressive steps
+        // return zero radii as the reference does, and the AMR backward of a
+        // step reads the step-0 radii from there -- is written by the preprocess)
         { StageTimer _t(kAmrLevels, s); launch_amr_levels(r.T, r.img, s); }
         stage_check(dbg, s, "amr_levels");
         const float* feats = colors_precomp ? colors_precomp : r.g.rgb;
@@ -787,6 +785,14 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "amr_variant") == 0) {
         set_amr_variant(value);
+        return 0;
+    }
+    if (std::strcmp(key, "amr_scramble") == 0) {
+        set_amr_scramble(value);
+        return 0;
+    }
+    if (std::strcmp(key, "sort_wide") == 0) {
+        set_sort_wide(value);
         return 0;
     }
     if (std::strcmp(key, "amr_batch") == 0) {

@@ -70,6 +70,8 @@ extern int g_xcd_map;
 void set_cull(int v);
 void set_amr_variant(int v);
 void set_amr_batch(int v);
+void set_sort_wide(int v);
+void set_amr_scramble(int v);
 void set_ritnet_mfma(int v);
 void set_ritnet_small_wgs(int v);
 void set_bwd_gauss_split(int v);  // 1: SH backward as its own kernel  // AMR blend geometry (as fwd_variant)  // row-group cull in the blend kernels (default on)

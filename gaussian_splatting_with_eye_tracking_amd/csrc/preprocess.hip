@@ -94,7 +94,11 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
                                                          uint32_t* __restrict__ tile_count) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= a.P) return;
+    // AMR: the geometry buffer keeps its own copy of the radii (the progressive
+    // steps return zero radii, their backward reads these); base: the caller's
+    const bool radii_copy = a.block == 32 && radii != g.radii;
     radii[idx] = 0;
+    if (radii_copy) g.radii[idx] = 0;
     g.tiles_touched[idx] = 0;
 
     // Every global load of this Gaussian is issued up front (one memory round
@@ -192,6 +196,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
     }
     g.depths[idx] = p_view.z;
     radii[idx] = iradius;
+    if (radii_copy) g.radii[idx] = iradius;
     reinterpret_cast<float2*>(g.means2D)[idx] = make_float2(pix_x, pix_y);
     reinterpret_cast<float4*>(g.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     g.tiles_touched[idx] = area;

@@ -595,7 +595,7 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     const uint32_t* __restrict__ levels, const uint32_t* __restrict__ levels_last, const float4* __restrict__ rec_a,
     const float4* __restrict__ rec_b, const float* __restrict__ rec_c, const uint32_t* __restrict__ point_list,
     const float* __restrict__ feats_override, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-    const float* __restrict__ bg, float* __restrict__ out_color, int foveaStep) {
+    const float* __restrict__ bg, float* __restrict__ out_color, int foveaStep, int scramble) {
 #pragma clang fp contract(fast)
     constexpr int kRgBatch = 16 * kPer;
     __shared__ float4 s_a[4][kRgBatch];
@@ -605,7 +605,9 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     const uint32_t bid = blockIdx.x, slot = bid >> 3;
     const int p = (int)(8 * (slot >> 2) + (bid & 7));
     if (p >= T) return;
-    const int tile = (int)order[p];
+    // scramble (A/B): a fixed permutation of the tile order (1031 is prime,
+    // so p -> 1031 p mod T is one whenever T is not a multiple of 1031)
+    const int tile = (int)order[scramble && T % 1031 != 0 ? (int)((1031ull * (uint32_t)p) % (uint32_t)T) : p];
     const int q = (int)(slot & 3);
     const uint32_t lane = threadIdx.x, h = lane >> 4, l16 = lane & 15;
     const uint32_t gcol = 2 * (q & 1) + (h & 1), grow = 2 * (q >> 1) + (h >> 1);
@@ -834,6 +836,8 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
 
 int g_amr_variant = 4;  // 4: 8x8 region sub-lists + records (default); 3: quadrant sub-lists; 0 = 1 x 4 px, 1 = 2 x 2, 2 = 4 x 1 full-list blocks
 void set_amr_variant(int v) { g_amr_variant = v; }
+int g_amr_scramble = 0;  // variant 4: 1 = units in a scrambled (not heaviest-first) tile order
+void set_amr_scramble(int v) { g_amr_scramble = v; }
 int g_amr_batch = 1;  // variant 4: entries staged per lane and batch (1 or 2)
 void set_amr_batch(int v) { g_amr_batch = v == 2 ? 2 : 1; }
 
@@ -852,7 +856,8 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
         hipLaunchKernelGGL((amr_region_render_kernel<R, PER>), dim3(nb), dim3(64), 0, s, W, H, tgx, T,            \
                            img.tile_order,                                                                          \
                            img.ranges, ab.region_lists, img.region_count, levels, levels_last, ab.rec_a, ab.rec_b, \
-                           ab.rec_c, b.point_list, ov, img.accum_alpha, img.n_contrib, bg, out_color, foveaStep)
+                           ab.rec_c, b.point_list, ov, img.accum_alpha, img.n_contrib, bg, out_color, foveaStep,   \
+                           g_amr_scramble)
         if (foveaStep > 0) {
             if (g_amr_batch == 2) GS_AMR_REGION(1, 2);
             else GS_AMR_REGION(1, 1);

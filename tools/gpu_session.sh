@@ -49,9 +49,12 @@ for step in "$@"; do
     ab_order) run ab_order_fwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render &&
               run ab_order_bwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render_bwd --backward ;;
     ab_pair) run ab_pair 400 python tools/ab_tuning.py --key bwd_variant --values 0 4 --stage render_bwd --backward ;;
-    pmc_ql) run pmc_ql 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS --kernel-trace -d gpurun_out/pmc_ql -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 3 --warmup 1 --no-profile ;;
+    pmc_ql) run pmc_ql 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS --kernel-trace -d gpurun_out/pmc_ql -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 3 --warmup 1 --no-profile --no-ext --no-cpu-baseline ;;
     ab_flush) run ab_flush 400 python tools/ab_tuning.py --key bwd_flush --values 0 1 2 --stage render_bwd --backward ;;
     ab_amrb) run ab_amrb 400 python tools/ab_tuning.py --key amr_batch --values 1 2 1 2 --stage amr_render --amr ;;
+    ab_sort) run ab_sort4 400 python tools/ab_tuning.py --key sort_wide --values 0 1 0 1 --stage sort_tiles --P 6100000 --W 1600 --H 1063 --rounds 4 &&
+             run ab_sort3 400 python tools/ab_tuning.py --key sort_wide --values 0 1 0 1 --stage sort_tiles --amr ;;
+    ab_scr) run ab_scr 400 python tools/ab_tuning.py --key amr_scramble --values 0 1 0 1 --stage amr_render --amr ;;
     ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 3 4 3 4 --stage amr_render --amr ;;
     ab_split) run ab_split2 400 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward &&
               run ab_split4 600 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
@@ -59,6 +62,9 @@ for step in "$@"; do
     pmc_sq2) run pmc_sq2 600 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_bwd_a) run pmc_bwd_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_bwd_a -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_bwd_b) run pmc_bwd_b 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_bwd_b -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
+    pmc_ql2) run pmc_ql2 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_ql2 -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 3 --warmup 1 --no-profile --no-ext --no-cpu-baseline ;;
+    pmc_fwd_a) run pmc_fwd_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_fwd_a -o run --output-format csv -- python3 tools/ab_tuning.py --key fwd_variant --values 2 --rounds 1 --iters 2 --stage render ;;
+    pmc_fwd_b) run pmc_fwd_b 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_WAVES SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_fwd_b -o run --output-format csv -- python3 tools/ab_tuning.py --key fwd_variant --values 2 --rounds 1 --iters 2 --stage render ;;
     mv) run pytest_mv 400 python -m pytest tests/test_gpu_multiview.py tests/test_gpu_dist_views.py -q -m gpu -p no:cacheprovider --timeout 300 -rf &&
         run bench_exchange 400 python tools/bench_exchange.py ;;
     eye) run pytest_eye 400 python -m pytest tests/test_gpu_eye_tracking.py -q -m gpu -p no:cacheprovider --timeout 300 -rf &&
