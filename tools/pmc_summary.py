@@ -41,6 +41,10 @@ STAGES = {
     "sort_tiles_small_kernel": "sort_tiles",
     "sort_tiles_large_kernel": "sort_tiles_large",
     "tile_scan_kernel": "tile_scan",
+    "amr_region_render_kernel<1,": "amr_render",
+    "amr_region_render_kernel<4,": "amr_render_once",
+    "amr_region_lists_kernel": "amr_lists",
+    "sort_tiles_wide_kernel": "sort_tiles",
     "amr_quad_render_kernel<1>": "amr_render",
     "amr_quad_render_kernel<4>": "amr_render_once",
     "amr_quad_lists_kernel": "amr_lists",
