@@ -171,6 +171,51 @@ def to_rasterizer_inputs(g: GaussianPly, device=None):
     return out
 
 
+def to_device_inputs(g: GaussianPly, device):
+    """The device path of `to_rasterizer_inputs`: the raw groups are uploaded
+    once (one host -> device copy each; the payload is memory-mapped) and
+    activated on the GPU by the HIP activation kernel of the training step
+    (csrc/train.hip activate_kernel: exp / sigmoid / normalize / SH concat in
+    one launch) -- the rasterizer inputs never exist on the host."""
+    import torch
+    from . import _C
+    dev = torch.device(device)
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev)  # noqa: E731
+    dc, rest, op, sc, rot = up(g.features_dc), up(g.features_rest), up(g.opacity), up(g.scaling), up(g.rotation)
+    P, M = g.P, 1 + g.features_rest.shape[1]
+    out = dict(means3D=up(g.xyz), opacities=torch.empty((P, 1), device=dev),
+               scales=torch.empty((P, 3), device=dev), rotations=torch.empty((P, 4), device=dev),
+               shs=torch.empty((P, M, 3), device=dev))
+    _C.activate(dc, rest, op, sc, rot, out["shs"], out["opacities"], out["scales"], out["rotations"])
+    return out
+
+
+def to_flat_model(g: GaussianPly, spatial_lr_scale: float, device, opt=None):
+    """load_ply (scene/gaussian_model.py:208-256) into the flat HBM training
+    state (training.FlatGaussianModel): the raw groups, uploaded as stored."""
+    import torch
+    from .training import FlatGaussianModel
+    up = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))  # noqa: E731
+    raw = {"xyz": up(g.xyz), "f_dc": up(g.features_dc), "f_rest": up(g.features_rest), "opacity": up(g.opacity),
+           "scaling": up(g.scaling), "rotation": up(g.rotation)}
+    m = FlatGaussianModel(raw, g.sh_degree, spatial_lr_scale, opt=opt, device=device)
+    m.active_sh_degree = g.sh_degree  # load_ply (:255)
+    return m
+
+
+def from_flat_model(model) -> GaussianPly:
+    """save_ply's inputs (scene/gaussian_model.py:191-206) from the flat device
+    buffer: one device -> host copy of all parameter segments."""
+    from .training import GROUPS, group_row_shape
+    host = model.params.detach().cpu().numpy()
+    v, lo = {}, 0
+    for g, end in zip(GROUPS, model.seg_end):
+        v[g] = host[lo:end].reshape((model.P,) + group_row_shape(g, model.max_sh_degree))
+        lo = end
+    return GaussianPly(xyz=v["xyz"], features_dc=v["f_dc"], features_rest=v["f_rest"], opacity=v["opacity"],
+                       scaling=v["scaling"], rotation=v["rotation"])
+
+
 def from_activated(means3D, opacities, scales, rotations, shs) -> GaussianPly:
     """Inverse activations (logit, log) -- for writing synthetic scenes."""
     op = np.clip(np.asarray(opacities, np.float64), 1e-7, 1 - 1e-7)
