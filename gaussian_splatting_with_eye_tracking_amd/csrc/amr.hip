@@ -15,6 +15,8 @@
 #include "gs_device.cuh"
 #include "gs_kernels.h"
 
+#include <algorithm>
+
 namespace gsamd {
 
 constexpr int kLvlThreads = 1024;
@@ -128,10 +130,14 @@ void launch_amr_levels(int T, const ImageView& img, hipStream_t s) {
 }
 
 // amr/cr/rasterizer_impl.cu:208-243 (setFoveaAMRLevelsKernel)
+// (+ the zero radii the progressive steps return, amr/rasterize_points.cu:
+// the caller's radii need no separate fill: threads t < P write radii[t] = 0)
 __global__ void __launch_bounds__(256) fovea_levels_kernel(int step, int T, uint32_t* __restrict__ last,
                                                            uint32_t* __restrict__ current,
-                                                           const uint32_t* __restrict__ levels) {
+                                                           const uint32_t* __restrict__ levels, int P,
+                                                           int* __restrict__ zero_radii) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (zero_radii && t < P) zero_radii[t] = 0;
     if (t >= T) return;
     const uint32_t L = levels[t];
     switch (step) {
@@ -156,10 +162,11 @@ __global__ void __launch_bounds__(256) fovea_levels_kernel(int step, int T, uint
     }
 }
 
-void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s) {
-    if (T == 0) return;
-    hipLaunchKernelGGL(fovea_levels_kernel, dim3((T + 255) / 256), dim3(256), 0, s, step, T, img.levels_last,
-                       img.levels_current, img.levels);
+void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s, int P, int* zero_radii) {
+    const int n = zero_radii ? std::max(T, P) : T;
+    if (n <= 0) return;
+    hipLaunchKernelGGL(fovea_levels_kernel, dim3((n + 255) / 256), dim3(256), 0, s, step, T, img.levels_last,
+                       img.levels_current, img.levels, P, zero_radii);
 }
 
 // Backward of render_once's interpolation (amr/cr/forward.cu:520-648, the

@@ -601,7 +601,7 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
                 throw GsError("foveaStep >= 1 needs the binning buffer returned by foveaStep 0");
             AmrBinningView ab;
             carve_binning(binning_buffer_precomp, K, &b, &ab);
-            launch_fovea_levels(foveaStep, T, img, s);
+            launch_fovea_levels(foveaStep, T, img, s, P, radii);  // + the step's zero radii
             stage_check(dbg, s, "fovea_levels");
             if (g_amr_variant != 4)  // variant 4 writes the zeros of the pixels it does not render itself
                 GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, s));

@@ -169,7 +169,7 @@ void launch_amr_quad_lists(int W, int H, const ImageView& img, const BinningView
 void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningView& b, const AmrBinningView& ab,
                              const GeomView& g, const float* features, int K, hipStream_t s);
 extern int g_amr_variant;
-void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s);
+void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s, int P = 0, int* zero_radii = nullptr);
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,
                        const float* bg, float* out_color, int foveaStep, hipStream_t s);

@@ -105,8 +105,9 @@ std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> rasterize_impl(
     auto float_opts = means3D_in.options().dtype(torch::kFloat32);
     // both forwards write every pixel (the AMR one zeros where it renders nothing)
     Tensor out_color = P == 0 ? torch::zeros({3, H, W}, float_opts) : torch::empty({3, H, W}, float_opts);
-    Tensor radii = (amr && foveaStep >= 1) || P == 0 ? torch::zeros({P}, means3D_in.options().dtype(torch::kInt32))
-                                                    : torch::empty({P}, means3D_in.options().dtype(torch::kInt32));
+    // (the AMR steps >= 1 write their zero radii in the fovea-levels launch)
+    Tensor radii = P == 0 ? torch::zeros({P}, means3D_in.options().dtype(torch::kInt32))
+                          : torch::empty({P}, means3D_in.options().dtype(torch::kInt32));
     auto byte_opts = means3D_in.options().dtype(torch::kByte);
     Tensor geomBuffer = torch::empty({0}, byte_opts);
     Tensor binningBuffer = torch::empty({0}, byte_opts);

@@ -158,7 +158,8 @@ int gs_rasterizer_mark_visible(int P, const float* means3D, const float* viewmat
  * place), the geometry/binning/image callbacks are not called;
  * <0: one-shot render of every level (render_once).
  * Every pixel of out_color is written (0 where the call renders nothing, as
- * the reference's zero-filled output), so it need not be initialised.
+ * the reference's zero-filled output), and steps 1..4 write radii = 0 (the
+ * reference's zero radii), so neither need be initialised.
  * Reads K back to the host once (both branches, as the reference does). */
 int gs_amr_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image, int P, int D, int M,
                               const float* background, int width, int height, const float* means3D,

@@ -316,7 +316,8 @@ def _amr_gpu_steps(sc, cam, interpolate_last=False, bg=(0.0, 0.0, 0.0), after_st
     acc = c0
     steps = [c0]
     for k in range(1, 5):
-        ck, _, gb, bb, ib = _RasterizeGaussians.apply(*args, k, acc, gb, bb, ib, interpolate_last and k == 4, s)
+        ck, rk, gb, bb, ib = _RasterizeGaussians.apply(*args, k, acc, gb, bb, ib, interpolate_last and k == 4, s)
+        assert rk.shape == radii.shape and not bool(rk.any())  # the steps return zero radii, as the reference
         steps.append(ck)
         acc = acc + ck
     torch.cuda.synchronize()
