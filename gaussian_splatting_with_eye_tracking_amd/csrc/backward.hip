@@ -48,9 +48,11 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
 #pragma clang fp contract(fast)
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
-    __shared__ float2 s_xy[kB];
+    // (x, y, r, g) and the scaled conic / opacity as two b128 reads, b as one
+    // b32 (LDS cycles per wave-read: b128 4, b96 8, b64 / b32 2)
+    __shared__ float4 s_a[kB];
     __shared__ float4 s_co[kB];
-    __shared__ float4 s_rgb[kB];
+    __shared__ float s_b[kB];
     // per-Gaussian sums: one wave parks its two half-wave partials (summed by
     // the flush; 4 row partials would double the LDS footprint and cost
     // workgroups per CU); several waves add into one row with LDS atomics
@@ -161,9 +163,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         if (tid < cnt) {
             const float2 xy = nxy;
             const float4 co = nco;
-            s_xy[tid] = xy;
+            s_a[tid] = make_float4(xy.x, xy.y, nrgb[0], nrgb[1]);
             s_co[tid] = splat_coef(co);
-            s_rgb[tid] = make_float4(nrgb[0], nrgb[1], nrgb[2], 0.f);
+            s_b[tid] = nrgb[2];
             gm = cull ? splat_group_mask(xy, co, (float)ox, (float)oy, (float)pstride) : 0xfu;
         }
         const int ntop = top - kB;  // the next batch: entries [ntop - ncnt, ntop)
@@ -294,7 +296,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             const int cbit = __builtin_ctzll(todo);
             todo &= todo - 1;
             const int j = 64 * c + cbit;
-            visit(cbit, s_xy[j], s_co[j], s_rgb[j]);
+            const float4 a4 = s_a[j];
+            visit(cbit, make_float2(a4.x, a4.y), s_co[j], make_float4(a4.z, a4.w, s_b[j], 0.f));
           }
         }
         __syncthreads();

@@ -257,8 +257,8 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                                                           float st, const uint32_t* __restrict__ point_list,
                                                           const float2* __restrict__ means2D,
                                                           const float* __restrict__ features,
-                                                          const float4* __restrict__ conic_opacity, float2* s_xy,
-                                                          float4* s_co, float4* s_rgb, uint64_t* s_bal,
+                                                          const float4* __restrict__ conic_opacity, float4* s_a,
+                                                          float4* s_co, float* s_b, uint64_t* s_bal,
                                                           bool cull) {
 #pragma clang fp contract(fast)
     constexpr uint32_t kB = 64 * kWaves;
@@ -289,9 +289,11 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
             const uint32_t id = point_list[range.x + b0 + tid];
             const float2 xy = means2D[id];
             const float4 co = conic_opacity[id];
-            s_xy[tid] = xy;
+            // (x, y, r, g) + the scaled conic / opacity as two b128 reads, b as
+            // one b32 (LDS cycles per wave-read: b128 4, b96 8, b64 / b32 2)
+            s_a[tid] = make_float4(xy.x, xy.y, features[3 * id], features[3 * id + 1]);
             s_co[tid] = splat_coef(co);
-            s_rgb[tid] = make_float4(features[3 * id], features[3 * id + 1], features[3 * id + 2], 0.f);
+            s_b[tid] = features[3 * id + 2];
             gm = cull ? splat_group_mask(xy, co, ox, oy, st) : 0xfu;
         }
         publish_group_masks<kWaves>(gm, s_bal);
@@ -319,9 +321,10 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                     const uint32_t bB = two ? (uint32_t)__builtin_ctzll(todo) : bA;
                     if (two) todo &= todo - 1;
                     const uint32_t jA = c * 64 + bA, jB = c * 64 + bB;
-                    const float2 xyA = s_xy[jA], xyB = s_xy[jB];
+                    const float4 sA = s_a[jA], sB = s_a[jB];
                     const float4 coA = s_co[jA], coB = s_co[jB];
-                    const float4 fA = s_rgb[jA], fB = s_rgb[jB];
+                    const float2 xyA = make_float2(sA.x, sA.y), xyB = make_float2(sB.x, sB.y);
+                    const float4 fA = make_float4(sA.z, sA.w, s_b[jA], 0.f), fB = make_float4(sB.z, sB.w, s_b[jB], 0.f);
                     const float dxA = xyA.x - px.x, dxB = xyB.x - px.x;
                     const float dyA = xyA.y - px.y[0], dyB = xyB.y - px.y[0];
                     const float pA = splat_p2(dxA, dyA, coA);
@@ -368,7 +371,8 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 const uint32_t bit = (uint32_t)__builtin_ctzll(todo);
                 todo &= todo - 1;
                 const uint32_t j = c * 64 + bit;
-                const float2 xy = s_xy[j];
+                const float4 a4 = s_a[j];
+                const float2 xy = make_float2(a4.x, a4.y);
                 const float4 co = s_co[j];
                 const float dx = xy.x - px.x;
                 const float pa = (co.x * dx) * dx, pb = co.y * dx;
@@ -388,7 +392,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                     const bool stop = hit && test_T < 0.0001f;
                     done[k] = done[k] || stop;
                     if (!hit || stop) continue;
-                    const float4 f = s_rgb[j];
+                    const float4 f = make_float4(a4.z, a4.w, s_b[j], 0.f);
                     const float w = alpha * st_.T[k];
                     st_.C[k][0] = __builtin_fmaf(f.x, w, st_.C[k][0]);
                     st_.C[k][1] = __builtin_fmaf(f.y, w, st_.C[k][1]);

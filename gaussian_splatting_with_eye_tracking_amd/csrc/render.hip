@@ -56,9 +56,9 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
                                                                  float* __restrict__ out_color, int cull,
                                                                  const uint32_t* __restrict__ order, int gx,
                                                                  int xcd) {
-    __shared__ float2 s_xy[64 * kWaves];
+    __shared__ float4 s_a[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
-    __shared__ float4 s_rgb[64 * kWaves];
+    __shared__ float s_b[64 * kWaves];
     __shared__ uint64_t s_bal[4 * kWaves];
     __shared__ uint32_t s_max;
     if (kWaves > 1 && threadIdx.x == 0) s_max = 0;
@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const BlendStateT<kPPL> st =
         blend_tile_t<kPPL, kWaves>(range, px, (float)ox, (float)oy, 1.0f, point_list,
-                                   means2D, features, conic_opacity, s_xy, s_co, s_rgb, s_bal, cull != 0);
+                                   means2D, features, conic_opacity, s_a, s_co, s_b, s_bal, cull != 0);
     write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
     uint32_t m = 0;
 #pragma unroll
@@ -144,9 +144,9 @@ __global__ void __launch_bounds__(64 * kWaves) amr_render_kernel(int W, int H, i
                                                                  const float* __restrict__ bg,
                                                                  float* __restrict__ out_color, int foveaStep,
                                                                  int cull) {
-    __shared__ float2 s_xy[64 * kWaves];
+    __shared__ float4 s_a[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
-    __shared__ float4 s_rgb[64 * kWaves];
+    __shared__ float s_b[64 * kWaves];
     __shared__ uint64_t s_bal[4 * kWaves];
     const int tile = (blockIdx.y >> 1) * tgx + (blockIdx.x >> 1);
     const uint32_t L_last = levels_last[tile];
@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(64 * kWaves) amr_render_kernel(int W, int H, i
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const BlendStateT<kPPL> st =
         blend_tile_t<kPPL, kWaves>(range, px, (float)bx, (float)by, 2.0f, point_list, means2D, features,
-                                   conic_opacity, s_xy, s_co, s_rgb, s_bal, cull != 0);
+                                   conic_opacity, s_a, s_co, s_b, s_bal, cull != 0);
     write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
 }
 
