@@ -416,16 +416,18 @@ def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange
     pg = params
 
     def step_views():
+        # each view's record is all-gathered as soon as it exists (overlapping
+        # the next view's forward + blend backward), the last in chunks that
+        # overlap the multi-view backward (data_parallel.ViewExchange)
         with torch.no_grad():
-            recs = []
-            for vw in views:
+            ex = DP.ViewExchange(P, vl, ctx.dev)
+            for j, vw in enumerate(views):
                 st = vw["st"]
                 K, _color, radii, geom, binning, img = _C.rasterize_gaussians(
                     st.bg, pg["means3D"], e0, pg["opacities"], pg["scales"], pg["rotations"], 1.0, e0,
                     st.viewmatrix, st.projmatrix, st.tanfovx, st.tanfovy, H, W, pg["shs"], 3, st.campos, False, False)
-                recs.append(DP.view_record(st, radii, geom, K, binning, img, vw["dpix"]))
-            rec = recs[0] if vl == 1 else torch.stack(recs)
-            return DP.exchange_view_records(rec, st0, pg["means3D"], pg["shs"], pg["scales"], pg["rotations"])
+                ex.add(j, DP.view_record(st, radii, geom, K, binning, img, vw["dpix"]))
+            return ex.finish(st0, pg["means3D"], pg["shs"], pg["scales"], pg["rotations"])
 
     flat = DP.FlatGrads(params)
     m2 = torch.zeros_like(params["means3D"], requires_grad=True)

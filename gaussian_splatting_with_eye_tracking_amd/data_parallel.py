@@ -156,6 +156,78 @@ def exchange_view_grads(settings, fwd, dL_dpix: torch.Tensor, means3D: torch.Ten
     return exchange_view_records(rec, settings, means3D, shs, scales, rotations, group, stats, chunks)
 
 
+class ViewExchange:
+    """The "views" exchange pipelined behind the rendering of a rank's views.
+
+    A rank with v views per step hands each view record to `add` as soon as
+    its blend backward has produced it: the record is all-gathered at once
+    (asynchronously, on the collective stream), so the transfer of view j
+    overlaps the forward + blend backward of views j + 1 ... v - 1 on the
+    compute stream.  The last view -- whose transfer has nothing left to hide
+    behind -- is gathered in `chunks` Gaussian ranges, each released to the
+    multi-view backward as it lands (exchange_view_records' overlap).  The
+    gathered records sit in rank-then-view order, so `finish` computes the
+    same sums in the same order as exchange_view_records: bit-identical
+    results.  Over one rank it just keeps the records."""
+
+    def __init__(self, P: int, views_per_rank: int, device, group=None, chunks: int = 4):
+        self.P, self.v, self.group, self.chunks = int(P), int(views_per_rank), group, max(1, int(chunks))
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.RL = view_record_numel(self.P)
+        self.buf = torch.empty((self.world, self.v, self.RL), dtype=torch.float32, device=device)
+        self.pending: List[object] = []
+        self.last: List[Tuple[int, int, object]] = []
+        self.cam_work = None
+
+    def _gather(self, src: torch.Tensor, j: int, lo: int, hi: int):
+        outs = [self.buf[r, j, lo:hi] for r in range(self.world)]
+        return dist.all_gather(outs, src.contiguous(), group=self.group, async_op=True)
+
+    def add(self, j: int, rec: torch.Tensor) -> None:
+        if self.world == 1:
+            self.buf[0, j].copy_(rec)
+            return
+        P = self.P
+        if j < self.v - 1 or P == 0:
+            self.pending.append(self._gather(rec, j, 0, self.RL))
+            return
+        self.cam_work = self._gather(rec[P * VIEW_ROW:], j, P * VIEW_ROW, self.RL)
+        step = max(1, -(-P // self.chunks))
+        for a in range(0, P, step):
+            b = min(P, a + step)
+            self.last.append((a, b, self._gather(rec[a * VIEW_ROW:b * VIEW_ROW], j, a * VIEW_ROW, b * VIEW_ROW)))
+
+    def finish(self, settings, means3D: torch.Tensor, shs: torch.Tensor, scales: torch.Tensor,
+               rotations: torch.Tensor, stats=None):
+        P = self.P
+        if P == 0:
+            for w in self.pending:
+                w.wait()
+            return _empty_param_grads(means3D, shs)
+        views = self.buf.view(self.world * self.v, self.RL)
+        if self.world == 1:
+            return multiview_param_grads(views, means3D, shs, settings.sh_degree, scales, rotations,
+                                         settings.scale_modifier, stats)
+        from . import _C
+        for w in self.pending:
+            w.wait()
+        self.cam_work.wait()
+        cams = views[:, P * VIEW_ROW:]
+        dev = means3D.device
+        M = shs.shape[1] if shs is not None and shs.numel() else 0
+        outs = (torch.empty((P, 3), device=dev), torch.empty((P, M, 3), device=dev), torch.empty((P, 1), device=dev),
+                torch.empty((P, 3), device=dev), torch.empty((P, 4), device=dev))
+        e = torch.empty(0, device=dev)
+        st = stats if stats is not None else (e, e, e)
+        for a, b, w in self.last:
+            w.wait()
+            _C.backward_gaussians_multiview_range(views[:, a * VIEW_ROW:b * VIEW_ROW], cams, a, means3D,
+                                                  shs if shs is not None else e, int(settings.sh_degree), scales,
+                                                  rotations, float(settings.scale_modifier), *outs, st[0], st[1],
+                                                  st[2])
+        return outs
+
+
 def _empty_param_grads(means3D: torch.Tensor, shs: Optional[torch.Tensor]):
     dev = means3D.device
     P = means3D.shape[0]

@@ -200,3 +200,48 @@ def test_view_record_gather_several_views_per_rank_and_empty_model():
     for r in range(world):
         np.testing.assert_array_equal(outs[r][0], exp)
         assert outs[r][1] == [(0, 3), (0, 16, 3), (0, 1), (0, 3), (0, 4)]
+
+
+def _pipelined_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import sys
+        sys.path.insert(0, ROOT)
+        from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+        P, v = 37, 3
+        n = DP.view_record_numel(P)
+        ex = DP.ViewExchange(P, v, "cpu", chunks=4)
+        for j in range(v):  # record of (rank, view j): its values say whose it is
+            ex.add(j, torch.arange(n, dtype=torch.float32) + 1000.0 * (rank * v + j))
+        for w in ex.pending:
+            w.wait()
+        ex.cam_work.wait()
+        for _a, _b, w in ex.last:
+            w.wait()
+        q.put((rank, ex.buf.view(world * v, n).numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_pipelined_view_gather_order():
+    """data_parallel.ViewExchange (per-view asynchronous gathers, the last view
+    in Gaussian chunks) lands every record in rank-then-view order, the order
+    exchange_view_records sums in, on every rank (world size 2, 3 views each)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+    n = DP.view_record_numel(37)
+    want = np.stack([np.arange(n, dtype=np.float32) + 1000.0 * k for k in range(world * 3)])
+    for r in range(world):
+        np.testing.assert_array_equal(outs[r], want)

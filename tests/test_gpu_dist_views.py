@@ -72,6 +72,20 @@ def _worker(rank, world, port, q):
                                          stats=stats, chunks=chunks)
             torch.cuda.synchronize()
             res[chunks] = [x.cpu().numpy() for x in g] + [x.cpu().numpy() for x in stats]
+        # two views per rank: the stacked exchange vs the pipelined one (each
+        # record gathered as it is produced, the last one in chunks)
+        rec2 = DP.view_record(s, fwd[2], fwd[3], fwd[0], fwd[4], fwd[5], dpix * 0.5 + 0.25)
+        stats = tuple(torch.zeros(P, device="cuda") for _ in range(3))
+        g = DP.exchange_view_records(torch.stack([rec, rec2]), s, t["means3D"], t["shs"], t["scales"],
+                                     t["rotations"], stats=stats, chunks=3)
+        res["stacked"] = [x.cpu().numpy() for x in g] + [x.cpu().numpy() for x in stats]
+        ex = DP.ViewExchange(P, 2, "cuda", chunks=3)
+        ex.add(0, rec)
+        ex.add(1, rec2)
+        stats = tuple(torch.zeros(P, device="cuda") for _ in range(3))
+        g = ex.finish(s, t["means3D"], t["shs"], t["scales"], t["rotations"], stats=stats)
+        torch.cuda.synchronize()
+        res["pipelined"] = [x.cpu().numpy() for x in g] + [x.cpu().numpy() for x in stats]
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -98,6 +112,9 @@ def test_two_rank_view_exchange():
         np.testing.assert_array_equal(outs[0][1][i], outs[1][1][i])   # replicas bit-identical
         np.testing.assert_array_equal(outs[0][3][i], outs[1][3][i])
         np.testing.assert_array_equal(outs[0][1][i], outs[0][3][i])   # chunked == one gather
+        np.testing.assert_array_equal(outs[0]["stacked"][i], outs[0]["pipelined"][i])  # pipelined == stacked
+        np.testing.assert_array_equal(outs[1]["stacked"][i], outs[1]["pipelined"][i])
+        np.testing.assert_array_equal(outs[0]["pipelined"][i], outs[1]["pipelined"][i])
     # == sum over the two views of the reference-API backward
     import gaussian_splatting_with_eye_tracking_amd._C as C
     want = None
