@@ -712,21 +712,28 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
 #pragma unroll
         for (int q = 0; q < kNG; q++) acc[q] = 0.f;
     }
-    a.dL_dcolor[3 * idx + 0] = acc[0];
-    a.dL_dcolor[3 * idx + 1] = acc[1];
-    a.dL_dcolor[3 * idx + 2] = acc[2];
+    // (dL_dcolor, dL_dconic, dL_dcov3D: NULL = not wanted -- the autograd
+    // wrapper discards them unless the matching precomputed input was given;
+    // the uniform tests cost nothing, the skipped stores 52 B per Gaussian)
+    if (a.dL_dcolor) {
+        a.dL_dcolor[3 * idx + 0] = acc[0];
+        a.dL_dcolor[3 * idx + 1] = acc[1];
+        a.dL_dcolor[3 * idx + 2] = acc[2];
+    }
     a.dL_dmean2D[3 * idx + 0] = acc[3];
     a.dL_dmean2D[3 * idx + 1] = acc[4];
     a.dL_dmean2D[3 * idx + 2] = 0.f;
-    reinterpret_cast<float4*>(a.dL_dconic)[idx] = make_float4(acc[5], acc[6], 0.f, acc[7]);
+    if (a.dL_dconic) reinterpret_cast<float4*>(a.dL_dconic)[idx] = make_float4(acc[5], acc[6], 0.f, acc[7]);
     a.dL_dopacity[idx] = acc[8];
 
     const int ncoef_out = a.M;  // dL_dsh is [P, M, 3]
     if (!vis) {
 #pragma unroll
         for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = 0.f;
+        if (a.dL_dcov3D) {
 #pragma unroll
-        for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = 0.f;
+            for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = 0.f;
+        }
         if (kHasSH && kSH16) {
 #pragma unroll
             for (int i = 0; i < 48; i++) lrow[i] = 0.f;
@@ -765,8 +772,10 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     float dcov[6];
     cov2d_backward(mx, my, mz, cov3D, acc[5], acc[6], acc[7], V, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy,
                    dmean, dcov);
+    if (a.dL_dcov3D) {
 #pragma unroll
-    for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = dcov[i];
+        for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = dcov[i];
+    }
 
     // ---- preprocessCUDA backward (backward.cu:370-387): projection part (+=)
     proj_backward(mx, my, mz, Pm, acc[3], acc[4], dmean);
@@ -868,7 +877,7 @@ void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hi
     const bool sc = a.scales != nullptr;
 #define GS_BG_LAUNCH(A, B, C) \
     hipLaunchKernelGGL((backward_gaussians_kernel<A, B, C>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped)
-    if (sh && g_bwd_gauss_split) {
+    if (sh && g_bwd_gauss_split && a.dL_dcolor) {  // (the split SH pass reads dL_dcolor back)
         if (sc) GS_BG_LAUNCH(false, true, false);
         else GS_BG_LAUNCH(false, false, false);
         if (sh16) hipLaunchKernelGGL((sh_backward_kernel<true>), grid, dim3(256), 0, s, a, g.clamped);

@@ -194,19 +194,24 @@ Grads8 BackwardImpl(int amr_step, bool interpolate, const Tensor& background, co
                     const Tensor& viewmatrix_in, const Tensor& projmatrix_in, const float tan_fovx,
                     const float tan_fovy, const Tensor& dL_dout_color_in, const Tensor& sh_in, const int degree,
                     const Tensor& campos_in, const Tensor& geomBuffer, const int R, const Tensor& binningBuffer,
-                    const Tensor& imageBuffer, const bool debug) {
+                    const Tensor& imageBuffer, const bool debug, const bool lean) {
     const int P = (int)means3D_in.size(0);
     const int H = (int)dL_dout_color_in.size(1);
     const int W = (int)dL_dout_color_in.size(2);
     const int M = sh_in.size(0) != 0 ? (int)sh_in.size(1) : 0;
     const at::OptionalDeviceGuard guard(device_of(means3D_in));
     auto opts = means3D_in.options();
+    // dL_dconic is never returned (base/rasterize_points.cu:185-196): not
+    // computed into memory at all.  lean (the autograd wrappers): the colour /
+    // covariance gradients only when their precomputed input was given --
+    // otherwise autograd drops them -- as empty tensors.
+    const bool want_colors = !lean || colors_in.numel() != 0;
+    const bool want_cov3D = !lean || cov3D_precomp_in.numel() != 0;
     Tensor dL_dmeans3D = torch::empty({P, 3}, opts);
     Tensor dL_dmeans2D = torch::empty({P, 3}, opts);
-    Tensor dL_dcolors = torch::empty({P, 3}, opts);
-    Tensor dL_dconic = torch::empty({P, 2, 2}, opts);
+    Tensor dL_dcolors = want_colors ? torch::empty({P, 3}, opts) : torch::empty({0}, opts);
     Tensor dL_dopacity = torch::empty({P, 1}, opts);
-    Tensor dL_dcov3D = torch::empty({P, 6}, opts);
+    Tensor dL_dcov3D = want_cov3D ? torch::empty({P, 6}, opts) : torch::empty({0}, opts);
     Tensor dL_dsh = torch::empty({P, M, 3}, opts);
     Tensor dL_dscales = torch::empty({P, 3}, opts);
     Tensor dL_drotations = torch::empty({P, 4}, opts);
@@ -234,8 +239,9 @@ Grads8 BackwardImpl(int amr_step, bool interpolate, const Tensor& background, co
                 fptr(rotations), fptr(cov3D_precomp), fptr(viewmatrix), fptr(projmatrix), fptr(campos), tan_fovx,
                 tan_fovy, radii.data_ptr<int>(), reinterpret_cast<char*>(geomBuffer.data_ptr()),
                 reinterpret_cast<char*>(binningBuffer.data_ptr()), reinterpret_cast<char*>(imageBuffer.data_ptr()),
-                fptr(dL_dout), fptr_mut(dL_dmeans2D), fptr_mut(dL_dconic), fptr_mut(dL_dopacity),
-                fptr_mut(dL_dcolors), fptr_mut(dL_dmeans3D), fptr_mut(dL_dcov3D), fptr_mut(dL_dsh),
+                fptr(dL_dout), fptr_mut(dL_dmeans2D), nullptr, fptr_mut(dL_dopacity),
+                want_colors ? fptr_mut(dL_dcolors) : nullptr, fptr_mut(dL_dmeans3D),
+                want_cov3D ? fptr_mut(dL_dcov3D) : nullptr, fptr_mut(dL_dsh),
                 fptr_mut(dL_dscales), fptr_mut(dL_drotations), debug, stream_of(means3D));
         } else {
             TORCH_CHECK(imageBuffer.numel() > 0, "the AMR backward needs the image buffer of the forward");
@@ -246,8 +252,8 @@ Grads8 BackwardImpl(int amr_step, bool interpolate, const Tensor& background, co
                 tan_fovy, radii.data_ptr<int>(), reinterpret_cast<char*>(geomBuffer.data_ptr()),
                 reinterpret_cast<char*>(binningBuffer.data_ptr()), reinterpret_cast<char*>(imageBuffer.data_ptr()),
                 amr_step, interpolate ? 1 : 0, fptr(dL_dout), interpolate ? fptr_mut(scratch) : nullptr,
-                fptr_mut(dL_dmeans2D), fptr_mut(dL_dconic), fptr_mut(dL_dopacity), fptr_mut(dL_dcolors),
-                fptr_mut(dL_dmeans3D), fptr_mut(dL_dcov3D), fptr_mut(dL_dsh), fptr_mut(dL_dscales),
+                fptr_mut(dL_dmeans2D), nullptr, fptr_mut(dL_dopacity), want_colors ? fptr_mut(dL_dcolors) : nullptr,
+                fptr_mut(dL_dmeans3D), want_cov3D ? fptr_mut(dL_dcov3D) : nullptr, fptr_mut(dL_dsh), fptr_mut(dL_dscales),
                 fptr_mut(dL_drotations), debug, stream_of(means3D));
         }
         check(rc, amr_step ? "amr_rasterize_gaussians_backward" : "rasterize_gaussians_backward");
@@ -266,7 +272,21 @@ Grads8 RasterizeGaussiansBackward(const Tensor& background, const Tensor& means3
                                   const Tensor& binningBuffer, const Tensor& imageBuffer, const bool debug) {
     return BackwardImpl(0, false, background, means3D, radii, colors, scales, rotations, scale_modifier,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
-                        geomBuffer, R, binningBuffer, imageBuffer, debug);
+                        geomBuffer, R, binningBuffer, imageBuffer, debug, false);
+}
+
+// The same, for the autograd wrappers: grad_colors_precomp / grad_cov3Ds_precomp
+// come back empty (not computed into memory) when those inputs were empty.
+Grads8 RasterizeGaussiansBackwardLean(const Tensor& background, const Tensor& means3D, const Tensor& radii,
+                                      const Tensor& colors, const Tensor& scales, const Tensor& rotations,
+                                      const float scale_modifier, const Tensor& cov3D_precomp,
+                                      const Tensor& viewmatrix, const Tensor& projmatrix, const float tan_fovx,
+                                      const float tan_fovy, const Tensor& dL_dout_color, const Tensor& sh,
+                                      const int degree, const Tensor& campos, const Tensor& geomBuffer, const int R,
+                                      const Tensor& binningBuffer, const Tensor& imageBuffer, const bool debug) {
+    return BackwardImpl(0, false, background, means3D, radii, colors, scales, rotations, scale_modifier,
+                        cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree, campos,
+                        geomBuffer, R, binningBuffer, imageBuffer, debug, true);
 }
 
 // The AMR backward (an extension: the reference's is unreachable): the
@@ -283,7 +303,7 @@ Grads8 AmrRasterizeGaussiansBackward(const Tensor& background, const Tensor& mea
     TORCH_CHECK(foveaStep != 0, "foveaStep 0 renders nothing: its gradient is zero");
     return BackwardImpl(foveaStep, interpolate_image, background, means3D, radii, colors, scales, rotations,
                         scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh,
-                        degree, campos, geomBuffer, R, binningBuffer, imageBuffer, debug);
+                        degree, campos, geomBuffer, R, binningBuffer, imageBuffer, debug, true);
 }
 
 // Data-parallel stage 1 (gsplat_amd.h): blend backward of one view -> its
@@ -731,6 +751,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.doc() = "MI355X (gfx950) Gaussian rasterizer -- PyTorch binding over include/gsplat_amd.h";
     m.def("rasterize_gaussians", &RasterizeGaussians);
     m.def("rasterize_gaussians_backward", &RasterizeGaussiansBackward);
+    m.def("rasterize_gaussians_backward_lean", &RasterizeGaussiansBackwardLean);
     m.def("amr_rasterize_gaussians_backward", &AmrRasterizeGaussiansBackward);
     m.def("mark_visible", &MarkVisible);
     m.def("rasterize_gaussians_backward_view_grads", &RasterizeGaussiansBackwardViewGrads);

@@ -73,8 +73,8 @@ class _RasterizeGaussians(torch.autograd.Function):
                 s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, grad_out_color, sh, s.sh_degree, s.campos,
                 geomBuffer, ctx.num_rendered, binningBuffer, imgBuffer, s.debug)
         (grad_means2D, grad_colors_precomp, grad_opacities, grad_means3D, grad_cov3Ds_precomp, grad_sh,
-         grad_scales, grad_rotations) = _call(_C.rasterize_gaussians_backward, args, s.debug, "snapshot_bw.dump",
-                                              "backward")
+         grad_scales, grad_rotations) = _call(_C.rasterize_gaussians_backward_lean, args, s.debug,
+                                              "snapshot_bw.dump", "backward")
         return (grad_means3D, grad_means2D, grad_sh, grad_colors_precomp, grad_opacities, grad_scales,
                 grad_rotations, grad_cov3Ds_precomp, None)
 

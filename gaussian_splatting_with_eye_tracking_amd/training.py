@@ -371,7 +371,7 @@ class FlatGaussianModel:
             s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, a["shs"], s.sh_degree, s.campos,
             s.prefiltered, s.debug)
         out3, d_image = _C.l1_ssim_loss(color, gt_image, float(lambda_dssim))
-        (d_means2D, _d_colors, d_opac, d_means3D, _d_cov3D, d_shs, d_scales, d_rot) = _C.rasterize_gaussians_backward(
+        (d_means2D, _d_colors, d_opac, d_means3D, _d_cov3D, d_shs, d_scales, d_rot) = _C.rasterize_gaussians_backward_lean(
             s.bg, xyz, radii, e, a["scales"], a["rotations"], s.scale_modifier, e, s.viewmatrix, s.projmatrix,
             s.tanfovx, s.tanfovy, d_image, a["shs"], s.sh_degree, s.campos, geom, num_rendered, binning, img,
             s.debug)

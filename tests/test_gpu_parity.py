@@ -124,6 +124,17 @@ def test_backward_parity(name, P, W, H, seed, variant):
         assert gg.shape == rg[n].shape, n
         assert np.all(np.isfinite(gg)), n
         assert G.rel_err(gg, rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(gg, rg[n]))
+    # the autograd wrappers' binding: the same bits, colour / covariance
+    # gradients only when their precomputed input was given
+    lean = C.rasterize_gaussians_backward_lean(s.bg, t["means3D"], radii, colt, scales, rots, s.scale_modifier, covt,
+                                               s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy,
+                                               torch.from_numpy(dpix).cuda(), sh, s.sh_degree, s.campos, geom, K,
+                                               binning, img, False)
+    for n, g, gl in zip(names, grads, lean):
+        if (n == "dL_dcolors" and colors is None) or (n == "dL_dcov3D" and cov is None):
+            assert gl.numel() == 0, n
+        else:
+            assert G.rel_err(gl.cpu().numpy(), g.cpu().numpy()) < 1e-5, n  # (float atomics: run-order noise)
 
 
 @pytest.mark.parametrize("xcd_map", [0, 1, 2, 3])
