@@ -748,8 +748,6 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     // All loads up front (one memory round trip per thread).
     const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
     float cov3D[6];
-#pragma unroll
-    for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D[6 * idx + i];
     float4 qrot = make_float4(0.f, 0.f, 0.f, 0.f);
     float scl[3] = {0.f, 0.f, 0.f};
     if (kHasScales) {
@@ -757,6 +755,13 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
         scl[0] = a.scales[3 * idx + 0];
         scl[1] = a.scales[3 * idx + 1];
         scl[2] = a.scales[3 * idx + 2];
+        // the forward's cov3D recomputed from the scale / rotation this pass
+        // reads anyway (same code, no contraction: the same bits) instead of
+        // 24 more bytes per Gaussian from the geometry buffer
+        compute_cov3d(scl, qrot, a.scale_modifier, cov3D);
+    } else {
+#pragma unroll
+        for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D[6 * idx + i];
     }
     float s[16][3];
     uint8_t cb = 0;
