@@ -799,6 +799,10 @@ int gs_set_tuning(const char* key, int value) {
         set_amr_batch(value);
         return 0;
     }
+    if (std::strcmp(key, "amr_fold") == 0) {
+        set_amr_fold(value);
+        return 0;
+    }
     if (std::strcmp(key, "xcd_map") == 0) {
         set_xcd_map(value);
         return 0;

@@ -70,6 +70,7 @@ extern int g_xcd_map;
 void set_cull(int v);
 void set_amr_variant(int v);
 void set_amr_batch(int v);
+void set_amr_fold(int v);
 void set_sort_wide(int v);
 void set_amr_scramble(int v);
 void set_ritnet_mfma(int v);

@@ -588,7 +588,7 @@ void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningVi
 // given colors_precomp): colours from it through point_list instead of the
 // step-0 records.
 // kPer: entries each lane stages per batch (a group stages 16 kPer)
-template <int kRounds, int kPer>
+template <int kRounds, int kPer, int kFold = 0>
 __global__ void __launch_bounds__(64) amr_region_render_kernel(
     int W, int H, int tgx, int T, const uint32_t* __restrict__ order, const uint32_t* __restrict__ ranges,
     const uint32_t* __restrict__ lists, const uint32_t* __restrict__ region_count,
@@ -744,7 +744,60 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
             // entries of this batch: [0, m) for the group, [0, mw) for the wave
             const int m = (int)min((uint32_t)kRgBatch, cnt > b0 ? cnt - b0 : 0u);
             const int mw = (int)min((uint32_t)kRgBatch, cmax - b0);
-            if constexpr (kRounds == 1) {
+            if constexpr (kFold > 0) {
+                // Two phases per sub-batch of kFold entries.  The alpha of
+                // every staged entry does not depend on T, so phase 1
+                // evaluates them as independent chains (full issue rate even
+                // with one wave per SIMD, the late steps' case); phase 2 is the
+                // reference's front-to-back fold in list order, a few
+                // dependent ops per entry.  Same operations on the same
+                // operands as the one-entry loop: same bits.
+#pragma unroll
+                for (int j0 = 0; j0 < kRgBatch; j0 += kFold) {
+                    float al[kFold][kSlots];
+                    uint32_t okm[kSlots];  // entries j < m passing the alpha tests
+#pragma unroll
+                    for (int k = 0; k < kSlots; k++) okm[k] = 0;
+#pragma unroll
+                    for (int e = 0; e < kFold; e++) {
+                        const int j = j0 + e;
+                        const float4 a = s_a[h][j];
+                        const float4 co = s_b[h][j];
+#pragma unroll
+                        for (int k = 0; k < kSlots; k++) {
+                            if (!active[k]) continue;  // wave-uniform
+                            const float pw = splat_p2(a.x - pxx[k], a.y - pxy[k], co);
+                            al[e][k] = fminf(0.99f, co.w * splat_exp(pw));
+                            okm[k] |= (j < m && !(pw > 0.0f) && !(al[e][k] < 1.0f / 255.0f)) ? 1u << e : 0u;
+                        }
+                    }
+                    bool alive = false;
+#pragma unroll
+                    for (int e = 0; e < kFold; e++) {
+                        const int j = j0 + e;
+#pragma unroll
+                        for (int k = 0; k < kSlots; k++) {
+                            if (!active[k]) continue;
+                            const float test_T = T_[k] * (1 - al[e][k]);
+                            const bool hit = ((okm[k] >> e) & 1u) && !done[k];
+                            const bool stop = hit && test_T < 0.0001f;
+                            done[k] = done[k] || stop;
+                            if (hit && !stop) {
+                                const float w = al[e][k] * T_[k];
+                                const float4 a = s_a[h][j];
+                                C[k][0] = __builtin_fmaf(a.z, w, C[k][0]);
+                                C[k][1] = __builtin_fmaf(a.w, w, C[k][1]);
+                                C[k][2] = __builtin_fmaf(s_c[h][j], w, C[k][2]);
+                                T_[k] = test_T;
+                                last[k] = s_pos[h][j] + 1;
+                            }
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < kSlots; k++) alive |= !done[k] && j0 + kFold < m;
+                    if (j0 + kFold < kRgBatch && __ballot(alive) == 0ull) break;
+                }
+            } else if constexpr (kRounds == 1) {
                 // two entries per iteration: their LDS reads share one wait and
                 // their alpha chains interleave; the blend stays in list order
                 for (int j = 0; j < mw; j += 2) {
@@ -840,6 +893,15 @@ int g_amr_scramble = 0;  // variant 4: 1 = units in a scrambled (not heaviest-fi
 void set_amr_scramble(int v) { g_amr_scramble = v; }
 int g_amr_batch = 1;  // variant 4: entries staged per lane and batch (1 or 2)
 void set_amr_batch(int v) { g_amr_batch = v == 2 ? 2 : 1; }
+// variant 4: bit k set = foveaStep k (bit 0: render_once) uses the
+// alpha-phase + fold-phase sub-batches; bit 5 = 16-entry sub-batches for the
+// steps (else 8)
+int g_amr_fold = 0x1e;
+int g_amr_fold_n = 8;
+void set_amr_fold(int v) {
+    g_amr_fold = v & 0x1f;
+    g_amr_fold_n = (v & 0x20) ? 16 : 8;
+}
 
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,
@@ -852,18 +914,22 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
         const int T = tgx * tgy;
         const float* ov = (foveaStep > 0 && features != g.rgb) ? features : nullptr;
         const int nb = 32 * ((T + 7) / 8);  // b = 8 (4 (p / 8) + q) + p % 8
-#define GS_AMR_REGION(R, PER)                                                                                     \
-        hipLaunchKernelGGL((amr_region_render_kernel<R, PER>), dim3(nb), dim3(64), 0, s, W, H, tgx, T,            \
+#define GS_AMR_REGION(R, PER, FOLD)                                                                               \
+        hipLaunchKernelGGL((amr_region_render_kernel<R, PER, FOLD>), dim3(nb), dim3(64), 0, s, W, H, tgx, T,            \
                            img.tile_order,                                                                          \
                            img.ranges, ab.region_lists, img.region_count, levels, levels_last, ab.rec_a, ab.rec_b, \
                            ab.rec_c, b.point_list, ov, img.accum_alpha, img.n_contrib, bg, out_color, foveaStep,   \
                            g_amr_scramble)
         if (foveaStep > 0) {
-            if (g_amr_batch == 2) GS_AMR_REGION(1, 2);
-            else GS_AMR_REGION(1, 1);
+            const bool fold = (g_amr_fold >> foveaStep) & 1;
+            if (fold && g_amr_fold_n == 16) GS_AMR_REGION(1, 1, 16);
+            else if (fold) GS_AMR_REGION(1, 1, 8);
+            else if (g_amr_batch == 2) GS_AMR_REGION(1, 2, 0);
+            else GS_AMR_REGION(1, 1, 0);
         } else {
-            if (g_amr_batch == 2) GS_AMR_REGION(4, 2);
-            else GS_AMR_REGION(4, 1);
+            if (g_amr_fold & 1) GS_AMR_REGION(4, 1, 4);
+            else if (g_amr_batch == 2) GS_AMR_REGION(4, 2, 0);
+            else GS_AMR_REGION(4, 1, 0);
         }
 #undef GS_AMR_REGION
         return;

@@ -335,13 +335,14 @@ def _amr_gpu_steps(sc, cam, interpolate_last=False, bg=(0.0, 0.0, 0.0), after_st
     return acc, radii, steps, (gb, bb, ib)
 
 
-@pytest.mark.parametrize("amr_variant,amr_batch", [(4, 1), (4, 2), (3, 1), (2, 1)])
+@pytest.mark.parametrize("amr_variant,amr_batch,amr_fold", [(4, 1, 0x1e), (4, 1, 0), (4, 2, 0), (3, 1, 0x1e),
+                                                            (2, 1, 0x1e)])
 @pytest.mark.parametrize("name,P,W,H,seed", [("amr_10k_256", 10000, 256, 256, 0), ("amr_ragged", 4000, 200, 120, 3),
                                              # 66 x 33 = 2178 tiles > 2048: the radix-select percentile path
                                              ("amr_big_grid", 3000, 2112, 1056, 8),
                                              # dense: long sub-lists (several 32-entry batches per region)
                                              ("amr_dense", 60000, 160, 96, 4)])
-def test_amr_foveated_steps(name, P, W, H, seed, amr_variant, amr_batch):
+def test_amr_foveated_steps(name, P, W, H, seed, amr_variant, amr_batch, amr_fold):
     """Every AMR blend variant (4: 8x8-region sub-lists + records, the
     default; 3: 16x16 quadrant sub-lists; 2: full 32-px lists) against the
     oracle: per-step images, and per pixel n_contrib / final T of the last
@@ -352,11 +353,13 @@ def test_amr_foveated_steps(name, P, W, H, seed, amr_variant, amr_batch):
     sc, cam = G.scene_and_camera(P, W, H, seed)
     C.set_tuning("amr_variant", amr_variant)
     C.set_tuning("amr_batch", amr_batch)
+    C.set_tuning("amr_fold", amr_fold)
     try:
         acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.1, 0.1))
     finally:
         C.set_tuning("amr_variant", 4)
         C.set_tuning("amr_batch", 1)
+        C.set_tuning("amr_fold", 0x1e)
     s = O.settings_from_camera(cam, bg=(0.1, 0.1, 0.1))
     kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
     racc, rradii, st, rsteps = O.amr_render_foveated(s, kw)
@@ -381,6 +384,32 @@ def test_amr_foveated_steps(name, P, W, H, seed, amr_variant, amr_batch):
     same = nc == rnc
     np.testing.assert_allclose(d["accum_alpha"].cpu().numpy()[rendered][same], st.final_T[rendered][same],
                                rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("P,W,H,seed", [(10000, 256, 256, 0), (60000, 160, 96, 4), (3000, 2112, 1056, 8)])
+def test_amr_fold_phases_bit_identical(P, W, H, seed):
+    """The steps' alpha-phase + fold-phase batches (amr_fold, the default)
+    evaluate the same operations on the same operands as the one-entry loop:
+    every step image, n_contrib and final T are bit-identical."""
+    import oracle as O
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    out = {}
+    for fold in (0, 0x1e):
+        C.set_tuning("amr_fold", fold)
+        try:
+            acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.2, 0.3))
+        finally:
+            C.set_tuning("amr_fold", 0x1e)
+        d = C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)
+        K = int(d["hdr"][0].item())
+        d = C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
+        # pixels some step rendered (the others are never written)
+        lv = d["levels"].cpu().numpy().astype(np.uint32)
+        rendered = torch.from_numpy((O.amr_pixel_rounds(W, H) <= O.amr_tile_levels_per_pixel(lv, W, H)).reshape(-1))
+        out[fold] = [s_.cpu() for s_ in steps] + [d["n_contrib"].cpu()[rendered], d["accum_alpha"].cpu()[rendered]]
+    for a, b in zip(out[0], out[0x1e]):
+        assert torch.equal(a, b)
 
 
 def test_amr_steps_with_nothing_in_front():

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--H", type=int, default=1080)
     ap.add_argument("--backward", action="store_true")
     ap.add_argument("--amr", action="store_true", help="time a 5-step foveated AMR frame instead")
+    ap.add_argument("--amr-once", action="store_true", help="time AMR render_once (foveaStep -2, interpolated)")
     args = ap.parse_args()
 
     from gaussian_splatting_with_eye_tracking_amd import _C
@@ -56,7 +57,7 @@ def main():
             torch.autograd.backward(color, dpix)
         return color
 
-    if args.amr:
+    if args.amr or args.amr_once:
         from diff_gaussian_rasterization_amr import GaussianRasterizationSettings as AS, _RasterizeGaussians as AR
         ast = AS(**st._asdict())
         e = torch.empty(0, device=dev)
@@ -65,6 +66,8 @@ def main():
 
         def run():  # noqa: F811  (gaussian_renderer_amr render(): fovea steps 0..4)
             with torch.no_grad():
+                if args.amr_once:
+                    return AR.apply(*a, -2, e, u8, u8, u8, True, ast)[0]
                 c, _, gb, bb, ib = AR.apply(*a, 0, e, u8, u8, u8, False, ast)
                 acc = c
                 for k in range(1, 5):

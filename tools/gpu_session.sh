@@ -59,6 +59,8 @@ for step in "$@"; do
                run ab_chunk4_cnt 400 python tools/ab_tuning.py --key bin_chunk --values 4096 8192 16384 32768 --stage count_tiles --P 6100000 --W 1600 --H 1063 --rounds 3 ;;
     ab_dup) run ab_dup2 400 python tools/ab_tuning.py --key bin_two_phase --values 0 1 0 1 --stage duplicate &&
             run ab_dup4 400 python tools/ab_tuning.py --key bin_two_phase --values 0 1 0 1 --stage duplicate --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
+    ab_fold) run ab_fold 400 python tools/ab_tuning.py --key amr_fold --values 0 30 62 --stage amr_render --amr &&
+             run ab_fold_once 400 python tools/ab_tuning.py --key amr_fold --values 0 1 --stage amr_render --amr-once ;;
     ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 3 4 3 4 --stage amr_render --amr ;;
     ab_split) run ab_split2 400 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward &&
               run ab_split4 600 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
