@@ -178,6 +178,7 @@ PreprocessArgs make_pp(const ForwardIn& in, int tile) {
     a.focal_x = (float)in.width / (2.0f * in.tan_fovx);
     a.block = tile;
     a.prefiltered = in.prefiltered;
+    a.store_cov3d = g_store_cov3d;
     return a;
 }
 
@@ -601,14 +602,18 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
                 throw GsError("foveaStep >= 1 needs the binning buffer returned by foveaStep 0");
             AmrBinningView ab;
             carve_binning(binning_buffer_precomp, K, &b, &ab);
-            launch_fovea_levels(foveaStep, T, img, s, P, radii);  // + the step's zero radii
-            stage_check(dbg, s, "fovea_levels");
-            if (g_amr_variant != 4)  // variant 4 writes the zeros of the pixels it does not render itself
+            // variant 4 folds the step's level update and zero radii into its
+            // render launch, and writes the zeros of the pixels it does not render
+            const bool fused = g_amr_variant == 4;
+            if (!fused) {
+                launch_fovea_levels(foveaStep, T, img, s, P, radii);  // + the step's zero radii
+                stage_check(dbg, s, "fovea_levels");
                 GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, s));
+            }
             const float* feats = colors_precomp ? colors_precomp : g.rgb;
             { StageTimer _t(kAmrRender, s);
-              launch_amr_render(W, H, img, img.levels_current, img.levels_last, b, ab, g, feats, background,
-                                out_color, foveaStep, s); }
+              launch_amr_render(W, H, img, fused ? img.levels : img.levels_current, img.levels_last, b, ab, g, feats,
+                                background, out_color, foveaStep, s, fused, P, radii); }
             stage_check(dbg, s, "amr_render");
             if (interpolate_image) {
                 if (!out_color_precomp) throw GsError("interpolate_image at foveaStep >= 1 needs out_color_precomp");
@@ -797,6 +802,10 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "amr_batch") == 0) {
         set_amr_batch(value);
+        return 0;
+    }
+    if (std::strcmp(key, "store_cov3d") == 0) {
+        set_store_cov3d(value);
         return 0;
     }
     if (std::strcmp(key, "amr_fold") == 0) {

@@ -27,6 +27,7 @@ struct PreprocessArgs {
     float tan_fovx, tan_fovy, focal_x, focal_y;
     int block;  // tile edge in pixels (16 base, 32 AMR)
     int prefiltered;
+    int store_cov3d;  // write the geometry buffer's cov3D (nothing in the path reads it back)
 };
 
 // base/cr/forward.cu:155-256 (+ the tile histogram the binning needs).
@@ -71,6 +72,8 @@ void set_cull(int v);
 void set_amr_variant(int v);
 void set_amr_batch(int v);
 void set_amr_fold(int v);
+void set_store_cov3d(int v);
+extern int g_store_cov3d;
 void set_sort_wide(int v);
 void set_amr_scramble(int v);
 void set_ritnet_mfma(int v);
@@ -173,7 +176,8 @@ extern int g_amr_variant;
 void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s, int P = 0, int* zero_radii = nullptr);
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,
-                       const float* bg, float* out_color, int foveaStep, hipStream_t s);
+                       const float* bg, float* out_color, int foveaStep, hipStream_t s, bool fused = false, int P = 0,
+                       int* zero_radii = nullptr);
 void launch_amr_interpolate(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                             float* out_color, int foveaStep, const float* out_color_precomp, hipStream_t s);
 

@@ -94,6 +94,7 @@ struct ImageView {
     uint32_t* tile_order;      // [T] tiles by descending blend work (launch order)
     uint32_t* quad_count;      // [T][4] AMR: entries of each 16x16 quadrant's sub-list
     uint32_t* region_count;    // [T][16] AMR: entries of each 8x8 region's sub-list
+    uint32_t* tile_done;       // [T] AMR steps: finished (tile, quadrant) units, mod 4
 };
 
 inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
@@ -113,6 +114,7 @@ inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
     g.tile_order = carve<uint32_t>(base, off, T);
     g.quad_count = carve<uint32_t>(base, off, 4 * T);
     g.region_count = carve<uint32_t>(base, off, 16 * T);
+    g.tile_done = carve<uint32_t>(base, off, T);
     if (v) *v = g;
     return align_up(off);
 }

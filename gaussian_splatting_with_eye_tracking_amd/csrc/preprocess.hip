@@ -136,8 +136,13 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
     // computeCov3D (forward.cu:118-152)
     if (!kCovPrecomp) {
         compute_cov3d(sc, q, a.scale_modifier, cov3D);
+        // the reference stores it for its backward; the backward here
+        // recomputes it from the scale / rotation it reads anyway (bit-identical),
+        // so the 24 B per Gaussian are written only on request (parity tests)
+        if (a.store_cov3d) {
 #pragma unroll
-        for (int i = 0; i < 6; i++) g.cov3D[6 * idx + i] = cov3D[i];
+            for (int i = 0; i < 6; i++) g.cov3D[6 * idx + i] = cov3D[i];
+        }
     }
 
     // computeCov2D (forward.cu:74-113)
@@ -230,6 +235,9 @@ static void launch_pp(const PreprocessArgs& a, const GeomView& g, int* radii, ui
     const int blocks = (a.P + 255) / 256;
     hipLaunchKernelGGL((preprocess_kernel<A, B, C>), dim3(blocks), dim3(256), 0, s, a, g, radii, tile_count);
 }
+
+int g_store_cov3d = 0;  // set_tuning("store_cov3d"): the parity tests read the geometry buffer's cov3D
+void set_store_cov3d(int v) { g_store_cov3d = v; }
 
 void launch_preprocess(const PreprocessArgs& a, const GeomView& g, int* radii, uint32_t* tile_count,
                        hipStream_t s) {

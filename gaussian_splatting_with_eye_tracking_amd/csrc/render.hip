@@ -501,7 +501,8 @@ __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, c
                                                                       float4* __restrict__ rec_b,
                                                                       float* __restrict__ rec_c,
                                                                       uint32_t* __restrict__ lists,
-                                                                      uint32_t* __restrict__ region_count) {
+                                                                      uint32_t* __restrict__ region_count,
+                                                                      uint32_t* __restrict__ tile_done) {
     constexpr int kW = kRlThreads / 64;
     // per pass: hits of (slot e, region g, wave w), then their exclusive
     // offsets in the pass's (e, w) order, per region
@@ -562,6 +563,7 @@ __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, c
         __syncthreads();  // s_cnt is rewritten by the next pass
     }
     if (tid < 16) region_count[16 * tile + tid] = s_base[tid];
+    if (tid == 0) tile_done[tile] = 0;  // the steps' unit counters start at 0 mod 4
 }
 
 void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningView& b, const AmrBinningView& ab,
@@ -569,13 +571,15 @@ void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningVi
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0) return;
     if (K == 0) {  // no lists to build; the counts must still read 0
-        (void)hipMemsetAsync(img.region_count, 0, sizeof(uint32_t) * 16 * (size_t)tgx * tgy, s);  // checked by the caller's stage_check
+        // (checked by the caller's stage_check)
+        (void)hipMemsetAsync(img.region_count, 0, sizeof(uint32_t) * 16 * (size_t)tgx * tgy, s);
+        (void)hipMemsetAsync(img.tile_done, 0, sizeof(uint32_t) * (size_t)tgx * tgy, s);
         return;
     }
     (void)features;  // in the rows (the preprocess saw colors_precomp / the SH colours)
     hipLaunchKernelGGL(amr_region_lists_kernel, dim3(tgx * tgy), dim3(kRlThreads), 0, s, tgx, img.ranges,
                        b.point_list, reinterpret_cast<const float4*>(g.grad_accum), ab.rec_a, ab.rec_b, ab.rec_c,
-                       ab.region_lists, img.region_count);
+                       ab.region_lists, img.region_count, img.tile_done);
 }
 
 // One wave per (tile, quadrant): its four 16-lane groups are the quadrant's
@@ -595,7 +599,9 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     const uint32_t* __restrict__ levels, const uint32_t* __restrict__ levels_last, const float4* __restrict__ rec_a,
     const float4* __restrict__ rec_b, const float* __restrict__ rec_c, const uint32_t* __restrict__ point_list,
     const float* __restrict__ feats_override, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
-    const float* __restrict__ bg, float* __restrict__ out_color, int foveaStep, int scramble) {
+    const float* __restrict__ bg, float* __restrict__ out_color, int foveaStep, int scramble,
+    uint32_t* __restrict__ lv_current, uint32_t* __restrict__ lv_last, uint32_t* __restrict__ tile_done, int P,
+    int* __restrict__ zero_radii) {
 #pragma clang fp contract(fast)
     constexpr int kRgBatch = 16 * kPer;
     __shared__ float4 s_a[4][kRgBatch];
@@ -603,6 +609,9 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     __shared__ float s_c[4][kRgBatch];
     __shared__ uint32_t s_pos[4][kRgBatch];
     const uint32_t bid = blockIdx.x, slot = bid >> 3;
+    // the step's zero radii (the reference's torch::full(0) for steps >= 1)
+    if (zero_radii)
+        for (int i = (int)(bid * 64 + threadIdx.x); i < P; i += (int)(gridDim.x * 64)) zero_radii[i] = 0;
     const int p = (int)(8 * (slot >> 2) + (bid & 7));
     if (p >= T) return;
     // scramble (A/B): a fixed permutation of the tile order (1031 is prime,
@@ -643,11 +652,42 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
             }
         }
     };
-    const uint32_t L_last = levels_last[tile];
-    uint32_t L = levels[tile];
+    // Fused step levels (lv_current given, the progressive steps): the
+    // reference's per-step level update (amr.hip fovea_levels_kernel,
+    // amr/cr/rasterizer_impl.cu's tile_AMR_levels_last / _current) evaluated
+    // by each of the tile's four units from the previous current level; the
+    // last unit of the tile to finish stores it (tile_done counts units mod 4),
+    // so every unit has read the previous value before it is replaced.
+    uint32_t L_last, L;
+    if (lv_current) {
+        const uint32_t Lp = levels[tile], prev = lv_current[tile];
+        if (foveaStep == 1) {
+            L_last = 0;
+            L = Lp >= 1u ? 1u : 0u;
+        } else if (foveaStep <= 4) {
+            L_last = prev;
+            L = Lp >= (uint32_t)foveaStep ? (uint32_t)foveaStep : prev;
+        } else {
+            L_last = 0;
+            L = Lp;
+        }
+    } else {
+        L_last = levels_last[tile];
+        L = levels[tile];
+    }
+    const uint32_t L_store = L;
+    auto finish_unit = [&]() {
+        if (lv_current && threadIdx.x == 0) {
+            if ((atomicAdd(&tile_done[tile], 1u) & 3u) == 3u) {
+                lv_last[tile] = L_last;
+                lv_current[tile] = L_store;
+            }
+        }
+    };
     // Block-uniform early exits (amr/cr/forward.cu:287-367).
     if (L <= L_last) {
         store_quadrant(true);
+        finish_unit();
         return;
     }
     if (L > 4) L = 4;
@@ -885,6 +925,7 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     }
     __syncthreads();  // single-wave workgroup: LDS fence only
     store_quadrant(false);
+    finish_unit();
 }
 
 int g_amr_variant = 4;  // 4: 8x8 region sub-lists + records (default); 3: quadrant sub-lists; 0 = 1 x 4 px, 1 = 2 x 2, 2 = 4 x 1 full-list blocks
@@ -905,7 +946,8 @@ void set_amr_fold(int v) {
 
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,
-                       const float* bg, float* out_color, int foveaStep, hipStream_t s) {
+                       const float* bg, float* out_color, int foveaStep, hipStream_t s, bool fused, int P,
+                       int* zero_radii) {
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0) return;
     if (g_amr_variant == 4) {
@@ -919,7 +961,8 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
                            img.tile_order,                                                                          \
                            img.ranges, ab.region_lists, img.region_count, levels, levels_last, ab.rec_a, ab.rec_b, \
                            ab.rec_c, b.point_list, ov, img.accum_alpha, img.n_contrib, bg, out_color, foveaStep,   \
-                           g_amr_scramble)
+                           g_amr_scramble, fused ? img.levels_current : nullptr, img.levels_last, img.tile_done, P,   \
+                           fused ? zero_radii : nullptr)
         if (foveaStep > 0) {
             const bool fold = (g_amr_fold >> foveaStep) & 1;
             if (fold && g_amr_fold_n == 16) GS_AMR_REGION(1, 1, 16);

@@ -297,6 +297,7 @@ typedef struct {
     uint32_t* tile_order; /* [T] blend launch order (descending work) */
     uint32_t* quad_count; /* [T][4] AMR quadrant sub-list lengths */
     uint32_t* region_count; /* [T][16] AMR 8x8-region sub-list lengths */
+    uint32_t* tile_done; /* [T] AMR steps: finished units per tile, mod 4 */
 } gs_image_view;
 
 typedef struct {
@@ -339,8 +340,13 @@ void gs_profile_set_mask(unsigned mask);
  * per tile x 4 px/lane, 1 = 2 waves x 2 px/lane, 2 = 4 waves x
  * 1 px/lane, the default), "bwd_variant" (0 = 1 wave x 4 px/lane, the default; 1 = 2 x 2; 2 = 4 x 1; 3 = 1 x 4 uncapped registers), "cull" (1 =
  * skip Gaussians whose alpha >= 1/255 box misses a 16x4 row group, the
- * default; 0 only to verify that the cull is exact).  Returns 0, or -1 for
- * an unknown key. */
+ * default; 0 only to verify that the cull is exact), "store_cov3d" (1 = the
+ * forward also writes the geometry buffer's cov3D, which nothing in the path
+ * reads back -- for buffer-level parity checks; default 0), "amr_fold" (bit k
+ * = AMR foveaStep k blends in alpha-phase + fold-phase batches, default 0x1e;
+ * bit 5 = 16-entry batches), "amr_variant", "amr_batch", "amr_scramble",
+ * "sort_wide", "xcd_map", "bin_chunk", "bwd_gauss_split".  Returns 0, or -1
+ * for an unknown key. */
 int gs_set_tuning(const char* key, int value);
 int gs_profile_stage_count(void);
 const char* gs_profile_stage_name(int i);

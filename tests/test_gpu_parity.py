@@ -52,7 +52,11 @@ def _oracle_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0
 def test_forward_buffers_bit_exact(name, P, W, H, seed):
     import gaussian_splatting_with_eye_tracking_amd._C as C
     sc, cam = G.scene_and_camera(P, W, H, seed)
-    _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
+    C.set_tuning("store_cov3d", 1)  # the geometry buffer's cov3D is written on request only
+    try:
+        _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
+    finally:
+        C.set_tuning("store_cov3d", 0)
     _, ref, _ = _oracle_forward(sc, cam)
     assert K == ref.num_rendered
     d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
