@@ -15,6 +15,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -123,6 +124,25 @@ void read_header(const uint32_t* hdr_dev, uint32_t out[4], hipStream_t s) {
     std::memcpy(out, h, 4 * sizeof(uint32_t));
 }
 
+// The same read-back in two halves: the copy (and an event behind it) is
+// enqueued, the caller enqueues work that does not depend on K, then waits for
+// the copy alone -- that work runs while the host reacts to K.
+hipEvent_t header_event() {
+    thread_local hipEvent_t e = nullptr;
+    if (!e) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+}
+
+void begin_header_read(const uint32_t* hdr_dev, hipStream_t s) {
+    GS_HIP(hipMemcpyAsync(pinned_words(), hdr_dev, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    GS_HIP(hipEventRecord(header_event(), s));
+}
+
+void finish_header_read(uint32_t out[4]) {
+    GS_HIP(hipEventSynchronize(header_event()));
+    std::memcpy(out, pinned_words(), 4 * sizeof(uint32_t));
+}
+
 char* call_resize(const gs_buffer& b, size_t n, const char* what) {
     if (!b.resize) throw GsError(std::string("no resize callback for ") + what);
     char* p = b.resize(b.ctx, n);
@@ -193,8 +213,11 @@ struct Binned {
 };
 
 // preprocess -> tile scan -> (K read-back) -> duplicate -> per-tile sort.
+// `before_k`: work that needs the scan but not K, enqueued behind the K copy
+// and run while the host waits for it.
 Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const gs_buffer& binning,
-                          const gs_buffer& image, int* radii, int tile, bool debug, hipStream_t s) {
+                          const gs_buffer& image, int* radii, int tile, bool debug, hipStream_t s,
+                          const std::function<void(Binned&)>& before_k = nullptr) {
     Binned r;
     const int W = in.width, H = in.height;
     const int gx = (W + tile - 1) / tile, gy = (H + tile - 1) / tile;
@@ -215,7 +238,13 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s); }
     stage_check(debug, s, "tile_scan");
     uint32_t hdr[4];
-    read_header(r.g.hdr, hdr, s);
+    if (before_k) {
+        begin_header_read(r.g.hdr, s);
+        before_k(r);
+        finish_header_read(hdr);
+    } else {
+        read_header(r.g.hdr, hdr, s);
+    }
     if (hdr[kHdrError])
         throw GsError("Point is filtered although prefiltered is set. This shouldn't happen!");
     r.K = (int)hdr[kHdrNumRendered];
@@ -625,31 +654,34 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
         }
         ForwardIn in{P, D, M, background, means3D, shs, colors_precomp, opacities, scales, rotations, cov3D_precomp,
                      viewmatrix, projmatrix, cam_pos, width, height, scale_modifier, tan_fovx, tan_fovy, prefiltered};
-        Binned r = preprocess_and_bin(in, geometry, binning, image, radii, tile, dbg, s);
+        // Everything that needs the tile counts / ranges but not K runs behind
+        // the K copy, while the host waits for it: the levels (percentiles of
+        // the counts), the step's level schedule, the tile order (by list
+        // length) and step 0's zero image.
+        auto before_k = [&](Binned& r) {
+            { StageTimer _t(kAmrLevels, s); launch_amr_levels(r.T, r.img, s); }
+            stage_check(dbg, s, "amr_levels");
+            if (g_amr_variant >= 3) launch_order_tiles(r.T, r.img, false, s);
+            if (foveaStep == 0 || g_amr_variant != 4)  // (variant 4 writes the zeros of the pixels it does not render)
+                GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, s));
+            if (foveaStep != 0) launch_fovea_levels(foveaStep, r.T, r.img, s);
+        };
+        Binned r = preprocess_and_bin(in, geometry, binning, image, radii, tile, dbg, s, before_k);
         // (the geometry buffer's own copy of the radii -- the progressive steps
         // return zero radii as the reference does, and the AMR backward of a
         // step reads the step-0 radii from there -- is written by the preprocess)
-        { StageTimer _t(kAmrLevels, s); launch_amr_levels(r.T, r.img, s); }
-        stage_check(dbg, s, "amr_levels");
         const float* feats = colors_precomp ? colors_precomp : r.g.rgb;
         if (g_amr_variant >= 3) {
-            // the AMR blend's work units: tiles heaviest first (by list length;
-            // the levels follow the same counts) and their sub-lists: 16x16
-            // quadrants in the dead sort-key space (variant 3) or the 8x8
-            // regions + blend records of the AMR binning layout (4)
+            // the AMR blend's work units: tiles heaviest first (ordered above)
+            // and their sub-lists: 16x16 quadrants in the dead sort-key space
+            // (variant 3) or the 8x8 regions + blend records of the AMR binning
+            // layout (4)
             { StageTimer _t(kAmrLists, s);
-              launch_order_tiles(r.T, r.img, false, s);
               if (g_amr_variant == 3) launch_amr_quad_lists(W, H, r.img, r.b, r.g, r.K, s);
               else launch_amr_region_lists(W, H, r.img, r.b, r.ab, r.g, feats, r.K, s); }
             stage_check(dbg, s, "amr_lists");
         }
-        if (foveaStep == 0) {  // step 0: buffers only, a zero image (amr/cr/rasterizer_impl.cu:651)
-            GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, s));
-            return r.K;
-        }
-        if (g_amr_variant != 4)  // variant 4 writes the zeros of the pixels it does not render itself
-            GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, s));
-        launch_fovea_levels(foveaStep, r.T, r.img, s);
+        if (foveaStep == 0) return r.K;  // step 0: buffers only, a zero image (amr/cr/rasterizer_impl.cu:651)
         { StageTimer _t(kAmrRender, s);
           launch_amr_render(W, H, r.img, r.img.levels, r.img.levels_last, r.b, r.ab, r.g, feats, background,
                             out_color, foveaStep, s); }
