@@ -127,6 +127,23 @@ def algorithmic_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: in
     return 0.0
 
 
+def stream_read_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: int, views: int = 1):
+    """Bytes of one launch of `stage` read as wave-contiguous streams, or None
+    when (nearly) all its reads are streams.  profiles/r02n_pmc_calib.json
+    (tools/pmc_calib.hip, 1 GiB buffer): FETCH_SIZE tallies a streamed 128-B
+    line at 64 B (the guide's x2) but a random 8 / 16 / 64-B gather miss at the
+    64-B sector it really moves (x1); scattered stores and 64-B atomic rows are
+    counted at their true granule by WRITE_SIZE.  So traffic = FETCH + WRITE +
+    (streamed bytes) / 2 for the gather-dominated blend kernels."""
+    if stage == "render":      # point_list ids; ranges
+        return 4.0 * Kb + 8.0 * T
+    if stage == "render_bwd":  # point_list ids; dL/dpix, final T, n_contrib; ranges + max_contrib
+        return 4.0 * Kb + 20.0 * N + 12.0 * T
+    if stage == "amr_render":  # list positions and tile-local records: 64-B-sector reads, none streamed
+        return 0.0
+    return None
+
+
 def config_key(P: int, W: int, H: int, tile: int) -> dict:
     return {"P": int(P), "W": int(W), "H": int(H), "tile": int(tile)}
 
@@ -153,13 +170,42 @@ def load_pmc(stage: str, key: dict, field: str):
     return None
 
 
-def make_roofline(stage: str, by: float, avg_ms: float, key: dict, src: str, per: float = 1.0) -> dict:
-    """`by` bytes in `avg_ms`; `per` = launches those cover (PMC values are per launch)."""
+def load_raw_kib(stage: str, key: dict):
+    """(FETCH_SIZE, WRITE_SIZE) KiB per launch of `stage` from the newest PMC
+    summary of THIS configuration, or None."""
+    for f in reversed(_pmc_files()):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("config") != key:
+            continue
+        v = d.get("raw_kib", {}).get(stage)
+        if v is not None:
+            return float(v["FETCH_SIZE"]), float(v["WRITE_SIZE"])
+    return None
+
+
+def make_roofline(stage: str, by: float, avg_ms: float, key: dict, src: str, per: float = 1.0,
+                  stream_read: float | None = None) -> dict:
+    """`by` bytes in `avg_ms`; `per` = launches those cover (PMC values are per
+    launch); `stream_read`: streamed read bytes per launch (stream_read_bytes)
+    -- given, traffic uses the gather calibration instead of doubling every
+    fetched byte."""
     ach = by / (avg_ms * 1e-3) / 1e9
     tr = load_pmc(stage, key, "per_launch_hbm_bytes")
+    traffic = tr[0] * per if tr else None
+    raw = load_raw_kib(stage, key) if stream_read is not None else None
+    calib = None
+    if raw is not None:
+        calib = (1024.0 * (raw[0] + raw[1]) + 0.5 * stream_read) * per
     r = {"kernel": stage, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tr[0] * per if tr else None,
+         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": calib if calib is not None else traffic,
          "traffic_source": tr[1] if tr else None, "algorithmic_bytes": by, "avg_ms": round(avg_ms, 4), "events": src}
+    if calib is not None:
+        r["traffic_note"] = ("FETCH + WRITE + streamed reads / 2 (gathers counted x1, streams x2: "
+                             "profiles/r02n_pmc_calib.json)")
+        r["traffic_all_fetch_x2"] = traffic
     vi = load_pmc(stage, key, "per_launch_valu_instructions")
     if vi is not None:  # the blend kernels' real bound (DESIGN.md §4)
         a_ = vi[0] * per / (avg_ms * 1e-3)
@@ -299,13 +345,17 @@ def workload_stats(settings, params, P: int, W: int, H: int, tile: int = 16):
     return dict(K=int(K), V=V, Kb=Kb, N=W * H, T=T)
 
 
-def stage_table(prof: dict, steps: int, P, ws, views=1) -> dict:
+def stage_table(prof: dict, steps: int, P, ws, views=1, key: dict | None = None) -> dict:
     out = {}
     for name, (ms, cnt) in prof.items():
         if cnt:
             st = {"avg_ms": ms / cnt, "launches": cnt, "ms_per_step": ms / steps}
             b = algorithmic_bytes(name, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"], views)
             st["algorithmic_GBps"] = round(b / (st["avg_ms"] * 1e-3) / 1e9, 1) if b else None
+            sr = stream_read_bytes(name, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"], views)
+            raw = load_raw_kib(name, key) if key is not None and sr is not None and b else None
+            if raw is not None:  # the blend kernels: gather-calibrated traffic (make_roofline)
+                st["traffic_over_algorithmic"] = round((1024.0 * (raw[0] + raw[1]) + 0.5 * sr) / b, 3)
             out[name] = st
     return out
 
@@ -367,14 +417,15 @@ def run_fwd_bwd(cfg_name: str, ctx: Ctx, steps: int, warmup: int) -> dict:
     if ctx.rank != 0:
         return res
     ws = workload_stats(settings, params, P, W, H)
-    stages = stage_table(prof, steps, P, ws)
+    stages = stage_table(prof, steps, P, ws, key=config_key(P, W, H, 16))
     roofline = None
     if stages:
         dom = max(stages, key=lambda n: stages[n]["ms_per_step"])
         ms_t, cnt_t = prof_timed.get(dom, (0.0, 0))
         avg_ms, src = (ms_t / cnt_t, "timed region") if cnt_t else (stages[dom]["avg_ms"], "stage-profile pass")
         by = algorithmic_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"])
-        roofline = make_roofline(dom, by, avg_ms, config_key(P, W, H, 16), src)
+        roofline = make_roofline(dom, by, avg_ms, config_key(P, W, H, 16), src,
+                                 stream_read=stream_read_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"]))
     res.update({
         "config": {"workload": f"{cfg_name}: {P} Gaussians, {W}x{H}, 16x16 tiles, forward+backward, 1 view per "
                                f"GPU per step", "P": P, "width": W, "height": H, "views_per_gpu_per_step": 1,
@@ -504,7 +555,8 @@ def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange
     if stages:
         dom = max(stages, key=lambda n: stages[n]["ms_per_step"])
         by = algorithmic_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"], G)
-        roofline = make_roofline(dom, by, stages[dom]["avg_ms"], config_key(P, W, H, 16), "stage-profile pass")
+        roofline = make_roofline(dom, by, stages[dom]["avg_ms"], config_key(P, W, H, 16), "stage-profile pass",
+                                 stream_read=stream_read_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"]))
     res.update({
         "config": {"workload": f"cfg5_8view_1080p_1M: {P} Gaussians, {W}x{H}, 16x16 tiles, {G} views per step "
                                f"(yaw -17.5..17.5 deg), {vl} per GPU, forward + blend backward + view-record "
@@ -662,7 +714,7 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
         ms = stages["amr_render"]["ms_per_frame"]
         # the PMC summary holds means per launch; the roofline is per frame
         roofline = make_roofline("amr_render", by, ms, config_key(P, W, H, 32), "stage-profile pass",
-                                 per=stages["amr_render"]["launches"] / steps)
+                                 per=stages["amr_render"]["launches"] / steps, stream_read=0.0)
         roofline["per"] = "frame (the 4 amr_render launches of steps 1..4 summed; traffic per frame)"
     res.update({
         "metric": "foveated AMR frames/sec (forward-only render(), 5 fovea steps) at 1080p, 1M Gaussians",

@@ -173,6 +173,14 @@ struct ForwardIn {
     int prefiltered;
 };
 
+// Per-call token for the header's error word (never 0: a zeroed header at
+// T == 0 must not read as an error).
+uint32_t next_error_token() {
+    thread_local uint32_t t = 0x9e3779b9u;
+    t = t * 1664525u + 1013904223u;
+    return t ? t : 1u;
+}
+
 PreprocessArgs make_pp(const ForwardIn& in, int tile) {
     PreprocessArgs a;
     a.P = in.P;
@@ -199,6 +207,9 @@ PreprocessArgs make_pp(const ForwardIn& in, int tile) {
     a.block = tile;
     a.prefiltered = in.prefiltered;
     a.store_cov3d = g_store_cov3d;
+    a.zero_words = nullptr;
+    a.zero_n = 0;
+    a.err_token = 0;
     return a;
 }
 
@@ -228,10 +239,20 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     char* ibase = call_resize(image, carve_image(nullptr, N, r.T, nullptr), "image");
     carve_image(ibase, N, r.T, &r.img);
     r.radii = radii ? radii : r.g.radii;
-    GS_HIP(hipMemsetAsync(r.g.hdr, 0, kHdrWords * sizeof(uint32_t), s));
-    if (r.T > 0) GS_HIP(hipMemsetAsync(r.img.tile_count, 0, sizeof(uint32_t) * r.T, s));
+    // The header needs no zeroing: the tile scan stores K and the tile
+    // statistics, and a prefiltered violation stores this call's token in the
+    // error word (stale words never equal it).  With the LDS-privatised count
+    // the preprocess zeroes the tile histogram; otherwise it adds into it.
     const bool lds_bin = r.T <= kLdsTiles;
-    { StageTimer _t(kPre, s); launch_preprocess(make_pp(in, tile), r.g, r.radii, lds_bin ? nullptr : r.img.tile_count, s); }
+    if (r.T == 0) GS_HIP(hipMemsetAsync(r.g.hdr, 0, kHdrWords * sizeof(uint32_t), s));
+    if (r.T > 0 && !lds_bin) GS_HIP(hipMemsetAsync(r.img.tile_count, 0, sizeof(uint32_t) * r.T, s));
+    PreprocessArgs pa = make_pp(in, tile);
+    pa.err_token = next_error_token();
+    if (r.T > 0 && lds_bin) {
+        pa.zero_words = r.img.tile_count;
+        pa.zero_n = r.T;
+    }
+    { StageTimer _t(kPre, s); launch_preprocess(pa, r.g, r.radii, lds_bin ? nullptr : r.img.tile_count, s); }
     stage_check(debug, s, "preprocess");
     if (lds_bin) { StageTimer _t(kCount, s); launch_count_tiles(in.P, r.g, r.radii, W, H, tile, r.img, s); }
     stage_check(debug, s, "count_tiles");
@@ -245,7 +266,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     } else {
         read_header(r.g.hdr, hdr, s);
     }
-    if (hdr[kHdrError])
+    if (in.prefiltered && hdr[kHdrError] == pa.err_token)
         throw GsError("Point is filtered although prefiltered is set. This shouldn't happen!");
     r.K = (int)hdr[kHdrNumRendered];
     const bool amr = tile == 32;  // the AMR layout appends records and region lists

@@ -28,6 +28,13 @@ struct PreprocessArgs {
     int block;  // tile edge in pixels (16 base, 32 AMR)
     int prefiltered;
     int store_cov3d;  // write the geometry buffer's cov3D (nothing in the path reads it back)
+    // Words the launch zeroes before anything reads them (the binning's tile
+    // histogram: no separate memset launch), and the value a prefiltered
+    // violation stores in the header's error word (a per-call token, so that
+    // word needs no zeroing either).
+    uint32_t* zero_words;
+    int zero_n;
+    uint32_t err_token;
 };
 
 // base/cr/forward.cu:155-256 (+ the tile histogram the binning needs).

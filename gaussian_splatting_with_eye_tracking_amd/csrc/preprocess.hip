@@ -93,6 +93,7 @@ template <bool kHasSH, bool kSH16, bool kCovPrecomp>
 __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomView g, int* __restrict__ radii,
                                                          uint32_t* __restrict__ tile_count) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    for (int i = idx; i < a.zero_n; i += (int)(gridDim.x * blockDim.x)) a.zero_words[i] = 0u;
     if (idx >= a.P) return;
     // AMR: the geometry buffer keeps its own copy of the radii (the progressive
     // steps return zero radii, their backward reads these); base: the caller's
@@ -125,7 +126,7 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
     // in_frustum (auxiliary.h:139-164): near plane only.
     const float3 p_view = transform_point_4x3(mx, my, mz, V);
     if (p_view.z <= 0.2f) {
-        if (a.prefiltered) atomicOr(&g.hdr[kHdrError], 1u);  // the reference __trap()s here
+        if (a.prefiltered) g.hdr[kHdrError] = a.err_token;  // the reference __trap()s here
         return;
     }
     const float4 p_hom = transform_point_4x4(mx, my, mz, Pm);

@@ -314,6 +314,16 @@ def test_prefiltered_violation_raises():
         C.rasterize_gaussians(s.bg, t["means3D"], torch.Tensor([]), t["opacities"], t["scales"], t["rotations"], 1.0,
                               torch.Tensor([]), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, 32, 32, t["shs"], 3,
                               s.campos, True, False)
+    # the header is not zeroed per call: the next calls (the caching allocator
+    # hands back the same geometry bytes, stale error word included) must not
+    # raise once every point is in front of the camera
+    ok = t["means3D"].clone()
+    ok[0, 2] = 5.0
+    for _ in range(3):
+        out = C.rasterize_gaussians(s.bg, ok, torch.Tensor([]), t["opacities"], t["scales"], t["rotations"], 1.0,
+                                    torch.Tensor([]), s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, 32, 32,
+                                    t["shs"], 3, s.campos, True, False)
+        assert out[0] > 0
 
 
 # ---------------------------------------------------------------- AMR ----
