@@ -861,6 +861,10 @@ int gs_set_tuning(const char* key, int value) {
         set_store_cov3d(value);
         return 0;
     }
+    if (std::strcmp(key, "amr_deep") == 0) {
+        set_amr_deep(value);
+        return 0;
+    }
     if (std::strcmp(key, "amr_fold") == 0) {
         set_amr_fold(value);
         return 0;

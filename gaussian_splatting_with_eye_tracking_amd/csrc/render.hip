@@ -606,8 +606,8 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     constexpr int kRgBatch = 16 * kPer;
     __shared__ float4 s_a[4][kRgBatch];
     __shared__ float4 s_b[4][kRgBatch];
-    __shared__ float s_c[4][kRgBatch];
-    __shared__ uint32_t s_pos[4][kRgBatch];
+    __shared__ __attribute__((aligned(16))) float s_c[4][kRgBatch];  // (b128 reads of 4 entries)
+    __shared__ __attribute__((aligned(16))) uint32_t s_pos[4][kRgBatch];
     const uint32_t bid = blockIdx.x, slot = bid >> 3;
     // the step's zero radii (the reference's torch::full(0) for steps >= 1)
     if (zero_radii)
@@ -796,6 +796,20 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
                 for (int j0 = 0; j0 < kRgBatch; j0 += kFold) {
                     float al[kFold][kSlots];
                     uint32_t okm[kSlots];  // entries j < m passing the alpha tests
+                    // the fold's colour and position of each entry, read once
+                    // here (the group's LDS reads are broadcasts, and at one
+                    // entry per pixel per step the LDS array, not the VALU,
+                    // is the busier unit): (r, g) from the record read the
+                    // alpha needs, b and the position four entries per b128
+                    float fr[kFold], fg[kFold], fb[kFold];
+                    uint32_t fp[kFold];
+#pragma unroll
+                    for (int e4 = 0; e4 < kFold; e4 += 4) {
+                        const float4 b4 = *reinterpret_cast<const float4*>(&s_c[h][j0 + e4]);
+                        const uint4 p4 = *reinterpret_cast<const uint4*>(&s_pos[h][j0 + e4]);
+                        fb[e4] = b4.x; fb[e4 + 1] = b4.y; fb[e4 + 2] = b4.z; fb[e4 + 3] = b4.w;
+                        fp[e4] = p4.x; fp[e4 + 1] = p4.y; fp[e4 + 2] = p4.z; fp[e4 + 3] = p4.w;
+                    }
 #pragma unroll
                     for (int k = 0; k < kSlots; k++) okm[k] = 0;
 #pragma unroll
@@ -803,6 +817,8 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
                         const int j = j0 + e;
                         const float4 a = s_a[h][j];
                         const float4 co = s_b[h][j];
+                        fr[e] = a.z;
+                        fg[e] = a.w;
 #pragma unroll
                         for (int k = 0; k < kSlots; k++) {
                             if (!active[k]) continue;  // wave-uniform
@@ -814,7 +830,6 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
                     bool alive = false;
 #pragma unroll
                     for (int e = 0; e < kFold; e++) {
-                        const int j = j0 + e;
 #pragma unroll
                         for (int k = 0; k < kSlots; k++) {
                             if (!active[k]) continue;
@@ -824,12 +839,11 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
                             done[k] = done[k] || stop;
                             if (hit && !stop) {
                                 const float w = al[e][k] * T_[k];
-                                const float4 a = s_a[h][j];
-                                C[k][0] = __builtin_fmaf(a.z, w, C[k][0]);
-                                C[k][1] = __builtin_fmaf(a.w, w, C[k][1]);
-                                C[k][2] = __builtin_fmaf(s_c[h][j], w, C[k][2]);
+                                C[k][0] = __builtin_fmaf(fr[e], w, C[k][0]);
+                                C[k][1] = __builtin_fmaf(fg[e], w, C[k][1]);
+                                C[k][2] = __builtin_fmaf(fb[e], w, C[k][2]);
                                 T_[k] = test_T;
-                                last[k] = s_pos[h][j] + 1;
+                                last[k] = fp[e] + 1;
                             }
                         }
                     }
@@ -937,6 +951,10 @@ void set_amr_batch(int v) { g_amr_batch = v == 2 ? 2 : 1; }
 // variant 4: bit k set = foveaStep k (bit 0: render_once) uses the
 // alpha-phase + fold-phase sub-batches; bit 5 = 16-entry sub-batches for the
 // steps (else 8)
+// variant 4 + fold: bit k set = foveaStep k stages 32 entries per batch
+// (two per lane: one batch of records in flight covers twice the blend work)
+int g_amr_deep = 0;
+void set_amr_deep(int v) { g_amr_deep = v; }
 int g_amr_fold = 0x1e;
 int g_amr_fold_n = 8;
 void set_amr_fold(int v) {
@@ -965,7 +983,8 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
                            fused ? zero_radii : nullptr)
         if (foveaStep > 0) {
             const bool fold = (g_amr_fold >> foveaStep) & 1;
-            if (fold && g_amr_fold_n == 16) GS_AMR_REGION(1, 1, 16);
+            if (fold && ((g_amr_deep >> foveaStep) & 1)) GS_AMR_REGION(1, 2, 8);
+            else if (fold && g_amr_fold_n == 16) GS_AMR_REGION(1, 1, 16);
             else if (fold) GS_AMR_REGION(1, 1, 8);
             else if (g_amr_batch == 2) GS_AMR_REGION(1, 2, 0);
             else GS_AMR_REGION(1, 1, 0);

@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--backward", action="store_true")
     ap.add_argument("--amr", action="store_true", help="time a 5-step foveated AMR frame instead")
     ap.add_argument("--amr-once", action="store_true", help="time AMR render_once (foveaStep -2, interpolated)")
+    ap.add_argument("--per-step", action="store_true", help="--amr: also time each fovea step's apply (events)")
     args = ap.parse_args()
 
     from gaussian_splatting_with_eye_tracking_amd import _C
@@ -68,12 +69,23 @@ def main():
             with torch.no_grad():
                 if args.amr_once:
                     return AR.apply(*a, -2, e, u8, u8, u8, True, ast)[0]
+                if args.per_step:
+                    evs[0].record()
                 c, _, gb, bb, ib = AR.apply(*a, 0, e, u8, u8, u8, False, ast)
+                if args.per_step:
+                    evs[1].record()
                 acc = c
                 for k in range(1, 5):
+                    if args.per_step:
+                        evs[2 * k].record()
                     c, _, gb, bb, ib = AR.apply(*a, k, acc, gb, bb, ib, False, ast)
+                    if args.per_step:
+                        evs[2 * k + 1].record()
                     acc = acc + c
             return acc
+
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(10)]
+    step_ms = {v: [] for v in args.values}
 
     ref_img = None
     results = {v: [] for v in args.values}
@@ -90,15 +102,24 @@ def main():
                 if d > 1e-5:
                     print(f"WARNING variant {v}: max image diff {d}")
             _C.profile_read(True)
+            acc_steps = np.zeros(5)
             for _ in range(args.iters):
                 run()
+                if args.amr and args.per_step:
+                    torch.cuda.synchronize()
+                    acc_steps += [evs[2 * k].elapsed_time(evs[2 * k + 1]) for k in range(5)]
             torch.cuda.synchronize()
+            if args.amr and args.per_step:
+                step_ms[v].append(acc_steps / args.iters)
             prof = _C.profile_read(True)
             ms, cnt = prof[args.stage]
             results[v].append(ms / max(cnt, 1))
     _C.profile_enable(False)
     out = {str(v): {"median_ms": float(np.median(x)), "min_ms": float(np.min(x)), "all": [round(a, 4) for a in x]}
            for v, x in results.items()}
+    if args.amr and args.per_step:
+        for v in args.values:
+            out[str(v)]["per_step_median_ms"] = [round(float(x), 4) for x in np.median(np.array(step_ms[v]), 0)]
     print(json.dumps({"key": args.key, "stage": args.stage, "results": out}))
 
 
