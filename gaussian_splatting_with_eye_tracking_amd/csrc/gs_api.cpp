@@ -861,6 +861,10 @@ int gs_set_tuning(const char* key, int value) {
         set_store_cov3d(value);
         return 0;
     }
+    if (std::strcmp(key, "amr_lists_per") == 0) {
+        set_amr_lists_per(value);
+        return 0;
+    }
     if (std::strcmp(key, "amr_deep") == 0) {
         set_amr_deep(value);
         return 0;

@@ -462,7 +462,11 @@ __global__ void __launch_bounds__(64) amr_quad_render_kernel(int W, int H, int t
 // One 256-thread workgroup per tile builds the records and the 16 lists
 // (ordered compaction by ballots, 256 entries per round).
 constexpr int kRlThreads = 256;
-constexpr int kRlPer = 4;  // entries per thread per pass (loads issued together)
+// entries per thread per pass (loads issued together): kRlPer * 256 entries a
+// pass (A/B at config 3, profiles/r02n_ab_lists_per.log: 2 -> 0.077 ms,
+// 4 -> 0.083, 8 -> 0.083: occupancy beats per-thread memory parallelism)
+int g_amr_lists_per = 2;
+void set_amr_lists_per(int v) { g_amr_lists_per = v; }
 // Region mask of one entry: the exact ellipse test (splat_rect_hit) on the
 // four 16x16 quadrants, refined to the 8x8 regions by the alpha >= 1/255
 // ellipse's bounding box (both conservative).  Bit g = 4 row + col.
@@ -494,6 +498,7 @@ __device__ __forceinline__ uint32_t region_mask(float2 xy, float4 co, float ox, 
 
 // rows: the per-Gaussian 64-B blend rows the AMR preprocess wrote into
 // grad_accum (preprocess.hip): (x, y, r, g), splat_coef, (b, raw conic).
+template <int kRlPer>
 __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, const uint32_t* __restrict__ ranges,
                                                                       const uint32_t* __restrict__ point_list,
                                                                       const float4* __restrict__ rows,
@@ -577,9 +582,17 @@ void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningVi
         return;
     }
     (void)features;  // in the rows (the preprocess saw colors_precomp / the SH colours)
-    hipLaunchKernelGGL(amr_region_lists_kernel, dim3(tgx * tgy), dim3(kRlThreads), 0, s, tgx, img.ranges,
-                       b.point_list, reinterpret_cast<const float4*>(g.grad_accum), ab.rec_a, ab.rec_b, ab.rec_c,
-                       ab.region_lists, img.region_count, img.tile_done);
+#define GS_RL_LAUNCH(PER)                                                                                       \
+    hipLaunchKernelGGL(amr_region_lists_kernel<PER>, dim3(tgx * tgy), dim3(kRlThreads), 0, s, tgx, img.ranges,     \
+                       b.point_list, reinterpret_cast<const float4*>(g.grad_accum), ab.rec_a, ab.rec_b, ab.rec_c,  \
+                       ab.region_lists, img.region_count, img.tile_done)
+    switch (g_amr_lists_per) {
+        case 2: GS_RL_LAUNCH(2); break;
+        case 5: GS_RL_LAUNCH(5); break;
+        case 8: GS_RL_LAUNCH(8); break;
+        default: GS_RL_LAUNCH(4); break;
+    }
+#undef GS_RL_LAUNCH
 }
 
 // One wave per (tile, quadrant): its four 16-lane groups are the quadrant's

@@ -400,6 +400,9 @@ def test_amr_foveated_steps(name, P, W, H, seed, amr_variant, amr_batch, amr_fol
                                rtol=1e-5, atol=1e-7)
 
 
+DEFAULT_AMR_LISTS_PER = 2  # render.hip g_amr_lists_per
+
+
 @pytest.mark.parametrize("P,W,H,seed", [(10000, 256, 256, 0), (60000, 160, 96, 4), (3000, 2112, 1056, 8)])
 def test_amr_fold_phases_bit_identical(P, W, H, seed):
     """The steps' alpha-phase + fold-phase batches (amr_fold, the default) and
@@ -410,15 +413,20 @@ def test_amr_fold_phases_bit_identical(P, W, H, seed):
     import gaussian_splatting_with_eye_tracking_amd._C as C
     sc, cam = G.scene_and_camera(P, W, H, seed)
     out = {}
-    variants = {"loop": (0, 0), "fold": (0x1e, 0), "deep": (0x1e, 0x1e)}
-    for name, (fold, deep) in variants.items():
+    # (amr_fold, amr_deep, amr_lists_per: entries per thread and pass of the
+    # region-lists build -- the lists must not depend on it)
+    variants = {"loop": (0, 0, 4), "fold": (0x1e, 0, 4), "deep": (0x1e, 0x1e, 4), "lists2": (0x1e, 0, 2),
+                "lists5": (0x1e, 0, 5), "lists8": (0x1e, 0, 8)}
+    for name, (fold, deep, lper) in variants.items():
         C.set_tuning("amr_fold", fold)
         C.set_tuning("amr_deep", deep)
+        C.set_tuning("amr_lists_per", lper)
         try:
             acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.2, 0.3))
         finally:
             C.set_tuning("amr_fold", 0x1e)
             C.set_tuning("amr_deep", 0)
+            C.set_tuning("amr_lists_per", DEFAULT_AMR_LISTS_PER)
         d = C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)
         K = int(d["hdr"][0].item())
         d = C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
@@ -426,7 +434,7 @@ def test_amr_fold_phases_bit_identical(P, W, H, seed):
         lv = d["levels"].cpu().numpy().astype(np.uint32)
         rendered = torch.from_numpy((O.amr_pixel_rounds(W, H) <= O.amr_tile_levels_per_pixel(lv, W, H)).reshape(-1))
         out[name] = [s_.cpu() for s_ in steps] + [d["n_contrib"].cpu()[rendered], d["accum_alpha"].cpu()[rendered]]
-    for name in ("fold", "deep"):
+    for name in ("fold", "deep", "lists2", "lists5", "lists8"):
         for a, b in zip(out["loop"], out[name]):
             assert torch.equal(a, b), name
 
