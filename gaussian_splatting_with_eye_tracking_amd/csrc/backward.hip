@@ -25,6 +25,8 @@
 // computeCov3D (:278-341) into one per-Gaussian pass that also emits the
 // reference's dL_dmeans2D / dL_dconic / dL_dopacity / dL_dcolors layout from
 // grad_accum, and writes every output element (zeros included).
+#include <algorithm>
+
 #include "gs_blend.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
@@ -70,6 +72,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // tiles with level >= k); < 0: render_once (rounds <= level).
     int tile;
     uint32_t ox, oy;
+    uint32_t gsel = 0xFu;  // row groups this block owns (a split heavy tile: a subset)
     // (a template parameter: run-time AMR branches cost the base kernel 12 %)
     constexpr uint32_t pstride = kAMR ? 2 : 1;
     if constexpr (kAMR) {
@@ -81,8 +84,13 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         ox = (uint32_t)(tile % gx) * 32 + sx;
         oy = (uint32_t)(tile / gx) * 32 + sy;
     } else {
-        tile = order ? (int)order[blockIdx.x]
-                     : xcd ? xcd_block_tile((int)blockIdx.x, gx, (int)(gridDim.x / gx)) : (int)blockIdx.x;
+        if (order) {
+            const uint32_t u = order[blockIdx.x];
+            tile = (int)(u & 0x0FFFFFFFu);
+            if (kWaves == 1 && (u >> 28)) gsel = u >> 28;
+        } else {
+            tile = xcd ? xcd_block_tile((int)blockIdx.x, gx, (int)(gridDim.x / gx)) : (int)blockIdx.x;
+        }
         ox = (uint32_t)(tile % gx) * 16;
         oy = (uint32_t)(tile / gx) * 16;
     }
@@ -91,7 +99,13 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     int m = kAMR ? n : min(n, (int)max_contrib[tile]);
     if (m == 0) return;  // block-uniform
 
-    const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, pstride);
+    PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, pstride);
+    if constexpr (kWaves == 1) {
+        // a split unit's other row groups are somebody else's: no pixel there
+        // (last = 0, so every one of their entries is culled below)
+#pragma unroll
+        for (int k = 0; k < kPPL; k++) px.inside[k] = px.inside[k] && ((gsel >> k) & 1u);
+    }
     const size_t plane = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
     // accum_rec . dL_dpix is all the reference's accum_rec / last_color
@@ -130,6 +144,10 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // wave per block (the only AMR instantiation) the wave max is the block's
     if constexpr (kAMR) {
         m = min(n, (int)wave_last);
+        if (m == 0) return;
+    } else if constexpr (kWaves == 1) {
+        // = max_contrib[tile] for a whole tile; a split unit's own, smaller max
+        m = min(m, __builtin_amdgcn_readfirstlane((int)wave_last));
         if (m == 0) return;
     }
     const float ddelx_dx = (float)(0.5 * W);
@@ -357,18 +375,35 @@ int g_bwd_flush = 0;
 void set_backward_flush(int v) { g_bwd_flush = v; }
 
 void set_backward_variant(int v) { g_bwd_variant = v; }
+// Heavy-tile split of the backward blend: the heaviest T * g_bwd_split_permille
+// / 1000 tiles run as g_bwd_split_ways units (row-group subsets) each, so the
+// launch's tail is not one wave walking the longest list for all 256 pixels.
+// Pixels and their per-pixel arithmetic are unchanged; only the grouping of
+// the per-(unit, Gaussian) atomic sums differs.
+int g_bwd_split_ways = 1;
+int g_bwd_split_permille = 0;
+void set_backward_split(int ways, int permille) {
+    g_bwd_split_ways = ways;
+    g_bwd_split_permille = permille;
+}
 
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s) {
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return;
     const uint32_t* order = nullptr;
+    int units = gx * gy;
     if (tile_order_enabled()) {
-        launch_order_tiles(gx * gy, img, true, s, gx, gy);
+        const bool one_wave = g_bwd_variant == 0 || g_bwd_variant == 3;
+        const int ways = (one_wave && !(g_xcd_map & 2) && (g_bwd_split_ways == 2 || g_bwd_split_ways == 4))
+                             ? g_bwd_split_ways : 1;
+        const int heavy = ways > 1 ? std::min(gx * gy, (int)((long)gx * gy * g_bwd_split_permille / 1000)) : 0;
+        launch_order_tiles(gx * gy, img, true, s, gx, gy, heavy, heavy ? ways : 1);
         order = img.tile_order;
+        units = gx * gy + (heavy ? (ways - 1) * heavy : 0);
     }
 #define GS_BWD_LAUNCH(PPL, WAVES, OCC, SWAP)                                                                    \
-    hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H,      \
+    hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP>), dim3(units), dim3(64 * WAVES), 0, s, W, H,      \
                        img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
                        dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1, 0, nullptr, g_bwd_flush)

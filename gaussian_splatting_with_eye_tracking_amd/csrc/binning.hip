@@ -20,6 +20,8 @@
 //      larger ones use an LDS chunk sort + in-block merge-path passes.
 // Per instance this moves ~20 B instead of the ~200 B of a 6-pass 64-bit
 // radix sort.
+#include <algorithm>
+
 #include "gs_blend.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
@@ -298,7 +300,8 @@ bool tile_order_enabled() { return g_tile_order != 0; }
 
 __global__ void __launch_bounds__(kOrderThreads) order_tiles_kernel(int T, const uint32_t* __restrict__ ranges,
                                                                     const uint32_t* __restrict__ max_contrib,
-                                                                    uint32_t* __restrict__ order) {
+                                                                    uint32_t* __restrict__ order, uint32_t split_tiles,
+                                                                    uint32_t split_ways) {
     __shared__ uint32_t hist[kOrderBuckets];
     __shared__ uint32_t s_wave[kOrderThreads / 64 + 1];
     const int tid = threadIdx.x;
@@ -317,7 +320,17 @@ __global__ void __launch_bounds__(kOrderThreads) order_tiles_kernel(int T, const
     __syncthreads();
     hist[tid] = base;
     __syncthreads();
-    for (int t = tid; t < T; t += kOrderThreads) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
+    for (int t = tid; t < T; t += kOrderThreads) {
+        const uint32_t r = atomicAdd(&hist[bucket(t)], 1u);
+        if (r < split_tiles) {  // one of the heaviest: split_ways units, each a set of row groups
+            for (uint32_t w = 0; w < split_ways; w++) {
+                const uint32_t sel = split_ways == 2 ? (w ? 0xCu : 0x3u) : 1u << w;
+                order[r * split_ways + w] = (uint32_t)t | (sel << 28);
+            }
+        } else {
+            order[r + (split_ways - 1) * split_tiles] = (uint32_t)t;
+        }
+    }
 }
 
 // XCD-aware variant (gs_blend.cuh placement): the tiles of XCD chunk x
@@ -359,15 +372,20 @@ __global__ void __launch_bounds__(kOrderThreads) order_tiles_xcd_kernel(int T, i
     }
 }
 
-void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s, int gx, int gy) {
+void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s, int gx, int gy,
+                        int split_tiles, int split_ways) {
     if (T <= 0) return;
-    if ((g_xcd_map & 2) && gx > 0 && T >= 8) {
+    if (split_ways != 2 && split_ways != 4) split_tiles = 0;
+    split_tiles = std::max(0, std::min(split_tiles, T));
+    if (split_tiles == 0) split_ways = 1;
+    if (split_tiles == 0 && (g_xcd_map & 2) && gx > 0 && T >= 8) {
         hipLaunchKernelGGL(order_tiles_xcd_kernel, dim3(1), dim3(kOrderThreads), 0, s, T, gx, gy, img.ranges,
                            use_max_contrib ? img.max_contrib : nullptr, img.tile_order);
         return;
     }
     hipLaunchKernelGGL(order_tiles_kernel, dim3(1), dim3(kOrderThreads), 0, s, T, img.ranges,
-                       use_max_contrib ? img.max_contrib : nullptr, img.tile_order);
+                       use_max_contrib ? img.max_contrib : nullptr, img.tile_order, (uint32_t)split_tiles,
+                       (uint32_t)split_ways);
 }
 
 // --------------------------------------------------------- tile sorting ---

@@ -885,6 +885,10 @@ int gs_set_tuning(const char* key, int value) {
         set_bin_chunk(value);
         return 0;
     }
+    if (std::strcmp(key, "bwd_split") == 0) {  // ways * 10000 + permille of the tiles split (0: off)
+        set_backward_split(value / 10000, value % 10000);
+        return 0;
+    }
     if (std::strcmp(key, "bwd_flush") == 0) {
         set_backward_flush(value);
         return 0;

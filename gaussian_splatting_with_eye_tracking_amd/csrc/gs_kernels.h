@@ -59,7 +59,13 @@ void set_bin_chunk(int gaussians_per_workgroup);
 // long tiles of a blend launch start early instead of forming its tail.
 // Work = range length, or min(range length, max_contrib) if use_max_contrib.
 // Used by the backward blend (render_bwd 1.15 -> 1.06 ms at config 2).
-void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s, int gx = 0, int gy = 0);
+// split_tiles > 0 (plain order only): the split_tiles heaviest tiles become
+// split_ways units each, entry = tile | (row-group set << 28) -- 2 ways: row
+// groups {0, 1} / {2, 3}, 4 ways: one row group each; the rest follow as
+// plain tile ids.  tile_order then holds T + (split_ways - 1) * split_tiles
+// entries (<= 4T).
+void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s, int gx = 0, int gy = 0,
+                        int split_tiles = 0, int split_ways = 1);
 bool tile_order_enabled();
 void set_tile_order(int v);
 void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int max_count_host, int num_large_host,
@@ -90,6 +96,7 @@ void set_ritnet_small_wgs(int v);
 void set_bwd_gauss_split(int v);  // 1: SH backward as its own kernel  // AMR blend geometry (as fwd_variant)  // row-group cull in the blend kernels (default on)
 void set_backward_variant(int v);
 void set_backward_flush(int v);
+void set_backward_split(int ways, int permille);  // heavy-tile split of the backward blend
 // Blend backward (base/cr/backward.cu:399-557) into g.grad_accum.
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s);

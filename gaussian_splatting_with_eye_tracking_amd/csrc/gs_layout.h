@@ -91,7 +91,8 @@ struct ImageView {
     uint32_t* levels_current;  // tile_AMR_levels_current
     uint32_t* pv;              // [4] percentile values (AMR)
     uint32_t* large_tiles;     // [T] list of tiles needing the large sort
-    uint32_t* tile_order;      // [T] tiles by descending blend work (launch order)
+    uint32_t* tile_order;      // [4T] tiles (or backward units: tile | row-group set << 28) by descending
+                               // blend work (launch order)
     uint32_t* quad_count;      // [T][4] AMR: entries of each 16x16 quadrant's sub-list
     uint32_t* region_count;    // [T][16] AMR: entries of each 8x8 region's sub-list
     uint32_t* tile_done;       // [T] AMR steps: finished (tile, quadrant) units, mod 4
@@ -111,7 +112,7 @@ inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
     g.levels_current = carve<uint32_t>(base, off, T);
     g.pv = carve<uint32_t>(base, off, 4);
     g.large_tiles = carve<uint32_t>(base, off, T);
-    g.tile_order = carve<uint32_t>(base, off, T);
+    g.tile_order = carve<uint32_t>(base, off, 4 * T);
     g.quad_count = carve<uint32_t>(base, off, 4 * T);
     g.region_count = carve<uint32_t>(base, off, 16 * T);
     g.tile_done = carve<uint32_t>(base, off, T);

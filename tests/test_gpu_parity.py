@@ -260,6 +260,19 @@ def test_bwd_gauss_split_matches_oracle(variant):
         C.set_tuning("bwd_gauss_split", 0)
 
 
+@pytest.mark.parametrize("split", [20300, 41000])
+def test_bwd_heavy_tile_split_matches_oracle(split):
+    """The backward blend with its heaviest tiles split into row-group units
+    (tuning "bwd_split": ways * 10000 + permille of the tiles; off by default,
+    measured slower, profiles/r02p_ab_bwd_split_*) against the oracle."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    try:
+        C.set_tuning("bwd_split", split)
+        test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
+    finally:
+        C.set_tuning("bwd_split", 0)
+
+
 def test_autograd_dropin_matches_direct_call():
     """The drop-in GaussianRasterizer (autograd) returns the same image and
     gradients as the raw _C calls, in the reference's gradient order."""

@@ -93,14 +93,26 @@ def main():
     for r in range(args.rounds):
         for v in args.values:
             _C.set_tuning(args.key, v)
+            if args.backward:
+                for x in (*t.values(), m2):
+                    x.grad = None
             img = run()  # warm
             torch.cuda.synchronize()
+            grads = [x.grad.detach().clone() for x in (*t.values(), m2)] if args.backward else []
+            if args.backward:
+                for x in (*t.values(), m2):
+                    x.grad = None
             if ref_img is None:
                 ref_img = img.detach().clone()
+                ref_grads = grads
             else:
                 d = float((img.detach() - ref_img).abs().max())
                 if d > 1e-5:
                     print(f"WARNING variant {v}: max image diff {d}")
+                for name, g, g0 in zip((*t.keys(), "means2D"), grads, ref_grads):
+                    rel = float((g - g0).abs().max() / g0.abs().max().clamp_min(1e-30))
+                    if rel > 1e-5:
+                        print(f"WARNING variant {v}: {name} grad max rel diff {rel:.2e}")
             _C.profile_read(True)
             acc_steps = np.zeros(5)
             for _ in range(args.iters):
