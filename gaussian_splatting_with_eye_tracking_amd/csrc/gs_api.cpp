@@ -19,6 +19,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/gsplat_amd.h"
@@ -143,6 +144,31 @@ void finish_header_read(uint32_t out[4]) {
     std::memcpy(out, pinned_words(), 4 * sizeof(uint32_t));
 }
 
+// Geometry buffers whose grad_accum rows the forward render zeroed and no
+// backward has consumed yet (keyed by the rows' address): the first backward
+// after such a forward skips its memset, any other zeroes the rows itself --
+// a second backward of one forward (retain_graph), an AMR geometry buffer
+// (its rows hold blend records), a forward that could not fuse the zeroing.
+std::mutex g_clean_mu;
+std::unordered_set<const float*> g_accum_clean;
+
+void set_accum_clean(const float* rows, bool clean) {
+    std::lock_guard<std::mutex> l(g_clean_mu);
+    if (clean) g_accum_clean.insert(rows);
+    else g_accum_clean.erase(rows);
+}
+
+bool take_accum_clean(const float* rows) {
+    std::lock_guard<std::mutex> l(g_clean_mu);
+    return g_accum_clean.erase(rows) > 0;
+}
+
+void zero_accum_unless_clean(const GeomView& g, int P, hipStream_t s) {
+    if (take_accum_clean(g.grad_accum)) return;
+    StageTimer _t(kZero, s);
+    GS_HIP(hipMemsetAsync(g.grad_accum, 0, sizeof(float) * kGradRow * (size_t)P, s));
+}
+
 char* call_resize(const gs_buffer& b, size_t n, const char* what) {
     if (!b.resize) throw GsError(std::string("no resize callback for ") + what);
     char* p = b.resize(b.ctx, n);
@@ -236,6 +262,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     const size_t N = (size_t)W * H;
     char* gbase = call_resize(geometry, carve_geom(nullptr, in.P, nullptr), "geometry");
     carve_geom(gbase, in.P, &r.g);
+    set_accum_clean(r.g.grad_accum, false);  // this forward decides afresh
     char* ibase = call_resize(image, carve_image(nullptr, N, r.T, nullptr), "image");
     carve_image(ibase, N, r.T, &r.img);
     r.radii = radii ? radii : r.g.radii;
@@ -302,7 +329,13 @@ int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image
                      viewmatrix, projmatrix, cam_pos, width, height, scale_modifier, tan_fovx, tan_fovy, prefiltered};
         Binned r = preprocess_and_bin(in, geometry, binning, image, radii, 16, debug != 0, s);
         const float* feats = colors_precomp ? colors_precomp : r.g.rgb;
-        { StageTimer _t(kRender, s); launch_render_forward(width, height, r.img, r.b, r.g, feats, background, out_color, s); }
+        bool zeroed;
+        {
+            StageTimer _t(kRender, s);
+            zeroed = launch_render_forward(width, height, r.img, r.b, r.g, feats, background, out_color, s,
+                                           r.g.grad_accum, (size_t)kGradRow * (size_t)P);
+        }
+        if (zeroed) set_accum_clean(r.g.grad_accum, true);
         stage_check(debug != 0, s, "render");
         return r.K;
     });
@@ -333,7 +366,7 @@ int rasterizer_backward_impl(int amr_mode, int P, int D, int M, int R, const flo
         carve_image(img_buffer, (size_t)width * height, T, &img);
         carve_binning(binning_buffer, R, &b);
         if (!radii) radii = g.radii;
-        { StageTimer _t(kZero, s); GS_HIP(hipMemsetAsync(g.grad_accum, 0, sizeof(float) * kGradRow * (size_t)P, s)); }
+        zero_accum_unless_clean(g, P, s);
         const float* colors = colors_precomp ? colors_precomp : g.rgb;
         if (R > 0) {
             StageTimer _t(kRenderBwd, s);
@@ -444,7 +477,7 @@ int gs_rasterizer_backward_view_grads(int P, int R, const float* background, int
         carve_image(img_buffer, (size_t)width * height, T, &img);
         carve_binning(binning_buffer, R, &b);
         if (!radii) radii = g.radii;
-        { StageTimer _t(kZero, s); GS_HIP(hipMemsetAsync(g.grad_accum, 0, sizeof(float) * kGradRow * (size_t)P, s)); }
+        zero_accum_unless_clean(g, P, s);
         const float* colors = colors_precomp ? colors_precomp : g.rgb;
         if (R > 0 && P > 0) { StageTimer _t(kRenderBwd, s); launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s); }
         stage_check(debug != 0, s, "render_backward");

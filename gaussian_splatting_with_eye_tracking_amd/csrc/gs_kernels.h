@@ -74,9 +74,11 @@ void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int ma
 void launch_reconstruct_keys(int T, const ImageView& img, const BinningView& b, const GeomView& g, uint64_t* keys,
                              hipStream_t s);
 
-// Blend (base/cr/forward.cu:261-374).
-void launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
-                           const float* features, const float* bg, float* out_color, hipStream_t s);
+// Blend (base/cr/forward.cu:261-374).  zero_rows: zeroed (zero_floats,
+// a multiple of 4, 16-B aligned) by the same launch; returns whether it was.
+bool launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
+                           const float* features, const float* bg, float* out_color, hipStream_t s,
+                           float* zero_rows = nullptr, size_t zero_floats = 0);
 // Tuning knob for A/B runs (gs_set_tuning("fwd_variant", v)).
 void set_forward_variant(int v);
 void set_xcd_map(int v);

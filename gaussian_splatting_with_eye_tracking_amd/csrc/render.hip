@@ -55,7 +55,14 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
                                                                  const float* __restrict__ bg,
                                                                  float* __restrict__ out_color, int cull,
                                                                  const uint32_t* __restrict__ order, int gx,
-                                                                 int xcd) {
+                                                                 int xcd, float4* __restrict__ zero4,
+                                                                 int zero_n4) {
+    // The backward's per-Gaussian accumulator rows (grad_accum, idle in the
+    // base forward) are zeroed here, behind the blend, instead of by a memset
+    // on the backward's critical path: fire-and-forget stores in a kernel
+    // bound by VALU / LDS, not HBM (gs_api.cpp: accum_clean).
+    for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < zero_n4; i += (int)(gridDim.x * blockDim.x))
+        zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     __shared__ float4 s_a[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
     __shared__ float s_b[64 * kWaves];
@@ -100,10 +107,13 @@ int g_fwd_variant = 2;  // 0: 1 wave x 4 px/lane, 1: 2 waves x 2 px/lane, 2: 4 w
 
 void set_forward_variant(int v) { g_fwd_variant = v; }
 
-void launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
-                           const float* features, const float* bg, float* out_color, hipStream_t s) {
+bool launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
+                           const float* features, const float* bg, float* out_color, hipStream_t s,
+                           float* zero_rows, size_t zero_floats) {
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
-    if (gx == 0 || gy == 0) return;
+    if (gx == 0 || gy == 0) return false;
+    float4* const zero4 = reinterpret_cast<float4*>(zero_rows);
+    const int zero_n4 = (zero_rows && zero_floats / 4 <= (size_t)INT32_MAX) ? (int)(zero_floats / 4) : 0;
     // Row-major launch: heaviest-first by range length measured slower here
     // (early termination makes the range a poor work estimate); the backward
     // orders by max_contrib instead (backward.hip).
@@ -112,13 +122,14 @@ void launch_render_forward(int W, int H, const ImageView& img, const BinningView
     hipLaunchKernelGGL((render_fwd_kernel<PPL, WAVES>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H, img.ranges, \
                        b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
-                       img.max_contrib, bg, out_color, g_cull, order, gx, g_xcd_map & 1)
+                       img.max_contrib, bg, out_color, g_cull, order, gx, g_xcd_map & 1, zero4, zero_n4)
     switch (g_fwd_variant) {
         case 0: GS_FWD_LAUNCH(4, 1); break;
         case 1: GS_FWD_LAUNCH(2, 2); break;
         default: GS_FWD_LAUNCH(1, 4); break;
     }
 #undef GS_FWD_LAUNCH
+    return zero_n4 > 0;
 }
 
 // ------------------------------------------------------------------- AMR ---

@@ -81,6 +81,8 @@ class _RasterizeGaussians(torch.autograd.Function):
                               radii if int(foveaStep) < 0 else torch.empty(0, dtype=torch.int32, device=radii.device),
                               sh, geomBuffer, binningBuffer, imgBuffer)
         ctx.mark_non_differentiable(radii, geomBuffer, binningBuffer, imgBuffer)
+        # no zero cotangents materialised for the radii and the byte buffers
+        ctx.set_materialize_grads(False)
         return color, radii, geomBuffer, binningBuffer, imgBuffer
 
     @staticmethod
@@ -98,7 +100,7 @@ class _RasterizeGaussians(torch.autograd.Function):
         reference's racy precomp-copy path) is not differentiated."""
         step = ctx.fovea_step
         nones = (None,) * 7
-        if step == 0:
+        if step == 0 or grad_color is None:
             return (None,) * 8 + nones
         if ctx.interpolate and step > 0:
             raise RuntimeError("the AMR backward differentiates interpolate_image only for render_once "

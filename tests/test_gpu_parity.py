@@ -295,6 +295,31 @@ def test_autograd_dropin_matches_direct_call():
                                   O.mark_visible(sc.means3D, cam.world_view_transform, cam.full_proj_transform))
 
 
+def test_second_backward_of_one_forward_rezeroes():
+    """The forward render zeroes the backward's accumulator rows (the first
+    backward skips its memset); a second backward of the same forward
+    (retain_graph) must zero them itself: equal gradients both times, and the
+    radii / unused-image cases hand autograd no materialised zeros."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    sc, cam = G.scene_and_camera(10000, 256, 256, 0)
+    s = G.torch_settings(cam)
+    t = G.scene_tensors(sc, requires_grad=True)
+    means2D = torch.zeros_like(t["means3D"], requires_grad=True)
+    color, radii = GaussianRasterizer(s)(means3D=t["means3D"], means2D=means2D, opacities=t["opacities"],
+                                         shs=t["shs"], scales=t["scales"], rotations=t["rotations"])
+    dpix = torch.randn_like(color)
+    keys = ("means3D", "opacities", "shs", "scales", "rotations")
+    g1 = torch.autograd.grad((color * dpix).sum(), [t[k] for k in keys] + [means2D], retain_graph=True)
+    g2 = torch.autograd.grad((color * dpix).sum(), [t[k] for k in keys] + [means2D])
+    for k, a, b in zip(keys + ("means2D",), g1, g2):
+        assert float((a - b).abs().max()) <= 1e-5 * max(float(a.abs().max()), 1e-30), k
+    # a loss on the radii alone: no gradient reaches the Gaussians
+    color, radii = GaussianRasterizer(s)(means3D=t["means3D"], means2D=means2D, opacities=t["opacities"],
+                                         shs=t["shs"], scales=t["scales"], rotations=t["rotations"])
+    gz = torch.autograd.grad(color.sum() * 0 + radii.float().sum() * 0, [t["means3D"]], allow_unused=True)
+    assert gz[0] is None or float(gz[0].abs().max()) == 0.0
+
+
 def test_empty_scene():
     from diff_gaussian_rasterization import GaussianRasterizer
     sc, cam = G.scene_and_camera(0, 64, 48)
