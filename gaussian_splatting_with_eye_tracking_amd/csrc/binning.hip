@@ -150,7 +150,9 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const float* __re
                                                         const float* __restrict__ depths,
                                                         const int* __restrict__ radii, int block, uint32_t gx,
                                                         uint32_t gy, uint32_t* __restrict__ cursor,
-                                                        uint64_t* __restrict__ pair_keys) {
+                                                        uint64_t* __restrict__ pair_keys,
+                                                        const uint32_t* __restrict__ hdr, uint32_t cap) {
+    if (hdr && hdr[kHdrNumRendered] > cap) return;  // speculative launch, K > cap (duplicate_lds_kernel)
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= P) return;
     const int rad = radii[idx];
@@ -237,7 +239,11 @@ __global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int c
                                                                     const int* __restrict__ radii, int block,
                                                                     uint32_t gx, uint32_t gy,
                                                                     uint32_t* __restrict__ cursor,
-                                                                    uint64_t* __restrict__ pair_keys) {
+                                                                    uint64_t* __restrict__ pair_keys,
+                                                                    const uint32_t* __restrict__ hdr, uint32_t cap) {
+    // speculative launch (hdr given): the keys fit the buffer only if K <= cap;
+    // otherwise nothing is touched (no cursor moved) and the host relaunches
+    if (hdr && hdr[kHdrNumRendered] > cap) return;
     extern __shared__ uint32_t slot[];
     const int T = (int)(gx * gy);
     for (int i = threadIdx.x; i < T; i += kBinThreads) slot[i] = 0;
@@ -275,18 +281,18 @@ void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H
 }
 
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
-                      const BinningView& b, hipStream_t s) {
+                      const BinningView& b, hipStream_t s, const uint32_t* spec_hdr, uint32_t spec_cap) {
     if (P == 0) return;
     const uint32_t gx = (uint32_t)((W + block - 1) / block), gy = (uint32_t)((H + block - 1) / block);
     if (gx * gy <= (uint32_t)kLdsTiles) {
         const int chunk = g_bin_chunk;
         hipLaunchKernelGGL(duplicate_lds_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
                            sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, g.depths, radii, block, gx, gy,
-                           img.tile_cursor, b.pair_keys);
+                           img.tile_cursor, b.pair_keys, spec_hdr, spec_cap);
         return;
     }
     hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, g.means2D, g.depths, radii,
-                       block, gx, gy, img.tile_cursor, b.pair_keys);
+                       block, gx, gy, img.tile_cursor, b.pair_keys, spec_hdr, spec_cap);
 }
 
 // ------------------------------------------------------- launch order ---

@@ -169,6 +169,13 @@ void zero_accum_unless_clean(const GeomView& g, int P, hipStream_t s) {
     GS_HIP(hipMemsetAsync(g.grad_accum, 0, sizeof(float) * kGradRow * (size_t)P, s));
 }
 
+// Capacity for the speculative duplicate: the last base forward's K plus
+// 1/8 (0 before the first call, or when speculation is switched off).
+int g_spec_dup = 1;  // set_tuning("spec_dup")
+thread_local size_t t_spec_cap = 0;
+size_t spec_capacity() { return g_spec_dup ? t_spec_cap : 0; }
+void note_k(int K) { t_spec_cap = K > 0 ? (size_t)K + (size_t)K / 8 + 4096 : 0; }
+
 char* call_resize(const gs_buffer& b, size_t n, const char* what) {
     if (!b.resize) throw GsError(std::string("no resize callback for ") + what);
     char* p = b.resize(b.ctx, n);
@@ -286,21 +293,40 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s); }
     stage_check(debug, s, "tile_scan");
     uint32_t hdr[4];
+    const bool amr = tile == 32;  // the AMR layout appends records and region lists
+    // Base forward: the duplicate is launched speculatively into a binning
+    // buffer sized for the capacity the last calls suggest, before K is on
+    // the host, so the GPU runs it while the host waits for K instead of
+    // idling through the read-back (~25 us per view at config 2).  The
+    // kernel does nothing if K > capacity; then the buffer is re-sized for K
+    // and the duplicate relaunched.  Only point_list (offset 0) outlives the
+    // forward, so a buffer carved for capacity >= K serves the backward as is.
+    bool dup_done = false;
+    const size_t cap = (!amr && !before_k && r.T > 0 && !debug) ? spec_capacity() : 0;
     if (before_k) {
         begin_header_read(r.g.hdr, s);
         before_k(r);
         finish_header_read(hdr);
+    } else if (cap > 0) {
+        begin_header_read(r.g.hdr, s);
+        char* sbase = call_resize(binning, carve_binning(nullptr, cap, nullptr), "binning");
+        carve_binning(sbase, cap, &r.b);
+        { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, r.g.hdr, (uint32_t)cap); }
+        finish_header_read(hdr);
+        dup_done = hdr[kHdrNumRendered] <= cap;
     } else {
         read_header(r.g.hdr, hdr, s);
     }
     if (in.prefiltered && hdr[kHdrError] == pa.err_token)
         throw GsError("Point is filtered although prefiltered is set. This shouldn't happen!");
     r.K = (int)hdr[kHdrNumRendered];
-    const bool amr = tile == 32;  // the AMR layout appends records and region lists
-    char* bbase = call_resize(binning, carve_binning(nullptr, r.K, nullptr, nullptr, amr), "binning");
-    carve_binning(bbase, r.K, &r.b, amr ? &r.ab : nullptr);
+    if (!amr) note_k(r.K);
+    if (!dup_done) {
+        char* bbase = call_resize(binning, carve_binning(nullptr, r.K, nullptr, nullptr, amr), "binning");
+        carve_binning(bbase, r.K, &r.b, amr ? &r.ab : nullptr);
+    }
     if (r.K > 0) {
-        { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s); }
+        if (!dup_done) { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s); }
         stage_check(debug, s, "duplicate");
         { StageTimer _t(kSort, s); launch_sort_tiles(r.T, r.img, r.b, (int)hdr[kHdrMaxTileCount], (int)hdr[kHdrNumLargeTiles], s); }
         stage_check(debug, s, "sort_tiles");
@@ -920,6 +946,10 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "bwd_split") == 0) {  // ways * 10000 + permille of the tiles split (0: off)
         set_backward_split(value / 10000, value % 10000);
+        return 0;
+    }
+    if (std::strcmp(key, "spec_dup") == 0) {  // speculative duplicate before the K read-back (base forward)
+        g_spec_dup = value;
         return 0;
     }
     if (std::strcmp(key, "bwd_flush") == 0) {

@@ -47,8 +47,11 @@ void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, c
 // Binning (replaces scan + duplicateWithKeys + radix sort + identifyTileRanges,
 // base/cr/rasterizer_impl.cu:277-318, with identical outputs).
 void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s);
+// spec_hdr: a speculative launch into a buffer of spec_cap keys, enqueued
+// before the host knows K; it does nothing when the header's K > spec_cap.
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
-                      const BinningView& b, hipStream_t s);
+                      const BinningView& b, hipStream_t s, const uint32_t* spec_hdr = nullptr,
+                      uint32_t spec_cap = 0);
 // Tile grids up to kLdsTiles are binned with workgroup-private LDS histograms
 // (count_tiles + chunked duplicate); larger grids use device atomics.
 constexpr int kLdsTiles = 16384;

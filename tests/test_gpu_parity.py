@@ -320,6 +320,41 @@ def test_second_backward_of_one_forward_rezeroes():
     assert gz[0] is None or float(gz[0].abs().max()) == 0.0
 
 
+def test_speculative_duplicate_matches_synchronous():
+    """The base forward launches the duplicate before K is on the host, into
+    a binning buffer sized by the previous call's K (+1/8): a call whose K
+    exceeds that capacity must relaunch it (here the 30k scene after the
+    10k one), a call within it must keep it; images and gradients are
+    bit-identical to the synchronous path (tuning "spec_dup" 0)."""
+    from diff_gaussian_rasterization import GaussianRasterizer
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    scenes = [G.scene_and_camera(P, 256, 192, seed) for P, seed in ((10000, 0), (30000, 1), (30000, 1), (8000, 2))]
+
+    def run():
+        out = []
+        for sc, cam in scenes:
+            s = G.torch_settings(cam)
+            t = G.scene_tensors(sc, requires_grad=True)
+            m2 = torch.zeros_like(t["means3D"], requires_grad=True)
+            color, radii = GaussianRasterizer(s)(means3D=t["means3D"], means2D=m2, opacities=t["opacities"],
+                                                 shs=t["shs"], scales=t["scales"], rotations=t["rotations"])
+            g = torch.autograd.grad((color * color).sum(), [t["means3D"], t["opacities"]])
+            out.append((color.detach().clone(), radii.clone()) + tuple(x.clone() for x in g))
+        return out
+
+    try:
+        C.set_tuning("spec_dup", 0)
+        ref = run()
+        C.set_tuning("spec_dup", 1)
+        spec = run()
+    finally:
+        C.set_tuning("spec_dup", 1)
+    for i, (a, b) in enumerate(zip(ref, spec)):
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), i
+        for x, y in zip(a[2:], b[2:]):
+            assert float((x - y).abs().max()) <= 1e-5 * max(float(x.abs().max()), 1e-30), i
+
+
 def test_empty_scene():
     from diff_gaussian_rasterization import GaussianRasterizer
     sc, cam = G.scene_and_camera(0, 64, 48)
