@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -128,19 +129,54 @@ void read_header(const uint32_t* hdr_dev, uint32_t out[4], hipStream_t s) {
 // The same read-back in two halves: the copy (and an event behind it) is
 // enqueued, the caller enqueues work that does not depend on K, then waits for
 // the copy alone -- that work runs while the host reacts to K.
-hipEvent_t header_event() {
-    thread_local hipEvent_t e = nullptr;
-    if (!e) GS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    return e;
+
+// With side_copy the copy runs on a side stream behind an event on s, so the
+// work enqueued on s after it (the speculative duplicate, the AMR step-0
+// levels) would start right after the tile scan instead of after the copy.
+struct SideStream {
+    hipStream_t s = nullptr;
+    hipEvent_t ready = nullptr;
+    hipEvent_t done = nullptr;
+};
+
+SideStream& side_stream() {
+    thread_local std::vector<SideStream> per_device;
+    int dev = 0;
+    GS_HIP(hipGetDevice(&dev));
+    if ((int)per_device.size() <= dev) per_device.resize(dev + 1);
+    SideStream& ss = per_device[dev];
+    if (!ss.s) {
+        GS_HIP(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
+        GS_HIP(hipEventCreateWithFlags(&ss.ready, hipEventDisableTiming));
+        GS_HIP(hipEventCreateWithFlags(&ss.done, hipEventDisableTiming));
+    }
+    return ss;
 }
 
+// (measured slower: cfg2 859 -> 834, cfg3 1576 -> 1548 frames/s,
+// profiles/r02p_ab_side_copy.log; the event record + cross-stream wait cost
+// more than the ~6 us dispatch gap they remove)
+int g_side_copy = -1;  // set_tuning("side_copy"); -1: GSAMD_SIDE_COPY (default 0)
+
 void begin_header_read(const uint32_t* hdr_dev, hipStream_t s) {
-    GS_HIP(hipMemcpyAsync(pinned_words(), hdr_dev, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    GS_HIP(hipEventRecord(header_event(), s));
+    if (g_side_copy < 0) {
+        const char* e = std::getenv("GSAMD_SIDE_COPY");
+        g_side_copy = e ? std::atoi(e) : 0;
+    }
+    SideStream& ss = side_stream();
+    if (!g_side_copy) {
+        GS_HIP(hipMemcpyAsync(pinned_words(), hdr_dev, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        GS_HIP(hipEventRecord(ss.done, s));
+        return;
+    }
+    GS_HIP(hipEventRecord(ss.ready, s));
+    GS_HIP(hipStreamWaitEvent(ss.s, ss.ready, 0));
+    GS_HIP(hipMemcpyAsync(pinned_words(), hdr_dev, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, ss.s));
+    GS_HIP(hipEventRecord(ss.done, ss.s));
 }
 
 void finish_header_read(uint32_t out[4]) {
-    GS_HIP(hipEventSynchronize(header_event()));
+    GS_HIP(hipEventSynchronize(side_stream().done));
     std::memcpy(out, pinned_words(), 4 * sizeof(uint32_t));
 }
 
@@ -946,6 +982,10 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "bwd_split") == 0) {  // ways * 10000 + permille of the tiles split (0: off)
         set_backward_split(value / 10000, value % 10000);
+        return 0;
+    }
+    if (std::strcmp(key, "side_copy") == 0) {  // K read-back on a side stream
+        g_side_copy = value;
         return 0;
     }
     if (std::strcmp(key, "spec_dup") == 0) {  // speculative duplicate before the K read-back (base forward)

@@ -294,7 +294,7 @@ typedef struct {
     uint32_t* levels_current;
     uint32_t* pv; /* [4] */
     uint32_t* large_tiles;
-    uint32_t* tile_order; /* [T] blend launch order (descending work) */
+    uint32_t* tile_order; /* [4T] blend launch order (descending work; backward units) */
     uint32_t* quad_count; /* [T][4] AMR quadrant sub-list lengths */
     uint32_t* region_count; /* [T][16] AMR 8x8-region sub-list lengths */
     uint32_t* tile_done; /* [T] AMR steps: finished units per tile, mod 4 */
