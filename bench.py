@@ -107,7 +107,9 @@ def algorithmic_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: in
     if stage == "preprocess":   # means 12 + radii 4 + tiles_touched 4 per P; per V: scales 12, rot 16,
         return 20.0 * P + 289.0 * V  # opacity 4, SH 192 in; depth 4, xy 8, conic 16, rgb 12, cov 24, clamped 1 out
     if stage == "render":       # per entry: id 4 + xy 8 + conic/opacity 16 + rgb 12; per pixel: colour 12,
-        return 40.0 * Kb + 20.0 * N + 12.0 * T  # final T 4, n_contrib 4; per tile: range 8 + max_contrib 4
+        # final T 4, n_contrib 4; per tile: range 8 + max_contrib 4; + the backward's 64-B accumulator
+        # rows, zeroed by this launch since r02p (the former zero_accum memset)
+        return 40.0 * Kb + 20.0 * N + 12.0 * T + 64.0 * P
     if stage == "render_bwd":   # per entry: the same 40 B + 9 accumulated floats 36; per pixel: dL/dpix 12,
         return 76.0 * Kb + 20.0 * N + 12.0 * T  # final T 4, n_contrib 4; per tile 12
     if stage == "bwd_gauss":    # radii 4 + all 75 gradient floats 300 per P; per V: accum 36, means 12,
