@@ -46,7 +46,13 @@ const char* gs_last_error(void);
 
 /* Replaces CudaRasterizer::Rasterizer::forward
  * (base/cr/rasterizer.h:35-59, base/cr/rasterizer_impl.cu:198-336).
- * Reads K back to the host once (to size the binning buffer). */
+ * Reads K back to the host once.  The binning buffer may be sized for more
+ * than K entries: the duplicate is launched before K reaches the host into a
+ * buffer sized from the previous call's K (+1/8), re-sized for K only when K
+ * exceeds that; only its first 4K bytes (point_list) are read afterwards, by
+ * gs_rasterizer_backward with R = the returned K.  Its size is therefore not
+ * gs_binning_bytes(K) in general (gs_binning_count_of_bytes gives the
+ * capacity, not K). */
 int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image, int P, int D, int M,
                           const float* background, int width, int height, const float* means3D, const float* shs,
                           const float* colors_precomp, const float* opacities, const float* scales,
