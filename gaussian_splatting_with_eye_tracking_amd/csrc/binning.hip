@@ -132,7 +132,96 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const ui
     }
 }
 
+// The same scan with tile i = k * kScanThreads + tid (slice k of the thread):
+// every count load and every range / cursor store is wave-contiguous (the
+// thread-contiguous layout above issues each store as 64 scattered sector
+// writes from the one CU).  The kS slices are scanned together: a 64-lane
+// shuffle scan per slice, the per-(wave, slice) totals through LDS, one
+// barrier; slice k's base is the total of slices < k.  Same sums, same order of
+// the integer adds' results: bit-identical ranges, cursors, K.
+template <int kS>
+__global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, const uint32_t* __restrict__ count,
+                                                                        uint32_t* __restrict__ ranges,
+                                                                        uint32_t* __restrict__ cursor,
+                                                                        uint32_t* __restrict__ large_tiles,
+                                                                        uint32_t* __restrict__ hdr) {
+    constexpr int kW = kScanThreads / 64;
+    __shared__ uint32_t s_tot[kW][kS];
+    __shared__ uint32_t s_max[kW];
+    __shared__ uint32_t nlarge;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t c[kS], incl[kS];
+    uint32_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < kS; k++) {
+        const int i = k * kScanThreads + tid;
+        c[k] = i < T ? count[i] : 0u;
+        incl[k] = c[k];
+        mx = max(mx, c[k]);
+    }
+    if (tid == 0) nlarge = 0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+        for (int k = 0; k < kS; k++) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl[k], d, 64);
+            if (lane >= d) incl[k] += y;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+    if (lane == 63) {
+#pragma unroll
+        for (int k = 0; k < kS; k++) s_tot[wave][k] = incl[k];
+        s_max[wave] = mx;
+    }
+    __syncthreads();
+    uint32_t run = 0;  // total of the slices before k
+#pragma unroll
+    for (int k = 0; k < kS; k++) {
+        uint32_t wbase = 0, stot = 0;
+#pragma unroll
+        for (int w = 0; w < kW; w++) {
+            const uint32_t v = s_tot[w][k];
+            stot += v;
+            wbase += w < wave ? v : 0u;
+        }
+        const int i = k * kScanThreads + tid;
+        if (i < T) {
+            const uint32_t ex = run + wbase + incl[k] - c[k];
+            // identifyTileRanges leaves empty tiles at (0,0) (rasterizer_impl.cu:310)
+            reinterpret_cast<uint2*>(ranges)[i] = make_uint2(c[k] ? ex : 0u, c[k] ? ex + c[k] : 0u);
+            cursor[i] = ex;
+            if (c[k] > (uint32_t)kSmallCap) large_tiles[atomicAdd(&nlarge, 1u)] = (uint32_t)i;
+        }
+        run += stot;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t m = 0;
+        for (int w = 0; w < kW; w++) m = max(m, s_max[w]);
+        hdr[kHdrNumRendered] = run;
+        hdr[kHdrMaxTileCount] = m;
+        hdr[kHdrNumLargeTiles] = nlarge;
+        hdr[kHdrT] = (uint32_t)T;
+    }
+}
+
+int g_scan_slices = 1;  // set_tuning("scan_slices"): 0 = the thread-contiguous scan
+void set_scan_slices(int v) { g_scan_slices = v; }
+
 void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s) {
+    if (g_scan_slices) {
+        const int slices = (T + kScanThreads - 1) / kScanThreads;
+#define GS_SLICE_LAUNCH(S)                                                                                        \
+    hipLaunchKernelGGL(tile_scan_slices_kernel<S>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count,         \
+                       img.ranges, img.tile_cursor, img.large_tiles, hdr)
+        if (slices <= 1) { GS_SLICE_LAUNCH(1); return; }
+        if (slices <= 2) { GS_SLICE_LAUNCH(2); return; }
+        if (slices <= 4) { GS_SLICE_LAUNCH(4); return; }
+        if (slices <= 8) { GS_SLICE_LAUNCH(8); return; }
+#undef GS_SLICE_LAUNCH
+    }
 #define GS_SCAN_LAUNCH(PER)                                                                                      \
     hipLaunchKernelGGL(tile_scan_kernel<PER>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count, img.ranges, \
                        img.tile_cursor, img.large_tiles, hdr)

@@ -984,6 +984,10 @@ int gs_set_tuning(const char* key, int value) {
         set_backward_split(value / 10000, value % 10000);
         return 0;
     }
+    if (std::strcmp(key, "scan_slices") == 0) {  // wave-contiguous tile scan (0: thread-contiguous)
+        set_scan_slices(value);
+        return 0;
+    }
     if (std::strcmp(key, "side_copy") == 0) {  // K read-back on a side stream
         g_side_copy = value;
         return 0;

@@ -273,6 +273,18 @@ def test_bwd_heavy_tile_split_matches_oracle(split):
         C.set_tuning("bwd_split", 0)
 
 
+@pytest.mark.parametrize("name,P,W,H,seed", CASES[1:3])
+def test_thread_contiguous_tile_scan_matches_oracle(name, P, W, H, seed):
+    """The thread-contiguous tile scan (tuning "scan_slices" 0; the default is
+    the wave-contiguous sliced scan every other test runs) against the oracle."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    try:
+        C.set_tuning("scan_slices", 0)
+        test_forward_buffers_bit_exact(name, P, W, H, seed)
+    finally:
+        C.set_tuning("scan_slices", 1)
+
+
 def test_autograd_dropin_matches_direct_call():
     """The drop-in GaussianRasterizer (autograd) returns the same image and
     gradients as the raw _C calls, in the reference's gradient order."""
