@@ -46,7 +46,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const float4* __restrict__ conic_opacity, const float* __restrict__ colors, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ bg,
     float* __restrict__ grad_accum, int cull, const uint32_t* __restrict__ order, int gx, int xcd,
-    int amr_mode, const uint32_t* __restrict__ levels, int flush_mode) {
+    int amr_mode, const uint32_t* __restrict__ levels, int flush_mode, const uint32_t* __restrict__ bucket_count,
+    const uint32_t* __restrict__ bucket_list) {
 #pragma clang fp contract(fast)
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
@@ -84,7 +85,23 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         ox = (uint32_t)(tile % gx) * 32 + sx;
         oy = (uint32_t)(tile / gx) * 32 + sy;
     } else {
-        if (order) {
+        if (kWaves == 1 && bucket_count) {
+            // rank blockIdx.x of the heaviest-first order: the bucket whose
+            // inclusive count first exceeds it (64 buckets, one per lane)
+            const uint32_t c = bucket_count[lane];
+            uint32_t incl = c;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+                if (lane >= d) incl += y;
+            }
+            const uint32_t rank = blockIdx.x;
+            const uint64_t past = __ballot(incl > rank);
+            if (past == 0ull) return;  // (counts short of the grid: cannot happen after a forward)
+            const int b = __builtin_ctzll(past);
+            const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)(incl - c), b);
+            tile = (int)bucket_list[(size_t)b * gridDim.x + (rank - base)];
+        } else if (order) {
             const uint32_t u = order[blockIdx.x];
             tile = (int)(u & 0x0FFFFFFFu);
             if (kWaves == 1 && (u >> 28)) gsel = u >> 28;
@@ -380,6 +397,10 @@ void set_backward_variant(int v) { g_bwd_variant = v; }
 // launch's tail is not one wave walking the longest list for all 256 pixels.
 // Pixels and their per-pixel arithmetic are unchanged; only the grouping of
 // the per-(unit, Gaussian) atomic sums differs.
+// Backward launch order from the forward render's 64 work buckets (no sort
+// kernel); 0: the one-workgroup counting sort (order_tiles_kernel).
+int g_bucket_order = 1;
+void set_bucket_order(int v) { g_bucket_order = v; }
 int g_bwd_split_ways = 1;
 int g_bwd_split_permille = 0;
 void set_backward_split(int ways, int permille) {
@@ -392,8 +413,14 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return;
     const uint32_t* order = nullptr;
+    const uint32_t *bcount = nullptr, *blist = nullptr;
     int units = gx * gy;
-    if (tile_order_enabled()) {
+    const bool one_wave_v = g_bwd_variant == 0 || g_bwd_variant == 3;
+    if (tile_order_enabled() && g_bucket_order && one_wave_v && !(g_xcd_map & 2) &&
+        !(g_bwd_split_ways == 2 || g_bwd_split_ways == 4)) {
+        bcount = img.bucket_count;  // filled by this image buffer's forward render
+        blist = img.bucket_list;
+    } else if (tile_order_enabled()) {
         const bool one_wave = g_bwd_variant == 0 || g_bwd_variant == 3;
         const int ways = (one_wave && !(g_xcd_map & 2) && (g_bwd_split_ways == 2 || g_bwd_split_ways == 4))
                              ? g_bwd_split_ways : 1;
@@ -406,7 +433,8 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
     hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP>), dim3(units), dim3(64 * WAVES), 0, s, W, H,      \
                        img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
-                       dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1, 0, nullptr, g_bwd_flush)
+                       dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1, 0, nullptr, g_bwd_flush, \
+                       bcount, blist)
     switch (g_bwd_variant) {
         case 1: GS_BWD_LAUNCH(2, 2, 4, true); break;
         case 2: GS_BWD_LAUNCH(1, 4, 4, true); break;
@@ -428,7 +456,7 @@ void launch_amr_render_backward(int W, int H, int mode, const ImageView& img, co
     hipLaunchKernelGGL((render_bwd_kernel<4, 1, 4, true, true>), dim3(4 * tgx * tgy), dim3(64), 0, s, W, H, img.ranges,
                        img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,
-                       dL_dpix, bg, g.grad_accum, g_cull, nullptr, tgx, 0, mode, img.levels, 0);
+                       dL_dpix, bg, g.grad_accum, g_cull, nullptr, tgx, 0, mode, img.levels, 0, nullptr, nullptr);
 }
 
 // ------------------------------------------------------ per-Gaussian bwd ---

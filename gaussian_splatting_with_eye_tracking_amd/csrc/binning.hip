@@ -74,11 +74,13 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const ui
                                                                  uint32_t* __restrict__ ranges,
                                                                  uint32_t* __restrict__ cursor,
                                                                  uint32_t* __restrict__ large_tiles,
-                                                                 uint32_t* __restrict__ hdr) {
+                                                                 uint32_t* __restrict__ hdr,
+                                                                 uint32_t* __restrict__ bucket_count) {
     __shared__ uint32_t s_wave[kScanThreads / 64 + 1];
     __shared__ uint32_t s_max[kScanThreads / 64];
     __shared__ uint32_t nlarge;
     const int tid = threadIdx.x;
+    if (tid < kOrderBuckets64) bucket_count[tid] = 0;  // the forward render appends to the buckets
     const int per = kPer > 0 ? kPer : (T + kScanThreads - 1) / kScanThreads;
     const int beg = min(T, tid * per), end = min(T, beg + per);
     uint32_t sum = 0, mx = 0;
@@ -144,8 +146,10 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, c
                                                                         uint32_t* __restrict__ ranges,
                                                                         uint32_t* __restrict__ cursor,
                                                                         uint32_t* __restrict__ large_tiles,
-                                                                        uint32_t* __restrict__ hdr) {
+                                                                        uint32_t* __restrict__ hdr,
+                                                                        uint32_t* __restrict__ bucket_count) {
     constexpr int kW = kScanThreads / 64;
+    if (threadIdx.x < kOrderBuckets64) bucket_count[threadIdx.x] = 0;  // the forward render appends
     __shared__ uint32_t s_tot[kW][kS];
     __shared__ uint32_t s_max[kW];
     __shared__ uint32_t nlarge;
@@ -215,7 +219,7 @@ void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s)
         const int slices = (T + kScanThreads - 1) / kScanThreads;
 #define GS_SLICE_LAUNCH(S)                                                                                        \
     hipLaunchKernelGGL(tile_scan_slices_kernel<S>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count,         \
-                       img.ranges, img.tile_cursor, img.large_tiles, hdr)
+                       img.ranges, img.tile_cursor, img.large_tiles, hdr, img.bucket_count)
         if (slices <= 1) { GS_SLICE_LAUNCH(1); return; }
         if (slices <= 2) { GS_SLICE_LAUNCH(2); return; }
         if (slices <= 4) { GS_SLICE_LAUNCH(4); return; }
@@ -224,7 +228,7 @@ void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s)
     }
 #define GS_SCAN_LAUNCH(PER)                                                                                      \
     hipLaunchKernelGGL(tile_scan_kernel<PER>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count, img.ranges, \
-                       img.tile_cursor, img.large_tiles, hdr)
+                       img.tile_cursor, img.large_tiles, hdr, img.bucket_count)
     const int per = (T + kScanThreads - 1) / kScanThreads;
     if (per <= 2) GS_SCAN_LAUNCH(2);
     else if (per <= 4) GS_SCAN_LAUNCH(4);

@@ -984,6 +984,10 @@ int gs_set_tuning(const char* key, int value) {
         set_backward_split(value / 10000, value % 10000);
         return 0;
     }
+    if (std::strcmp(key, "bucket_order") == 0) {  // backward order from the forward's work buckets
+        set_bucket_order(value);
+        return 0;
+    }
     if (std::strcmp(key, "scan_slices") == 0) {  // wave-contiguous tile scan (0: thread-contiguous)
         set_scan_slices(value);
         return 0;

@@ -102,7 +102,8 @@ void set_bwd_gauss_split(int v);  // 1: SH backward as its own kernel  // AMR bl
 void set_backward_variant(int v);
 void set_backward_flush(int v);
 void set_backward_split(int ways, int permille);
-void set_scan_slices(int v);  // heavy-tile split of the backward blend
+void set_scan_slices(int v);
+void set_bucket_order(int v);  // heavy-tile split of the backward blend
 // Blend backward (base/cr/backward.cu:399-557) into g.grad_accum.
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s);

@@ -56,7 +56,8 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
                                                                  float* __restrict__ out_color, int cull,
                                                                  const uint32_t* __restrict__ order, int gx,
                                                                  int xcd, float4* __restrict__ zero4,
-                                                                 int zero_n4) {
+                                                                 int zero_n4, uint32_t* __restrict__ bucket_count,
+                                                                 uint32_t* __restrict__ bucket_list) {
     // The backward's per-Gaussian accumulator rows (grad_accum, idle in the
     // base forward) are zeroed here, behind the blend, instead of by a memset
     // on the backward's critical path: fire-and-forget stores in a kernel
@@ -82,12 +83,20 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
 #pragma unroll
     for (int k = 0; k < kPPL; k++) m = max(m, px.inside[k] ? st.last[k] : 0u);
     m = wave_max_u32(m);
-    if (kWaves == 1) {
-        if (threadIdx.x == 0) max_contrib[tile] = m;
-    } else {
+    if (kWaves > 1) {
         if ((threadIdx.x & 63) == 0) atomicMax(&s_max, m);
         __syncthreads();
-        if (threadIdx.x == 0) max_contrib[tile] = s_max;
+        m = s_max;
+    }
+    if (threadIdx.x == 0) {
+        max_contrib[tile] = m;
+        // the backward's heaviest-first launch order: this tile joins its work
+        // bucket's list (render_bwd_kernel finds its tile from the counts; no
+        // sort kernel between the passes)
+        if (bucket_count) {
+            const uint32_t b = order_bucket64(min(range.y - range.x, m));
+            bucket_list[(size_t)b * gridDim.x + atomicAdd(&bucket_count[b], 1u)] = (uint32_t)tile;
+        }
     }
 }
 
@@ -122,7 +131,8 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
     hipLaunchKernelGGL((render_fwd_kernel<PPL, WAVES>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H, img.ranges, \
                        b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
-                       img.max_contrib, bg, out_color, g_cull, order, gx, g_xcd_map & 1, zero4, zero_n4)
+                       img.max_contrib, bg, out_color, g_cull, order, gx, g_xcd_map & 1, zero4, zero_n4,     \
+                       img.bucket_count, img.bucket_list)
     switch (g_fwd_variant) {
         case 0: GS_FWD_LAUNCH(4, 1); break;
         case 1: GS_FWD_LAUNCH(2, 2); break;

@@ -285,6 +285,21 @@ def test_thread_contiguous_tile_scan_matches_oracle(name, P, W, H, seed):
         C.set_tuning("scan_slices", 1)
 
 
+@pytest.mark.parametrize("bucket_order", [0, 1])
+def test_bwd_launch_order_sources_match_oracle(bucket_order):
+    """The backward's heaviest-first tile order from the one-workgroup
+    counting sort (0) or from the 64 work buckets the forward render appends
+    its tiles to (1, the default: no order kernel) against the oracle; the
+    second-backward test reuses the buckets of one forward."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    try:
+        C.set_tuning("bucket_order", bucket_order)
+        test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
+        test_backward_parity("ragged_3k_250x130", 3000, 250, 130, 7, "colors_precomp")
+    finally:
+        C.set_tuning("bucket_order", 1)
+
+
 def test_autograd_dropin_matches_direct_call():
     """The drop-in GaussianRasterizer (autograd) returns the same image and
     gradients as the raw _C calls, in the reference's gradient order."""
