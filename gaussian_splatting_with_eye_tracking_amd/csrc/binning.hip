@@ -66,6 +66,15 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
 }
 
 // ------------------------------------------------------------ tile scan ---
+// The host's copy of the first four header words, stored straight into
+// mapped, coherent host memory (vector stores over the fabric) by the scan:
+// the forward's read-back then needs no copy kernel, only an event after the
+// scan.
+__device__ __forceinline__ void mirror_header(uint32_t* m, uint32_t K, uint32_t err, uint32_t maxc, uint32_t nlarge) {
+    *reinterpret_cast<uint4*>(m) = make_uint4(K, err, maxc, nlarge);  // kHdrNumRendered, kHdrError, kHdrMaxTileCount, kHdrNumLargeTiles
+}
+
+
 // kPer > 0: T <= 1024 kPer, each thread's kPer counts loaded by an unrolled
 // loop (all loads in flight at once, no serial load-add chain: 16 -> 5 us at
 // 8160 tiles); kPer = 0: any T, run-time loop.
@@ -75,7 +84,8 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const ui
                                                                  uint32_t* __restrict__ cursor,
                                                                  uint32_t* __restrict__ large_tiles,
                                                                  uint32_t* __restrict__ hdr,
-                                                                 uint32_t* __restrict__ bucket_count) {
+                                                                 uint32_t* __restrict__ bucket_count,
+                                                                 uint32_t* __restrict__ hdr_mirror) {
     __shared__ uint32_t s_wave[kScanThreads / 64 + 1];
     __shared__ uint32_t s_max[kScanThreads / 64];
     __shared__ uint32_t nlarge;
@@ -131,6 +141,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const ui
         hdr[kHdrMaxTileCount] = m;
         hdr[kHdrNumLargeTiles] = nlarge;
         hdr[kHdrT] = (uint32_t)T;
+        if (hdr_mirror) mirror_header(hdr_mirror, total, hdr[kHdrError], m, nlarge);
     }
 }
 
@@ -147,7 +158,8 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, c
                                                                         uint32_t* __restrict__ cursor,
                                                                         uint32_t* __restrict__ large_tiles,
                                                                         uint32_t* __restrict__ hdr,
-                                                                        uint32_t* __restrict__ bucket_count) {
+                                                                        uint32_t* __restrict__ bucket_count,
+                                                                        uint32_t* __restrict__ hdr_mirror) {
     constexpr int kW = kScanThreads / 64;
     if (threadIdx.x < kOrderBuckets64) bucket_count[threadIdx.x] = 0;  // the forward render appends
     __shared__ uint32_t s_tot[kW][kS];
@@ -208,18 +220,19 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, c
         hdr[kHdrMaxTileCount] = m;
         hdr[kHdrNumLargeTiles] = nlarge;
         hdr[kHdrT] = (uint32_t)T;
+        if (hdr_mirror) mirror_header(hdr_mirror, run, hdr[kHdrError], m, nlarge);
     }
 }
 
 int g_scan_slices = 1;  // set_tuning("scan_slices"): 0 = the thread-contiguous scan
 void set_scan_slices(int v) { g_scan_slices = v; }
 
-void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s) {
+void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror) {
     if (g_scan_slices) {
         const int slices = (T + kScanThreads - 1) / kScanThreads;
 #define GS_SLICE_LAUNCH(S)                                                                                        \
     hipLaunchKernelGGL(tile_scan_slices_kernel<S>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count,         \
-                       img.ranges, img.tile_cursor, img.large_tiles, hdr, img.bucket_count)
+                       img.ranges, img.tile_cursor, img.large_tiles, hdr, img.bucket_count, hdr_mirror)
         if (slices <= 1) { GS_SLICE_LAUNCH(1); return; }
         if (slices <= 2) { GS_SLICE_LAUNCH(2); return; }
         if (slices <= 4) { GS_SLICE_LAUNCH(4); return; }
@@ -228,7 +241,7 @@ void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s)
     }
 #define GS_SCAN_LAUNCH(PER)                                                                                      \
     hipLaunchKernelGGL(tile_scan_kernel<PER>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count, img.ranges, \
-                       img.tile_cursor, img.large_tiles, hdr, img.bucket_count)
+                       img.tile_cursor, img.large_tiles, hdr, img.bucket_count, hdr_mirror)
     const int per = (T + kScanThreads - 1) / kScanThreads;
     if (per <= 2) GS_SCAN_LAUNCH(2);
     else if (per <= 4) GS_SCAN_LAUNCH(4);

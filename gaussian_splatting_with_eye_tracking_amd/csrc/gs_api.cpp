@@ -21,6 +21,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_set>
+#include <utility>
 #include <vector>
 
 #include "../../include/gsplat_amd.h"
@@ -119,6 +120,32 @@ uint32_t* pinned_words() {
     return p;
 }
 
+// Mapped, coherent host words the tile scan writes the header into (no copy
+// kernel): thread-local like pinned_words; (host pointer, device pointer).
+int g_hdr_mirror = -1;  // set_tuning("hdr_mirror"); -1: GSAMD_HDR_MIRROR (default 0)
+
+bool hdr_mirror_on() {
+    if (g_hdr_mirror < 0) {
+        const char* e = std::getenv("GSAMD_HDR_MIRROR");
+        g_hdr_mirror = e ? std::atoi(e) : 0;
+    }
+    return g_hdr_mirror != 0;
+}
+
+std::pair<uint32_t*, uint32_t*> mirror_words() {
+    thread_local uint32_t* h = nullptr;
+    thread_local uint32_t* d = nullptr;
+    if (!h) {
+        void* q = nullptr;
+        GS_HIP(hipHostMalloc(&q, 64, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
+        void* dq = nullptr;
+        GS_HIP(hipHostGetDevicePointer(&dq, q, 0));
+        h = static_cast<uint32_t*>(q);
+        d = static_cast<uint32_t*>(dq);
+    }
+    return {h, d};
+}
+
 void read_header(const uint32_t* hdr_dev, uint32_t out[4], hipStream_t s) {
     uint32_t* h = pinned_words();
     GS_HIP(hipMemcpyAsync(h, hdr_dev, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -158,7 +185,11 @@ SideStream& side_stream() {
 // more than the ~6 us dispatch gap they remove)
 int g_side_copy = -1;  // set_tuning("side_copy"); -1: GSAMD_SIDE_COPY (default 0)
 
-void begin_header_read(const uint32_t* hdr_dev, hipStream_t s) {
+void begin_header_read(const uint32_t* hdr_dev, hipStream_t s, const uint32_t* mirror = nullptr) {
+    if (mirror) {  // the scan stores the words into host memory itself
+        GS_HIP(hipEventRecord(side_stream().done, s));
+        return;
+    }
     if (g_side_copy < 0) {
         const char* e = std::getenv("GSAMD_SIDE_COPY");
         g_side_copy = e ? std::atoi(e) : 0;
@@ -175,8 +206,13 @@ void begin_header_read(const uint32_t* hdr_dev, hipStream_t s) {
     GS_HIP(hipEventRecord(ss.done, ss.s));
 }
 
-void finish_header_read(uint32_t out[4]) {
+void finish_header_read(uint32_t out[4], const uint32_t* mirror = nullptr) {
     GS_HIP(hipEventSynchronize(side_stream().done));
+    if (mirror) {
+        const volatile uint32_t* m = mirror;
+        for (int i = 0; i < 4; i++) out[i] = m[i];
+        return;
+    }
     std::memcpy(out, pinned_words(), 4 * sizeof(uint32_t));
 }
 
@@ -326,7 +362,9 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     stage_check(debug, s, "preprocess");
     if (lds_bin) { StageTimer _t(kCount, s); launch_count_tiles(in.P, r.g, r.radii, W, H, tile, r.img, s); }
     stage_check(debug, s, "count_tiles");
-    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s); }
+    const std::pair<uint32_t*, uint32_t*> mirror =
+        (r.T > 0 && hdr_mirror_on()) ? mirror_words() : std::pair<uint32_t*, uint32_t*>{nullptr, nullptr};
+    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second); }
     stage_check(debug, s, "tile_scan");
     uint32_t hdr[4];
     const bool amr = tile == 32;  // the AMR layout appends records and region lists
@@ -340,16 +378,19 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     bool dup_done = false;
     const size_t cap = (!amr && !before_k && r.T > 0 && !debug) ? spec_capacity() : 0;
     if (before_k) {
-        begin_header_read(r.g.hdr, s);
+        begin_header_read(r.g.hdr, s, mirror.first);
         before_k(r);
-        finish_header_read(hdr);
+        finish_header_read(hdr, mirror.first);
     } else if (cap > 0) {
-        begin_header_read(r.g.hdr, s);
+        begin_header_read(r.g.hdr, s, mirror.first);
         char* sbase = call_resize(binning, carve_binning(nullptr, cap, nullptr), "binning");
         carve_binning(sbase, cap, &r.b);
         { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, r.g.hdr, (uint32_t)cap); }
-        finish_header_read(hdr);
+        finish_header_read(hdr, mirror.first);
         dup_done = hdr[kHdrNumRendered] <= cap;
+    } else if (mirror.first) {
+        begin_header_read(r.g.hdr, s, mirror.first);
+        finish_header_read(hdr, mirror.first);
     } else {
         read_header(r.g.hdr, hdr, s);
     }
@@ -990,6 +1031,10 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "scan_slices") == 0) {  // wave-contiguous tile scan (0: thread-contiguous)
         set_scan_slices(value);
+        return 0;
+    }
+    if (std::strcmp(key, "hdr_mirror") == 0) {  // header read-back stored by the scan into mapped host memory
+        g_hdr_mirror = value;
         return 0;
     }
     if (std::strcmp(key, "side_copy") == 0) {  // K read-back on a side stream

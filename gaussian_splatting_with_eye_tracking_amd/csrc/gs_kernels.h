@@ -46,7 +46,9 @@ void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, c
 
 // Binning (replaces scan + duplicateWithKeys + radix sort + identifyTileRanges,
 // base/cr/rasterizer_impl.cu:277-318, with identical outputs).
-void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s);
+// hdr_mirror: device address of 16 mapped host bytes that receive header
+// words 0..3 (K, error, max tile count, large tiles) when the scan finishes.
+void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror = nullptr);
 // spec_hdr: a speculative launch into a buffer of spec_cap keys, enqueued
 // before the host knows K; it does nothing when the header's K > spec_cap.
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
