@@ -88,7 +88,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         if (kWaves == 1 && bucket_count) {
             // rank blockIdx.x of the heaviest-first order: the bucket whose
             // inclusive count first exceeds it (64 buckets, one per lane)
-            const uint32_t c = bucket_count[lane];
+            // (256 buckets: 4 per lane)
+            const uint4 c4 = reinterpret_cast<const uint4*>(bucket_count)[lane];
+            const uint32_t c = c4.x + c4.y + c4.z + c4.w;
             uint32_t incl = c;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
@@ -98,9 +100,16 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             const uint32_t rank = blockIdx.x;
             const uint64_t past = __ballot(incl > rank);
             if (past == 0ull) return;  // (counts short of the grid: cannot happen after a forward)
-            const int b = __builtin_ctzll(past);
-            const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)(incl - c), b);
-            tile = (int)bucket_list[(size_t)b * gridDim.x + (rank - base)];
+            const int L = __builtin_ctzll(past);
+            uint32_t r = rank - (uint32_t)__builtin_amdgcn_readlane((int)(incl - c), L);
+            const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)c4.x, L),
+                           q1 = (uint32_t)__builtin_amdgcn_readlane((int)c4.y, L),
+                           q2 = (uint32_t)__builtin_amdgcn_readlane((int)c4.z, L);
+            int b = 4 * L;
+            if (r >= q0) { r -= q0; b++;
+                if (r >= q1) { r -= q1; b++;
+                    if (r >= q2) { r -= q2; b++; } } }
+            tile = (int)bucket_list[(size_t)b * gridDim.x + r];
         } else if (order) {
             const uint32_t u = order[blockIdx.x];
             tile = (int)(u & 0x0FFFFFFFu);

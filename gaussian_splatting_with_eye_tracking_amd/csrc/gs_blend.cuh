@@ -223,9 +223,9 @@ __device__ __forceinline__ uint32_t splat_group_mask(float2 xy, float4 co, float
 }
 
 // Backward launch order: the work bucket of a tile whose blend reads w
-// entries, 0 = heaviest (4 log2(w + 1): steps of 2^(1/4), 64 buckets).
+// entries, 0 = heaviest (16 log2(w + 1): steps of 2^(1/16), 256 buckets).
 __device__ __forceinline__ uint32_t order_bucket64(uint32_t w) {
-    return 63u - min((uint32_t)(4.0f * __log2f((float)w + 1.0f)), 63u);
+    return 255u - min((uint32_t)(16.0f * __log2f((float)w + 1.0f)), 255u);
 }
 
 // Scalar copy of a wave-uniform 64-bit value held in VGPRs.

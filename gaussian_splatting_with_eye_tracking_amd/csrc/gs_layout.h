@@ -96,10 +96,10 @@ struct ImageView {
     uint32_t* quad_count;      // [T][4] AMR: entries of each 16x16 quadrant's sub-list
     uint32_t* region_count;    // [T][16] AMR: entries of each 8x8 region's sub-list
     uint32_t* tile_done;       // [T] AMR steps: finished (tile, quadrant) units, mod 4
-    uint32_t* bucket_count;    // [kOrderBuckets64] tiles per work bucket (base forward render appends)
+    uint32_t* bucket_count;    // [kOrderBuckets64 = 256] tiles per work bucket (base forward render appends)
     uint32_t* bucket_list;     // [kOrderBuckets64][T] the tiles of each bucket, in append order
 };
-constexpr int kOrderBuckets64 = 64;
+constexpr int kOrderBuckets64 = 256;  // (name kept: the bucket count of the backward order)
 
 inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
     size_t off = 0;

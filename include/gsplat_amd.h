@@ -304,8 +304,8 @@ typedef struct {
     uint32_t* quad_count; /* [T][4] AMR quadrant sub-list lengths */
     uint32_t* region_count; /* [T][16] AMR 8x8-region sub-list lengths */
     uint32_t* tile_done; /* [T] AMR steps: finished units per tile, mod 4 */
-    uint32_t* bucket_count; /* [64] base forward: tiles per work bucket (heaviest first) */
-    uint32_t* bucket_list;  /* [64][T] base forward: the tiles of each bucket */
+    uint32_t* bucket_count; /* [256] base forward: tiles per work bucket (heaviest first) */
+    uint32_t* bucket_list;  /* [256][T] base forward: the tiles of each bucket */
 } gs_image_view;
 
 typedef struct {
