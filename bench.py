@@ -30,7 +30,8 @@ barrier + synchronize, the time is the max over ranks.  ``roofline``: HIP
 events the library records on its launch stream (gs_profile_*) around the
 dominant kernel inside the timed region, with the algorithmic bytes of
 DESIGN.md §4; ``traffic`` comes only from a committed PMC summary of the
-SAME configuration (profiles/*pmc_summary.json, keyed by P, W, H, tile).
+SAME configuration AND the same build (profiles/*pmc_summary.json, keyed by
+P, W, H, tile and the native sources' digest, ``build_digest()``).
 """
 from __future__ import annotations
 
@@ -154,18 +155,41 @@ def _pmc_files():
     return sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_summary.json")))
 
 
-def load_pmc(stage: str, key: dict, field: str):
-    """`field` ("per_launch_hbm_bytes" or "per_launch_valu_instructions") of
-    `stage` from the newest committed PMC summary of THIS configuration
-    (its "config" equals `key`), or None.  Summaries of another configuration
-    -- or with no recorded configuration -- are never used."""
+_DIGEST = None
+
+
+def build_digest() -> str:
+    """Digest of the native sources + flags the library is built from
+    (gaussian_splatting_with_eye_tracking_amd/build.py: source_digest)."""
+    global _DIGEST
+    if _DIGEST is None:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location(
+            "_gsamd_build_digest", os.path.join(ROOT, "gaussian_splatting_with_eye_tracking_amd", "build.py"))
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        _DIGEST = m.source_digest()
+    return _DIGEST
+
+
+def _matching_summaries(key: dict):
+    """Committed PMC summaries of THIS configuration and THIS build, newest
+    first.  Summaries of another configuration or build -- or with neither
+    recorded -- are never used."""
     for f in reversed(_pmc_files()):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if d.get("config") != key:
+        if d.get("config") != key or d.get("build") != build_digest():
             continue
+        yield f, d
+
+
+def load_pmc(stage: str, key: dict, field: str):
+    """`field` ("per_launch_hbm_bytes" or "per_launch_valu_instructions") of
+    `stage` (per stage invocation) from the newest matching summary, or None."""
+    for f, d in _matching_summaries(key):
         v = d.get(field, {}).get(stage)
         if v is not None:
             return float(v), os.path.relpath(f, ROOT)
@@ -173,15 +197,9 @@ def load_pmc(stage: str, key: dict, field: str):
 
 
 def load_raw_kib(stage: str, key: dict):
-    """(FETCH_SIZE, WRITE_SIZE) KiB per launch of `stage` from the newest PMC
-    summary of THIS configuration, or None."""
-    for f in reversed(_pmc_files()):
-        try:
-            d = json.load(open(f))
-        except (OSError, ValueError):
-            continue
-        if d.get("config") != key:
-            continue
+    """(FETCH_SIZE, WRITE_SIZE) KiB per invocation of `stage` from the newest
+    matching summary, or None."""
+    for f, d in _matching_summaries(key):
         v = d.get("raw_kib", {}).get(stage)
         if v is not None:
             return float(v["FETCH_SIZE"]), float(v["WRITE_SIZE"])
@@ -203,7 +221,8 @@ def make_roofline(stage: str, by: float, avg_ms: float, key: dict, src: str, per
         calib = (1024.0 * (raw[0] + raw[1]) + 0.5 * stream_read) * per
     r = {"kernel": stage, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": calib if calib is not None else traffic,
-         "traffic_source": tr[1] if tr else None, "algorithmic_bytes": by, "avg_ms": round(avg_ms, 4), "events": src}
+         "traffic_source": tr[1] if tr else None, "algorithmic_bytes": by, "avg_ms": round(avg_ms, 4), "events": src,
+         "build": build_digest()}
     if calib is not None:
         r["traffic_note"] = ("FETCH + WRITE + streamed reads / 2 (gathers counted x1, streams x2: "
                              "profiles/r02n_pmc_calib.json)")

@@ -113,6 +113,21 @@ def build_torch_ext(verbose: bool = False) -> str:
     return out
 
 
+def source_digest() -> str:
+    """16-hex digest of everything the native library is built from (sources,
+    headers, compiler flags).  Profiles record it so bench.py attaches counter
+    summaries only to the build they were measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    files = [os.path.join(CSRC, s) for s in HIP_SOURCES] + sorted(_headers()) + [os.path.join(CSRC, "torch_ext.cpp")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    h.update(" ".join(f for f in HIP_FLAGS if not f.startswith("-I")).encode())  # (paths differ per box)
+    return h.hexdigest()[:16]
+
+
 def build_all(verbose: bool = False) -> None:
     build_hip_lib(verbose=verbose)
     build_torch_ext(verbose=verbose)

@@ -827,11 +827,16 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
         scl[0] = a.scales[3 * idx + 0];
         scl[1] = a.scales[3 * idx + 1];
         scl[2] = a.scales[3 * idx + 2];
+    }
+    if (kHasScales && !a.has_cov_precomp) {
         // the forward's cov3D recomputed from the scale / rotation this pass
         // reads anyway (same code, no contraction: the same bits) instead of
         // 24 more bytes per Gaussian from the geometry buffer
         compute_cov3d(scl, qrot, a.scale_modifier, cov3D);
     } else {
+        // cov3D_precomp given (alone, or together with scales / rotations: the
+        // forward rendered the precomputed covariance, backward.cu:160 reads
+        // it, and the scales still receive the cov3D backward, :395-396)
 #pragma unroll
         for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D[6 * idx + i];
     }

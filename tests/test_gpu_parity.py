@@ -22,15 +22,15 @@ CASES = [
 ]
 
 
-def _gpu_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0.0, 0.0)):
+def _gpu_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0.0, 0.0), keep_scales=False):
     import gaussian_splatting_with_eye_tracking_amd._C as C
     s = G.torch_settings(cam, bg=bg)
     t = G.scene_tensors(sc)
     e = torch.Tensor([])
     sh = t["shs"] if colors_precomp is None else e
     col = e if colors_precomp is None else torch.from_numpy(colors_precomp).cuda()
-    scales = t["scales"] if cov3D_precomp is None else e
-    rots = t["rotations"] if cov3D_precomp is None else e
+    scales = t["scales"] if cov3D_precomp is None or keep_scales else e
+    rots = t["rotations"] if cov3D_precomp is None or keep_scales else e
     cov = e if cov3D_precomp is None else torch.from_numpy(cov3D_precomp).cuda()
     out = C.rasterize_gaussians(s.bg, t["means3D"], col, t["opacities"], scales, rots, s.scale_modifier, cov,
                                 s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh,
@@ -39,12 +39,13 @@ def _gpu_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0.0,
     return s, t, out
 
 
-def _oracle_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0.0, 0.0)):
+def _oracle_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0.0, 0.0), keep_scales=False):
     import oracle as O
     s = O.settings_from_camera(cam, bg=bg)
+    both = cov3D_precomp is None or keep_scales
     kw = dict(shs=sc.shs if colors_precomp is None else None, colors_precomp=colors_precomp,
-              scales=sc.scales if cov3D_precomp is None else None,
-              rotations=sc.rotations if cov3D_precomp is None else None, cov3D_precomp=cov3D_precomp)
+              scales=sc.scales if both else None,
+              rotations=sc.rotations if both else None, cov3D_precomp=cov3D_precomp)
     return s, O.forward(s, sc.means3D, sc.opacities, **kw), kw
 
 
@@ -91,8 +92,14 @@ def test_forward_image(name, P, W, H, seed):
 
 
 @pytest.mark.parametrize("name,P,W,H,seed", CASES[:3])
-@pytest.mark.parametrize("variant", ["sh", "colors_precomp", "cov3D_precomp"])
+@pytest.mark.parametrize("variant", ["sh", "colors_precomp", "cov3D_precomp", "cov3D_precomp_and_scales"])
 def test_backward_parity(name, P, W, H, seed, variant):
+    # cov3D_precomp_and_scales: both covariance inputs, as the raw binding and
+    # the C ABI accept them -- the forward renders the precomputed covariance,
+    # the backward's cov2D step must read it (base/cr/backward.cu:160,
+    # rasterizer_impl.cu:411) while the scales / rotations still receive the
+    # cov3D backward (backward.cu:395-396).  The covariance is deliberately not
+    # the one the scales would give.
     import oracle as O
     from gaussian_splatting_with_eye_tracking_amd import synthetic as S
     sc, cam = G.scene_and_camera(P, W, H, seed)
@@ -100,21 +107,24 @@ def test_backward_parity(name, P, W, H, seed, variant):
     cov = None
     if variant == "colors_precomp":
         colors = np.random.default_rng(seed + 5).uniform(0, 1, (P, 3)).astype(np.float32)
-    if variant == "cov3D_precomp":
+    both = variant == "cov3D_precomp_and_scales"
+    if variant.startswith("cov3D_precomp"):
         _, r0, _ = _oracle_forward(sc, cam)
         cov = r0.cov3D.copy()
         # invisible Gaussians have no computed cov3D: give them a valid one
         cov[r0.radii <= 0] = np.array([1e-4, 0, 0, 1e-4, 0, 1e-4], np.float32)
+        if both:
+            cov *= np.float32(1.3)
     bg = (0.2, 0.1, 0.05)
-    s, t, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam, colors, cov, bg=bg)
-    os_, ref, kw = _oracle_forward(sc, cam, colors, cov, bg=bg)
+    s, t, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam, colors, cov, bg=bg, keep_scales=both)
+    os_, ref, kw = _oracle_forward(sc, cam, colors, cov, bg=bg, keep_scales=both)
     dpix = S.make_cotangent(H, W, seed + 1)
     import gaussian_splatting_with_eye_tracking_amd._C as C
     e = torch.Tensor([])
     sh = t["shs"] if colors is None else e
     colt = e if colors is None else torch.from_numpy(colors).cuda()
-    scales = t["scales"] if cov is None else e
-    rots = t["rotations"] if cov is None else e
+    scales = t["scales"] if cov is None or both else e
+    rots = t["rotations"] if cov is None or both else e
     covt = e if cov is None else torch.from_numpy(cov).cuda()
     grads = C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, colt, scales, rots, s.scale_modifier, covt,
                                            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy,

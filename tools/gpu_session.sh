@@ -7,6 +7,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+# the digest of the native sources this session runs (tools/pmc_summary.py records it)
+python -c "import bench; print(bench.build_digest())" > gpurun_out/build_digest.txt
 fault() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
 run() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
