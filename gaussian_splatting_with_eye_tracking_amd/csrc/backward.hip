@@ -99,7 +99,14 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             }
             const uint32_t rank = blockIdx.x;
             const uint64_t past = __ballot(incl > rank);
-            if (past == 0ull) return;  // (counts short of the grid: cannot happen after a forward)
+            // counts that do not cover the grid exactly (an image buffer whose
+            // base forward render did not fill the buckets, e.g. from another
+            // caller or size): every block takes the identity order instead,
+            // so each tile is still processed exactly once
+            const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            if (total != gridDim.x || past == 0ull) {
+                tile = (int)blockIdx.x;
+            } else {
             const int L = __builtin_ctzll(past);
             uint32_t r = rank - (uint32_t)__builtin_amdgcn_readlane((int)(incl - c), L);
             const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)c4.x, L),
@@ -110,6 +117,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 if (r >= q1) { r -= q1; b++;
                     if (r >= q2) { r -= q2; b++; } } }
             tile = (int)bucket_list[(size_t)b * gridDim.x + r];
+            }
         } else if (order) {
             const uint32_t u = order[blockIdx.x];
             tile = (int)(u & 0x0FFFFFFFu);
@@ -1073,11 +1081,11 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
     const bool live = local < a.count;
     const int idx = a.g0 + local;
     float* lrow = kStage ? s_sh + threadIdx.x * kShRow : nullptr;
-    const float* rows = a.rows + (size_t)local * kViewRow;
-    const size_t vstride = a.row_view_stride;
+    // view v's row of this Gaussian (a.rows[v] points at Gaussian g0's)
+    const size_t roff = (size_t)local * kViewRow;
     bool any = false;
     if (live)
-        for (int v = 0; v < a.V; v++) any |= __float_as_uint(rows[v * vstride + 9]) != 0u;
+        for (int v = 0; v < a.V; v++) any |= __float_as_uint(a.rows[v][roff + 9]) != 0u;
     if (live && !any) {
 #pragma unroll
         for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = 0.f;
@@ -1110,7 +1118,7 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
                 st_max = a.max_radii[idx];
             }
             for (int v = 0; v < a.V; v++) {
-                const float* row = rows + v * vstride;
+                const float* row = a.rows[v] + roff;
                 const uint32_t w9 = __float_as_uint(row[9]);
                 if (w9 == 0u) continue;  // not visible in view v: no terms (the reference's radii > 0 filter)
                 // mean2D.y, conic x, y, w (rows are 40 B: 8-B aligned only)
@@ -1118,7 +1126,7 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
                 const float2 r1b = *reinterpret_cast<const float2*>(row + 6);
                 const float4 r1 = make_float4(r1a.x, r1a.y, r1b.x, r1b.y);
                 const float gx = row[3], dop_v = row[8];
-                const float* cam = a.cams + v * a.cam_stride;
+                const float* cam = a.cams[v];
                 const Mat4 V = load_mat4(cam);
                 const Mat4 Pm = load_mat4(cam + 16);
                 const float tan_fovx = cam[37], tan_fovy = cam[38];
@@ -1169,12 +1177,12 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
             }
             float ddir[3] = {0.f, 0.f, 0.f};
             for (int v = 0; v < a.V; v++) {
-                const float* row = rows + v * vstride;
+                const float* row = a.rows[v] + roff;
                 const uint32_t w9 = __float_as_uint(row[9]);
                 if (w9 == 0u) continue;
                 const float acc[3] = {row[0], row[1], row[2]};
                 const uint8_t cb = (uint8_t)(w9 >> 24);
-                const float* cam = a.cams + v * a.cam_stride;
+                const float* cam = a.cams[v];
                 float dsh_c[16], dRGB[3];
                 if constexpr (kStage) {
                     sh_backward_terms(a.D, cam + 32, mx, my, mz, ShRowPtr{lrow}, cb, acc, dsh_c, dRGB, ddir);

@@ -66,6 +66,34 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* s
 }
 
 // ------------------------------------------------------------ tile scan ---
+// Tile i's count is the sum of its kBinSlots sub-bucket counts (slot-major
+// [kBinSlots][T]: every load is wave-contiguous).
+__device__ __forceinline__ uint32_t slot_total(const uint32_t* __restrict__ count, int T, int i, int nslots) {
+    uint32_t c = count[i];
+#pragma unroll
+    for (int s = 1; s < kBinSlots; s++)
+        if (s < nslots) c += count[(size_t)s * T + i];
+    return c;
+}
+
+// Sub-bucket cursors of tile i (slots back to back from the tile's start),
+// and the tile's total in place of slot 0's count (tile_count[0..T) = totals
+// after the scan: AMR n_intersections, parse_buffers).
+__device__ __forceinline__ void slot_cursors(uint32_t* __restrict__ count, uint32_t* __restrict__ cursor, int T,
+                                             int i, uint32_t start, uint32_t total, int nslots) {
+    cursor[i] = start;
+    if (nslots > 1) {
+        uint32_t run = start + count[i];
+#pragma unroll
+        for (int s = 1; s < kBinSlots; s++) {
+            if (s >= nslots) break;
+            cursor[(size_t)s * T + i] = run;
+            run += count[(size_t)s * T + i];
+        }
+        count[i] = total;
+    }
+}
+
 // The host's copy of the first four header words, stored straight into
 // mapped, coherent host memory (vector stores over the fabric) by the scan:
 // the forward's read-back then needs no copy kernel, only an event after the
@@ -79,25 +107,25 @@ __device__ __forceinline__ void mirror_header(uint32_t* m, uint32_t K, uint32_t 
 // loop (all loads in flight at once, no serial load-add chain: 16 -> 5 us at
 // 8160 tiles); kPer = 0: any T, run-time loop.
 template <int kPer>
-__global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const uint32_t* __restrict__ count,
+__global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, uint32_t* __restrict__ count,
                                                                  uint32_t* __restrict__ ranges,
                                                                  uint32_t* __restrict__ cursor,
                                                                  uint32_t* __restrict__ large_tiles,
                                                                  uint32_t* __restrict__ hdr,
                                                                  uint32_t* __restrict__ bucket_count,
-                                                                 uint32_t* __restrict__ hdr_mirror) {
+                                                                 uint32_t* __restrict__ hdr_mirror, int nslots) {
     __shared__ uint32_t s_wave[kScanThreads / 64 + 1];
     __shared__ uint32_t s_max[kScanThreads / 64];
     __shared__ uint32_t nlarge;
     const int tid = threadIdx.x;
-    if (tid < kOrderBuckets64) bucket_count[tid] = 0;  // the forward render appends to the buckets
+    if (bucket_count && tid < kOrderBuckets64) bucket_count[tid] = 0;  // the forward render appends to the buckets
     const int per = kPer > 0 ? kPer : (T + kScanThreads - 1) / kScanThreads;
     const int beg = min(T, tid * per), end = min(T, beg + per);
     uint32_t sum = 0, mx = 0;
     uint32_t cv[kPer > 0 ? kPer : 1];
     if constexpr (kPer > 0) {
 #pragma unroll
-        for (int k = 0; k < kPer; k++) cv[k] = beg + k < end ? count[beg + k] : 0u;
+        for (int k = 0; k < kPer; k++) cv[k] = beg + k < end ? slot_total(count, T, beg + k, nslots) : 0u;
 #pragma unroll
         for (int k = 0; k < kPer; k++) {
             sum += cv[k];
@@ -105,7 +133,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const ui
         }
     } else {
         for (int i = beg; i < end; i++) {
-            const uint32_t c = count[i];
+            const uint32_t c = slot_total(count, T, i, nslots);
             sum += c;
             mx = max(mx, c);
         }
@@ -119,7 +147,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const ui
     auto emit = [&](int i, uint32_t c) {
         // identifyTileRanges leaves empty tiles at (0,0) (rasterizer_impl.cu:310).
         reinterpret_cast<uint2*>(ranges)[i] = make_uint2(c ? run : 0u, c ? run + c : 0u);
-        cursor[i] = run;
+        slot_cursors(count, cursor, T, i, run, c, nslots);
         if (c > (uint32_t)kSmallCap) {
             const uint32_t slot = atomicAdd(&nlarge, 1u);
             large_tiles[slot] = (uint32_t)i;
@@ -131,7 +159,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const ui
         for (int k = 0; k < kPer; k++)
             if (beg + k < end) emit(beg + k, cv[k]);
     } else {
-        for (int i = beg; i < end; i++) emit(i, count[i]);
+        for (int i = beg; i < end; i++) emit(i, slot_total(count, T, i, nslots));
     }
     __syncthreads();
     if (tid == 0) {
@@ -153,15 +181,16 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, const ui
 // barrier; slice k's base is the total of slices < k.  Same sums, same order of
 // the integer adds' results: bit-identical ranges, cursors, K.
 template <int kS>
-__global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, const uint32_t* __restrict__ count,
+__global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, uint32_t* __restrict__ count,
                                                                         uint32_t* __restrict__ ranges,
                                                                         uint32_t* __restrict__ cursor,
                                                                         uint32_t* __restrict__ large_tiles,
                                                                         uint32_t* __restrict__ hdr,
                                                                         uint32_t* __restrict__ bucket_count,
-                                                                        uint32_t* __restrict__ hdr_mirror) {
+                                                                        uint32_t* __restrict__ hdr_mirror,
+                                                                        int nslots) {
     constexpr int kW = kScanThreads / 64;
-    if (threadIdx.x < kOrderBuckets64) bucket_count[threadIdx.x] = 0;  // the forward render appends
+    if (bucket_count && threadIdx.x < kOrderBuckets64) bucket_count[threadIdx.x] = 0;  // the forward render appends
     __shared__ uint32_t s_tot[kW][kS];
     __shared__ uint32_t s_max[kW];
     __shared__ uint32_t nlarge;
@@ -171,7 +200,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, c
 #pragma unroll
     for (int k = 0; k < kS; k++) {
         const int i = k * kScanThreads + tid;
-        c[k] = i < T ? count[i] : 0u;
+        c[k] = i < T ? slot_total(count, T, i, nslots) : 0u;
         incl[k] = c[k];
         mx = max(mx, c[k]);
     }
@@ -207,7 +236,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, c
             const uint32_t ex = run + wbase + incl[k] - c[k];
             // identifyTileRanges leaves empty tiles at (0,0) (rasterizer_impl.cu:310)
             reinterpret_cast<uint2*>(ranges)[i] = make_uint2(c[k] ? ex : 0u, c[k] ? ex + c[k] : 0u);
-            cursor[i] = ex;
+            slot_cursors(count, cursor, T, i, ex, c[k], nslots);
             if (c[k] > (uint32_t)kSmallCap) large_tiles[atomicAdd(&nlarge, 1u)] = (uint32_t)i;
         }
         run += stot;
@@ -227,12 +256,12 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, c
 int g_scan_slices = 1;  // set_tuning("scan_slices"): 0 = the thread-contiguous scan
 void set_scan_slices(int v) { g_scan_slices = v; }
 
-void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror) {
+void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror, int nslots) {
     if (g_scan_slices) {
         const int slices = (T + kScanThreads - 1) / kScanThreads;
 #define GS_SLICE_LAUNCH(S)                                                                                        \
     hipLaunchKernelGGL(tile_scan_slices_kernel<S>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count,         \
-                       img.ranges, img.tile_cursor, img.large_tiles, hdr, img.bucket_count, hdr_mirror)
+                       img.ranges, img.tile_cursor, img.large_tiles, hdr, img.bucket_count, hdr_mirror, nslots)
         if (slices <= 1) { GS_SLICE_LAUNCH(1); return; }
         if (slices <= 2) { GS_SLICE_LAUNCH(2); return; }
         if (slices <= 4) { GS_SLICE_LAUNCH(4); return; }
@@ -241,7 +270,7 @@ void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s,
     }
 #define GS_SCAN_LAUNCH(PER)                                                                                      \
     hipLaunchKernelGGL(tile_scan_kernel<PER>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count, img.ranges, \
-                       img.tile_cursor, img.large_tiles, hdr, img.bucket_count, hdr_mirror)
+                       img.tile_cursor, img.large_tiles, hdr, img.bucket_count, hdr_mirror, nslots)
     const int per = (T + kScanThreads - 1) / kScanThreads;
     if (per <= 2) GS_SCAN_LAUNCH(2);
     else if (per <= 4) GS_SCAN_LAUNCH(4);
@@ -305,6 +334,16 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const float* __re
 // Slot order inside a bucket stays arbitrary; sort_tiles makes it exact.
 constexpr int kBinThreads = 1024;
 int g_bin_chunk = 4096;
+int g_dup_diag = 0;
+// sub-bucket slots the LDS binning spreads its chunks over (1..kBinSlots;
+// the scan sums all kBinSlots, unused ones stay zero)
+int g_bin_slots = 0;  // 0: auto (bin_slots_for)
+void set_bin_slots(int v) { g_bin_slots = std::max(0, std::min(kBinSlots, v)); }
+// Measured (profiles/r03b_ab_bin_slots*): the sub-buckets save ~30 us of the
+// duplicate at config 4 (6.1M Gaussians) and ~4 us at config 2, where the
+// scan's 8x count loads cost more (+6 us): slots only for large scenes.
+int bin_slots_for(int P) { return g_bin_slots ? g_bin_slots : (P >= 2000000 ? kBinSlots : 1); }
+void set_dup_diag(int v) { g_dup_diag = v; }
 void set_bin_chunk(int v) { g_bin_chunk = max(kBinThreads, v); }
 
 __device__ __forceinline__ bool gaussian_rect(int idx, const float* __restrict__ means2D,
@@ -320,7 +359,7 @@ __device__ __forceinline__ bool gaussian_rect(int idx, const float* __restrict__
 __global__ void __launch_bounds__(kBinThreads) count_tiles_kernel(int P, int chunk, const float* __restrict__ means2D,
                                                                   const int* __restrict__ radii, int block,
                                                                   uint32_t gx, uint32_t gy,
-                                                                  uint32_t* __restrict__ tile_count) {
+                                                                  uint32_t* __restrict__ tile_count, uint32_t nslots) {
     extern __shared__ uint32_t hist[];
     const int T = (int)(gx * gy);
     for (int i = threadIdx.x; i < T; i += kBinThreads) hist[i] = 0;
@@ -333,9 +372,10 @@ __global__ void __launch_bounds__(kBinThreads) count_tiles_kernel(int P, int chu
             for (uint32_t x = r.x0; x < r.x1; x++) atomicAdd(&hist[y * gx + x], 1u);
     }
     __syncthreads();
+    uint32_t* cnt = tile_count + (size_t)(blockIdx.x % nslots) * T;  // this chunk's sub-bucket slot
     for (int i = threadIdx.x; i < T; i += kBinThreads) {
         const uint32_t c = hist[i];
-        if (c) atomicAdd(&tile_count[i], c);
+        if (c) atomicAdd(&cnt[i], c);
     }
 }
 
@@ -346,7 +386,8 @@ __global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int c
                                                                     uint32_t gx, uint32_t gy,
                                                                     uint32_t* __restrict__ cursor,
                                                                     uint64_t* __restrict__ pair_keys,
-                                                                    const uint32_t* __restrict__ hdr, uint32_t cap) {
+                                                                    const uint32_t* __restrict__ hdr, uint32_t cap,
+                                                                    int diag, uint32_t nslots) {
     // speculative launch (hdr given): the keys fit the buffer only if K <= cap;
     // otherwise nothing is touched (no cursor moved) and the host relaunches
     if (hdr && hdr[kHdrNumRendered] > cap) return;
@@ -363,9 +404,12 @@ __global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int c
     }
     __syncthreads();
     // one returning atomic per non-empty tile: the chunk's run in the bucket
+    // (g_dup_diag, timing diagnostics only -- wrong keys: 1 = no key stores,
+    // 2 = runs at offset 0 without the device atomics)
+    uint32_t* cur = cursor + (size_t)(blockIdx.x % nslots) * T;  // the slot count_tiles counted this chunk in
     for (int i = threadIdx.x; i < T; i += kBinThreads) {
         const uint32_t c = slot[i];
-        if (c) slot[i] = atomicAdd(&cursor[i], c);
+        if (c) slot[i] = diag == 2 ? 0u : atomicAdd(&cur[i], c);
     }
     __syncthreads();
     for (int idx = beg + threadIdx.x; idx < end; idx += kBinThreads) {
@@ -373,7 +417,10 @@ __global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int c
         if (!gaussian_rect(idx, means2D, radii, block, gx, gy, r)) continue;
         const uint64_t key = ((uint64_t)float_bits(depths[idx]) << 32) | (uint32_t)idx;
         for (uint32_t y = r.y0; y < r.y1; y++)
-            for (uint32_t x = r.x0; x < r.x1; x++) pair_keys[atomicAdd(&slot[y * gx + x], 1u)] = key;
+            for (uint32_t x = r.x0; x < r.x1; x++) {
+                const uint32_t sl = atomicAdd(&slot[y * gx + x], 1u);
+                if (diag != 1) pair_keys[sl] = key;
+            }
     }
 }
 
@@ -383,7 +430,8 @@ void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H
     if (P == 0 || gx * gy == 0) return;
     const int chunk = g_bin_chunk;
     hipLaunchKernelGGL(count_tiles_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
-                       sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, radii, block, gx, gy, img.tile_count);
+                       sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, radii, block, gx, gy, img.tile_count,
+                       (uint32_t)bin_slots_for(P));
 }
 
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
@@ -394,7 +442,7 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
         const int chunk = g_bin_chunk;
         hipLaunchKernelGGL(duplicate_lds_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
                            sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, g.depths, radii, block, gx, gy,
-                           img.tile_cursor, b.pair_keys, spec_hdr, spec_cap);
+                           img.tile_cursor, b.pair_keys, spec_hdr, spec_cap, g_dup_diag, (uint32_t)bin_slots_for(P));
         return;
     }
     hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, g.means2D, g.depths, radii,
@@ -700,6 +748,142 @@ __global__ void __launch_bounds__(kThreads) sort_tiles_wide_kernel(int lo, int h
     sort_tile_regs<4, kThreads / 64>(pair_keys + beg, n, point_list + beg, lds);
 }
 
+// ---- bucket sort of one tile (n <= 256 kE keys).
+// The bitonic networks above cost ~78 compare-exchange stages per key at
+// n = 4096 (~20 ps per key at config 2 and config 4 alike).  Here the tile's
+// keys go into nb ~ n / 2 buckets by their depth bits relative to the tile's
+// min / max (a monotone map: bucket = (depth - min) >> sh), one LDS atomic
+// count per key, one scan, one LDS atomic slot per key (arbitrary order inside
+// a bucket); then each key's final position is its bucket's start plus the
+// number of keys of its bucket that are smaller -- keys are (depth, idx),
+// unique, so that is a total order, the same (depth, idx) order the bitonic
+// networks and the reference's stable radix sort produce.  Per key: ~10
+// VALU + the rank loop over its bucket (~2 keys on average, the wave's longest
+// bucket bounds the loop).  A tile whose longest bucket exceeds kBucketMax
+// (depths clustered far below the tile's range) takes the bitonic network
+// instead, so no distribution is slower than before.
+constexpr int kBucketMax = 64;
+int g_sort_algo = 1;  // set_tuning("sort_algo"): 0 = bitonic networks only, 1 = bucket sort
+void set_sort_algo(int v) { g_sort_algo = v; }
+
+template <int kE>
+__global__ void __launch_bounds__(kSortThreads) sort_tiles_bucket_kernel(int lo, int hi,
+                                                                          const uint32_t* __restrict__ ranges,
+                                                                          const uint64_t* __restrict__ pair_keys,
+                                                                          uint32_t* __restrict__ point_list) {
+    constexpr int kT = kSortThreads;
+    constexpr int kW = kT / 64;
+    constexpr int kN = kT * kE;   // keys per tile
+    constexpr int kNB = kN / 2;   // buckets at full capacity
+    __shared__ uint64_t s_tmp[kN];
+    __shared__ uint32_t s_start[kNB];
+    __shared__ uint32_t s_fill[kNB];
+    __shared__ uint32_t s_red[2 * kW];
+    __shared__ uint32_t s_wave[kW + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tile = blockIdx.x;
+    const uint32_t beg = ranges[2 * tile], end = ranges[2 * tile + 1];
+    const int n = (int)(end - beg);
+    if (n <= lo || n > hi) return;
+    const uint64_t* keys = pair_keys + beg;
+    uint32_t* out = point_list + beg;
+    if (n == 1) {
+        if (tid == 0) out[0] = (uint32_t)keys[0];
+        return;
+    }
+    // buckets in use: a power of two >= n / 2 (block-uniform)
+    int lg = 6;
+    while ((1 << lg) < (n + 1) / 2) lg++;
+    const int nb = 1 << lg;  // <= kNB
+    uint64_t k[kE];
+    uint32_t dmin = ~0u, dmax = 0u;
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+        const int i = e * kT + tid;
+        k[e] = i < n ? keys[i] : ~0ull;
+        if (i < n) {
+            const uint32_t d = (uint32_t)(k[e] >> 32);
+            dmin = min(dmin, d);
+            dmax = max(dmax, d);
+        }
+    }
+    for (int b = tid; b < nb; b += kT) s_fill[b] = 0u;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        dmin = min(dmin, (uint32_t)__shfl_xor((int)dmin, off, 64));
+        dmax = max(dmax, (uint32_t)__shfl_xor((int)dmax, off, 64));
+    }
+    if (lane == 0) {
+        s_red[wave] = dmin;
+        s_red[kW + wave] = dmax;
+    }
+    __syncthreads();
+    dmin = s_red[0];
+    dmax = s_red[kW];
+#pragma unroll
+    for (int w = 1; w < kW; w++) {
+        dmin = min(dmin, s_red[w]);
+        dmax = max(dmax, s_red[kW + w]);
+    }
+    const uint32_t range = dmax - dmin;
+    const int bl = range ? 32 - __builtin_clz(range) : 0;
+    const int sh = bl > lg ? bl - lg : 0;  // (range >> sh) < nb
+    uint32_t bk[kE];
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+        const int i = e * kT + tid;
+        bk[e] = ((uint32_t)(k[e] >> 32) - dmin) >> sh;
+        if (i < n) atomicAdd(&s_fill[bk[e]], 1u);
+    }
+    __syncthreads();
+    // exclusive scan of the nb counts: thread t owns buckets [t per, (t + 1) per)
+    const int per = nb >= kT ? nb / kT : 1;
+    const int b0 = tid * per;
+    uint32_t local = 0, cmax = 0;
+    for (int q = 0; q < per; q++) {
+        const uint32_t c = b0 + q < nb ? s_fill[b0 + q] : 0u;
+        local += c;
+        cmax = max(cmax, c);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor((int)cmax, off, 64));
+    if (lane == 0) s_red[wave] = cmax;  // (s_red's min half was read before the barrier above)
+    uint32_t total;
+    uint32_t run = block_exclusive_scan<kT>(local, s_wave, total);  // (its barriers publish s_red too)
+    for (int q = 0; q < per; q++) {
+        if (b0 + q < nb) {
+            const uint32_t c = s_fill[b0 + q];
+            s_start[b0 + q] = run;
+            s_fill[b0 + q] = run;
+            run += c;
+        }
+    }
+    uint32_t bmax = s_red[0];
+#pragma unroll
+    for (int w = 1; w < kW; w++) bmax = max(bmax, s_red[w]);
+    __syncthreads();
+    if (bmax > (uint32_t)kBucketMax) {  // block-uniform: clustered depths
+        sort_tile_regs<kE, kW>(keys, n, out, s_tmp);
+        return;
+    }
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+        const int i = e * kT + tid;
+        if (i < n) s_tmp[atomicAdd(&s_fill[bk[e]], 1u)] = k[e];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < kE; e++) {
+        const int i = e * kT + tid;
+        if (i < n) {
+            const uint32_t bs = s_start[bk[e]], be = s_fill[bk[e]];
+            uint32_t r = 0;
+            for (uint32_t j = bs; j < be; j++) r += s_tmp[j] < k[e] ? 1u : 0u;
+            out[bs + r] = (uint32_t)k[e];
+        }
+    }
+}
+
 // Merge-path split: number of elements taken from A for the first `diag`
 // outputs of merge(A[0..na), B[0..nb)); keys are unique.
 __device__ __forceinline__ int merge_path(const uint64_t* A, int na, const uint64_t* B, int nb, int diag) {
@@ -765,6 +949,20 @@ __global__ void __launch_bounds__(kLargeThreads) sort_tiles_large_kernel(const u
 void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int max_count_host, int num_large_host,
                        hipStream_t s) {
     if (T == 0) return;
+    if (g_sort_algo == 1) {
+        hipLaunchKernelGGL(sort_tiles_bucket_kernel<4>, dim3(T), dim3(kSortThreads), 0, s, 0, 1024, img.ranges,
+                           b.pair_keys, b.point_list);
+        if (max_count_host > 1024)
+            hipLaunchKernelGGL(sort_tiles_bucket_kernel<8>, dim3(T), dim3(kSortThreads), 0, s, 1024, 2048,
+                               img.ranges, b.pair_keys, b.point_list);
+        if (max_count_host > 2048)
+            hipLaunchKernelGGL(sort_tiles_bucket_kernel<16>, dim3(T), dim3(kSortThreads), 0, s, 2048, kSmallCap,
+                               img.ranges, b.pair_keys, b.point_list);
+        if (num_large_host > 0)
+            hipLaunchKernelGGL(sort_tiles_large_kernel, dim3(num_large_host), dim3(kLargeThreads), 0, s,
+                               img.large_tiles, img.ranges, b.pair_keys, b.scratch, b.point_list);
+        return;
+    }
     // n <= 1024 with 8 KiB of LDS; 1024 < n <= 4096 with 32 KiB (launched
     // only if such a tile exists: the forward read back the maximum count)
     hipLaunchKernelGGL(sort_tiles_small_kernel<4>, dim3(T), dim3(kSortThreads), 0, s, 0, 1024, img.ranges,

@@ -13,6 +13,7 @@
 //   * simple-knn has no host synchronisation at all (the reference has 2).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -244,9 +245,48 @@ void zero_accum_unless_clean(const GeomView& g, int P, hipStream_t s) {
 // Capacity for the speculative duplicate: the last base forward's K plus
 // 1/8 (0 before the first call, or when speculation is switched off).
 int g_spec_dup = 1;  // set_tuning("spec_dup")
-thread_local size_t t_spec_cap = 0;
-size_t spec_capacity() { return g_spec_dup ? t_spec_cap : 0; }
-void note_k(int K) { t_spec_cap = K > 0 ? (size_t)K + (size_t)K / 8 + 4096 : 0; }
+// The speculative duplicate's capacity, remembered per (device, W, H, P):
+// workloads that alternate render sizes or scenes (train 1080p / eval
+// thumbnails) keep one prediction each instead of over-sizing the small
+// renders and missing on the large ones.  A few entries per thread, least
+// recently used replaced; an unknown key runs the synchronous path.
+struct SpecKey {
+    int dev, W, H, P;
+    bool operator==(const SpecKey& o) const { return dev == o.dev && W == o.W && H == o.H && P == o.P; }
+};
+struct SpecEntry {
+    SpecKey key;
+    size_t cap;
+    uint64_t used;
+};
+constexpr int kSpecEntries = 8;
+thread_local SpecEntry t_spec[kSpecEntries] = {};
+thread_local uint64_t t_spec_clock = 0;
+SpecKey spec_key(int W, int H, int P) {
+    int dev = -1;
+    if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    return SpecKey{dev, W, H, P};
+}
+size_t spec_capacity(const SpecKey& k) {
+    if (!g_spec_dup) return 0;
+    for (SpecEntry& e : t_spec)
+        if (e.cap && e.key == k) {
+            e.used = ++t_spec_clock;
+            return e.cap;
+        }
+    return 0;
+}
+void note_k(const SpecKey& k, int K) {
+    const size_t cap = K > 0 ? (size_t)K + (size_t)K / 8 + 4096 : 0;
+    SpecEntry* victim = &t_spec[0];
+    for (SpecEntry& e : t_spec) {
+        if (e.cap && e.key == k) { victim = &e; break; }
+        if (!e.cap || e.used < victim->used) victim = &e;
+    }
+    victim->key = k;
+    victim->cap = cap;
+    victim->used = ++t_spec_clock;
+}
 
 char* call_resize(const gs_buffer& b, size_t n, const char* what) {
     if (!b.resize) throw GsError(std::string("no resize callback for ") + what);
@@ -280,9 +320,13 @@ struct ForwardIn {
 
 // Per-call token for the header's error word (never 0: a zeroed header at
 // T == 0 must not read as an error).
+// Drawn from one process-wide counter (hashed), so no two calls -- on any
+// thread -- share a token, and a stale word left by another call never reads
+// as this call's error.
 uint32_t next_error_token() {
-    thread_local uint32_t t = 0x9e3779b9u;
-    t = t * 1664525u + 1013904223u;
+    static std::atomic<uint32_t> counter{0};
+    uint32_t t = counter.fetch_add(1u, std::memory_order_relaxed) + 1u;
+    t ^= t >> 16; t *= 0x7feb352du; t ^= t >> 15; t *= 0x846ca68bu; t ^= t >> 16;  // bijective mix
     return t ? t : 1u;
 }
 
@@ -342,8 +386,8 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     char* gbase = call_resize(geometry, carve_geom(nullptr, in.P, nullptr), "geometry");
     carve_geom(gbase, in.P, &r.g);
     set_accum_clean(r.g.grad_accum, false);  // this forward decides afresh
-    char* ibase = call_resize(image, carve_image(nullptr, N, r.T, nullptr), "image");
-    carve_image(ibase, N, r.T, &r.img);
+    char* ibase = call_resize(image, carve_image(nullptr, N, r.T, nullptr, tile), "image");
+    carve_image(ibase, N, r.T, &r.img, tile);
     r.radii = radii ? radii : r.g.radii;
     // The header needs no zeroing: the tile scan stores K and the tile
     // statistics, and a prefiltered violation stores this call's token in the
@@ -351,12 +395,12 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     // the preprocess zeroes the tile histogram; otherwise it adds into it.
     const bool lds_bin = r.T <= kLdsTiles;
     if (r.T == 0) GS_HIP(hipMemsetAsync(r.g.hdr, 0, kHdrWords * sizeof(uint32_t), s));
-    if (r.T > 0 && !lds_bin) GS_HIP(hipMemsetAsync(r.img.tile_count, 0, sizeof(uint32_t) * r.T, s));
+    if (r.T > 0 && !lds_bin) GS_HIP(hipMemsetAsync(r.img.tile_count, 0, sizeof(uint32_t) * kBinSlots * r.T, s));
     PreprocessArgs pa = make_pp(in, tile);
     pa.err_token = next_error_token();
     if (r.T > 0 && lds_bin) {
         pa.zero_words = r.img.tile_count;
-        pa.zero_n = r.T;
+        pa.zero_n = kBinSlots * r.T;
     }
     { StageTimer _t(kPre, s); launch_preprocess(pa, r.g, r.radii, lds_bin ? nullptr : r.img.tile_count, s); }
     stage_check(debug, s, "preprocess");
@@ -364,7 +408,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     stage_check(debug, s, "count_tiles");
     const std::pair<uint32_t*, uint32_t*> mirror =
         (r.T > 0 && hdr_mirror_on()) ? mirror_words() : std::pair<uint32_t*, uint32_t*>{nullptr, nullptr};
-    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second); }
+    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second, bin_slots_for(in.P)); }
     stage_check(debug, s, "tile_scan");
     uint32_t hdr[4];
     const bool amr = tile == 32;  // the AMR layout appends records and region lists
@@ -376,7 +420,8 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     // and the duplicate relaunched.  Only point_list (offset 0) outlives the
     // forward, so a buffer carved for capacity >= K serves the backward as is.
     bool dup_done = false;
-    const size_t cap = (!amr && !before_k && r.T > 0 && !debug) ? spec_capacity() : 0;
+    const SpecKey skey = spec_key(W, H, in.P);
+    const size_t cap = (!amr && !before_k && r.T > 0 && !debug) ? spec_capacity(skey) : 0;
     if (before_k) {
         begin_header_read(r.g.hdr, s, mirror.first);
         before_k(r);
@@ -397,7 +442,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     if (in.prefiltered && hdr[kHdrError] == pa.err_token)
         throw GsError("Point is filtered although prefiltered is set. This shouldn't happen!");
     r.K = (int)hdr[kHdrNumRendered];
-    if (!amr) note_k(r.K);
+    if (!amr) note_k(skey, r.K);
     if (!dup_done) {
         char* bbase = call_resize(binning, carve_binning(nullptr, r.K, nullptr, nullptr, amr), "binning");
         carve_binning(bbase, r.K, &r.b, amr ? &r.ab : nullptr);
@@ -466,7 +511,7 @@ int rasterizer_backward_impl(int amr_mode, int P, int D, int M, int R, const flo
         ImageView img;
         BinningView b;
         carve_geom(geom_buffer, P, &g);
-        carve_image(img_buffer, (size_t)width * height, T, &img);
+        carve_image(img_buffer, (size_t)width * height, T, &img, tile);
         carve_binning(binning_buffer, R, &b);
         if (!radii) radii = g.radii;
         zero_accum_unless_clean(g, P, s);
@@ -550,7 +595,7 @@ int gs_amr_rasterizer_backward(int P, int D, int M, int R, const float* backgrou
             if (!dL_dpix_scratch) throw GsError("gs_amr_rasterizer_backward: interpolation needs dL_dpix_scratch");
             const int T = ((width + 31) / 32) * ((height + 31) / 32);
             ImageView img;
-            carve_image(img_buffer, (size_t)width * height, T, &img);
+            carve_image(img_buffer, (size_t)width * height, T, &img, 32);
             launch_amr_interp_fold(width, height, img, dL_dpix, dL_dpix_scratch, s);
             stage_check(debug != 0, s, "amr_interp_fold");
             g = dL_dpix_scratch;
@@ -577,7 +622,7 @@ int gs_rasterizer_backward_view_grads(int P, int R, const float* background, int
         ImageView img;
         BinningView b;
         carve_geom(geom_buffer, P, &g);
-        carve_image(img_buffer, (size_t)width * height, T, &img);
+        carve_image(img_buffer, (size_t)width * height, T, &img, tile);
         carve_binning(binning_buffer, R, &b);
         if (!radii) radii = g.radii;
         zero_accum_unless_clean(g, P, s);
@@ -592,14 +637,14 @@ int gs_rasterizer_backward_view_grads(int P, int R, const float* background, int
 }
 
 namespace {
-int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* rows, size_t row_view_stride,
-                   const float* cams, size_t cam_stride, const float* means3D, const float* shs, const float* scales,
-                   const float* rotations, float scale_modifier, float* dL_dmeans3D, float* dL_dsh,
-                   float* dL_dopacity, float* dL_dscales, float* dL_drotations, float* grad_norm_accum, float* denom,
-                   float* max_radii, void* stream) {
+// rows[v] / cams[v]: view v's row of Gaussian g0 and its camera, summed in v order
+int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* const* rows, const float* const* cams,
+                   const float* means3D, const float* shs, const float* scales, const float* rotations,
+                   float scale_modifier, float* dL_dmeans3D, float* dL_dsh, float* dL_dopacity, float* dL_dscales,
+                   float* dL_drotations, float* grad_norm_accum, float* denom, float* max_radii, void* stream) {
     return guarded([&]() -> int {
         if (P <= 0 || count == 0) return 0;
-        if (V <= 0) throw GsError("gs_backward_gaussians_multiview: V must be positive");
+        if (V <= 0 || V > kMaxViews) throw GsError("gs_backward_gaussians_multiview: V must be in [1, 64]");
         if (g0 < 0 || count < 0 || g0 + count > P) throw GsError("gs_backward_gaussians_multiview: bad range");
         if (!scales || !rotations)
             throw GsError("gs_backward_gaussians_multiview: scales and rotations are required (no cov3D_precomp)");
@@ -607,14 +652,15 @@ int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* r
             throw GsError("gs_backward_gaussians_multiview: SH with 1..16 coefficients, degree <= 3");
         if (grad_norm_accum && (!denom || !max_radii))
             throw GsError("gs_backward_gaussians_multiview: statistics need grad_norm_accum, denom and max_radii");
-        MultiViewArgs a;
+        MultiViewArgs a{};
         a.P = P; a.D = D; a.M = M; a.V = V;
         a.g0 = g0;
         a.count = count;
-        a.rows = rows;
-        a.row_view_stride = row_view_stride;
-        a.cams = cams;
-        a.cam_stride = cam_stride;
+        for (int v = 0; v < V; v++) {
+            if (!rows[v] || !cams[v]) throw GsError("gs_backward_gaussians_multiview: null view row / camera");
+            a.rows[v] = rows[v];
+            a.cams[v] = cams[v];
+        }
         a.means3D = means3D;
         a.shs = shs;
         a.scales = scales;
@@ -634,6 +680,27 @@ int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* r
         return 0;
     });
 }
+
+// strided views: view v's rows at rows + v * row_view_stride
+int multiview_strided(int P, int g0, int count, int D, int M, int V, const float* rows, size_t row_view_stride,
+                      const float* cams, size_t cam_stride, const float* means3D, const float* shs,
+                      const float* scales, const float* rotations, float scale_modifier, float* dL_dmeans3D,
+                      float* dL_dsh, float* dL_dopacity, float* dL_dscales, float* dL_drotations,
+                      float* grad_norm_accum, float* denom, float* max_radii, void* stream) {
+    const float* rp[kMaxViews] = {};
+    const float* cp[kMaxViews] = {};
+    if (V > kMaxViews) {
+        g_err = "gs_backward_gaussians_multiview: V must be in [1, 64]";
+        return -1;
+    }
+    for (int v = 0; v < V; v++) {
+        rp[v] = rows + (size_t)v * row_view_stride;
+        cp[v] = cams + (size_t)v * cam_stride;
+    }
+    return multiview_impl(P, g0, count, D, M, V, rp, cp, means3D, shs, scales, rotations, scale_modifier,
+                          dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations, grad_norm_accum, denom,
+                          max_radii, stream);
+}
 }  // namespace
 
 int gs_backward_gaussians_multiview(int P, int D, int M, int V, const float* views, const float* means3D,
@@ -642,9 +709,9 @@ int gs_backward_gaussians_multiview(int P, int D, int M, int V, const float* vie
                                     float* dL_dscales, float* dL_drotations, float* grad_norm_accum, float* denom,
                                     float* max_radii, void* stream) {
     const size_t rec = (size_t)P * kViewRow + kCamWords;
-    return multiview_impl(P, 0, P, D, M, V, views, rec, views + (size_t)P * kViewRow, rec, means3D, shs, scales,
-                          rotations, scale_modifier, dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations,
-                          grad_norm_accum, denom, max_radii, stream);
+    return multiview_strided(P, 0, P, D, M, V, views, rec, views + (size_t)P * kViewRow, rec, means3D, shs, scales,
+                             rotations, scale_modifier, dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations,
+                             grad_norm_accum, denom, max_radii, stream);
 }
 
 int gs_backward_gaussians_multiview_range(int P, int g0, int count, int D, int M, int V, const float* rows,
@@ -654,9 +721,24 @@ int gs_backward_gaussians_multiview_range(int P, int g0, int count, int D, int M
                                           float* dL_dsh, float* dL_dopacity, float* dL_dscales,
                                           float* dL_drotations, float* grad_norm_accum, float* denom,
                                           float* max_radii, void* stream) {
-    return multiview_impl(P, g0, count, D, M, V, rows, row_view_stride, cams, cam_stride, means3D, shs, scales,
-                          rotations, scale_modifier, dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations,
-                          grad_norm_accum, denom, max_radii, stream);
+    return multiview_strided(P, g0, count, D, M, V, rows, row_view_stride, cams, cam_stride, means3D, shs, scales,
+                             rotations, scale_modifier, dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations,
+                             grad_norm_accum, denom, max_radii, stream);
+}
+
+int gs_backward_gaussians_multiview_views(int P, int g0, int count, int D, int M, int V, const float* const* rows,
+                                          const float* const* cams, const float* means3D, const float* shs,
+                                          const float* scales, const float* rotations, float scale_modifier,
+                                          float* dL_dmeans3D, float* dL_dsh, float* dL_dopacity, float* dL_dscales,
+                                          float* dL_drotations, float* grad_norm_accum, float* denom,
+                                          float* max_radii, void* stream) {
+    if (!rows || !cams) {
+        g_err = "gs_backward_gaussians_multiview_views: rows / cams arrays are required";
+        return -1;
+    }
+    return multiview_impl(P, g0, count, D, M, V, rows, cams, means3D, shs, scales, rotations, scale_modifier,
+                          dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations, grad_norm_accum, denom,
+                          max_radii, stream);
 }
 
 int gs_ritnet_conv(int ksize, int nseg, const float* const* in, const int* in_channels, const int* in_upsample,
@@ -777,7 +859,7 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
             ImageView img;
             BinningView b;
             carve_geom(geom_buffer_precomp, P, &g);
-            carve_image(image_buffer_precomp, (size_t)W * H, T, &img);
+            carve_image(image_buffer_precomp, (size_t)W * H, T, &img, 32);
             int K = num_rendered_hint;
             if (K < 0) {  // the reference reads K back here (amr/cr/rasterizer_impl.cu:337-340)
                 uint32_t hdr[4];
@@ -868,10 +950,10 @@ int gs_amr_fovea_levels(char* image_buffer, size_t image_buffer_bytes, int width
         }
         const int tile = 32;
         const size_t T = (size_t)((width + tile - 1) / tile) * ((height + tile - 1) / tile);
-        if (image_buffer_bytes < carve_image(nullptr, (size_t)width * height, T, nullptr))
+        if (image_buffer_bytes < carve_image(nullptr, (size_t)width * height, T, nullptr, tile))
             throw GsError("gs_amr_fovea_levels: image buffer too small for width x height");
         ImageView img;
-        carve_image(image_buffer, (size_t)width * height, T, &img);
+        carve_image(image_buffer, (size_t)width * height, T, &img, tile);
         hipStream_t s = static_cast<hipStream_t>(stream);
         launch_fovea_override(width, height, img, nfovea, cx, cy, r, min_level, replace, s);
         stage_check(false, s, "amr_fovea_levels");
@@ -1017,6 +1099,18 @@ int gs_set_tuning(const char* key, int value) {
         set_tile_order(value);
         return 0;
     }
+    if (std::strcmp(key, "sort_algo") == 0) {
+        set_sort_algo(value);
+        return 0;
+    }
+    if (std::strcmp(key, "bin_slots") == 0) {
+        set_bin_slots(value);
+        return 0;
+    }
+    if (std::strcmp(key, "dup_diag") == 0) {
+        set_dup_diag(value);
+        return 0;
+    }
     if (std::strcmp(key, "bin_chunk") == 0) {
         set_bin_chunk(value);
         return 0;
@@ -1088,7 +1182,7 @@ size_t gs_geom_bytes(int P) { return carve_geom(nullptr, (size_t)P, nullptr); }
 
 size_t gs_image_bytes(int width, int height, int tile) {
     const size_t T = (size_t)((width + tile - 1) / tile) * ((height + tile - 1) / tile);
-    return carve_image(nullptr, (size_t)width * height, T, nullptr);
+    return carve_image(nullptr, (size_t)width * height, T, nullptr, tile);
 }
 
 size_t gs_binning_bytes(int K) { return carve_binning(nullptr, (size_t)K, nullptr); }
@@ -1124,7 +1218,7 @@ int gs_geom_view_of(char* base, int P, gs_geom_view* out) {
 int gs_image_view_of(char* base, int width, int height, int tile, gs_image_view* out) {
     const size_t T = (size_t)((width + tile - 1) / tile) * ((height + tile - 1) / tile);
     ImageView v;
-    carve_image(base, (size_t)width * height, T, &v);
+    carve_image(base, (size_t)width * height, T, &v, tile);
     static_assert(sizeof(ImageView) == sizeof(gs_image_view), "view layout");
     std::memcpy(out, &v, sizeof(v));
     return 0;
@@ -1146,7 +1240,7 @@ int gs_reconstruct_keys(char* geom_buffer, char* binning_buffer, char* img_buffe
         ImageView img;
         BinningView b;
         carve_geom(geom_buffer, P, &g);
-        carve_image(img_buffer, (size_t)width * height, T, &img);
+        carve_image(img_buffer, (size_t)width * height, T, &img, tile);
         carve_binning(binning_buffer, K, &b);
         if (K > 0) launch_reconstruct_keys(T, img, b, g, keys_out, static_cast<hipStream_t>(stream));
         stage_check(false, static_cast<hipStream_t>(stream), "reconstruct_keys");

@@ -48,7 +48,7 @@ void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, c
 // base/cr/rasterizer_impl.cu:277-318, with identical outputs).
 // hdr_mirror: device address of 16 mapped host bytes that receive header
 // words 0..3 (K, error, max tile count, large tiles) when the scan finishes.
-void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror = nullptr);
+void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror, int nslots);
 // spec_hdr: a speculative launch into a buffer of spec_cap keys, enqueued
 // before the host knows K; it does nothing when the header's K > spec_cap.
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
@@ -60,6 +60,10 @@ constexpr int kLdsTiles = 16384;
 void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
                         hipStream_t s);
 void set_bin_chunk(int gaussians_per_workgroup);
+void set_dup_diag(int v);  // timing diagnostics only (wrong keys)
+void set_sort_algo(int v);  // 0 = bitonic networks, 1 = bucket sort (default)
+void set_bin_slots(int v);  // 0 = auto
+int bin_slots_for(int P);   // sub-bucket slots of the LDS binning for a P-Gaussian forward
 // img.tile_order = tiles sorted by descending work (heaviest first) so the
 // long tiles of a blend launch start early instead of forming its tail.
 // Work = range length, or min(range length, max_contrib) if use_max_contrib.
@@ -142,13 +146,12 @@ void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hi
 // the multi-view per-Gaussian backward.
 constexpr int kViewRow = 10;   // words per Gaussian per view
 constexpr int kCamWords = 40;  // view 16, proj 16, campos 3, W, H, tan_fovx, tan_fovy, pad
+constexpr int kMaxViews = 64;  // views summed by one multi-view launch
 struct MultiViewArgs {
     int P, D, M, V;
-    int g0, count;           // this launch: Gaussians [g0, g0 + count)
-    const float* rows;       // view 0's row of Gaussian g0 ([kViewRow] words per Gaussian)
-    size_t row_view_stride;  // floats from one view's rows to the next view's
-    const float* cams;       // view 0's camera ([kCamWords])
-    size_t cam_stride;       // floats from one view's camera to the next
+    int g0, count;                  // this launch: Gaussians [g0, g0 + count)
+    const float* rows[kMaxViews];   // view v's row of Gaussian g0 ([kViewRow] words per Gaussian), summed in v order
+    const float* cams[kMaxViews];   // view v's camera ([kCamWords])
     const float* means3D;
     const float* shs;  // nullable (colors precomputed: no SH gradient)
     const float* scales;

@@ -83,8 +83,9 @@ struct ImageView {
     float* accum_alpha;   // [N]
     uint32_t* n_contrib;  // [N]
     uint32_t* ranges;     // [T][2]
-    uint32_t* tile_count;  // [T] (= n_intersections for AMR)
-    uint32_t* tile_cursor;
+    uint32_t* tile_count;  // [kBinSlots][T] per-slot counts; after the tile scan [0..T) holds the totals
+                           // (= n_intersections for AMR)
+    uint32_t* tile_cursor; // [kBinSlots][T] sub-bucket cursors
     uint32_t* max_contrib;
     uint32_t* levels;          // tile_AMR_levels
     uint32_t* levels_last;     // tile_AMR_levels_last
@@ -100,15 +101,25 @@ struct ImageView {
     uint32_t* bucket_list;     // [kOrderBuckets64][T] the tiles of each bucket, in append order
 };
 constexpr int kOrderBuckets64 = 256;  // (name kept: the bucket count of the backward order)
+// Each tile's bucket is split into kBinSlots sub-buckets, one per
+// binning-workgroup slot (blockIdx % kBinSlots = the XCD the round-robin
+// dispatch puts the workgroup on): the runs that concurrently running chunks
+// of one XCD append to a tile are then adjacent in memory, and that XCD's L2
+// merges their scattered 8-B key stores into whole lines before write-back
+// (instead of one 32-B write granule per key).  The per-tile sort makes the
+// order inside a tile exact either way.
+constexpr int kBinSlots = 8;
 
-inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
+// tile: 16 (base) or 32 (AMR); the backward's work buckets (256 x T words,
+// filled by the base forward render) are carved for the base layout only.
+inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v, int tile) {
     size_t off = 0;
     ImageView g;
     g.accum_alpha = carve<float>(base, off, N);
     g.n_contrib = carve<uint32_t>(base, off, N);
     g.ranges = carve<uint32_t>(base, off, 2 * T);
-    g.tile_count = carve<uint32_t>(base, off, T);
-    g.tile_cursor = carve<uint32_t>(base, off, T);
+    g.tile_count = carve<uint32_t>(base, off, (size_t)kBinSlots * T);
+    g.tile_cursor = carve<uint32_t>(base, off, (size_t)kBinSlots * T);
     g.max_contrib = carve<uint32_t>(base, off, T);
     g.levels = carve<uint32_t>(base, off, T);
     g.levels_last = carve<uint32_t>(base, off, T);
@@ -119,8 +130,12 @@ inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v) {
     g.quad_count = carve<uint32_t>(base, off, 4 * T);
     g.region_count = carve<uint32_t>(base, off, 16 * T);
     g.tile_done = carve<uint32_t>(base, off, T);
-    g.bucket_count = carve<uint32_t>(base, off, kOrderBuckets64);
-    g.bucket_list = carve<uint32_t>(base, off, (size_t)kOrderBuckets64 * T);
+    g.bucket_count = nullptr;
+    g.bucket_list = nullptr;
+    if (tile != 32) {
+        g.bucket_count = carve<uint32_t>(base, off, kOrderBuckets64);
+        g.bucket_list = carve<uint32_t>(base, off, (size_t)kOrderBuckets64 * T);
+    }
     if (v) *v = g;
     return align_up(off);
 }

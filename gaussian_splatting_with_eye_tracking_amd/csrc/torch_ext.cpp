@@ -435,6 +435,59 @@ void BackwardGaussiansMultiviewRange(const Tensor& rows_in, const Tensor& cams_i
           "backward_gaussians_multiview_range");
 }
 
+// Stage 2 over separately stored views: rows[v] = view v's rows of Gaussians
+// [g0, g0 + count) (a contiguous [count * 10] slice), cams[v] = its camera
+// ([40]); views summed in list order.  Each all-gathered piece can stay in its
+// own [world, n] buffer.
+void BackwardGaussiansMultiviewViews(const std::vector<Tensor>& rows, const std::vector<Tensor>& cams, const int g0,
+                                     const Tensor& means3D_in, const Tensor& sh_in, const int degree,
+                                     const Tensor& scales_in, const Tensor& rotations_in, const float scale_modifier,
+                                     Tensor dL_dmeans3D, Tensor dL_dsh, Tensor dL_dopacity, Tensor dL_dscales,
+                                     Tensor dL_drotations, Tensor grad_norm_accum, Tensor denom, Tensor max_radii) {
+    const int P = (int)means3D_in.size(0);
+    const int V = (int)rows.size();
+    TORCH_CHECK(V >= 1 && V <= 64 && (int)cams.size() == V, "1 to 64 views, one camera each");
+    TORCH_CHECK(rows[0].dim() == 1 && rows[0].numel() % 10 == 0, "rows[v] must be a 1-D [count * 10] slice");
+    const int count = (int)(rows[0].numel() / 10);
+    TORCH_CHECK(g0 >= 0 && g0 + count <= P, "Gaussian range out of bounds");
+    const int M = sh_in.numel() != 0 ? (int)sh_in.size(1) : 0;
+    for (const Tensor* t : {&dL_dmeans3D, &dL_dopacity, &dL_dscales, &dL_drotations})
+        TORCH_CHECK(t->is_contiguous() && t->size(0) == P && t->scalar_type() == torch::kFloat32,
+                    "outputs must be contiguous float32 [P, ...] tensors");
+    TORCH_CHECK(M == 0 || (dL_dsh.is_contiguous() && dL_dsh.numel() == (int64_t)P * M * 3), "dL_dsh must be [P, M, 3]");
+    const bool stats = grad_norm_accum.numel() != 0;
+    if (stats) {
+        for (const Tensor* t : {&grad_norm_accum, &denom, &max_radii}) {
+            TORCH_CHECK(t->numel() == P && t->is_contiguous() && t->is_cuda() && t->scalar_type() == torch::kFloat32,
+                        "statistics tensors must be contiguous float32 device tensors with P elements");
+        }
+    }
+    const at::OptionalDeviceGuard guard(device_of(means3D_in));
+    const Tensor means3D = means3D_in.contiguous(), sh = sh_in.contiguous(), scales = scales_in.contiguous(),
+                 rotations = rotations_in.contiguous();
+    require_device(means3D, "means3D");
+    std::vector<const float*> rp(V), cp(V);
+    for (int v = 0; v < V; v++) {
+        TORCH_CHECK(rows[v].dim() == 1 && rows[v].numel() == (int64_t)count * 10 && rows[v].is_contiguous(),
+                    "rows[v] must be contiguous [count * 10] slices of equal length");
+        TORCH_CHECK(cams[v].dim() == 1 && cams[v].numel() == 40 && cams[v].is_contiguous(), "cams[v] must be [40]");
+        require_like(rows[v], means3D, "rows");
+        require_like(cams[v], means3D, "cams");
+        rp[v] = rows[v].data_ptr<float>();
+        cp[v] = cams[v].data_ptr<float>();
+    }
+    require_like(scales, means3D, "scales", 3LL * P);
+    require_like(rotations, means3D, "rotations", 4LL * P);
+    require_like(sh, means3D, "sh", (int64_t)P * M * 3);
+    check(gs_backward_gaussians_multiview_views(
+              P, g0, count, degree, M, V, rp.data(), cp.data(), fptr(means3D), fptr(sh), fptr(scales),
+              fptr(rotations), scale_modifier, fptr_mut(dL_dmeans3D), M ? fptr_mut(dL_dsh) : nullptr,
+              fptr_mut(dL_dopacity), fptr_mut(dL_dscales), fptr_mut(dL_drotations),
+              stats ? grad_norm_accum.data_ptr<float>() : nullptr, stats ? denom.data_ptr<float>() : nullptr,
+              stats ? max_radii.data_ptr<float>() : nullptr, stream_of(means3D)),
+          "backward_gaussians_multiview_views");
+}
+
 // ---- eye-tracking front end (ritnet.hip) ----
 // out [32, H, W] = conv over the virtual concatenation of `ins` (each
 // [C, h, w]; up[i] = 1: read through nearest 2x upsampling).
@@ -757,6 +810,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("rasterize_gaussians_backward_view_grads", &RasterizeGaussiansBackwardViewGrads);
     m.def("backward_gaussians_multiview", &BackwardGaussiansMultiview);
     m.def("backward_gaussians_multiview_range", &BackwardGaussiansMultiviewRange);
+    m.def("backward_gaussians_multiview_views", &BackwardGaussiansMultiviewViews);
     m.def("ritnet_conv", &RitnetConv);
     m.def("avgpool2", &AvgPool2);
     m.def("ritnet_head", &RitnetHead);

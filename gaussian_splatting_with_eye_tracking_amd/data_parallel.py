@@ -173,29 +173,72 @@ class ViewExchange:
     def __init__(self, P: int, views_per_rank: int, device, group=None, chunks: int = 4):
         self.P, self.v, self.group, self.chunks = int(P), int(views_per_rank), group, max(1, int(chunks))
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.nccl = self.world > 1 and dist.get_backend(group) == "nccl"
         self.RL = view_record_numel(self.P)
-        self.buf = torch.empty((self.world, self.v, self.RL), dtype=torch.float32, device=device)
+        self.device = device
+        if self.world == 1:
+            self.buf = torch.empty((self.v, self.RL), dtype=torch.float32, device=device)
+        # every gather lands in its own contiguous [world, n] buffer (one
+        # all_gather_into_tensor on RCCL, no flatten copy); the multi-view
+        # kernel then reads view (r, j) through a per-view row pointer
+        self.full: List[torch.Tensor] = []        # views 0 .. v-2: [world, RL]
         self.pending: List[object] = []
-        self.last: List[Tuple[int, int, object]] = []
+        self.last: List[Tuple[int, int, torch.Tensor, object]] = []  # (a, b, [world, (b-a)*10], work)
+        self.cam_stage = None
         self.cam_work = None
 
-    def _gather(self, src: torch.Tensor, j: int, lo: int, hi: int):
-        outs = [self.buf[r, j, lo:hi] for r in range(self.world)]
-        return dist.all_gather(outs, src.contiguous(), group=self.group, async_op=True)
+    def _gather(self, src: torch.Tensor):
+        src = src.contiguous()
+        out = torch.empty((self.world, src.numel()), dtype=src.dtype, device=src.device)
+        if self.nccl:
+            w = dist.all_gather_into_tensor(out, src, group=self.group, async_op=True)
+        else:
+            w = dist.all_gather(list(out.unbind(0)), src, group=self.group, async_op=True)
+        return out, w
 
     def add(self, j: int, rec: torch.Tensor) -> None:
         if self.world == 1:
-            self.buf[0, j].copy_(rec)
+            self.buf[j].copy_(rec)
             return
         P = self.P
         if j < self.v - 1 or P == 0:
-            self.pending.append(self._gather(rec, j, 0, self.RL))
+            out, w = self._gather(rec)
+            self.full.append(out)
+            self.pending.append(w)
             return
-        self.cam_work = self._gather(rec[P * VIEW_ROW:], j, P * VIEW_ROW, self.RL)
+        self.cam_stage, self.cam_work = self._gather(rec[P * VIEW_ROW:])
         step = max(1, -(-P // self.chunks))
         for a in range(0, P, step):
             b = min(P, a + step)
-            self.last.append((a, b, self._gather(rec[a * VIEW_ROW:b * VIEW_ROW], j, a * VIEW_ROW, b * VIEW_ROW)))
+            out, w = self._gather(rec[a * VIEW_ROW:b * VIEW_ROW])
+            self.last.append((a, b, out, w))
+
+    # views in rank-then-view order (the order exchange_view_records sums in)
+    def _cams(self) -> List[torch.Tensor]:
+        P = self.P
+        return [self.full[j][r, P * VIEW_ROW:] if j < self.v - 1 else self.cam_stage[r]
+                for r in range(self.world) for j in range(self.v)]
+
+    def _rows(self, a: int, b: int, chunk: torch.Tensor) -> List[torch.Tensor]:
+        return [self.full[j][r, a * VIEW_ROW:b * VIEW_ROW] if j < self.v - 1 else chunk[r]
+                for r in range(self.world) for j in range(self.v)]
+
+    def wait(self) -> None:
+        for w in self.pending:
+            w.wait()
+        if self.cam_work is not None:
+            self.cam_work.wait()
+        for _a, _b, _c, w in self.last:
+            w.wait()
+
+    def records(self) -> torch.Tensor:
+        """The gathered records as one [world * v, RL] tensor in summation
+        order (a copy, for checks; finish() reads them in place)."""
+        if self.world == 1:
+            return self.buf.clone()
+        self.wait()
+        pieces = [self._rows(a, b, ch) for a, b, ch, _w in self.last]  # per chunk: one slice per view
+        return torch.stack([torch.cat([p[i] for p in pieces] + [c]) for i, c in enumerate(self._cams())])
 
     def finish(self, settings, means3D: torch.Tensor, shs: torch.Tensor, scales: torch.Tensor,
                rotations: torch.Tensor, stats=None):
@@ -204,27 +247,26 @@ class ViewExchange:
             for w in self.pending:
                 w.wait()
             return _empty_param_grads(means3D, shs)
-        views = self.buf.view(self.world * self.v, self.RL)
         if self.world == 1:
-            return multiview_param_grads(views, means3D, shs, settings.sh_degree, scales, rotations,
+            return multiview_param_grads(self.buf, means3D, shs, settings.sh_degree, scales, rotations,
                                          settings.scale_modifier, stats)
         from . import _C
         for w in self.pending:
             w.wait()
         self.cam_work.wait()
-        cams = views[:, P * VIEW_ROW:]
+        cams = self._cams()
         dev = means3D.device
         M = shs.shape[1] if shs is not None and shs.numel() else 0
         outs = (torch.empty((P, 3), device=dev), torch.empty((P, M, 3), device=dev), torch.empty((P, 1), device=dev),
                 torch.empty((P, 3), device=dev), torch.empty((P, 4), device=dev))
         e = torch.empty(0, device=dev)
         st = stats if stats is not None else (e, e, e)
-        for a, b, w in self.last:
+        for a, b, chunk, w in self.last:
             w.wait()
-            _C.backward_gaussians_multiview_range(views[:, a * VIEW_ROW:b * VIEW_ROW], cams, a, means3D,
-                                                  shs if shs is not None else e, int(settings.sh_degree), scales,
-                                                  rotations, float(settings.scale_modifier), *outs, st[0], st[1],
-                                                  st[2])
+            _C.backward_gaussians_multiview_views(self._rows(a, b, chunk), cams, a, means3D,
+                                                  shs if shs is not None else e,
+                                                  int(settings.sh_degree), scales, rotations,
+                                                  float(settings.scale_modifier), *outs, st[0], st[1], st[2])
         return outs
 
 

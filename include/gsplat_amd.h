@@ -118,6 +118,17 @@ int gs_backward_gaussians_multiview_range(int P, int g0, int count, int D, int M
                                           float* dL_drotations, float* grad_norm_accum, float* denom,
                                           float* max_radii, void* stream);
 
+/* The same over V <= 64 views whose rows need not share a stride: rows[v]
+ * (host array of device pointers) is view v's row of Gaussian g0, cams[v]
+ * its 40-word camera; views are summed in v order.  Lets every all-gathered
+ * piece stay in its own contiguous [world, n] buffer (no flatten copies). */
+int gs_backward_gaussians_multiview_views(int P, int g0, int count, int D, int M, int V, const float* const* rows,
+                                          const float* const* cams, const float* means3D, const float* shs,
+                                          const float* scales, const float* rotations, float scale_modifier,
+                                          float* dL_dmeans3D, float* dL_dsh, float* dL_dopacity, float* dL_dscales,
+                                          float* dL_drotations, float* grad_norm_accum, float* denom,
+                                          float* max_radii, void* stream);
+
 /* Eye-tracking front end (RITnet/densenet.py:17-144,
  * track_render.py:50-97).  Activations are [C][H][W] float32 planes.
  *
@@ -304,8 +315,8 @@ typedef struct {
     uint32_t* quad_count; /* [T][4] AMR quadrant sub-list lengths */
     uint32_t* region_count; /* [T][16] AMR 8x8-region sub-list lengths */
     uint32_t* tile_done; /* [T] AMR steps: finished units per tile, mod 4 */
-    uint32_t* bucket_count; /* [256] base forward: tiles per work bucket (heaviest first) */
-    uint32_t* bucket_list;  /* [256][T] base forward: the tiles of each bucket */
+    uint32_t* bucket_count; /* [256] base forward: tiles per work bucket (heaviest first); NULL for tile 32 */
+    uint32_t* bucket_list;  /* [256][T] base forward: the tiles of each bucket; NULL for tile 32 */
 } gs_image_view;
 
 typedef struct {

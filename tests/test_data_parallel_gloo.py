@@ -214,12 +214,7 @@ def _pipelined_worker(rank, world, port, q):
         ex = DP.ViewExchange(P, v, "cpu", chunks=4)
         for j in range(v):  # record of (rank, view j): its values say whose it is
             ex.add(j, torch.arange(n, dtype=torch.float32) + 1000.0 * (rank * v + j))
-        for w in ex.pending:
-            w.wait()
-        ex.cam_work.wait()
-        for _a, _b, w in ex.last:
-            w.wait()
-        q.put((rank, ex.buf.view(world * v, n).numpy().copy()))
+        q.put((rank, ex.records().numpy().copy()))
     finally:
         dist.destroy_process_group()
 

@@ -151,6 +151,117 @@ def test_backward_parity(name, P, W, H, seed, variant):
             assert G.rel_err(gl.cpu().numpy(), g.cpu().numpy()) < 1e-5, n  # (float atomics: run-order noise)
 
 
+@pytest.mark.parametrize("slots", [1, 3, 8, 0])
+def test_bin_slots_bit_exact(slots):
+    """The binning's per-slot sub-buckets (gs_layout.h kBinSlots) change only
+    where inside a tile's range the duplicate lands each key; after the
+    per-tile sort point_list, keys and ranges are the oracle's bit for bit."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    P, W, H, seed = 20000, 128, 128, 11
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    C.set_tuning("bin_slots", slots)
+    try:
+        _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
+    finally:
+        C.set_tuning("bin_slots", 0)  # auto
+    _, ref, _ = _oracle_forward(sc, cam)
+    assert K == ref.num_rendered
+    d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
+    np.testing.assert_array_equal(d["ranges"].cpu().numpy().astype(np.uint32), ref.ranges)
+    np.testing.assert_array_equal(d["point_list"].cpu().numpy().astype(np.uint32), ref.point_list)
+    np.testing.assert_array_equal(d["tile_count"].cpu().numpy().astype(np.uint32), ref.ranges[:, 1] - ref.ranges[:, 0])
+    assert G.image_l1(color.cpu().numpy(), ref.color) < G.IMAGE_L1_TOL
+
+
+def _clustered_scene(P, cam, seed, kind):
+    """Depth distributions that stress the per-tile sort: 'ties' -- a third of
+    the Gaussians are exact copies (same mean, so the same depth bits: the
+    order falls to the index, as after clone densification); 'cluster' -- 90 %
+    of the depths within 0.1 % of each other plus a few far outliers (the
+    bucket map's range is wide, its buckets crowded: the bitonic fallback);
+    'two' -- two depth planes."""
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    sc = S.make_scene(P, cam, seed=seed)
+    rng = np.random.default_rng(seed + 99)
+    m = sc.means3D.copy()
+    f = np.where(rng.random(P) < 0.5, 1.0, rng.random(P))  # half uniform, half towards the centre
+    m[:, :2] *= f[:, None].astype(np.float32)  # (tiles of every size class)
+    if kind == "ties":
+        src = rng.integers(0, P // 20, P // 3)
+        dst = rng.choice(np.arange(P // 20, P), P // 3, replace=False)
+        m[dst] = m[src]
+    elif kind == "cluster":
+        z = np.where(rng.random(P) < 0.9, 5.0 + 0.005 * rng.random(P), 2.0 + 18.0 * rng.random(P)).astype(np.float32)
+        m[:, :2] *= (z / m[:, 2])[:, None]
+        m[:, 2] = z
+    else:
+        z = np.where(rng.random(P) < 0.5, 4.0, 9.0).astype(np.float32)
+        m[:, :2] *= (z / m[:, 2])[:, None]
+        m[:, 2] = z
+    sc.means3D = m.astype(np.float32)
+    return sc
+
+
+@pytest.mark.parametrize("kind", ["ties", "cluster", "two"])
+@pytest.mark.parametrize("sort_algo", [0, 1])
+def test_tile_sort_adversarial_depths(kind, sort_algo):
+    """point_list / ranges bit-exact against the oracle's stable (depth, idx)
+    order for both tile sorts (bucket sort, bitonic networks) on tiles of
+    every size class (<= 1024, <= 2048, <= 4096 and the merge path)."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    P, W, H = 100000, 256, 192
+    cam = S.make_camera(W, H)
+    sc = _clustered_scene(P, cam, 5, kind)
+    C.set_tuning("sort_algo", sort_algo)
+    try:
+        _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
+    finally:
+        C.set_tuning("sort_algo", 1)
+    _, ref, _ = _oracle_forward(sc, cam)
+    assert K == ref.num_rendered
+    n = ref.ranges[:, 1] - ref.ranges[:, 0]
+    assert all(((n > a) & (n <= b)).any() for a, b in ((1, 1024), (1024, 2048), (2048, 4096), (4096, 1 << 30)))
+    d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
+    np.testing.assert_array_equal(d["ranges"].cpu().numpy().astype(np.uint32), ref.ranges)
+    np.testing.assert_array_equal(d["point_list"].cpu().numpy().astype(np.uint32), ref.point_list)
+    np.testing.assert_array_equal(d["point_list_keys"].cpu().numpy().view(np.uint64), ref.point_list_keys)
+
+
+def test_backward_with_unfilled_work_buckets():
+    """render_bwd takes its heaviest-first order from the work buckets the
+    base forward render fills.  An image buffer whose buckets do not cover
+    the grid (zeroed here, as after a forward that never rendered) must not
+    drop tiles: every block falls back to the identity order and the
+    gradients are unchanged (atomic-order noise only)."""
+    import ctypes
+    import os
+    import gaussian_splatting_with_eye_tracking_amd as pkg
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    P, W, H, seed = 3000, 250, 130, 7
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    dpix = torch.from_numpy(S.make_cotangent(H, W, seed + 1)).cuda()
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(pkg.__file__), "libgsplat_amd.so"))
+    view = (ctypes.c_void_p * 17)()
+    base = 1 << 20
+    assert lib.gs_image_view_of(ctypes.c_void_p(base), W, H, 16, ctypes.byref(view)) == 0
+    off = view[15] - base  # bucket_count
+    e = torch.Tensor([])
+    out = []
+    for corrupt in (False, True):
+        s, t, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
+        if corrupt:
+            img[off:off + 1024].zero_()
+        g = C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, e, t["scales"], t["rotations"],
+                                           s.scale_modifier, e, s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy,
+                                           dpix, t["shs"], s.sh_degree, s.campos, geom, K, binning, img, False)
+        out.append([x.cpu().numpy() for x in g])
+    for a, b in zip(*out):
+        assert np.all(np.isfinite(b))
+        assert G.rel_err(b, a) < 1e-5
+
+
 @pytest.mark.parametrize("xcd_map", [0, 1, 2, 3])
 def test_xcd_placement_is_result_invariant(xcd_map):
     """XCD-aware tile placement (gs_blend.cuh; bit 0 forward, bit 1
