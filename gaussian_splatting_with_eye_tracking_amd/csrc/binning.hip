@@ -766,17 +766,17 @@ constexpr int kBucketMax = 64;
 int g_sort_algo = 1;  // set_tuning("sort_algo"): 0 = bitonic networks only, 1 = bucket sort
 void set_sort_algo(int v) { g_sort_algo = v; }
 
-template <int kE>
-__global__ void __launch_bounds__(kSortThreads) sort_tiles_bucket_kernel(int lo, int hi,
-                                                                          const uint32_t* __restrict__ ranges,
-                                                                          const uint64_t* __restrict__ pair_keys,
-                                                                          uint32_t* __restrict__ point_list) {
-    constexpr int kT = kSortThreads;
+// kT threads, kE keys each (n <= kT kE); nb ~ n >> kBS buckets.
+template <int kT, int kE, int kBS>
+__global__ void __launch_bounds__(kT) sort_tiles_bucket_kernel(int lo, int hi, const uint32_t* __restrict__ ranges,
+                                                                const uint64_t* __restrict__ pair_keys,
+                                                                uint32_t* __restrict__ point_list) {
     constexpr int kW = kT / 64;
-    constexpr int kN = kT * kE;   // keys per tile
-    constexpr int kNB = kN / 2;   // buckets at full capacity
+    constexpr int kN = kT * kE;                // keys per tile
+    constexpr int kNB = kN >> kBS;            // buckets at full capacity
     __shared__ uint64_t s_tmp[kN];
-    __shared__ uint32_t s_start[kNB];
+    // bucket counts, then (scan) starts, then (fill) ends: after the fill,
+    // bucket b spans [b ? s_fill[b - 1] : 0, s_fill[b])
     __shared__ uint32_t s_fill[kNB];
     __shared__ uint32_t s_red[2 * kW];
     __shared__ uint32_t s_wave[kW + 1];
@@ -791,9 +791,9 @@ __global__ void __launch_bounds__(kSortThreads) sort_tiles_bucket_kernel(int lo,
         if (tid == 0) out[0] = (uint32_t)keys[0];
         return;
     }
-    // buckets in use: a power of two >= n / 2 (block-uniform)
+    // buckets in use: a power of two >= n >> kBS, >= 64 (block-uniform)
     int lg = 6;
-    while ((1 << lg) < (n + 1) / 2) lg++;
+    while ((1 << lg) < ((n + (1 << kBS) - 1) >> kBS)) lg++;
     const int nb = 1 << lg;  // <= kNB
     uint64_t k[kE];
     uint32_t dmin = ~0u, dmax = 0u;
@@ -853,8 +853,7 @@ __global__ void __launch_bounds__(kSortThreads) sort_tiles_bucket_kernel(int lo,
     for (int q = 0; q < per; q++) {
         if (b0 + q < nb) {
             const uint32_t c = s_fill[b0 + q];
-            s_start[b0 + q] = run;
-            s_fill[b0 + q] = run;
+            s_fill[b0 + q] = run;  // start = the fill pointer
             run += c;
         }
     }
@@ -876,13 +875,17 @@ __global__ void __launch_bounds__(kSortThreads) sort_tiles_bucket_kernel(int lo,
     for (int e = 0; e < kE; e++) {
         const int i = e * kT + tid;
         if (i < n) {
-            const uint32_t bs = s_start[bk[e]], be = s_fill[bk[e]];
+            const uint32_t b = bk[e];
+            const uint32_t bs = b ? s_fill[b - 1] : 0u, be = s_fill[b];
             uint32_t r = 0;
             for (uint32_t j = bs; j < be; j++) r += s_tmp[j] < k[e] ? 1u : 0u;
             out[bs + r] = (uint32_t)k[e];
         }
     }
 }
+
+int g_sort_variant = 0;  // set_tuning("sort_variant"): geometry of the bucket kernels (A/B)
+void set_sort_variant(int v) { g_sort_variant = v; }
 
 // Merge-path split: number of elements taken from A for the first `diag`
 // outputs of merge(A[0..na), B[0..nb)); keys are unique.
@@ -950,14 +953,42 @@ void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int ma
                        hipStream_t s) {
     if (T == 0) return;
     if (g_sort_algo == 1) {
-        hipLaunchKernelGGL(sort_tiles_bucket_kernel<4>, dim3(T), dim3(kSortThreads), 0, s, 0, 1024, img.ranges,
-                           b.pair_keys, b.point_list);
-        if (max_count_host > 1024)
-            hipLaunchKernelGGL(sort_tiles_bucket_kernel<8>, dim3(T), dim3(kSortThreads), 0, s, 1024, 2048,
-                               img.ranges, b.pair_keys, b.point_list);
-        if (max_count_host > 2048)
-            hipLaunchKernelGGL(sort_tiles_bucket_kernel<16>, dim3(T), dim3(kSortThreads), 0, s, 2048, kSmallCap,
-                               img.ranges, b.pair_keys, b.point_list);
+#define GS_BK(TH, E, BS, LO, HI)                                                                      \
+    hipLaunchKernelGGL((sort_tiles_bucket_kernel<TH, E, BS>), dim3(T), dim3(TH), 0, s, LO, HI, img.ranges, \
+                       b.pair_keys, b.point_list)
+        switch (g_sort_variant) {
+            case 1:  // 256 threads for every class
+                GS_BK(256, 4, 1, 0, 1024);
+                if (max_count_host > 1024) GS_BK(256, 8, 1, 1024, 2048);
+                if (max_count_host > 2048) GS_BK(256, 16, 1, 2048, kSmallCap);
+                break;
+            case 2:  // 1024 threads for the largest class
+                GS_BK(256, 4, 1, 0, 1024);
+                if (max_count_host > 1024) GS_BK(512, 4, 1, 1024, 2048);
+                if (max_count_host > 2048) GS_BK(1024, 4, 1, 2048, kSmallCap);
+                break;
+            case 3:  // ~n / 4 buckets
+                GS_BK(256, 4, 2, 0, 1024);
+                if (max_count_host > 1024) GS_BK(512, 4, 2, 1024, 2048);
+                if (max_count_host > 2048) GS_BK(512, 8, 2, 2048, kSmallCap);
+                break;
+            case 4:  // 128 threads for the smallest class
+                GS_BK(128, 8, 1, 0, 1024);
+                if (max_count_host > 1024) GS_BK(512, 4, 1, 1024, 2048);
+                if (max_count_host > 2048) GS_BK(512, 8, 1, 2048, kSmallCap);
+                break;
+            case 5:
+                GS_BK(256, 4, 1, 0, 1024);
+                if (max_count_host > 1024) GS_BK(512, 4, 1, 1024, 2048);
+                if (max_count_host > 2048) GS_BK(512, 8, 1, 2048, kSmallCap);
+                break;
+            default:  // measured best at configs 2, 3 and 4 (profiles/r03c_ab_sort_variant_*)
+                GS_BK(256, 4, 1, 0, 1024);
+                if (max_count_host > 1024) GS_BK(512, 4, 1, 1024, 2048);
+                if (max_count_host > 2048) GS_BK(512, 8, 2, 2048, kSmallCap);
+                break;
+        }
+#undef GS_BK
         if (num_large_host > 0)
             hipLaunchKernelGGL(sort_tiles_large_kernel, dim3(num_large_host), dim3(kLargeThreads), 0, s,
                                img.large_tiles, img.ranges, b.pair_keys, b.scratch, b.point_list);

@@ -1099,6 +1099,10 @@ int gs_set_tuning(const char* key, int value) {
         set_tile_order(value);
         return 0;
     }
+    if (std::strcmp(key, "sort_variant") == 0) {
+        set_sort_variant(value);
+        return 0;
+    }
     if (std::strcmp(key, "sort_algo") == 0) {
         set_sort_algo(value);
         return 0;

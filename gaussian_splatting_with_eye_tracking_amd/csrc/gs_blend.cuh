@@ -258,7 +258,36 @@ struct BlendStateT {
 // Front-to-back blend of `range` for the thread's kPPL pixels.  Called by the
 // whole workgroup (kWaves waves); LDS batches hold 64*kWaves Gaussians.
 // (ox, oy, st): the block origin and pixel stride, for the row-group cull.
-template <int kPPL, int kWaves>
+// One Gaussian against the lane's pixel, as selects instead of exec-masked
+// branches (kSel): the reference's per-pixel continues / early stop
+// (forward.cu:333-352) become values -- a rejected pair gets alpha 0, which
+// leaves C (C + f * 0 * T), T (T * (1 - 0)) and the stop test (T >= 1e-4 for
+// every pixel still blending) unchanged bit for bit; `last` moves only for
+// alpha != 0.  A finished pixel carries cap = 0 instead of 0.99 in the
+// alpha clamp min(cap, o G), so it rejects every later Gaussian (NaN G
+// included: fminf returns the number) with no extra instruction.  Per pair
+// ~26 VALU and no SALU instead of ~25 VALU + ~20 SALU of exec-mask
+// bookkeeping.
+__device__ __forceinline__ void blend_one_sel(float2 xy, float4 co, float4 f, float pxx, float pxy, uint32_t contributor,
+                                              float& T, float (&C)[3], uint32_t& last, float& cap) {
+    const float dx = xy.x - pxx, dy = xy.y - pxy;
+    const float p = splat_p2(dx, dy, co);
+    float a = fminf(cap, co.w * splat_exp(p));
+    a = (p > 0.0f) ? 0.0f : a;           // power > 0: skipped
+    a = (a < 1.0f / 255.0f) ? 0.0f : a;  // alpha < 1/255: skipped
+    const float test_T = T * (1.0f - a);
+    const bool stop = test_T < 0.0001f;  // false whenever a == 0 (T >= 1e-4)
+    cap = stop ? 0.0f : cap;
+    a = stop ? 0.0f : a;
+    const float w = a * T;
+    C[0] = __builtin_fmaf(f.x, w, C[0]);
+    C[1] = __builtin_fmaf(f.y, w, C[1]);
+    C[2] = __builtin_fmaf(f.z, w, C[2]);
+    T = stop ? T : test_T;
+    last = (a != 0.0f) ? contributor : last;
+}
+
+template <int kPPL, int kWaves, bool kSel = false>
 __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const PixelSetT<kPPL>& px, float ox, float oy,
                                                           float st, const uint32_t* __restrict__ point_list,
                                                           const float2* __restrict__ means2D,
@@ -314,6 +343,30 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
             for (int k = 0; k < kPPL; k++) {
                 mk[k] = uniform_u64(s_bal[c * 4 + wave * kPPL + k]);
                 todo |= mk[k];
+            }
+            if constexpr (kPPL == 1 && kSel) {
+                // select form (blend_one_sel), two Gaussians per iteration; the
+                // wave's early exit is tested once per 64 batch slots
+                float cap = done[0] ? 0.0f : 0.99f;
+                while (todo) {
+                    const uint32_t bA = (uint32_t)__builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    const bool two = todo != 0;  // wave-uniform
+                    const uint32_t bB = two ? (uint32_t)__builtin_ctzll(todo) : bA;
+                    if (two) todo &= todo - 1;
+                    const uint32_t jA = c * 64 + bA, jB = c * 64 + bB;
+                    const float4 sA = s_a[jA], sB = s_a[jB];
+                    const float4 coA = s_co[jA], coB = s_co[jB];
+                    const float bAc = s_b[jA], bBc = s_b[jB];
+                    blend_one_sel(make_float2(sA.x, sA.y), coA, make_float4(sA.z, sA.w, bAc, 0.f), px.x, px.y[0],
+                                  b0 + jA + 1, st_.T[0], st_.C[0], st_.last[0], cap);
+                    if (two)
+                        blend_one_sel(make_float2(sB.x, sB.y), coB, make_float4(sB.z, sB.w, bBc, 0.f), px.x, px.y[0],
+                                      b0 + jB + 1, st_.T[0], st_.C[0], st_.last[0], cap);
+                }
+                done[0] = cap == 0.0f;
+                if (__ballot(!done[0]) == 0ull) wave_alive = false;
+                continue;
             }
             if constexpr (kPPL == 1) {
                 // One row group per wave: every set bit of todo is a visit.  Two

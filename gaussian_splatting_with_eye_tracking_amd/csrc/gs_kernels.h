@@ -61,7 +61,8 @@ void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H
                         hipStream_t s);
 void set_bin_chunk(int gaussians_per_workgroup);
 void set_dup_diag(int v);  // timing diagnostics only (wrong keys)
-void set_sort_algo(int v);  // 0 = bitonic networks, 1 = bucket sort (default)
+void set_sort_algo(int v);
+void set_sort_variant(int v);  // 0 = bitonic networks, 1 = bucket sort (default)
 void set_bin_slots(int v);  // 0 = auto
 int bin_slots_for(int P);   // sub-bucket slots of the LDS binning for a P-Gaussian forward
 // img.tile_order = tiles sorted by descending work (heaviest first) so the

@@ -43,8 +43,8 @@ __device__ __forceinline__ void write_pixels(const PixelSetT<kPPL>& px, const Bl
 }
 
 // One 16x16 tile per workgroup of kWaves waves (kPPL pixels per lane).
-template <int kPPL, int kWaves>
-__global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
+template <int kPPL, int kWaves, int kMinWaves = 1, bool kSel = false>
+__global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
                                                                  const uint32_t* __restrict__ point_list,
                                                                  const float2* __restrict__ means2D,
                                                                  const float* __restrict__ features,
@@ -76,7 +76,7 @@ __global__ void __launch_bounds__(64 * kWaves) render_fwd_kernel(int W, int H, c
     const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, 1);
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const BlendStateT<kPPL> st =
-        blend_tile_t<kPPL, kWaves>(range, px, (float)ox, (float)oy, 1.0f, point_list,
+        blend_tile_t<kPPL, kWaves, kSel>(range, px, (float)ox, (float)oy, 1.0f, point_list,
                                    means2D, features, conic_opacity, s_a, s_co, s_b, s_bal, cull != 0);
     write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
     uint32_t m = 0;
@@ -112,7 +112,11 @@ void set_cull(int v) { g_cull = v; }
 int g_xcd_map = 1;
 void set_xcd_map(int v) { g_xcd_map = v; }
 
-int g_fwd_variant = 2;  // 0: 1 wave x 4 px/lane, 1: 2 waves x 2 px/lane, 2: 4 waves x 1 px/lane
+// 0: 1 wave x 4 px/lane, 1: 2 waves x 2 px/lane, 2: 4 waves x 1 px/lane; 3: 2 at <= 64 VGPRs (8 waves
+// per SIMD: 0.307 -> 0.299 ms at config 2, profiles/r03c_ab_fwd_variant_cfg2.log); 5: 3 with the
+// select-form blend (gs_blend.cuh blend_one_sel: 0.305 -> 0.277 ms at config 2, 0.237 -> 0.223 ms at
+// config 4, profiles/r03d_ab_fwd_select_cfg{2,4}.log); 6: 5 at the default occupancy
+int g_fwd_variant = 5;
 
 void set_forward_variant(int v) { g_fwd_variant = v; }
 
@@ -127,8 +131,9 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
     // (early termination makes the range a poor work estimate); the backward
     // orders by max_contrib instead (backward.hip).
     const uint32_t* order = nullptr;
-#define GS_FWD_LAUNCH(PPL, WAVES)                                                                                \
-    hipLaunchKernelGGL((render_fwd_kernel<PPL, WAVES>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H, img.ranges, \
+#define GS_FWD_LAUNCH(PPL, WAVES, ...)                                                                           \
+    hipLaunchKernelGGL((render_fwd_kernel<PPL, WAVES, ##__VA_ARGS__>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H, \
+                       img.ranges, \
                        b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
                        img.max_contrib, bg, out_color, g_cull, order, gx, g_xcd_map & 1, zero4, zero_n4,     \
@@ -136,7 +141,11 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
     switch (g_fwd_variant) {
         case 0: GS_FWD_LAUNCH(4, 1); break;
         case 1: GS_FWD_LAUNCH(2, 2); break;
-        default: GS_FWD_LAUNCH(1, 4); break;
+        case 2: GS_FWD_LAUNCH(1, 4); break;
+        case 3: GS_FWD_LAUNCH(1, 4, 8); break;  // <= 64 VGPRs: 8 waves per SIMD
+        case 4: GS_FWD_LAUNCH(1, 4, 6); break;
+        case 6: GS_FWD_LAUNCH(1, 4, 1, true); break;
+        default: GS_FWD_LAUNCH(1, 4, 8, true); break;  // 5: 3 + the select-form blend
     }
 #undef GS_FWD_LAUNCH
     return zero_n4 > 0;

@@ -203,8 +203,8 @@ def _clustered_scene(P, cam, seed, kind):
 
 
 @pytest.mark.parametrize("kind", ["ties", "cluster", "two"])
-@pytest.mark.parametrize("sort_algo", [0, 1])
-def test_tile_sort_adversarial_depths(kind, sort_algo):
+@pytest.mark.parametrize("sort_algo,variant", [(0, 0), (1, 0), (1, 1), (1, 2), (1, 3), (1, 4)])
+def test_tile_sort_adversarial_depths(kind, sort_algo, variant):
     """point_list / ranges bit-exact against the oracle's stable (depth, idx)
     order for both tile sorts (bucket sort, bitonic networks) on tiles of
     every size class (<= 1024, <= 2048, <= 4096 and the merge path)."""
@@ -214,10 +214,12 @@ def test_tile_sort_adversarial_depths(kind, sort_algo):
     cam = S.make_camera(W, H)
     sc = _clustered_scene(P, cam, 5, kind)
     C.set_tuning("sort_algo", sort_algo)
+    C.set_tuning("sort_variant", variant)
     try:
         _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
     finally:
         C.set_tuning("sort_algo", 1)
+        C.set_tuning("sort_variant", 0)
     _, ref, _ = _oracle_forward(sc, cam)
     assert K == ref.num_rendered
     n = ref.ranges[:, 1] - ref.ranges[:, 0]
@@ -339,7 +341,7 @@ def test_config2_full_size_parity_and_psnr():
 
 
 @pytest.mark.parametrize("bwd_variant", [0, 1, 2, 3])
-@pytest.mark.parametrize("fwd_variant", [0, 1, 2])
+@pytest.mark.parametrize("fwd_variant", [0, 1, 2, 3, 4, 5, 6])
 def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
     """Every forward / backward blend geometry (gs_set_tuning) against the oracle."""
     import oracle as O
