@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ bg,
     float* __restrict__ grad_accum, int cull, const uint32_t* __restrict__ order, int gx, int xcd,
     int amr_mode, const uint32_t* __restrict__ levels, int flush_mode, const uint32_t* __restrict__ bucket_count,
-    const uint32_t* __restrict__ bucket_list) {
+    const uint32_t* __restrict__ bucket_list, const uint8_t* __restrict__ hit_codes, const uint32_t* __restrict__ hdr) {
 #pragma clang fp contract(fast)
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
@@ -142,6 +142,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     }
     const size_t plane = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
+    // row group k's pixel y is py0 + 4 k stride: exact small-integer floats, the
+    // same operand the forward subtracts (3 fewer live registers than px.y[])
+    const float py0 = px.y[0];
     // accum_rec . dL_dpix is all the reference's accum_rec / last_color
     // recurrences (backward.cu:500-507) feed into dL_dalpha, so each pixel
     // carries that one scalar instead of 2 x 3.
@@ -184,6 +187,10 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         m = min(m, __builtin_amdgcn_readfirstlane((int)wave_last));
         if (m == 0) return;
     }
+    // Row masks: the forward's exact hit codes when it left them (gs_blend.cuh
+    // blend_tile_t: bit r = row group r has a pixel that blended the entry,
+    // i.e. a pixel this backward takes it at), else the geometric cull.
+    const bool use_codes = !kAMR && hit_codes != nullptr && hdr != nullptr && hdr[kHdrHitCodes] == 1u;
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
     const int comp = lane & 15;
@@ -218,7 +225,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             s_a[tid] = make_float4(xy.x, xy.y, nrgb[0], nrgb[1]);
             s_co[tid] = splat_coef(co);
             s_b[tid] = nrgb[2];
-            gm = cull ? splat_group_mask(xy, co, (float)ox, (float)oy, (float)pstride) : 0xfu;
+            gm = use_codes ? (uint32_t)hit_codes[range.x + top - 1 - tid]
+                 : cull ? splat_group_mask(xy, co, (float)ox, (float)oy, (float)pstride) : 0xfu;
         }
         const int ntop = top - kB;  // the next batch: entries [ntop - ncnt, ntop)
         const bool has_next = ntop > 0 && tid < min(kB, ntop);
@@ -267,7 +275,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
 #pragma unroll
             for (int k = 0; k < kPPL; k++) {
                 if (!((mk[k] >> cbit) & 1ull)) continue;  // wave-uniform: culled for this row group
-                const float dy = xy.y - px.y[k];
+                const float dy = xy.y - (py0 + (float)(4 * k * (int)pstride));
                 const float p2 = splat_p2(pa, pb, dy, pc);  // the forward's bits
                 const float G = splat_exp(p2);
                 const float alpha = fminf(0.99f, pc.w * G);
@@ -426,19 +434,20 @@ void set_backward_split(int ways, int permille) {
 }
 
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
-                            const float* colors, const float* bg, const float* dL_dpix, hipStream_t s) {
+                            const float* colors, const float* bg, const float* dL_dpix, hipStream_t s, int K) {
+    const size_t hit_codes_k = (size_t)(K > 0 ? K : 0);  // (the forward's instance count: where its codes are)
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return;
     const uint32_t* order = nullptr;
     const uint32_t *bcount = nullptr, *blist = nullptr;
     int units = gx * gy;
-    const bool one_wave_v = g_bwd_variant == 0 || g_bwd_variant == 3;
+    const bool one_wave_v = g_bwd_variant == 0 || g_bwd_variant == 3 || g_bwd_variant == 5;
     if (tile_order_enabled() && g_bucket_order && one_wave_v && !(g_xcd_map & 2) &&
         !(g_bwd_split_ways == 2 || g_bwd_split_ways == 4)) {
         bcount = img.bucket_count;  // filled by this image buffer's forward render
         blist = img.bucket_list;
     } else if (tile_order_enabled()) {
-        const bool one_wave = g_bwd_variant == 0 || g_bwd_variant == 3;
+        const bool one_wave = g_bwd_variant == 0 || g_bwd_variant == 3 || g_bwd_variant == 5;
         const int ways = (one_wave && !(g_xcd_map & 2) && (g_bwd_split_ways == 2 || g_bwd_split_ways == 4))
                              ? g_bwd_split_ways : 1;
         const int heavy = ways > 1 ? std::min(gx * gy, (int)((long)gx * gy * g_bwd_split_permille / 1000)) : 0;
@@ -446,16 +455,20 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         order = img.tile_order;
         units = gx * gy + (heavy ? (ways - 1) * heavy : 0);
     }
+    // hit codes cover whole tiles: not with the heavy-tile split (its units
+    // own row-group subsets of a tile and the tile order word carries them)
+    const bool gsel_codes = units == gx * gy;
 #define GS_BWD_LAUNCH(PPL, WAVES, OCC, SWAP)                                                                    \
     hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP>), dim3(units), dim3(64 * WAVES), 0, s, W, H,      \
                        img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
                        dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1, 0, nullptr, g_bwd_flush, \
-                       bcount, blist)
+                       bcount, blist, gsel_codes ? hit_codes_at(b.point_list, hit_codes_k) : nullptr, g.hdr)
     switch (g_bwd_variant) {
         case 1: GS_BWD_LAUNCH(2, 2, 4, true); break;
         case 2: GS_BWD_LAUNCH(1, 4, 4, true); break;
         case 3: GS_BWD_LAUNCH(4, 1, 4, false); break;
+        case 5: GS_BWD_LAUNCH(4, 1, 5, true); break;  // 96 VGPRs: 5 waves per SIMD
         default: GS_BWD_LAUNCH(4, 1, 4, true); break;
     }
 #undef GS_BWD_LAUNCH
@@ -473,7 +486,8 @@ void launch_amr_render_backward(int W, int H, int mode, const ImageView& img, co
     hipLaunchKernelGGL((render_bwd_kernel<4, 1, 4, true, true>), dim3(4 * tgx * tgy), dim3(64), 0, s, W, H, img.ranges,
                        img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,
-                       dL_dpix, bg, g.grad_accum, g_cull, nullptr, tgx, 0, mode, img.levels, 0, nullptr, nullptr);
+                       dL_dpix, bg, g.grad_accum, g_cull, nullptr, tgx, 0, mode, img.levels, 0, nullptr, nullptr,
+                       nullptr, nullptr);
 }
 
 // ------------------------------------------------------ per-Gaussian bwd ---

@@ -481,7 +481,8 @@ int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image
         {
             StageTimer _t(kRender, s);
             zeroed = launch_render_forward(width, height, r.img, r.b, r.g, feats, background, out_color, s,
-                                           r.g.grad_accum, (size_t)kGradRow * (size_t)P);
+                                           r.g.grad_accum, (size_t)kGradRow * (size_t)P,
+                                           hit_codes_at(r.b.point_list, (size_t)r.K));
         }
         if (zeroed) set_accum_clean(r.g.grad_accum, true);
         stage_check(debug != 0, s, "render");
@@ -519,7 +520,7 @@ int rasterizer_backward_impl(int amr_mode, int P, int D, int M, int R, const flo
         if (R > 0) {
             StageTimer _t(kRenderBwd, s);
             if (amr_mode != 0) launch_amr_render_backward(width, height, amr_mode, img, b, g, colors, background, dL_dpix, s);
-            else launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s);
+            else launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s, R);
         }
         stage_check(debug != 0, s, "render_backward");
         BackwardGaussArgs a;
@@ -627,7 +628,7 @@ int gs_rasterizer_backward_view_grads(int P, int R, const float* background, int
         if (!radii) radii = g.radii;
         zero_accum_unless_clean(g, P, s);
         const float* colors = colors_precomp ? colors_precomp : g.rgb;
-        if (R > 0 && P > 0) { StageTimer _t(kRenderBwd, s); launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s); }
+        if (R > 0 && P > 0) { StageTimer _t(kRenderBwd, s); launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s, R); }
         stage_check(debug != 0, s, "render_backward");
         launch_pack_view_grads(P, g, radii, colors_precomp == nullptr, viewmatrix, projmatrix, campos, width, height,
                                tan_fovx, tan_fovy, out_record, s);
@@ -1097,6 +1098,10 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "tile_order") == 0) {
         set_tile_order(value);
+        return 0;
+    }
+    if (std::strcmp(key, "hit_codes") == 0) {
+        set_hit_codes(value);
         return 0;
     }
     if (std::strcmp(key, "sort_variant") == 0) {

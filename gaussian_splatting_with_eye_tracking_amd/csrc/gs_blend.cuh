@@ -268,7 +268,7 @@ struct BlendStateT {
 // included: fminf returns the number) with no extra instruction.  Per pair
 // ~26 VALU and no SALU instead of ~25 VALU + ~20 SALU of exec-mask
 // bookkeeping.
-__device__ __forceinline__ void blend_one_sel(float2 xy, float4 co, float4 f, float pxx, float pxy, uint32_t contributor,
+__device__ __forceinline__ bool blend_one_sel(float2 xy, float4 co, float4 f, float pxx, float pxy, uint32_t contributor,
                                               float& T, float (&C)[3], uint32_t& last, float& cap) {
     const float dx = xy.x - pxx, dy = xy.y - pxy;
     const float p = splat_p2(dx, dy, co);
@@ -284,7 +284,9 @@ __device__ __forceinline__ void blend_one_sel(float2 xy, float4 co, float4 f, fl
     C[1] = __builtin_fmaf(f.y, w, C[1]);
     C[2] = __builtin_fmaf(f.z, w, C[2]);
     T = stop ? T : test_T;
-    last = (a != 0.0f) ? contributor : last;
+    const bool blended = a != 0.0f;
+    last = blended ? contributor : last;
+    return blended;
 }
 
 template <int kPPL, int kWaves, bool kSel = false>
@@ -294,11 +296,30 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                                                           const float* __restrict__ features,
                                                           const float4* __restrict__ conic_opacity, float4* s_a,
                                                           float4* s_co, float* s_b, uint64_t* s_bal,
-                                                          bool cull) {
+                                                          bool cull, uint8_t* __restrict__ hit_codes = nullptr,
+                                                          uint64_t* s_hit = nullptr) {
 #pragma clang fp contract(fast)
     constexpr uint32_t kB = 64 * kWaves;
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = tid >> 6;
+    // Exact row-group hit codes (kSel, kPPL == 1, hit_codes given): bit w of
+    // entry j's code = some pixel of wave w's row group blended entry j --
+    // precisely the (row group, entry) pairs with a contributing pixel in the
+    // backward (a pixel blends entry j iff j < n_contrib and the alpha tests
+    // pass, backward.cu:466-482).  Wave w collects its 64-bit hit set per 64
+    // batch slots in s_hit[c kWaves + w]; the batch's codes are stored after
+    // the next barrier.
+    constexpr bool kRec = kSel && kPPL == 1;
+    const bool rec = kRec && hit_codes != nullptr;
+    auto flush_codes = [&](uint32_t fb0) {
+        if (fb0 + tid < range.y - range.x) {
+            const uint32_t c = tid >> 6, bit = tid & 63;
+            uint32_t code = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; w++) code |= (uint32_t)((s_hit[c * kWaves + w] >> bit) & 1ull) << w;
+            hit_codes[range.x + fb0 + tid] = (uint8_t)code;
+        }
+    };
     BlendStateT<kPPL> st_;
     bool done[kPPL];
 #pragma unroll
@@ -309,7 +330,8 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
         done[k] = !px.inside[k];
     }
     const uint32_t n = range.y - range.x;
-    for (uint32_t b0 = 0; b0 < n; b0 += kB) {
+    uint32_t b0 = 0;
+    for (; b0 < n; b0 += kB) {
         bool any = false;
 #pragma unroll
         for (int k = 0; k < kPPL; k++) any |= !done[k];
@@ -319,6 +341,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
         } else {
             if (!__syncthreads_or(any)) break;
         }
+        if (rec && b0 > 0) flush_codes(b0 - kB);  // the previous batch's codes (s_hit rewritten after the next barrier)
         uint32_t gm = 0;
         if (b0 + tid < n) {
             const uint32_t id = point_list[range.x + b0 + tid];
@@ -333,6 +356,9 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
         }
         publish_group_masks<kWaves>(gm, s_bal);
         __syncthreads();
+        if (rec && (tid & 63) == 0)
+#pragma unroll
+            for (int c = 0; c < kWaves; c++) s_hit[c * kWaves + wave] = 0ull;
         if (__ballot(any) == 0ull) continue;  // this wave is done; keep joining the barriers
         bool wave_alive = true;
 #pragma unroll 1
@@ -348,6 +374,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 // select form (blend_one_sel), two Gaussians per iteration; the
                 // wave's early exit is tested once per 64 batch slots
                 float cap = done[0] ? 0.0f : 0.99f;
+                uint64_t hits = 0;
                 while (todo) {
                     const uint32_t bA = (uint32_t)__builtin_ctzll(todo);
                     todo &= todo - 1;
@@ -358,12 +385,17 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                     const float4 sA = s_a[jA], sB = s_a[jB];
                     const float4 coA = s_co[jA], coB = s_co[jB];
                     const float bAc = s_b[jA], bBc = s_b[jB];
-                    blend_one_sel(make_float2(sA.x, sA.y), coA, make_float4(sA.z, sA.w, bAc, 0.f), px.x, px.y[0],
-                                  b0 + jA + 1, st_.T[0], st_.C[0], st_.last[0], cap);
-                    if (two)
-                        blend_one_sel(make_float2(sB.x, sB.y), coB, make_float4(sB.z, sB.w, bBc, 0.f), px.x, px.y[0],
-                                      b0 + jB + 1, st_.T[0], st_.C[0], st_.last[0], cap);
+                    const bool hA = blend_one_sel(make_float2(sA.x, sA.y), coA, make_float4(sA.z, sA.w, bAc, 0.f),
+                                                  px.x, px.y[0], b0 + jA + 1, st_.T[0], st_.C[0], st_.last[0], cap);
+                    if (kRec) hits |= __ballot(hA) != 0ull ? 1ull << bA : 0ull;
+                    if (two) {
+                        const bool hB = blend_one_sel(make_float2(sB.x, sB.y), coB, make_float4(sB.z, sB.w, bBc, 0.f),
+                                                      px.x, px.y[0], b0 + jB + 1, st_.T[0], st_.C[0], st_.last[0],
+                                                      cap);
+                        if (kRec) hits |= __ballot(hB) != 0ull ? 1ull << bB : 0ull;
+                    }
                 }
+                if (rec && (tid & 63) == 0) s_hit[c * kWaves + wave] = hits;
                 done[0] = cap == 0.0f;
                 if (__ballot(!done[0]) == 0ull) wave_alive = false;
                 continue;
@@ -465,6 +497,10 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 }
             }
         }
+    }
+    if (rec) {  // the last processed batch (b0 - kB; every thread leaves the loop together)
+        __syncthreads();
+        if (b0 > 0) flush_codes(b0 - kB);
     }
     return st_;
 }

@@ -62,6 +62,7 @@ void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H
 void set_bin_chunk(int gaussians_per_workgroup);
 void set_dup_diag(int v);  // timing diagnostics only (wrong keys)
 void set_sort_algo(int v);
+void set_hit_codes(int v);
 void set_sort_variant(int v);  // 0 = bitonic networks, 1 = bucket sort (default)
 void set_bin_slots(int v);  // 0 = auto
 int bin_slots_for(int P);   // sub-bucket slots of the LDS binning for a P-Gaussian forward
@@ -88,7 +89,7 @@ void launch_reconstruct_keys(int T, const ImageView& img, const BinningView& b, 
 // a multiple of 4, 16-B aligned) by the same launch; returns whether it was.
 bool launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                            const float* features, const float* bg, float* out_color, hipStream_t s,
-                           float* zero_rows = nullptr, size_t zero_floats = 0);
+                           float* zero_rows = nullptr, size_t zero_floats = 0, uint8_t* hit_codes = nullptr);
 // Tuning knob for A/B runs (gs_set_tuning("fwd_variant", v)).
 void set_forward_variant(int v);
 void set_xcd_map(int v);
@@ -113,7 +114,7 @@ void set_scan_slices(int v);
 void set_bucket_order(int v);  // heavy-tile split of the backward blend
 // Blend backward (base/cr/backward.cu:399-557) into g.grad_accum.
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
-                            const float* colors, const float* bg, const float* dL_dpix, hipStream_t s);
+                            const float* colors, const float* bg, const float* dL_dpix, hipStream_t s, int K);
 
 struct BackwardGaussArgs {
     int P, D, M;

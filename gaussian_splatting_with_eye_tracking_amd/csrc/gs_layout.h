@@ -35,6 +35,7 @@ enum HdrWord : int {
     kHdrNumLargeTiles = 3,
     kHdrP = 4,
     kHdrT = 5,
+    kHdrHitCodes = 6,     // 1: the base forward render stored exact row-group hit codes (hit_codes_of)
     kHdrWords = 64,
 };
 
@@ -145,6 +146,17 @@ struct BinningView {
     uint64_t* pair_keys;   // [K]  (depth_bits << 32 | gaussian idx), grouped by tile
     uint64_t* scratch;     // [K]  merge-sort ping-pong
 };
+
+// Base forward: once the tile lists are sorted, pair_keys is dead; K bytes at
+// the offset a K-entry carve gives pair_keys hold the render's exact row-group
+// hit code of every sorted instance (bit r: row group r of the tile has a
+// pixel that blended it), which the backward uses as its row masks.  The
+// offset comes from K, not from the buffer's carve: the speculative
+// duplicate carves the forward's buffer for a capacity >= K, while the
+// backward carves it for K (both leave point_list at 0).
+inline uint8_t* hit_codes_at(uint32_t* point_list, size_t K) {
+    return reinterpret_cast<uint8_t*>(point_list) + align_up(sizeof(uint32_t) * K);
+}
 
 // AMR (32-px tiles): once the tile lists are sorted, pair_keys and scratch
 // (>= 16 K bytes, contiguous up to alignment) are dead; they hold the

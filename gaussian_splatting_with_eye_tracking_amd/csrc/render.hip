@@ -57,7 +57,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
                                                                  const uint32_t* __restrict__ order, int gx,
                                                                  int xcd, float4* __restrict__ zero4,
                                                                  int zero_n4, uint32_t* __restrict__ bucket_count,
-                                                                 uint32_t* __restrict__ bucket_list) {
+                                                                 uint32_t* __restrict__ bucket_list,
+                                                                 uint8_t* __restrict__ hit_codes,
+                                                                 uint32_t* __restrict__ hdr) {
     // The backward's per-Gaussian accumulator rows (grad_accum, idle in the
     // base forward) are zeroed here, behind the blend, instead of by a memset
     // on the backward's critical path: fire-and-forget stores in a kernel
@@ -68,8 +70,13 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
     __shared__ float4 s_co[64 * kWaves];
     __shared__ float s_b[64 * kWaves];
     __shared__ uint64_t s_bal[4 * kWaves];
+    __shared__ uint64_t s_hit[kWaves * kWaves];
     __shared__ uint32_t s_max;
     if (kWaves > 1 && threadIdx.x == 0) s_max = 0;
+    // whether this forward leaves exact row-group hit codes for the backward
+    // (the select-form 4 x 1 geometry records them; every other leaves 0)
+    constexpr bool kRec = kSel && kPPL == 1;
+    if (hdr && blockIdx.x == 0 && threadIdx.x == 0) hdr[kHdrHitCodes] = (kRec && hit_codes) ? 1u : 0u;
     const int tile = order ? (int)order[blockIdx.x]
                            : xcd ? xcd_block_tile((int)blockIdx.x, gx, (int)(gridDim.x / gx)) : (int)blockIdx.x;
     const uint32_t ox = (uint32_t)(tile % gx) * 16, oy = (uint32_t)(tile / gx) * 16;
@@ -77,7 +84,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const BlendStateT<kPPL> st =
         blend_tile_t<kPPL, kWaves, kSel>(range, px, (float)ox, (float)oy, 1.0f, point_list,
-                                   means2D, features, conic_opacity, s_a, s_co, s_b, s_bal, cull != 0);
+                                   means2D, features, conic_opacity, s_a, s_co, s_b, s_bal, cull != 0,
+                                   kRec ? hit_codes : nullptr, s_hit);
     write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
     uint32_t m = 0;
 #pragma unroll
@@ -101,6 +109,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
 }
 
 int g_cull = 1;         // row-group cull on (gs_blend.cuh); 0 only for the exactness A/B test
+int g_hit_codes = 1;    // the forward records exact row-group hit codes for the backward (set_tuning("hit_codes"))
+void set_hit_codes(int v) { g_hit_codes = v; }
 void set_cull(int v) { g_cull = v; }
 
 // XCD-aware tile placement (gs_blend.cuh): bit 0 the forward blend, bit 1 the
@@ -122,7 +132,7 @@ void set_forward_variant(int v) { g_fwd_variant = v; }
 
 bool launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                            const float* features, const float* bg, float* out_color, hipStream_t s,
-                           float* zero_rows, size_t zero_floats) {
+                           float* zero_rows, size_t zero_floats, uint8_t* hit_codes) {
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return false;
     float4* const zero4 = reinterpret_cast<float4*>(zero_rows);
@@ -137,7 +147,7 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
                        b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
                        img.max_contrib, bg, out_color, g_cull, order, gx, g_xcd_map & 1, zero4, zero_n4,     \
-                       img.bucket_count, img.bucket_list)
+                       img.bucket_count, img.bucket_list, g_hit_codes ? hit_codes : nullptr, g.hdr)
     switch (g_fwd_variant) {
         case 0: GS_FWD_LAUNCH(4, 1); break;
         case 1: GS_FWD_LAUNCH(2, 2); break;
