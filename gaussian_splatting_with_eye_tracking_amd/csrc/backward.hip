@@ -441,13 +441,13 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
     const uint32_t* order = nullptr;
     const uint32_t *bcount = nullptr, *blist = nullptr;
     int units = gx * gy;
-    const bool one_wave_v = g_bwd_variant == 0 || g_bwd_variant == 3 || g_bwd_variant == 5;
+    const bool one_wave_v = g_bwd_variant == 0 || g_bwd_variant == 3 || g_bwd_variant >= 5;
     if (tile_order_enabled() && g_bucket_order && one_wave_v && !(g_xcd_map & 2) &&
         !(g_bwd_split_ways == 2 || g_bwd_split_ways == 4)) {
         bcount = img.bucket_count;  // filled by this image buffer's forward render
         blist = img.bucket_list;
     } else if (tile_order_enabled()) {
-        const bool one_wave = g_bwd_variant == 0 || g_bwd_variant == 3 || g_bwd_variant == 5;
+        const bool one_wave = g_bwd_variant == 0 || g_bwd_variant == 3 || g_bwd_variant >= 5;
         const int ways = (one_wave && !(g_xcd_map & 2) && (g_bwd_split_ways == 2 || g_bwd_split_ways == 4))
                              ? g_bwd_split_ways : 1;
         const int heavy = ways > 1 ? std::min(gx * gy, (int)((long)gx * gy * g_bwd_split_permille / 1000)) : 0;
@@ -458,8 +458,9 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
     // hit codes cover whole tiles: not with the heavy-tile split (its units
     // own row-group subsets of a tile and the tile order word carries them)
     const bool gsel_codes = units == gx * gy;
-#define GS_BWD_LAUNCH(PPL, WAVES, OCC, SWAP)                                                                    \
-    hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP>), dim3(units), dim3(64 * WAVES), 0, s, W, H,      \
+#define GS_BWD_LAUNCH(PPL, WAVES, OCC, SWAP, ...)                                                               \
+    hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP, ##__VA_ARGS__>), dim3(units), dim3(64 * WAVES), 0, s, \
+                       W, H,                                                                                      \
                        img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
                        dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1, 0, nullptr, g_bwd_flush, \
