@@ -50,14 +50,16 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz / 4 cycles per wave64 f32 VALU
-# instruction.  Measured (tools/valu_rate.hip, profiles/r03e_valu_rate.log):
-# with 8 waves per SIMD independent v_fma_f32 chains retire one wave64
-# instruction per 4.41 cycles per SIMD (s_memtime: 2.4 GHz), v_pk_fma_f32 (two
-# f32 FMAs per lane) per 4.8 -- i.e. 16 f32 lanes per cycle unpacked, and the
-# 157 TF f32 vector peak needs packed math.  (Rounds 1-2 priced the blend
-# kernels against 2 cycles per instruction: half the real rate.)
-VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 4
+# VALU issue peak, measured (tools/valu_rate.hip, profiles/r03g_valu_rate.log):
+# with 8 waves per SIMD, independent v_fma_f32 chains retire one wave64
+# instruction per 4.43 cycles per SIMD at the 2.4 GHz s_memtime clock
+# (0.2257 wave-instructions per SIMD-cycle: 5.55e11 per second over the
+# chip), v_pk_fma_f32 (two f32 FMAs per lane) per 4.8 -- so f32 runs at ~16
+# lanes per cycle unpacked and the 157 TF vector peak is the packed rate.
+# (Rounds 1-2 priced the blend kernels at 2 cycles per instruction, half the
+# real rate.)  A mix with cheaper ops (moves, selects) can retire faster than
+# this FMA-chain rate, so the fraction is a guide, not a bound.
+VALU_PEAK_WAVE_INSTR_PER_S = 0.2257 * 256 * 4 * 2.4e9
 METRIC = "rendered views/sec (fwd+bwd) at 1080p, 1M Gaussians; achieved HBM GB/s %"
 
 CONFIGS = {

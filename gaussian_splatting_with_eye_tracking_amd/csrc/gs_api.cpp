@@ -1100,6 +1100,10 @@ int gs_set_tuning(const char* key, int value) {
         set_tile_order(value);
         return 0;
     }
+    if (std::strcmp(key, "pp_dma") == 0) {
+        set_pp_dma(value);
+        return 0;
+    }
     if (std::strcmp(key, "hit_codes") == 0) {
         set_hit_codes(value);
         return 0;

@@ -62,6 +62,7 @@ void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H
 void set_bin_chunk(int gaussians_per_workgroup);
 void set_dup_diag(int v);  // timing diagnostics only (wrong keys)
 void set_sort_algo(int v);
+void set_pp_dma(int v);
 void set_hit_codes(int v);
 void set_sort_variant(int v);  // 0 = bitonic networks, 1 = bucket sort (default)
 void set_bin_slots(int v);  // 0 = auto

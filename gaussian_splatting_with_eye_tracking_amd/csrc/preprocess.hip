@@ -89,10 +89,33 @@ __device__ __forceinline__ float3 eval_sh_color(int deg, const float (&c)[16][3]
     return make_float3(res[0], res[1], res[2]);
 }
 
-template <bool kHasSH, bool kSH16, bool kCovPrecomp>
-__global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomView g, int* __restrict__ radii,
-                                                         uint32_t* __restrict__ tile_count) {
+// kDma (SH16): each wave copies its 64 Gaussians' 192-B SH rows (12 KB,
+// contiguous) global -> LDS with 12 wave-contiguous global_load_lds_dwordx4
+// (no VGPRs) at the top of the kernel, so the coalesced copy runs under the
+// geometry math; each visible thread then reads its row from LDS.  Culled
+// Gaussians' rows are copied too (~15 % more SH bytes at configs 2 / 4) --
+// the price of whole-line requests instead of 12 scattered 16-B loads per
+// thread.
+constexpr int kPpThreads = 256;
+template <bool kHasSH, bool kSH16, bool kCovPrecomp, bool kDma = false>
+__global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a, GeomView g, int* __restrict__ radii,
+                                                                uint32_t* __restrict__ tile_count) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ __attribute__((aligned(16))) float s_sh[kDma ? kPpThreads * 48 : 1];
+    if constexpr (kDma) {
+        // wave w: rows [64 w, 64 w + 64) of the block; lane l's 16-B pieces l + 64 i
+        const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const size_t row0 = (size_t)blockIdx.x * kPpThreads + 64 * w;
+        const size_t nfl = (size_t)a.P * 48;
+        const float* src = a.shs + row0 * 48;
+        float* dst = s_sh + 64 * 48 * w;
+#pragma unroll
+        for (int i = 0; i < 12; i++) {
+            const size_t f = (size_t)(64 * i + lane) * 4;
+            if (row0 * 48 + f < nfl)
+                __builtin_amdgcn_global_load_lds(src + f, dst + 256 * i, 16, 0, 0);
+        }
+    }
     for (int i = idx; i < a.zero_n; i += (int)(gridDim.x * blockDim.x)) a.zero_words[i] = 0u;
     if (idx >= a.P) return;
     // AMR: the geometry buffer keeps its own copy of the radii (the progressive
@@ -188,7 +211,17 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
         // SH only for Gaussians that survive the cull (computeColorFromSH runs
         // after the rect test in the reference too, forward.cu:240-247)
         float shc[16][3];
-        load_sh<kSH16>(a.D, a.M, a.shs + (size_t)idx * a.M * 3, shc);
+        if constexpr (kDma) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA rows have landed
+            const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
+            const float* row = s_sh + 48 * threadIdx.x;
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) shc[k][ch] = k < ncoef ? row[3 * k + ch] : 0.f;
+        } else {
+            load_sh<kSH16>(a.D, a.M, a.shs + (size_t)idx * a.M * 3, shc);
+        }
         // computeColorFromSH: dir = normalize(mean - campos)
         float dx = mx - a.cam_pos[0], dy = my - a.cam_pos[1], dz = mz - a.cam_pos[2];
         const float len = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
@@ -231,10 +264,18 @@ __global__ void __launch_bounds__(256) preprocess_kernel(PreprocessArgs a, GeomV
             for (uint32_t x = r.x0; x < r.x1; x++) atomicAdd(&tile_count[y * gx + x], 1u);
 }
 
+int g_pp_dma = 1;  // set_tuning("pp_dma"): SH rows through LDS-DMA (kDma) for SH16
+void set_pp_dma(int v) { g_pp_dma = v; }
+
 template <bool A, bool B, bool C>
 static void launch_pp(const PreprocessArgs& a, const GeomView& g, int* radii, uint32_t* tile_count, hipStream_t s) {
-    const int blocks = (a.P + 255) / 256;
-    hipLaunchKernelGGL((preprocess_kernel<A, B, C>), dim3(blocks), dim3(256), 0, s, a, g, radii, tile_count);
+    const int blocks = (a.P + kPpThreads - 1) / kPpThreads;
+    if (A && B && g_pp_dma)
+        hipLaunchKernelGGL((preprocess_kernel<A, B, C, true>), dim3(blocks), dim3(kPpThreads), 0, s, a, g, radii,
+                           tile_count);
+    else
+        hipLaunchKernelGGL((preprocess_kernel<A, B, C>), dim3(blocks), dim3(kPpThreads), 0, s, a, g, radii,
+                           tile_count);
 }
 
 int g_store_cov3d = 0;  // set_tuning("store_cov3d"): the parity tests read the geometry buffer's cov3D

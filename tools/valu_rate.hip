@@ -55,6 +55,59 @@ __global__ void __launch_bounds__(256) exp_kernel(float* out, int iters, float a
     if (s == 12345.678f) out[threadIdx.x] = s;
 }
 
+// v_cndmask_b32 chains (the select-form blends are full of them)
+__global__ void __launch_bounds__(256) cnd_kernel(float* out, int iters, float a, float b, unsigned long long*) {
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) v[c] = threadIdx.x * 1e-3f + c;
+    const bool m = (threadIdx.x & 1) != 0;
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            v[c] = m ? v[c] : a;
+            asm volatile("" : "+v"(v[c]));
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; c++) s += v[c];
+    if (s == 12345.678f) out[threadIdx.x] = s;
+}
+
+// v_add_u32 chains (integer ALU)
+__global__ void __launch_bounds__(256) iadd_kernel(float* out, int iters, float a, float b, unsigned long long*) {
+    unsigned v[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) v[c] = threadIdx.x + c;
+    const unsigned k = (unsigned)iters * 7u + 3u;
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int c = 0; c < 8; c++) v[c] = v[c] + k;
+    }
+    unsigned s = 0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) s += v[c];
+    if (s == 12345u) out[threadIdx.x] = (float)s;
+}
+
+// v_cmp + v_cndmask pairs (a select on a compare)
+__global__ void __launch_bounds__(256) cmpsel_kernel(float* out, int iters, float a, float b, unsigned long long*) {
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) v[c] = threadIdx.x * 1e-3f + c;
+    for (int i = 0; i < iters; i++) {
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+            v[c] = v[c] > a ? v[c] : b;
+            asm volatile("" : "+v"(v[c]));
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; c++) s += v[c];
+    if (s == 12345.678f) out[threadIdx.x] = s;
+}
+
 int main() {
     float* out;
     hipMalloc(&out, 1024 * sizeof(float));
@@ -96,5 +149,8 @@ int main() {
     run("v_fma_f32 x16 chains", fma_kernel<16>, 16);
     run("v_pk_fma_f32 x8 chains", pkfma_kernel<8>, 8);
     run("v_exp_f32 + v_mul x8 chains", exp_kernel, 16);
+    run("v_cndmask_b32 x8 chains", cnd_kernel, 8);
+    run("v_add_u32 x8 chains", iadd_kernel, 8);
+    run("v_cmp + v_cndmask x8 chains (per pair)", cmpsel_kernel, 16);
     return 0;
 }
