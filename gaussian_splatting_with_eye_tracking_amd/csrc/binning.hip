@@ -103,6 +103,22 @@ __device__ __forceinline__ void mirror_header(uint32_t* m, uint32_t K, uint32_t 
 }
 
 
+// Row-banded duplicate (below): a tile row's tiles are consecutive, so its
+// instances are one contiguous range of the sorted layout, starting at the
+// exclusive prefix of its first tile.  The scan stores that start (and the
+// staging cursor) per row.
+struct BandScan {
+    uint32_t* start;  // nullptr: direct duplicate
+    uint32_t* cursor;
+    uint32_t gx;
+    __device__ __forceinline__ void emit(int i, uint32_t ex) const {
+        if (!start || (uint32_t)i % gx) return;
+        const uint32_t row = (uint32_t)i / gx;
+        start[row] = ex;
+        cursor[row] = ex;
+    }
+};
+
 // kPer > 0: T <= 1024 kPer, each thread's kPer counts loaded by an unrolled
 // loop (all loads in flight at once, no serial load-add chain: 16 -> 5 us at
 // 8160 tiles); kPer = 0: any T, run-time loop.
@@ -113,7 +129,8 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, uint32_t
                                                                  uint32_t* __restrict__ large_tiles,
                                                                  uint32_t* __restrict__ hdr,
                                                                  uint32_t* __restrict__ bucket_count,
-                                                                 uint32_t* __restrict__ hdr_mirror, int nslots) {
+                                                                 uint32_t* __restrict__ hdr_mirror, int nslots,
+                                                                 BandScan band) {
     __shared__ uint32_t s_wave[kScanThreads / 64 + 1];
     __shared__ uint32_t s_max[kScanThreads / 64];
     __shared__ uint32_t nlarge;
@@ -148,6 +165,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, uint32_t
         // identifyTileRanges leaves empty tiles at (0,0) (rasterizer_impl.cu:310).
         reinterpret_cast<uint2*>(ranges)[i] = make_uint2(c ? run : 0u, c ? run + c : 0u);
         slot_cursors(count, cursor, T, i, run, c, nslots);
+        band.emit(i, run);
         if (c > (uint32_t)kSmallCap) {
             const uint32_t slot = atomicAdd(&nlarge, 1u);
             large_tiles[slot] = (uint32_t)i;
@@ -188,7 +206,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, u
                                                                         uint32_t* __restrict__ hdr,
                                                                         uint32_t* __restrict__ bucket_count,
                                                                         uint32_t* __restrict__ hdr_mirror,
-                                                                        int nslots) {
+                                                                        int nslots, BandScan band) {
     constexpr int kW = kScanThreads / 64;
     if (bucket_count && threadIdx.x < kOrderBuckets64) bucket_count[threadIdx.x] = 0;  // the forward render appends
     __shared__ uint32_t s_tot[kW][kS];
@@ -237,6 +255,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, u
             // identifyTileRanges leaves empty tiles at (0,0) (rasterizer_impl.cu:310)
             reinterpret_cast<uint2*>(ranges)[i] = make_uint2(c[k] ? ex : 0u, c[k] ? ex + c[k] : 0u);
             slot_cursors(count, cursor, T, i, ex, c[k], nslots);
+            band.emit(i, ex);
             if (c[k] > (uint32_t)kSmallCap) large_tiles[atomicAdd(&nlarge, 1u)] = (uint32_t)i;
         }
         run += stot;
@@ -256,12 +275,18 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, u
 int g_scan_slices = 1;  // set_tuning("scan_slices"): 0 = the thread-contiguous scan
 void set_scan_slices(int v) { g_scan_slices = v; }
 
-void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror, int nslots) {
+void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror, int nslots,
+                      int gx, bool banded) {
+    BandScan band{nullptr, nullptr, (uint32_t)std::max(gx, 1)};
+    if (banded) {
+        band.start = img.band_start;
+        band.cursor = img.band_cursor;
+    }
     if (g_scan_slices) {
         const int slices = (T + kScanThreads - 1) / kScanThreads;
 #define GS_SLICE_LAUNCH(S)                                                                                        \
     hipLaunchKernelGGL(tile_scan_slices_kernel<S>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count,         \
-                       img.ranges, img.tile_cursor, img.large_tiles, hdr, img.bucket_count, hdr_mirror, nslots)
+                       img.ranges, img.tile_cursor, img.large_tiles, hdr, img.bucket_count, hdr_mirror, nslots, band)
         if (slices <= 1) { GS_SLICE_LAUNCH(1); return; }
         if (slices <= 2) { GS_SLICE_LAUNCH(2); return; }
         if (slices <= 4) { GS_SLICE_LAUNCH(4); return; }
@@ -270,7 +295,7 @@ void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s,
     }
 #define GS_SCAN_LAUNCH(PER)                                                                                      \
     hipLaunchKernelGGL(tile_scan_kernel<PER>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count, img.ranges, \
-                       img.tile_cursor, img.large_tiles, hdr, img.bucket_count, hdr_mirror, nslots)
+                       img.tile_cursor, img.large_tiles, hdr, img.bucket_count, hdr_mirror, nslots, band)
     const int per = (T + kScanThreads - 1) / kScanThreads;
     if (per <= 2) GS_SCAN_LAUNCH(2);
     else if (per <= 4) GS_SCAN_LAUNCH(4);
@@ -338,11 +363,29 @@ int g_dup_diag = 0;
 // sub-bucket slots the LDS binning spreads its chunks over (1..kBinSlots;
 // the scan sums all kBinSlots, unused ones stay zero)
 int g_bin_slots = 0;  // 0: auto (bin_slots_for)
+int g_dup_band = 1;  // set_tuning("dup_band"): 1 = row-banded duplicate, 0 = direct
+// set_tuning("band_threads"): the banded duplicate's workgroup shape (0 auto;
+// 512: 512 threads x 1 source; 513: 512 x 2 sources per thread; 514: 512 x 2
+// sources, 4 items per round; 1024: 1024 x 1).  Measured
+// (profiles/r03h_ab_threads_cfg*.json): 1024 best at config 2 (77.6 us, direct
+// duplicate 87.3), 513 at config 4 (282 us, direct 318).
+int g_band_threads = 0;
+int g_band_split = 0;  // set_tuning("band_split"): workgroups per tile row in the split pass (0: auto)
+void set_dup_band(int v) { g_dup_band = v; }
+void set_band_split(int v) { g_band_split = std::max(0, v); }
+void set_band_threads(int v) { g_band_threads = v; }
+constexpr int kBandBins = 1024;  // bins of one coalesced append round (rows, or the tiles of a row)
+bool dup_banded(int gx, int gy) {
+    return g_dup_band > 0 && gx * gy <= kLdsTiles && gx <= kBandBins && gy <= kBandBins;
+}
 void set_bin_slots(int v) { g_bin_slots = std::max(0, std::min(kBinSlots, v)); }
 // Measured (profiles/r03b_ab_bin_slots*): the sub-buckets save ~30 us of the
 // duplicate at config 4 (6.1M Gaussians) and ~4 us at config 2, where the
 // scan's 8x count loads cost more (+6 us): slots only for large scenes.
-int bin_slots_for(int P) { return g_bin_slots ? g_bin_slots : (P >= 2000000 ? kBinSlots : 1); }
+int bin_slots_for(int P, int gx, int gy) {
+    if (dup_banded(gx, gy)) return 1;  // the banded duplicate reserves per-tile runs itself
+    return g_bin_slots ? g_bin_slots : (P >= 2000000 ? kBinSlots : 1);
+}
 void set_dup_diag(int v) { g_dup_diag = v; }
 void set_bin_chunk(int v) { g_bin_chunk = max(kBinThreads, v); }
 
@@ -431,18 +474,328 @@ void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H
     const int chunk = g_bin_chunk;
     hipLaunchKernelGGL(count_tiles_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
                        sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, radii, block, gx, gy, img.tile_count,
-                       (uint32_t)bin_slots_for(P));
+                       (uint32_t)bin_slots_for(P, (int)gx, (int)gy));
+}
+
+// ------------------------------------------------- banded duplicate ---
+// Measured: the direct duplicate's cost follows its scattered store
+// REQUESTS, not its bytes -- at config 4 ~22M lane-scattered 8-B stores
+// take ~240 of its ~310 us, and staging half as many entries with the same
+// scatter pattern costs the same (profiles/r03h_band*).  A wave's store is
+// only cheap when its 64 lanes hit a few contiguous segments.  So both
+// passes below append through a workgroup-level LDS reorder
+// (coalesced_append): each round, every thread emits up to kRound items
+// (bin, payload); an LDS histogram + workgroup scan gives each bin a local
+// range, ONE returning atomic per non-empty bin reserves its global run, the
+// items are placed bin-major in LDS and written out by consecutive threads
+// -- consecutive addresses within each run.  With bins = the tile ROWS
+// (gy <= 1024) the runs per round are ~64 items long:
+//   stage: one entry per (Gaussian, tile row it touches) -- the key in
+//          scratch, its column span x0 | x1 << 16 in point_list (both dead
+//          until the sort) -- appended into the row's range of the sorted
+//          layout (capacity = the row's instances >= its entries);
+//   split: workgroups per row read its entries coalesced and append each
+//          (entry, tile) key into the tile's range, bins = the row's tiles.
+// Per tile the multiset of keys is the direct duplicate's; the sort makes
+// the order exact (bit-identical point_list).
+constexpr int kStageChunk = 4096;  // Gaussians per stage workgroup (runs reserved once per row per chunk)
+
+// kNT threads per workgroup; each owns kBandBins / kNT consecutive bins in
+// the per-bin steps.
+template <int kNT, int kRound>  // items per thread per round
+struct AppendLds {
+    uint32_t cnt[kBandBins];  // round counts -> local offsets
+    uint32_t dst[kBandBins];  // global slot - local offset, this round
+    uint32_t run[kBandBins];  // the workgroup's next global slot per bin (runs reserved up front)
+    uint32_t wave[kNT / 64 + 1];
+    uint64_t key[kNT * kRound];
+    uint32_t aux[kNT * kRound];
+    uint32_t to[kNT * kRound];
+};
+
+// The workgroup's whole histogram (accumulated in L.run by the caller) ->
+// its runs: ONE returning device atomic per non-empty bin per workgroup.
+template <int kNT, int kRound>
+__device__ __forceinline__ void reserve_runs(AppendLds<kNT, kRound>& L, uint32_t* __restrict__ cursor,
+                                             uint32_t nbins) {
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbins; b += kNT) {
+        const uint32_t c = L.run[b];
+        if (c) L.run[b] = atomicAdd(&cursor[b], c);
+    }
+    __syncthreads();
+}
+
+// One round: items (bin[r], key[r], aux[r]) for r < n (per thread) are
+// placed bin-major in LDS and written out by consecutive threads at the
+// workgroup's runs -- consecutive addresses inside each run.  LDS only (the
+// runs are reserved); must be called by the whole workgroup.
+template <bool kAux, int kNT, int kRound>
+__device__ __forceinline__ void coalesced_append(AppendLds<kNT, kRound>& L, int n, const uint32_t* bin,
+                                                 const uint64_t* key, const uint32_t* aux,
+                                                 uint64_t* __restrict__ out_key, uint32_t* __restrict__ out_aux,
+                                                 uint32_t limit) {
+    constexpr int kBPT = kBandBins / kNT;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < kBPT; q++) L.cnt[tid * kBPT + q] = 0;
+    __syncthreads();
+    uint32_t rank[kRound];
+#pragma unroll
+    for (int r = 0; r < kRound; r++)
+        if (r < n) rank[r] = atomicAdd(&L.cnt[bin[r]], 1u);
+    __syncthreads();
+    uint32_t c[kBPT], sum = 0;
+#pragma unroll
+    for (int q = 0; q < kBPT; q++) {
+        c[q] = L.cnt[tid * kBPT + q];
+        sum += c[q];
+    }
+    uint32_t total;
+    uint32_t lo = block_exclusive_scan<kNT>(sum, L.wave, total);
+#pragma unroll
+    for (int q = 0; q < kBPT; q++) {
+        const int bq = tid * kBPT + q;
+        if (c[q]) {
+            const uint32_t base = L.run[bq];
+            L.dst[bq] = base - lo;
+            L.run[bq] = base + c[q];
+        }
+        L.cnt[bq] = lo;
+        lo += c[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kRound; r++) {
+        if (r < n) {
+            const uint32_t i = L.cnt[bin[r]] + rank[r];
+            L.key[i] = key[r];
+            if constexpr (kAux) L.aux[i] = aux[r];
+            L.to[i] = L.dst[bin[r]] + i;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < total; i += kNT) {
+        const uint32_t t = L.to[i];
+        if (t >= limit) continue;  // never past the buffer (the runs are exact; this only bounds a bug)
+        out_key[t] = L.key[i];
+        if constexpr (kAux) out_aux[t] = L.aux[i];
+    }
+}
+
+// Sources (kSPT per thread: Gaussians, or staged entries) expand to count
+// consecutive bins from first; the workgroup's expansion is handed out in
+// blocks of kRound consecutive pairs per thread (the block's first pair ->
+// its source by a binary search over the scanned counts, then a forward
+// walk), kRound x kNT pairs per append round.
+template <int kNS>
+struct SourceLds {
+    uint64_t key[kNS];
+    uint32_t aux[kNS];
+    uint32_t first[kNS];
+    uint32_t pref[kNS];  // exclusive prefix of the counts
+    uint32_t wave[kNS / 64 + 1];
+};
+
+template <bool kAux, int kNT, int kRound, int kSPT>
+__device__ __forceinline__ void expand_sources(SourceLds<kNT * kSPT>& S, AppendLds<kNT, kRound>& L,
+                                               const uint32_t* cnt, const uint64_t* key, const uint32_t* aux,
+                                               const uint32_t* first, uint64_t* __restrict__ out_key,
+                                               uint32_t* __restrict__ out_aux, uint32_t limit) {
+    constexpr int kNS = kNT * kSPT;
+    const int tid = threadIdx.x;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int q = 0; q < kSPT; q++) sum += cnt[q];
+    uint32_t np;
+    uint32_t pre = block_exclusive_scan<kNT>(sum, S.wave, np);
+#pragma unroll
+    for (int q = 0; q < kSPT; q++) {
+        const int i = tid * kSPT + q;
+        S.key[i] = key[q];
+        if constexpr (kAux) S.aux[i] = aux[q];
+        S.first[i] = first[q];
+        S.pref[i] = pre;
+        pre += cnt[q];
+    }
+    __syncthreads();
+    for (uint32_t j0 = 0; j0 < np; j0 += kNT * kRound) {
+        uint32_t bin[kRound], ax[kRound];
+        uint64_t ky[kRound];
+        int n = 0;
+        // the last source with pref <= j (a source with count 0 shares its
+        // pref with the next; the last of equal prefs is the one with pairs)
+        uint32_t j = j0 + (uint32_t)(tid * kRound);
+        int lo = 0;
+        if (j < np) {
+            int hi = kNS - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (S.pref[mid] <= j) lo = mid; else hi = mid - 1;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < kRound; r++, j++) {
+            if (j < np) {
+                while (lo + 1 < kNS && S.pref[lo + 1] <= j) lo++;
+                bin[n] = S.first[lo] + (j - S.pref[lo]);
+                ky[n] = S.key[lo];
+                if constexpr (kAux) ax[n] = S.aux[lo];
+                n++;
+            }
+        }
+        coalesced_append<kAux, kNT, kRound>(L, n, bin, ky, ax, out_key, out_aux, limit);
+        __syncthreads();
+    }
+}
+
+template <int kNT, int kRound, int kSPT>
+struct BandLds {
+    AppendLds<kNT, kRound> a;
+    SourceLds<kNT * kSPT> src;
+};
+
+template <int kNT, int kRound, int kSPT>
+__global__ void __launch_bounds__(kNT) band_stage_kernel(int P, const float* __restrict__ means2D,
+                                                         const float* __restrict__ depths,
+                                                         const int* __restrict__ radii, int block, uint32_t gx,
+                                                         uint32_t gy, uint32_t* __restrict__ row_cursor,
+                                                         uint64_t* __restrict__ stage_keys,
+                                                         uint32_t* __restrict__ stage_cols,
+                                                         const uint32_t* __restrict__ hdr, uint32_t cap,
+                                                         uint32_t limit) {
+    if (hdr && hdr[kHdrNumRendered] > cap) return;  // speculative launch, K > cap (duplicate_lds_kernel)
+    constexpr int kStageG = kStageChunk / kNT;
+    static_assert(kStageG % kSPT == 0, "whole source groups");
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    BandLds<kNT, kRound, kSPT>& B = *reinterpret_cast<BandLds<kNT, kRound, kSPT>*>(lds_raw);
+    // the thread's Gaussians: kSPT consecutive indices per group
+    uint32_t cnt[kStageG], cols[kStageG], y0[kStageG];
+    uint64_t key[kStageG];
+#pragma unroll
+    for (int g = 0; g < kStageG; g++) {
+        const int idx = blockIdx.x * kStageChunk + ((g / kSPT) * kNT + threadIdx.x) * kSPT + g % kSPT;
+        cnt[g] = cols[g] = y0[g] = 0;
+        key[g] = 0;
+        Rect rc;
+        if (idx < P && gaussian_rect(idx, means2D, radii, block, gx, gy, rc) && rc.x1 > rc.x0) {
+            cnt[g] = rc.y1 - rc.y0;  // one entry per tile row
+            y0[g] = rc.y0;
+            cols[g] = rc.x0 | (rc.x1 << 16);
+            key[g] = ((uint64_t)float_bits(depths[idx]) << 32) | (uint32_t)idx;
+        }
+    }
+    for (int b = threadIdx.x; b < kBandBins; b += kNT) B.a.run[b] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < kStageG; g++)
+        for (uint32_t y = y0[g]; y < y0[g] + cnt[g]; y++) atomicAdd(&B.a.run[y], 1u);
+    reserve_runs(B.a, row_cursor, gy);
+#pragma unroll
+    for (int g = 0; g < kStageG; g += kSPT)
+        expand_sources<true, kNT, kRound, kSPT>(B.src, B.a, cnt + g, key + g, cols + g, y0 + g, stage_keys,
+                                                stage_cols, limit);
+}
+
+template <int kNT, int kRound, int kSPT>
+__global__ void __launch_bounds__(kNT) band_split_kernel(uint32_t gx, int split, const uint32_t* __restrict__ row_start,
+                                                         const uint32_t* __restrict__ row_cursor,
+                                                         const uint64_t* __restrict__ stage_keys,
+                                                         const uint32_t* __restrict__ stage_cols,
+                                                         uint32_t* __restrict__ tile_cursor,
+                                                         uint64_t* __restrict__ pair_keys,
+                                                         const uint32_t* __restrict__ hdr, uint32_t cap,
+                                                         uint32_t limit) {
+    if (hdr && hdr[kHdrNumRendered] > cap) return;
+    constexpr uint32_t kCh = kNT * kSPT;  // entries per chunk
+    extern __shared__ __align__(16) unsigned char lds_raw[];
+    BandLds<kNT, kRound, kSPT>& B = *reinterpret_cast<BandLds<kNT, kRound, kSPT>*>(lds_raw);
+    const uint32_t row = blockIdx.x / (uint32_t)split, part = blockIdx.x % (uint32_t)split;
+    const uint32_t beg = row_start[row], n_ent = row_cursor[row] - beg;
+    const uint32_t stride = (uint32_t)split * kCh;
+    // the workgroup's entries: chunks of kCh at part, part + split, ...;
+    // thread tid holds entries c0 + tid kSPT + q
+    for (int b = threadIdx.x; b < kBandBins; b += kNT) B.a.run[b] = 0;
+    __syncthreads();
+    constexpr int kU = 8 / kSPT;  // histogram pass: kU x kSPT loads in flight per thread
+    for (uint32_t c0 = part * kCh; c0 < n_ent; c0 += kU * stride) {
+        uint32_t c[kU * kSPT];
+#pragma unroll
+        for (int u = 0; u < kU; u++)
+#pragma unroll
+            for (int q = 0; q < kSPT; q++) {
+                const uint32_t e = c0 + (uint32_t)u * stride + threadIdx.x * kSPT + q;
+                c[u * kSPT + q] = e < n_ent ? stage_cols[beg + e] : 0u;
+            }
+#pragma unroll
+        for (int u = 0; u < kU * kSPT; u++)
+            for (uint32_t x = c[u] & 0xffffu; x < (c[u] >> 16); x++) atomicAdd(&B.a.run[x], 1u);
+    }
+    reserve_runs(B.a, tile_cursor + row * gx, gx);
+    for (uint32_t c0 = part * kCh; c0 < n_ent; c0 += stride) {
+        uint32_t cnt[kSPT], x0[kSPT];
+        uint64_t key[kSPT];
+#pragma unroll
+        for (int q = 0; q < kSPT; q++) {
+            const uint32_t e = c0 + threadIdx.x * kSPT + q;
+            cnt[q] = x0[q] = 0;
+            key[q] = 0;
+            if (e < n_ent) {
+                const uint32_t c = stage_cols[beg + e];
+                key[q] = stage_keys[beg + e];
+                x0[q] = c & 0xffffu;
+                cnt[q] = (c >> 16) - x0[q];
+            }
+        }
+        expand_sources<false, kNT, kRound, kSPT>(B.src, B.a, cnt, key, x0, x0, pair_keys, nullptr, limit);
+    }
+}
+
+template <int kNT, int kR, int kSPT>
+void launch_banded(int P, const GeomView& g, const int* radii, int block, uint32_t gx, uint32_t gy, int split,
+                   const ImageView& img, const BinningView& b, hipStream_t s, uint32_t n_keys,
+                   const uint32_t* spec_hdr, uint32_t spec_cap) {
+    using Lds = BandLds<kNT, kR, kSPT>;
+    static bool attr = false;
+    if (!attr) {  // > 64 KiB of dynamic LDS
+        (void)hipFuncSetAttribute((const void*)band_stage_kernel<kNT, kR, kSPT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Lds));
+        (void)hipFuncSetAttribute((const void*)band_split_kernel<kNT, kR, kSPT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Lds));
+        attr = true;
+    }
+    hipLaunchKernelGGL((band_stage_kernel<kNT, kR, kSPT>), dim3((P + kStageChunk - 1) / kStageChunk), dim3(kNT),
+                       sizeof(Lds), s, P, g.means2D, g.depths, radii, block, gx, gy, img.band_cursor, b.scratch,
+                       b.point_list, spec_hdr, spec_cap, n_keys);
+    hipLaunchKernelGGL((band_split_kernel<kNT, kR, kSPT>), dim3(gy * split), dim3(kNT), sizeof(Lds), s, gx, split,
+                       img.band_start, img.band_cursor, b.scratch, b.point_list, img.tile_cursor, b.pair_keys,
+                       spec_hdr, spec_cap, n_keys);
 }
 
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
-                      const BinningView& b, hipStream_t s, const uint32_t* spec_hdr, uint32_t spec_cap) {
+                      const BinningView& b, hipStream_t s, uint32_t n_keys, const uint32_t* spec_hdr,
+                      uint32_t spec_cap) {
     if (P == 0) return;
     const uint32_t gx = (uint32_t)((W + block - 1) / block), gy = (uint32_t)((H + block - 1) / block);
+    if (dup_banded((int)gx, (int)gy)) {
+        // ~4 split workgroups per CU over the rows
+        const int nt = g_band_threads ? g_band_threads : (P >= 2000000 ? 513 : 1024);
+        const int want = 4096;  // split workgroups in all
+        const int split = g_band_split ? g_band_split : std::max(1, std::min(256, (want + (int)gy - 1) / (int)gy));
+        switch (nt) {
+        case 1024: launch_banded<1024, 2, 1>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap); break;
+        case 513: launch_banded<512, 2, 2>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap); break;
+        case 514: launch_banded<512, 4, 2>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap); break;
+        default: launch_banded<512, 2, 1>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap); break;
+        }
+        return;
+    }
     if (gx * gy <= (uint32_t)kLdsTiles) {
         const int chunk = g_bin_chunk;
         hipLaunchKernelGGL(duplicate_lds_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
                            sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, g.depths, radii, block, gx, gy,
-                           img.tile_cursor, b.pair_keys, spec_hdr, spec_cap, g_dup_diag, (uint32_t)bin_slots_for(P));
+                           img.tile_cursor, b.pair_keys, spec_hdr, spec_cap, g_dup_diag,
+                           (uint32_t)bin_slots_for(P, (int)gx, (int)gy));
         return;
     }
     hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, g.means2D, g.depths, radii,

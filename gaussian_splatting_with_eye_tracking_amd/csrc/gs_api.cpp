@@ -408,7 +408,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     stage_check(debug, s, "count_tiles");
     const std::pair<uint32_t*, uint32_t*> mirror =
         (r.T > 0 && hdr_mirror_on()) ? mirror_words() : std::pair<uint32_t*, uint32_t*>{nullptr, nullptr};
-    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second, bin_slots_for(in.P)); }
+    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second, bin_slots_for(in.P, gx, gy), gx, dup_banded(gx, gy)); }
     stage_check(debug, s, "tile_scan");
     uint32_t hdr[4];
     const bool amr = tile == 32;  // the AMR layout appends records and region lists
@@ -430,7 +430,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
         begin_header_read(r.g.hdr, s, mirror.first);
         char* sbase = call_resize(binning, carve_binning(nullptr, cap, nullptr), "binning");
         carve_binning(sbase, cap, &r.b);
-        { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, r.g.hdr, (uint32_t)cap); }
+        { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, (uint32_t)cap, r.g.hdr, (uint32_t)cap); }
         finish_header_read(hdr, mirror.first);
         dup_done = hdr[kHdrNumRendered] <= cap;
     } else if (mirror.first) {
@@ -448,7 +448,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
         carve_binning(bbase, r.K, &r.b, amr ? &r.ab : nullptr);
     }
     if (r.K > 0) {
-        if (!dup_done) { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s); }
+        if (!dup_done) { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, (uint32_t)r.K); }
         stage_check(debug, s, "duplicate");
         { StageTimer _t(kSort, s); launch_sort_tiles(r.T, r.img, r.b, (int)hdr[kHdrMaxTileCount], (int)hdr[kHdrNumLargeTiles], s); }
         stage_check(debug, s, "sort_tiles");
@@ -1098,6 +1098,18 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "tile_order") == 0) {
         set_tile_order(value);
+        return 0;
+    }
+    if (std::strcmp(key, "dup_band") == 0) {
+        set_dup_band(value);
+        return 0;
+    }
+    if (std::strcmp(key, "band_threads") == 0) {
+        set_band_threads(value);
+        return 0;
+    }
+    if (std::strcmp(key, "band_split") == 0) {
+        set_band_split(value);
         return 0;
     }
     if (std::strcmp(key, "pp_dma") == 0) {

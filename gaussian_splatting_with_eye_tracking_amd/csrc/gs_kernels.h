@@ -48,11 +48,14 @@ void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, c
 // base/cr/rasterizer_impl.cu:277-318, with identical outputs).
 // hdr_mirror: device address of 16 mapped host bytes that receive header
 // words 0..3 (K, error, max tile count, large tiles) when the scan finishes.
-void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror, int nslots);
+void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror, int nslots,
+                      int gx, bool banded);
 // spec_hdr: a speculative launch into a buffer of spec_cap keys, enqueued
 // before the host knows K; it does nothing when the header's K > spec_cap.
+// n_keys: the instance capacity the binning buffer was carved for (K, or the
+// speculative capacity); the banded duplicate never writes past it.
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
-                      const BinningView& b, hipStream_t s, const uint32_t* spec_hdr = nullptr,
+                      const BinningView& b, hipStream_t s, uint32_t n_keys, const uint32_t* spec_hdr = nullptr,
                       uint32_t spec_cap = 0);
 // Tile grids up to kLdsTiles are binned with workgroup-private LDS histograms
 // (count_tiles + chunked duplicate); larger grids use device atomics.
@@ -66,7 +69,11 @@ void set_pp_dma(int v);
 void set_hit_codes(int v);
 void set_sort_variant(int v);  // 0 = bitonic networks, 1 = bucket sort (default)
 void set_bin_slots(int v);  // 0 = auto
-int bin_slots_for(int P);   // sub-bucket slots of the LDS binning for a P-Gaussian forward
+int bin_slots_for(int P, int gx, int gy);  // sub-bucket slots of the LDS binning for a P-Gaussian forward
+bool dup_banded(int gx, int gy);           // the row-banded duplicate runs for this tile grid
+void set_dup_band(int v);
+void set_band_split(int v);
+void set_band_threads(int v);
 // img.tile_order = tiles sorted by descending work (heaviest first) so the
 // long tiles of a blend launch start early instead of forming its tail.
 // Work = range length, or min(range length, max_contrib) if use_max_contrib.

@@ -100,6 +100,8 @@ struct ImageView {
     uint32_t* tile_done;       // [T] AMR steps: finished (tile, quadrant) units, mod 4
     uint32_t* bucket_count;    // [kOrderBuckets64 = 256] tiles per work bucket (base forward render appends)
     uint32_t* bucket_list;     // [kOrderBuckets64][T] the tiles of each bucket, in append order
+    uint32_t* band_start;      // [<= T] banded duplicate: first instance of each band's tile range
+    uint32_t* band_cursor;     // [<= T] banded duplicate: staging cursor of each band
 };
 constexpr int kOrderBuckets64 = 256;  // (name kept: the bucket count of the backward order)
 // Each tile's bucket is split into kBinSlots sub-buckets, one per
@@ -131,6 +133,8 @@ inline size_t carve_image(char* base, size_t N, size_t T, ImageView* v, int tile
     g.quad_count = carve<uint32_t>(base, off, 4 * T);
     g.region_count = carve<uint32_t>(base, off, 16 * T);
     g.tile_done = carve<uint32_t>(base, off, T);
+    g.band_start = carve<uint32_t>(base, off, T);
+    g.band_cursor = carve<uint32_t>(base, off, T);
     g.bucket_count = nullptr;
     g.bucket_list = nullptr;
     if (tile != 32) {

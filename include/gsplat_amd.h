@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_AMD_ABI_VERSION 1
+#define GSPLAT_AMD_ABI_VERSION 2
 
 /* Resize the caller-owned byte buffer `ctx` to `nbytes` and return its
  * (device, >=256-B aligned) base pointer, or NULL on failure.
@@ -317,6 +317,8 @@ typedef struct {
     uint32_t* tile_done; /* [T] AMR steps: finished units per tile, mod 4 */
     uint32_t* bucket_count; /* [256] base forward: tiles per work bucket (heaviest first); NULL for tile 32 */
     uint32_t* bucket_list;  /* [256][T] base forward: the tiles of each bucket; NULL for tile 32 */
+    uint32_t* band_start;   /* [<= T] banded duplicate: first instance of each band (row of 2^k tiles) */
+    uint32_t* band_cursor;  /* [<= T] banded duplicate: staging cursor of each band */
 } gs_image_view;
 
 typedef struct {

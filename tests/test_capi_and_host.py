@@ -45,7 +45,7 @@ def test_host_layout_helpers():
     lib.gs_image_bytes.restype = ctypes.c_size_t
     lib.gs_binning_bytes.restype = ctypes.c_size_t
     lib.gs_knn_workspace_bytes.restype = ctypes.c_size_t
-    assert lib.gs_abi_version() == 1
+    assert lib.gs_abi_version() == 2  # 2: gs_image_view gained the band arrays
     g1, g2 = lib.gs_geom_bytes(1000), lib.gs_geom_bytes(2000)
     assert g2 > g1 > 1000 * (4 + 4 + 8 + 16 + 12 + 24 + 1 + 4 + 64)
     assert lib.gs_image_bytes(1920, 1080, 16) >= 1920 * 1080 * 8 + 120 * 68 * 8
@@ -93,7 +93,7 @@ def test_torch_extension_surface():
     for n in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "amr_rasterize_gaussians",
               "distCUDA2", "parse_buffers", "profile_enable", "profile_read", "set_tuning"):
         assert hasattr(_C, n), n
-    assert _C.abi_version() == 1
+    assert _C.abi_version() == 2
     assert all(os.path.exists(p) and p.startswith(ROOT) for p in native_library_paths())
 
 

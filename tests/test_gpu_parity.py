@@ -173,6 +173,39 @@ def test_bin_slots_bit_exact(slots):
     assert G.image_l1(color.cpu().numpy(), ref.color) < G.IMAGE_L1_TOL
 
 
+@pytest.mark.parametrize("band,split,W,H,threads", [(0, 0, 200, 120, 512), (1, 0, 200, 120, 512),
+                                                      (1, 1, 200, 120, 512), (1, 3, 128, 128, 512),
+                                                      (1, 64, 1000, 40, 512), (1, 0, 16400, 16, 512),
+                                                      (1, 0, 200, 120, 513), (1, 3, 1000, 40, 513),
+                                                      (1, 0, 200, 120, 514), (1, 2, 200, 120, 1024)])
+def test_dup_band_bit_exact(band, split, W, H, threads):
+    """The row-banded duplicate (binning.hip band_stage_kernel /
+    band_split_kernel) stages (Gaussian, tile row) entries and splits them
+    into tile runs through LDS-reordered appends; any split count, a grid
+    wider than one append round's 1024 bins (16400 px: the direct
+    duplicate) and the speculative path (second forward) all give the
+    oracle's point_list and ranges bit for bit."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    P, seed = 20000, 12
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    C.set_tuning("dup_band", band)
+    C.set_tuning("band_split", split)
+    C.set_tuning("band_threads", threads)
+    try:
+        _gpu_forward(sc, cam)  # the second forward runs the duplicate speculatively
+        _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
+    finally:
+        C.set_tuning("dup_band", 1)
+        C.set_tuning("band_split", 0)
+        C.set_tuning("band_threads", 0)
+    _, ref, _ = _oracle_forward(sc, cam)
+    assert K == ref.num_rendered
+    d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
+    np.testing.assert_array_equal(d["ranges"].cpu().numpy().astype(np.uint32), ref.ranges)
+    np.testing.assert_array_equal(d["point_list"].cpu().numpy().astype(np.uint32), ref.point_list)
+    assert G.image_l1(color.cpu().numpy(), ref.color) < G.IMAGE_L1_TOL
+
+
 def _clustered_scene(P, cam, seed, kind):
     """Depth distributions that stress the per-tile sort: 'ties' -- a third of
     the Gaussians are exact copies (same mean, so the same depth bits: the
@@ -245,7 +278,7 @@ def test_backward_with_unfilled_work_buckets():
     from gaussian_splatting_with_eye_tracking_amd import synthetic as S
     dpix = torch.from_numpy(S.make_cotangent(H, W, seed + 1)).cuda()
     lib = ctypes.CDLL(os.path.join(os.path.dirname(pkg.__file__), "libgsplat_amd.so"))
-    view = (ctypes.c_void_p * 17)()
+    view = (ctypes.c_void_p * 19)()  # gs_image_view: 19 pointers
     base = 1 << 20
     assert lib.gs_image_view_of(ctypes.c_void_p(base), W, H, 16, ctypes.byref(view)) == 0
     off = view[15] - base  # bucket_count

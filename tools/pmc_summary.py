@@ -48,6 +48,8 @@ STAGES = [
     ("render_bwd_kernel", "render_bwd"),
     ("render_fwd_kernel", "render"),
     ("duplicate_lds_kernel", "duplicate"),
+    ("band_stage_kernel", "duplicate"),
+    ("band_split_kernel", "duplicate"),
     ("duplicate_kernel", "duplicate"),
     ("count_tiles_kernel", "count_tiles"),
     ("backward_gaussians_kernel", "bwd_gauss"),
