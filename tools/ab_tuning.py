@@ -31,10 +31,14 @@ def main():
     ap.add_argument("--amr", action="store_true", help="time a 5-step foveated AMR frame instead")
     ap.add_argument("--amr-once", action="store_true", help="time AMR render_once (foveaStep -2, interpolated)")
     ap.add_argument("--per-step", action="store_true", help="--amr: also time each fovea step's apply (events)")
+    ap.add_argument("--set", nargs="*", default=[], help="fixed tunings key=value applied before the A/B")
     args = ap.parse_args()
 
     from gaussian_splatting_with_eye_tracking_amd import _C
     from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    for kv in args.set:
+        k, v = kv.split("=")
+        _C.set_tuning(k, int(v))
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     dev = torch.device("cuda:0")
     cam = S.make_camera(args.W, args.H)
@@ -132,7 +136,7 @@ def main():
     if args.amr and args.per_step:
         for v in args.values:
             out[str(v)]["per_step_median_ms"] = [round(float(x), 4) for x in np.median(np.array(step_ms[v]), 0)]
-    print(json.dumps({"key": args.key, "stage": args.stage, "results": out}))
+    print(json.dumps({"key": args.key, "stage": args.stage, "set": args.set, "results": out}))
 
 
 if __name__ == "__main__":
