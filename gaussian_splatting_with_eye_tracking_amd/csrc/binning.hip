@@ -363,7 +363,7 @@ int g_dup_diag = 0;
 // sub-bucket slots the LDS binning spreads its chunks over (1..kBinSlots;
 // the scan sums all kBinSlots, unused ones stay zero)
 int g_bin_slots = 0;  // 0: auto (bin_slots_for)
-int g_dup_band = 1;  // set_tuning("dup_band"): 1 = row-banded duplicate, 0 = direct
+int g_dup_band = 1;  // set_tuning("dup_band"): 1 = row-banded duplicate (16-px grids), 2 = any grid, 0 = direct
 // set_tuning("band_threads"): the banded duplicate's workgroup shape (0 auto;
 // 512: 512 threads x 1 source; 513: 512 x 2 sources per thread; 514: 512 x 2
 // sources, 4 items per round; 1024: 1024 x 1).  Measured
@@ -375,15 +375,20 @@ void set_dup_band(int v) { g_dup_band = v; }
 void set_band_split(int v) { g_band_split = std::max(0, v); }
 void set_band_threads(int v) { g_band_threads = v; }
 constexpr int kBandBins = 1024;  // bins of one coalesced append round (rows, or the tiles of a row)
-bool dup_banded(int gx, int gy) {
-    return g_dup_band > 0 && gx * gy <= kLdsTiles && gx <= kBandBins && gy <= kBandBins;
+// Banded only on the base 16-px grid: on the AMR 32-px grid (34 tile rows
+// at 1080p, ~2.2 instances per Gaussian) the direct duplicate is cheaper
+// (46 vs 56 us at config 3, profiles/r03h_ab_amr_band.json); g_dup_band = 2
+// forces it for any grid (tests).
+bool dup_banded(int gx, int gy, int block) {
+    if (g_dup_band <= 0 || gx * gy > kLdsTiles || gx > kBandBins || gy > kBandBins) return false;
+    return block == 16 || g_dup_band == 2;
 }
 void set_bin_slots(int v) { g_bin_slots = std::max(0, std::min(kBinSlots, v)); }
 // Measured (profiles/r03b_ab_bin_slots*): the sub-buckets save ~30 us of the
 // duplicate at config 4 (6.1M Gaussians) and ~4 us at config 2, where the
 // scan's 8x count loads cost more (+6 us): slots only for large scenes.
-int bin_slots_for(int P, int gx, int gy) {
-    if (dup_banded(gx, gy)) return 1;  // the banded duplicate reserves per-tile runs itself
+int bin_slots_for(int P, int gx, int gy, int block) {
+    if (dup_banded(gx, gy, block)) return 1;  // the banded duplicate reserves per-tile runs itself
     return g_bin_slots ? g_bin_slots : (P >= 2000000 ? kBinSlots : 1);
 }
 void set_dup_diag(int v) { g_dup_diag = v; }
@@ -474,7 +479,7 @@ void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H
     const int chunk = g_bin_chunk;
     hipLaunchKernelGGL(count_tiles_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
                        sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, radii, block, gx, gy, img.tile_count,
-                       (uint32_t)bin_slots_for(P, (int)gx, (int)gy));
+                       (uint32_t)bin_slots_for(P, (int)gx, (int)gy, block));
 }
 
 // ------------------------------------------------- banded duplicate ---
@@ -777,7 +782,7 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
                       uint32_t spec_cap) {
     if (P == 0) return;
     const uint32_t gx = (uint32_t)((W + block - 1) / block), gy = (uint32_t)((H + block - 1) / block);
-    if (dup_banded((int)gx, (int)gy)) {
+    if (dup_banded((int)gx, (int)gy, block)) {
         // ~4 split workgroups per CU over the rows
         const int nt = g_band_threads ? g_band_threads : (P >= 2000000 ? 513 : 1024);
         const int want = 4096;  // split workgroups in all
@@ -795,7 +800,7 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
         hipLaunchKernelGGL(duplicate_lds_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
                            sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, g.depths, radii, block, gx, gy,
                            img.tile_cursor, b.pair_keys, spec_hdr, spec_cap, g_dup_diag,
-                           (uint32_t)bin_slots_for(P, (int)gx, (int)gy));
+                           (uint32_t)bin_slots_for(P, (int)gx, (int)gy, block));
         return;
     }
     hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, g.means2D, g.depths, radii,

@@ -408,7 +408,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     stage_check(debug, s, "count_tiles");
     const std::pair<uint32_t*, uint32_t*> mirror =
         (r.T > 0 && hdr_mirror_on()) ? mirror_words() : std::pair<uint32_t*, uint32_t*>{nullptr, nullptr};
-    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second, bin_slots_for(in.P, gx, gy), gx, dup_banded(gx, gy)); }
+    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second, bin_slots_for(in.P, gx, gy, tile), gx, dup_banded(gx, gy, tile)); }
     stage_check(debug, s, "tile_scan");
     uint32_t hdr[4];
     const bool amr = tile == 32;  // the AMR layout appends records and region lists

@@ -69,8 +69,8 @@ void set_pp_dma(int v);
 void set_hit_codes(int v);
 void set_sort_variant(int v);  // 0 = bitonic networks, 1 = bucket sort (default)
 void set_bin_slots(int v);  // 0 = auto
-int bin_slots_for(int P, int gx, int gy);  // sub-bucket slots of the LDS binning for a P-Gaussian forward
-bool dup_banded(int gx, int gy);           // the row-banded duplicate runs for this tile grid
+int bin_slots_for(int P, int gx, int gy, int block);  // sub-bucket slots of the LDS binning (P-Gaussian forward)
+bool dup_banded(int gx, int gy, int block);           // the row-banded duplicate runs for this tile grid
 void set_dup_band(int v);
 void set_band_split(int v);
 void set_band_threads(int v);

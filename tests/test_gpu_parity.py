@@ -656,6 +656,29 @@ def test_amr_foveated_steps(name, P, W, H, seed, amr_variant, amr_batch, amr_fol
                                rtol=1e-5, atol=1e-7)
 
 
+@pytest.mark.parametrize("name,P,W,H,seed", [("amr_10k_256", 10000, 256, 256, 0), ("amr_ragged", 4000, 200, 120, 3)])
+def test_amr_forced_banded_duplicate(name, P, W, H, seed):
+    """The row-banded duplicate forced onto the AMR 32-px grid (dup_band 2;
+    by default AMR grids use the direct duplicate): point_list and ranges are
+    the oracle's bit for bit and the frame matches."""
+    import oracle as O
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    C.set_tuning("dup_band", 2)
+    try:
+        acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam)
+    finally:
+        C.set_tuning("dup_band", 1)
+    s = O.settings_from_camera(cam)
+    kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
+    racc, rradii, st, rsteps = O.amr_render_foveated(s, kw)
+    K = st.fwd.num_rendered
+    d = C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
+    np.testing.assert_array_equal(d["ranges"].cpu().numpy().astype(np.uint32), st.fwd.ranges)
+    np.testing.assert_array_equal(d["point_list"].cpu().numpy().astype(np.uint32), st.fwd.point_list)
+    assert G.image_l1(acc.cpu().numpy(), racc) < G.IMAGE_L1_TOL
+
+
 DEFAULT_AMR_LISTS_PER = 2  # render.hip g_amr_lists_per
 
 
