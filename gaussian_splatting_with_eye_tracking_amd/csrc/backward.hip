@@ -914,7 +914,7 @@ constexpr int kShRow = 49;
 
 template <bool kHasSH, bool kHasScales, bool kSH16>
 __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussArgs a, const float* __restrict__ grad_accum,
-                                                                 const uint8_t* __restrict__ clamped_bits) {
+                                                                 const uint8_t* __restrict__ clamped_bits, int stage_mlp) {
     constexpr bool kStage = kHasSH && kSH16;
     __shared__ float s_dsh[kStage ? 256 * kShRow : 1];
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -922,10 +922,25 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
         const int g0 = blockIdx.x * blockDim.x;
         const int n = min(256, a.P - g0);
         const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)g0 * 12;
-        for (int f = threadIdx.x; f < n * 12; f += 256) {
-            const float4 v = in[f];
-            float* r = s_dsh + (f / 12) * kShRow + 4 * (f % 12);
-            r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+        if (n == 256 && stage_mlp) {
+            // a full workgroup: the 12 loads of each thread issued back to back
+            // (one memory round trip; the loop below waits for each load before
+            // its LDS write -- 12 round trips at 3 waves per SIMD)
+            float4 v[12];
+#pragma unroll
+            for (int k = 0; k < 12; k++) v[k] = in[threadIdx.x + 256 * k];
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                const int f = threadIdx.x + 256 * k;
+                float* r = s_dsh + (f / 12) * kShRow + 4 * (f % 12);
+                r[0] = v[k].x; r[1] = v[k].y; r[2] = v[k].z; r[3] = v[k].w;
+            }
+        } else {
+            for (int f = threadIdx.x; f < n * 12; f += 256) {
+                const float4 v = in[f];
+                float* r = s_dsh + (f / 12) * kShRow + 4 * (f % 12);
+                r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+            }
         }
         __syncthreads();
     }
@@ -973,6 +988,8 @@ __global__ void __launch_bounds__(256) sh_backward_kernel(BackwardGaussArgs a, c
 
 int g_bwd_gauss_split = 0;
 void set_bwd_gauss_split(int v) { g_bwd_gauss_split = v; }
+int g_bg_stage_mlp = 1;  // set_tuning("bg_stage_mlp"): the SH staging loads issued back to back
+void set_bg_stage_mlp(int v) { g_bg_stage_mlp = v; }
 
 void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hipStream_t s) {
     if (a.P == 0) return;
@@ -981,7 +998,8 @@ void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hi
     const bool sh16 = sh && a.M == 16;
     const bool sc = a.scales != nullptr;
 #define GS_BG_LAUNCH(A, B, C) \
-    hipLaunchKernelGGL((backward_gaussians_kernel<A, B, C>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped)
+    hipLaunchKernelGGL((backward_gaussians_kernel<A, B, C>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped, \
+                       g_bg_stage_mlp)
     if (sh && g_bwd_gauss_split && a.dL_dcolor) {  // (the split SH pass reads dL_dcolor back)
         if (sc) GS_BG_LAUNCH(false, true, false);
         else GS_BG_LAUNCH(false, false, false);

@@ -1100,6 +1100,10 @@ int gs_set_tuning(const char* key, int value) {
         set_tile_order(value);
         return 0;
     }
+    if (std::strcmp(key, "bg_stage_mlp") == 0) {
+        set_bg_stage_mlp(value);
+        return 0;
+    }
     if (std::strcmp(key, "dup_band") == 0) {
         set_dup_band(value);
         return 0;

@@ -74,6 +74,7 @@ bool dup_banded(int gx, int gy, int block);           // the row-banded duplicat
 void set_dup_band(int v);
 void set_band_split(int v);
 void set_band_threads(int v);
+void set_bg_stage_mlp(int v);
 // img.tile_order = tiles sorted by descending work (heaviest first) so the
 // long tiles of a blend launch start early instead of forming its tail.
 // Work = range length, or min(range length, max_contrib) if use_max_contrib.
