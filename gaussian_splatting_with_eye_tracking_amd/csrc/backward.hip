@@ -39,7 +39,7 @@ constexpr int kAccRow = 9;   // LDS accumulator row (floats; odd stride: 9 scala
 // One 16x16 tile per workgroup of kWaves wave64s, kPPL pixels per lane
 // (kWaves * 64 * kPPL = 256; gs_blend.cuh mapping).  kMinWaves: waves per
 // SIMD the register allocation must allow.
-template <int kPPL, int kWaves, int kMinWaves, bool kSwap, bool kAMR = false>
+template <int kPPL, int kWaves, int kMinWaves, bool kSwap, bool kAMR = false, int kSel = 0>
 __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     int W, int H, const uint32_t* __restrict__ ranges, const uint32_t* __restrict__ max_contrib,
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
@@ -49,19 +49,33 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     int amr_mode, const uint32_t* __restrict__ levels, int flush_mode, const uint32_t* __restrict__ bucket_count,
     const uint32_t* __restrict__ bucket_list, const uint8_t* __restrict__ hit_codes, const uint32_t* __restrict__ hdr) {
 #pragma clang fp contract(fast)
+    static_assert(!kSel || (kWaves == 1 && kSwap), "the select form is the 1-wave transposed-sum geometry");
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
     // (x, y, r, g) and the scaled conic / opacity as two b128 reads, b as one
     // b32 (LDS cycles per wave-read: b128 4, b96 8, b64 / b32 2)
     __shared__ float4 s_a[kB];
     __shared__ float4 s_co[kB];
-    __shared__ float s_b[kB];
+    // (b at a 16-B stride: one LDS address serves all three record reads)
+    __shared__ float4 s_b[kB];
     // per-Gaussian sums: one wave parks its two half-wave partials (summed by
     // the flush; 4 row partials would double the LDS footprint and cost
     // workgroups per CU); several waves add into one row with LDS atomics
     constexpr int kRowsPerG = (kWaves == 1 && !kSwap) ? 2 : 1;
     __shared__ float s_acc[kB * kRowsPerG * kAccRow];
     __shared__ uint64_t s_bal[4 * kWaves];
+    // kSel == 2: the per-Gaussian sums are finished in groups of 8 Gaussians --
+    // each visit parks its two transposed registers (16 column partials of
+    // each of g0..g7, swap_rows8_pk) in a staging slot, and one pass over 8
+    // slots sums them with 64 lanes at once (lane = (slot, value)) instead of
+    // 8 DPP adds per Gaussian.  Layout: reduce lane l's 16 partials are 4
+    // float4s at l * 4 + i * kStagePitch (i = 0..3), so each b128 read is 64
+    // consecutive dwords per 16 lanes; the pitch's 16-float pad spreads the
+    // writers' 4 column groups over all 64 banks.
+    constexpr int kStageSlots = 8;
+    constexpr int kStagePitch = 272;
+    __shared__ __attribute__((aligned(16))) float s_stage[kSel == 2 ? 3 * kStagePitch + 256 : 1];
+    __shared__ uint32_t s_stage_j[kSel == 2 ? kStageSlots : 1];  // batch slot j of each staging slot
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -214,6 +228,14 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         nrgb[0] = colors[3 * nid]; nrgb[1] = colors[3 * nid + 1]; nrgb[2] = colors[3 * nid + 2];
         s_id[0][tid] = nid;
     }
+    // kSel staging reduce: lane (slot = lane / 8, value q = lane % 8) sums the 16
+    // column partials of value q parked by slot's Gaussian (za rows hold values
+    // swap_sum_slot(r), zb rows 4 + swap_sum_slot(r); swap_sum_slot is its own
+    // inverse) and stores the total into that Gaussian's accumulator row.
+    const int st_slot = lane >> 3, st_q = lane & 7;
+    // writer lane: row r = lane / 16 of za / zb holds values swap_sum_slot(r) /
+    // 4 + swap_sum_slot(r), column c = lane % 16 is element c of that sum
+    const int st_dst = ((lane & 15) >> 2) * kStagePitch + 4 * swap_sum_slot(lane >> 4) + (lane & 3);
     int par = 0;
     for (int top = m; top > 0; top -= kB, par ^= 1) {  // entries [top-cnt, top), back to front
         const int cnt = min(kB, top);
@@ -224,7 +246,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             const float4 co = nco;
             s_a[tid] = make_float4(xy.x, xy.y, nrgb[0], nrgb[1]);
             s_co[tid] = splat_coef(co);
-            s_b[tid] = nrgb[2];
+            s_b[tid].x = nrgb[2];
             gm = use_codes ? (uint32_t)hit_codes[range.x + top - 1 - tid]
                  : cull ? splat_group_mask(xy, co, (float)ox, (float)oy, (float)pstride) : 0xfu;
         }
@@ -235,6 +257,20 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         if (kWaves > 1)
             for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
         uint64_t written = 0;  // kWaves == 1: batch slots whose partial rows were stored
+        int nst = 0;           // kSel == 2: staging slots in use (wave-uniform)
+        auto stage_reduce = [&](const int n) {
+            if (lane < 8 * n) {
+                const float* src = &s_stage[4 * lane];
+                const float4 a = *reinterpret_cast<const float4*>(src);
+                const float4 b = *reinterpret_cast<const float4*>(src + kStagePitch);
+                const float4 c = *reinterpret_cast<const float4*>(src + 2 * kStagePitch);
+                const float4 d = *reinterpret_cast<const float4*>(src + 3 * kStagePitch);
+                const gs_f2 x0 = gs_f2{a.x, a.y} + gs_f2{b.x, b.y}, x1 = gs_f2{a.z, a.w} + gs_f2{b.z, b.w};
+                const gs_f2 x2 = gs_f2{c.x, c.y} + gs_f2{d.x, d.y}, x3 = gs_f2{c.z, c.w} + gs_f2{d.z, d.w};
+                const gs_f2 y = (x0 + x1) + (x2 + x3);
+                s_acc[s_stage_j[st_slot] * kAccRow + st_q] = y.x + y.y;
+            }
+        };
         __syncthreads();
         // first batch slot this wave needs: contributor = top-1-j < wave_last
         // (readfirstlane: wave_last is uniform after the xor-shuffle max, but the
@@ -272,6 +308,42 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             // applies o, the conic and the constants.
             float c0 = 0.f, c1 = 0.f, c2 = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f;
             bool any = false;
+            if constexpr (kSel) {
+                // Select form: a rejected pixel takes alpha = G = 0, i.e.
+                // rinv = 1 (T unchanged), dchannel = t = 0 and acc_dot += 0 --
+                // the same bits as the branchy form for every accepted pixel, no
+                // exec-mask bookkeeping and no ballot: a visited Gaussian is
+                // always summed (with the forward's hit codes a visited row
+                // group has a pixel that blended; under the geometric cull an
+                // all-rejected visit sums zeros, which the flush skips).
+#pragma unroll
+                for (int k = 0; k < kPPL; k++) {
+                    if (!((mk[k] >> cbit) & 1ull)) continue;  // wave-uniform
+                    const float dy = xy.y - (py0 + (float)(4 * k * (int)pstride));
+                    const float p2 = splat_p2(pa, pb, dy, pc);
+                    const float Gr = splat_exp(p2);
+                    const float ar = fminf(0.99f, pc.w * Gr);
+                    const bool ok = contributor < last[k] && !(p2 > 0.0f) && !(ar < 1.0f / 255.0f);
+                    const float G = ok ? Gr : 0.f;
+                    const float alpha = ok ? ar : 0.f;
+                    const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
+                    T[k] = T[k] * rinv;
+                    const float dchannel_dcolor = alpha * T[k];
+                    const float c_dot = cf.x * dpx[k][0] + cf.y * dpx[k][1] + cf.z * dpx[k][2];
+                    const float diff = c_dot - acc_dot[k];
+                    const float dL_dalpha = diff * T[k] + nbg[k] * rinv;
+                    acc_dot[k] = __builtin_fmaf(alpha, diff, acc_dot[k]);
+                    c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
+                    c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
+                    c2 = __builtin_fmaf(dchannel_dcolor, dpx[k][2], c2);
+                    const float t = G * dL_dalpha;
+                    const float tdy = t * dy;
+                    s0 += t;
+                    s1 += tdy;
+                    s2 = __builtin_fmaf(tdy, dy, s2);
+                }
+                any = true;
+            } else
 #pragma unroll
             for (int k = 0; k < kPPL; k++) {
                 if (!((mk[k] >> cbit) & 1ull)) continue;  // wave-uniform: culled for this row group
@@ -317,10 +389,26 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             g[6] = dx * g[4];
             g[7] = dx * s1;
             g[8] = s2;
-            if (__ballot(any) != 0ull) {  // wave-uniform
-                if (kSwap) {  // full sums by transposition: 2 values per row leader + g8 in lane 63
+            if (kSel ? any : __ballot(any) != 0ull) {  // wave-uniform
+                if constexpr (kSel == 2) {
                     float za, zb;
-                    swap_sum9(g, za, zb);
+                    swap_rows8_pk(g, za, zb);
+                    float* st = &s_stage[st_dst + 32 * nst];
+                    st[0] = za;
+                    st[16] = zb;
+                    if (lane == 63) {
+                        s_acc[j * kAccRow + 8] = g[8];
+                        s_stage_j[nst] = (uint32_t)j;
+                    }
+                    written |= 1ull << j;
+                    if (++nst == kStageSlots) {
+                        stage_reduce(kStageSlots);
+                        nst = 0;
+                    }
+                } else if (kSwap) {  // full sums by transposition: 2 values per row leader + g8 in lane 63
+                    float za, zb;
+                    if constexpr (kSel == 1) swap_sum9_pk(g, za, zb);
+                    else swap_sum9(g, za, zb);
                     if ((lane & 15) == 15) {
                         float* row = &s_acc[j * kAccRow];
                         const int q = swap_sum_slot(lane >> 4);
@@ -357,8 +445,11 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             todo &= todo - 1;
             const int j = 64 * c + cbit;
             const float4 a4 = s_a[j];
-            visit(cbit, make_float2(a4.x, a4.y), s_co[j], make_float4(a4.z, a4.w, s_b[j], 0.f));
+            visit(cbit, make_float2(a4.x, a4.y), s_co[j], make_float4(a4.z, a4.w, s_b[j].x, 0.f));
           }
+        }
+        if constexpr (kSel == 2) {
+            if (nst) stage_reduce(nst);
         }
         __syncthreads();
         if (has_next) {  // gathers for the next batch, ahead of the flush atomics
@@ -409,14 +500,16 @@ extern int g_cull;  // render.hip
 // 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave x 4 px with the
 // half-wave DPP-tree sums instead of the permlane transposition
 // (1 wave x 4 px capped at 5 or 6 waves per SIMD spills: measured slower)
-int g_bwd_variant = 0;
+// 7: the select-form blend with staged sums (the default since round 3)
+constexpr int kDefaultBwdVariant = 7;
+int g_bwd_variant = kDefaultBwdVariant;
 // Flush of the per-(tile, Gaussian) sums: 0 = memory-side atomics (the only
 // correct mode); 1 = plain stores of the same shape, 2 = no flush -- timing
 // diagnostics for the A/B tool only (they produce wrong gradients).
 int g_bwd_flush = 0;
 void set_backward_flush(int v) { g_bwd_flush = v; }
 
-void set_backward_variant(int v) { g_bwd_variant = v; }
+void set_backward_variant(int v) { g_bwd_variant = v < 0 ? kDefaultBwdVariant : v; }  // < 0: the default
 // Heavy-tile split of the backward blend: the heaviest T * g_bwd_split_permille
 // / 1000 tiles run as g_bwd_split_ways units (row-group subsets) each, so the
 // launch's tail is not one wave walking the longest list for all 256 pixels.
@@ -470,6 +563,8 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         case 2: GS_BWD_LAUNCH(1, 4, 4, true); break;
         case 3: GS_BWD_LAUNCH(4, 1, 4, false); break;
         case 5: GS_BWD_LAUNCH(4, 1, 5, true); break;  // 96 VGPRs: 5 waves per SIMD
+        case 6: GS_BWD_LAUNCH(4, 1, 4, true, false, 1); break;  // select form
+        case 7: GS_BWD_LAUNCH(4, 1, 4, true, false, 2); break;  // select form, staged sums
         default: GS_BWD_LAUNCH(4, 1, 4, true); break;
     }
 #undef GS_BWD_LAUNCH

@@ -679,6 +679,88 @@ __device__ __forceinline__ float pl_add16(float a, float b) {
     return __builtin_bit_cast(float, r0) + __builtin_bit_cast(float, r1);
 }
 
+// The same sums with the two add levels as packed f32 adds (v_pk_add_f32, one
+// issue for two lanes' worth of values): the swaps pair (g0, g4) and (g2, g6)
+// so that each level's operands already sit in adjacent registers -- 4 + 2
+// swaps, 3 packed adds and the 14 DPP adds: 23 VALU issues instead of 26.
+typedef float gs_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ gs_f2 pl_swap32(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
+                                                    false, false);
+    const uint32_t r0 = r[0], r1 = r[1];
+    return gs_f2{__builtin_bit_cast(float, r0), __builtin_bit_cast(float, r1)};
+}
+__device__ __forceinline__ gs_f2 pl_swap16(float a, float b) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
+                                                    false, false);
+    const uint32_t r0 = r[0], r1 = r[1];
+    return gs_f2{__builtin_bit_cast(float, r0), __builtin_bit_cast(float, r1)};
+}
+
+__device__ __forceinline__ void swap_sum9_pk(float (&g)[9], float& za, float& zb) {
+    const gs_f2 p0 = pl_swap32(g[0], g[1]), p4 = pl_swap32(g[4], g[5]);
+    const gs_f2 p2 = pl_swap32(g[2], g[3]), p6 = pl_swap32(g[6], g[7]);
+    const gs_f2 abef = gs_f2{p0.x, p4.x} + gs_f2{p0.y, p4.y};
+    const gs_f2 cdgh = gs_f2{p2.x, p6.x} + gs_f2{p2.y, p6.y};
+    const gs_f2 q0 = pl_swap16(abef.x, cdgh.x), q1 = pl_swap16(abef.y, cdgh.y);
+    const gs_f2 z = gs_f2{q0.x, q1.x} + gs_f2{q0.y, q1.y};
+    za = z.x;
+    zb = z.y;
+    float e = g[8];
+    asm volatile(
+        "s_nop 1\n"
+        "v_add_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %2, %2, %2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %2, %2, %2 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %2, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "v_add_f32_dpp %2, %2, %2 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+        "s_nop 1\n"
+        "v_add_f32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
+        "s_nop 1\n"
+        "v_add_f32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
+        : "+v"(za), "+v"(zb), "+v"(e));
+    g[8] = e;
+}
+
+// Transposition half of swap_sum9_pk, for sums finished elsewhere: after it
+// row r (lanes 16r..16r+15) of za holds the 16 column partials of value
+// swap_sum_slot(r), zb those of 4 + swap_sum_slot(r); g[8] gets the full DPP
+// sum (in lane 63).  9 swap / packed-add issues + 6 DPP adds.
+template <int kCtrl, int kRowMask, bool kBound>
+__device__ __forceinline__ float dpp_add(float e) {
+    return e + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e), kCtrl, kRowMask,
+                                                                      0xf, kBound));
+}
+__device__ __forceinline__ void swap_rows8_pk(float (&g)[9], float& za, float& zb) {
+    const gs_f2 p0 = pl_swap32(g[0], g[1]), p4 = pl_swap32(g[4], g[5]);
+    const gs_f2 p2 = pl_swap32(g[2], g[3]), p6 = pl_swap32(g[6], g[7]);
+    const gs_f2 abef = gs_f2{p0.x, p4.x} + gs_f2{p0.y, p4.y};
+    const gs_f2 cdgh = gs_f2{p2.x, p6.x} + gs_f2{p2.y, p6.y};
+    const gs_f2 q0 = pl_swap16(abef.x, cdgh.x), q1 = pl_swap16(abef.y, cdgh.y);
+    const gs_f2 z = gs_f2{q0.x, q1.x} + gs_f2{q0.y, q1.y};
+    za = z.x;
+    zb = z.y;
+    // g8: the plain DPP tree (compiler-scheduled, so it interleaves with the
+    // swaps above instead of waiting out its own hazards)
+    float e = g[8];
+    e = dpp_add<0x111, 0xf, true>(e);   // row_shr:1
+    e = dpp_add<0x112, 0xf, true>(e);   // row_shr:2
+    e = dpp_add<0x114, 0xf, true>(e);   // row_shr:4
+    e = dpp_add<0x118, 0xf, true>(e);   // row_shr:8
+    // all rows enabled (so the move folds into the add): only lane 63's total
+    // is used, and it takes rows 3 + 2 and then lane 31 = rows 1 + 0
+    e = dpp_add<0x142, 0xf, true>(e);  // row_bcast:15
+    e = dpp_add<0x143, 0xf, true>(e);  // row_bcast:31
+    g[8] = e;
+}
+
 __device__ __forceinline__ void swap_sum9(float (&g)[9], float& za, float& zb) {
     const float ab = pl_add32(g[0], g[1]), cd = pl_add32(g[2], g[3]);
     const float ef = pl_add32(g[4], g[5]), gh = pl_add32(g[6], g[7]);

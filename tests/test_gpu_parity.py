@@ -373,7 +373,7 @@ def test_config2_full_size_parity_and_psnr():
         assert G.rel_err(g.cpu().numpy(), rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(g.cpu().numpy(), rg[n]))
 
 
-@pytest.mark.parametrize("bwd_variant", [0, 1, 2, 3, 5])
+@pytest.mark.parametrize("bwd_variant", [0, 1, 2, 3, 5, 6, 7])
 @pytest.mark.parametrize("fwd_variant", [0, 1, 2, 3, 4, 5, 6])
 def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
     """Every forward / backward blend geometry (gs_set_tuning) against the oracle."""
@@ -395,7 +395,7 @@ def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
         torch.cuda.synchronize()
     finally:
         C.set_tuning("fwd_variant", 2)
-        C.set_tuning("bwd_variant", 0)
+        C.set_tuning("bwd_variant", -1)
     os_, ref, kw = _oracle_forward(sc, cam, bg=(0.2, 0.1, 0.05))
     assert G.image_l1(color.cpu().numpy(), ref.color) < G.IMAGE_L1_TOL
     rg = O.backward(os_, ref, sc.means3D, dpix, **kw)
