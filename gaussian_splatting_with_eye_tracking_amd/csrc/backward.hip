@@ -174,9 +174,13 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         wave_last = max(wave_last, last[k]);
 #pragma unroll
         for (int c = 0; c < 3; c++) dpx[k][c] = px.inside[k] ? dL_dpixels[c * plane + pid] : 0.f;
-        acc_dot[k] = 0.f;
         // (-T_final / (1 - alpha)) * bg.dL_dpix = nbg * 1/(1 - alpha)
         nbg[k] = -Tf * (bg0 * dpx[k][0] + bg1 * dpx[k][1] + bg2 * dpx[k][2]);
+        // kSel: the background term folded into the recurrence -- with
+        // B = T_final bg.dL_dpix / T (so the reference's bg term is -T_new B),
+        // acc_dot + B obeys the same accum recurrence as acc_dot and starts at
+        // bg.dL_dpix: dL_dalpha = T_new (c.dL_dpix - (acc_dot + B)).
+        acc_dot[k] = kSel ? bg0 * dpx[k][0] + bg1 * dpx[k][1] + bg2 * dpx[k][2] : 0.f;
     }
     // entries at or past the wave's max n_contrib are skipped by all its pixels
 #pragma unroll
@@ -329,9 +333,11 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                     const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
                     T[k] = T[k] * rinv;
                     const float dchannel_dcolor = alpha * T[k];
-                    const float c_dot = cf.x * dpx[k][0] + cf.y * dpx[k][1] + cf.z * dpx[k][2];
-                    const float diff = c_dot - acc_dot[k];
-                    const float dL_dalpha = diff * T[k] + nbg[k] * rinv;
+                    // (c - accum_rec - B) . dL_dpix as one fma chain
+                    const float diff = __builtin_fmaf(cf.z, dpx[k][2],
+                                                      __builtin_fmaf(cf.y, dpx[k][1],
+                                                                     __builtin_fmaf(cf.x, dpx[k][0], -acc_dot[k])));
+                    const float dL_dalpha = diff * T[k];
                     acc_dot[k] = __builtin_fmaf(alpha, diff, acc_dot[k]);
                     c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
                     c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
