@@ -62,20 +62,20 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // the flush; 4 row partials would double the LDS footprint and cost
     // workgroups per CU); several waves add into one row with LDS atomics
     constexpr int kRowsPerG = (kWaves == 1 && !kSwap) ? 2 : 1;
-    __shared__ float s_acc[kB * kRowsPerG * kAccRow];
+    __shared__ float s_acc[kB * kRowsPerG * kAccRow + (kSel == 2 ? 1 : 0)];  // (+ a dummy entry: kSel == 2)
     __shared__ uint64_t s_bal[4 * kWaves];
-    // kSel == 2: the per-Gaussian sums are finished in groups of 8 Gaussians --
+    // kSel == 2: the per-Gaussian sums are finished in groups of 7 Gaussians --
     // each visit parks its two transposed registers (16 column partials of
-    // each of g0..g7, swap_rows8_pk) in a staging slot, and one pass over 8
-    // slots sums them with 64 lanes at once (lane = (slot, value)) instead of
-    // 8 DPP adds per Gaussian.  Layout: reduce lane l's 16 partials are 4
-    // float4s at l * 4 + i * kStagePitch (i = 0..3), so each b128 read is 64
-    // consecutive dwords per 16 lanes; the pitch's 16-float pad spreads the
-    // writers' 4 column groups over all 64 banks.
-    constexpr int kStageSlots = 8;
+    // each of g0..g7, swap_rows8_pk) and g8's 4 row sums in a staging slot,
+    // and one pass over 7 slots sums them with 63 lanes at once (lane = 9 *
+    // slot + value) instead of 14 DPP adds per Gaussian.  Layout: reduce lane
+    // l's 16 partials are 4 float4s at l * 4 + i * kStagePitch (i = 0..3), so
+    // each b128 read is 64 consecutive dwords per 16 lanes; the pitch's
+    // 16-float pad spreads the writers' 4 column groups over all 64 banks.
+    // A g8 lane's 4 partials are its first float4; its other three stay zero.
+    constexpr int kStageSlots = 7;
     constexpr int kStagePitch = 272;
     __shared__ __attribute__((aligned(16))) float s_stage[kSel == 2 ? 3 * kStagePitch + 256 : 1];
-    __shared__ uint32_t s_stage_j[kSel == 2 ? kStageSlots : 1];  // batch slot j of each staging slot
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -236,10 +236,18 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // column partials of value q parked by slot's Gaussian (za rows hold values
     // swap_sum_slot(r), zb rows 4 + swap_sum_slot(r); swap_sum_slot is its own
     // inverse) and stores the total into that Gaussian's accumulator row.
-    const int st_slot = lane >> 3, st_q = lane & 7;
+    const int st_slot = lane / 9, st_q = lane - 9 * (lane / 9);
+    // reduce output: row jj's entry st_q; lane 63 (no slot) sums zeros into a
+    // dummy row, so a full group's pass needs no lane mask
+    const int st_mul = lane == 63 ? 0 : kAccRow, st_base = lane == 63 ? kB * kAccRow : st_q;
+    if constexpr (kSel == 2) {
+        for (int i = lane; i < 3 * kStagePitch + 256; i += 64) s_stage[i] = 0.f;
+    }
     // writer lane: row r = lane / 16 of za / zb holds values swap_sum_slot(r) /
-    // 4 + swap_sum_slot(r), column c = lane % 16 is element c of that sum
+    // 4 + swap_sum_slot(r), column c = lane % 16 is element c of that sum;
+    // lane 16 r + 15 also holds g8's row-r sum, element r of value 8
     const int st_dst = ((lane & 15) >> 2) * kStagePitch + 4 * swap_sum_slot(lane >> 4) + (lane & 3);
+    const int st_g8 = 32 + (lane >> 4);
     int par = 0;
     for (int top = m; top > 0; top -= kB, par ^= 1) {  // entries [top-cnt, top), back to front
         const int cnt = min(kB, top);
@@ -262,8 +270,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
         uint64_t written = 0;  // kWaves == 1: batch slots whose partial rows were stored
         int nst = 0;           // kSel == 2: staging slots in use (wave-uniform)
+        uint64_t js = 0;       // kSel == 2: batch slot j of staging slot s in bits [6 s, 6 s + 6)
         auto stage_reduce = [&](const int n) {
-            if (lane < 8 * n) {
+            if (n == kStageSlots || lane < 9 * n) {
                 const float* src = &s_stage[4 * lane];
                 const float4 a = *reinterpret_cast<const float4*>(src);
                 const float4 b = *reinterpret_cast<const float4*>(src + kStagePitch);
@@ -272,7 +281,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 const gs_f2 x0 = gs_f2{a.x, a.y} + gs_f2{b.x, b.y}, x1 = gs_f2{a.z, a.w} + gs_f2{b.z, b.w};
                 const gs_f2 x2 = gs_f2{c.x, c.y} + gs_f2{d.x, d.y}, x3 = gs_f2{c.z, c.w} + gs_f2{d.z, d.w};
                 const gs_f2 y = (x0 + x1) + (x2 + x3);
-                s_acc[s_stage_j[st_slot] * kAccRow + st_q] = y.x + y.y;
+                const uint32_t jj = (uint32_t)(js >> (6 * st_slot)) & 63u;
+                s_acc[jj * st_mul + st_base] = y.x + y.y;
             }
         };
         __syncthreads();
@@ -399,18 +409,19 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 if constexpr (kSel == 2) {
                     float za, zb;
                     swap_rows8_pk(g, za, zb);
-                    float* st = &s_stage[st_dst + 32 * nst];
+                    float* st = &s_stage[st_dst + 36 * nst];
                     st[0] = za;
                     st[16] = zb;
-                    if (lane == 63) {
-                        s_acc[j * kAccRow + 8] = g[8];
-                        s_stage_j[nst] = (uint32_t)j;
-                    }
+                    if ((lane & 15) == 15) s_stage[st_g8 + 36 * nst] = g[8];
+                    js |= (uint64_t)j << (6 * nst);
                     written |= 1ull << j;
-                    if (++nst == kStageSlots) {
-                        stage_reduce(kStageSlots);
-                        nst = 0;
-                    }
+                    // (the resets as selects outside the reduce's lane-masked
+                    // region: assigned inside it, the slot state would be
+                    // treated as divergent and kept in VGPRs)
+                    const bool full = ++nst == kStageSlots;
+                    if (full) stage_reduce(kStageSlots);
+                    nst = full ? 0 : nst;
+                    js = full ? 0ull : js;
                 } else if (kSwap) {  // full sums by transposition: 2 values per row leader + g8 in lane 63
                     float za, zb;
                     if constexpr (kSel == 1) swap_sum9_pk(g, za, zb);

@@ -731,8 +731,8 @@ __device__ __forceinline__ void swap_sum9_pk(float (&g)[9], float& za, float& zb
 
 // Transposition half of swap_sum9_pk, for sums finished elsewhere: after it
 // row r (lanes 16r..16r+15) of za holds the 16 column partials of value
-// swap_sum_slot(r), zb those of 4 + swap_sum_slot(r); g[8] gets the full DPP
-// sum (in lane 63).  9 swap / packed-add issues + 6 DPP adds.
+// swap_sum_slot(r), zb those of 4 + swap_sum_slot(r); g[8] holds row r's sum
+// in lane 16 r + 15.  9 swap / packed-add issues + 4 DPP adds.
 template <int kCtrl, int kRowMask, bool kBound>
 __device__ __forceinline__ float dpp_add(float e) {
     return e + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e), kCtrl, kRowMask,
@@ -747,17 +747,14 @@ __device__ __forceinline__ void swap_rows8_pk(float (&g)[9], float& za, float& z
     const gs_f2 z = gs_f2{q0.x, q1.x} + gs_f2{q0.y, q1.y};
     za = z.x;
     zb = z.y;
-    // g8: the plain DPP tree (compiler-scheduled, so it interleaves with the
-    // swaps above instead of waiting out its own hazards)
+    // g8: the DPP row tree (compiler-scheduled, so it interleaves with the
+    // swaps above instead of waiting out its own hazards); lane 16 r + 15
+    // ends with row r's sum
     float e = g[8];
     e = dpp_add<0x111, 0xf, true>(e);   // row_shr:1
     e = dpp_add<0x112, 0xf, true>(e);   // row_shr:2
     e = dpp_add<0x114, 0xf, true>(e);   // row_shr:4
     e = dpp_add<0x118, 0xf, true>(e);   // row_shr:8
-    // all rows enabled (so the move folds into the add): only lane 63's total
-    // is used, and it takes rows 3 + 2 and then lane 31 = rows 1 + 0
-    e = dpp_add<0x142, 0xf, true>(e);  // row_bcast:15
-    e = dpp_add<0x143, 0xf, true>(e);  // row_bcast:31
     g[8] = e;
 }
 
