@@ -289,6 +289,35 @@ __device__ __forceinline__ bool blend_one_sel(float2 xy, float4 co, float4 f, fl
     return blended;
 }
 
+// The select form with the finished state in T's sign instead of an alpha cap:
+// a pixel that stops keeps T = -|T| (its final transmittance, negated), so
+// T (1 - a) < 1e-4 holds for every later Gaussian and a = 0 follows from the
+// stop test itself -- alpha is the plain min(0.99, o G) (a constant clamp:
+// no NaN-canonicalising max of a loop-carried cap) and the cap's select is
+// gone; the stop select writes -|T| through the VOP3 source modifiers.  The
+// last contributor is tracked as the entry's LDS byte offset (lo, the VGPR the
+// record reads already use) and converted once per 64 entries.  Bits for
+// every pixel still blending are those of blend_one_sel.
+__device__ __forceinline__ bool blend_one_sel2(float2 xy, float4 co, float4 f, float pxx, float pxy, uint32_t lo,
+                                               float& T, float (&C)[3], uint32_t& last_lo) {
+    const float dx = xy.x - pxx, dy = xy.y - pxy;
+    const float p = splat_p2(dx, dy, co);
+    float a = fminf(0.99f, co.w * splat_exp(p));
+    a = (p > 0.0f) ? 0.0f : a;           // power > 0: skipped
+    a = (a < 1.0f / 255.0f) ? 0.0f : a;  // alpha < 1/255: skipped
+    const float test_T = T * (1.0f - a);
+    const bool stop = test_T < 0.0001f;  // false whenever a == 0 and T >= 1e-4; true for every finished pixel
+    a = stop ? 0.0f : a;
+    const float w = a * T;
+    C[0] = __builtin_fmaf(f.x, w, C[0]);
+    C[1] = __builtin_fmaf(f.y, w, C[1]);
+    C[2] = __builtin_fmaf(f.z, w, C[2]);
+    T = stop ? -fabsf(T) : test_T;
+    const bool blended = a != 0.0f;
+    last_lo = blended ? lo : last_lo;
+    return blended;
+}
+
 template <int kPPL, int kWaves, bool kSel = false>
 __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const PixelSetT<kPPL>& px, float ox, float oy,
                                                           float st, const uint32_t* __restrict__ point_list,
@@ -324,7 +353,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
     bool done[kPPL];
 #pragma unroll
     for (int k = 0; k < kPPL; k++) {
-        st_.T[k] = 1.0f;
+        st_.T[k] = (kSel && kPPL == 1 && !px.inside[k]) ? -1.0f : 1.0f;  // (kSel: finished = negative T)
         st_.C[k][0] = st_.C[k][1] = st_.C[k][2] = 0.f;
         st_.last[k] = 0;
         done[k] = !px.inside[k];
@@ -351,7 +380,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
             // one b32 (LDS cycles per wave-read: b128 4, b96 8, b64 / b32 2)
             s_a[tid] = make_float4(xy.x, xy.y, features[3 * id], features[3 * id + 1]);
             s_co[tid] = splat_coef(co);
-            s_b[tid] = features[3 * id + 2];
+            s_b[tid * (kSel ? 4 : 1)] = features[3 * id + 2];  // (kSel: at a 16-B stride, one address for all reads)
             gm = cull ? splat_group_mask(xy, co, ox, oy, st) : 0xfu;
         }
         publish_group_masks<kWaves>(gm, s_bal);
@@ -371,32 +400,42 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 todo |= mk[k];
             }
             if constexpr (kPPL == 1 && kSel) {
-                // select form (blend_one_sel), two Gaussians per iteration; the
-                // wave's early exit is tested once per 64 batch slots
-                float cap = done[0] ? 0.0f : 0.99f;
+                // select form (blend_one_sel2), two Gaussians per iteration; the
+                // wave's early exit is tested once per 64 batch slots.  A
+                // finished pixel carries a negative T (outside pixels start at
+                // -1), which every later stop test rejects.
                 uint64_t hits = 0;
+                uint32_t last_lo = ~0u;
+                const char* sa = reinterpret_cast<const char*>(s_a);
+                const char* sco = reinterpret_cast<const char*>(s_co);
+                const char* sb = reinterpret_cast<const char*>(s_b);
                 while (todo) {
                     const uint32_t bA = (uint32_t)__builtin_ctzll(todo);
                     todo &= todo - 1;
                     const bool two = todo != 0;  // wave-uniform
                     const uint32_t bB = two ? (uint32_t)__builtin_ctzll(todo) : bA;
                     if (two) todo &= todo - 1;
-                    const uint32_t jA = c * 64 + bA, jB = c * 64 + bB;
-                    const float4 sA = s_a[jA], sB = s_a[jB];
-                    const float4 coA = s_co[jA], coB = s_co[jB];
-                    const float bAc = s_b[jA], bBc = s_b[jB];
-                    const bool hA = blend_one_sel(make_float2(sA.x, sA.y), coA, make_float4(sA.z, sA.w, bAc, 0.f),
-                                                  px.x, px.y[0], b0 + jA + 1, st_.T[0], st_.C[0], st_.last[0], cap);
+                    const uint32_t loA = (c * 64 + bA) * 16, loB = (c * 64 + bB) * 16;
+                    const float4 sA = *reinterpret_cast<const float4*>(sa + loA);
+                    const float4 sB = *reinterpret_cast<const float4*>(sa + loB);
+                    const float4 coA = *reinterpret_cast<const float4*>(sco + loA);
+                    const float4 coB = *reinterpret_cast<const float4*>(sco + loB);
+                    const float bAc = *reinterpret_cast<const float*>(sb + loA);
+                    const float bBc = *reinterpret_cast<const float*>(sb + loB);
+                    const bool hA = blend_one_sel2(make_float2(sA.x, sA.y), coA, make_float4(sA.z, sA.w, bAc, 0.f),
+                                                   px.x, px.y[0], loA, st_.T[0], st_.C[0], last_lo);
                     if (kRec) hits |= __ballot(hA) != 0ull ? 1ull << bA : 0ull;
                     if (two) {
-                        const bool hB = blend_one_sel(make_float2(sB.x, sB.y), coB, make_float4(sB.z, sB.w, bBc, 0.f),
-                                                      px.x, px.y[0], b0 + jB + 1, st_.T[0], st_.C[0], st_.last[0],
-                                                      cap);
+                        const bool hB = blend_one_sel2(make_float2(sB.x, sB.y), coB,
+                                                       make_float4(sB.z, sB.w, bBc, 0.f), px.x, px.y[0], loB,
+                                                       st_.T[0], st_.C[0], last_lo);
                         if (kRec) hits |= __ballot(hB) != 0ull ? 1ull << bB : 0ull;
                     }
                 }
+                // lo = 16 j, contributor = b0 + j + 1
+                if (last_lo != ~0u) st_.last[0] = b0 + (last_lo >> 4) + 1;
                 if (rec && (tid & 63) == 0) s_hit[c * kWaves + wave] = hits;
-                done[0] = cap == 0.0f;
+                done[0] = st_.T[0] < 0.0f;
                 if (__ballot(!done[0]) == 0ull) wave_alive = false;
                 continue;
             }
@@ -502,6 +541,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
         __syncthreads();
         if (b0 > 0) flush_codes(b0 - kB);
     }
+    if constexpr (kPPL == 1 && kSel) st_.T[0] = fabsf(st_.T[0]);  // (finished pixels: -T_final)
     return st_;
 }
 

@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
         zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     __shared__ float4 s_a[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
-    __shared__ float s_b[64 * kWaves];
+    __shared__ __attribute__((aligned(16))) float s_b[64 * kWaves * (kSel ? 4 : 1)];  // (kSel: 16-B stride)
     __shared__ uint64_t s_bal[4 * kWaves];
     __shared__ uint64_t s_hit[kWaves * kWaves];
     __shared__ uint32_t s_max;
