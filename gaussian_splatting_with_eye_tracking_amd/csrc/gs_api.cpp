@@ -1088,6 +1088,10 @@ int gs_set_tuning(const char* key, int value) {
         set_amr_deep(value);
         return 0;
     }
+    if (std::strcmp(key, "amr_sel") == 0) {
+        set_amr_sel(value);
+        return 0;
+    }
     if (std::strcmp(key, "amr_fold") == 0) {
         set_amr_fold(value);
         return 0;

@@ -645,7 +645,7 @@ void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningVi
 // given colors_precomp): colours from it through point_list instead of the
 // step-0 records.
 // kPer: entries each lane stages per batch (a group stages 16 kPer)
-template <int kRounds, int kPer, int kFold = 0>
+template <int kRounds, int kPer, int kFold = 0, bool kSelF = false>
 __global__ void __launch_bounds__(64) amr_region_render_kernel(
     int W, int H, int tgx, int T, const uint32_t* __restrict__ order, const uint32_t* __restrict__ ranges,
     const uint32_t* __restrict__ lists, const uint32_t* __restrict__ region_count,
@@ -770,6 +770,13 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     auto load_rec = [&](const uint32_t (&pos)[kPer], float4 (&a)[kPer], float4 (&bb)[kPer], float (&c)[kPer]) {
 #pragma unroll
         for (int u = 0; u < kPer; u++) {
+            if (kSelF && pos[u] == 0xffffffffu) {
+                // kSelF: past the group's list an all-zero record (p = 0,
+                // alpha = 0 * exp2(0) = 0: rejected by the alpha test), so the
+                // fold needs no per-entry bound test
+                a[u] = bb[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                c[u] = 0.f;
+            }
             if (pos[u] != 0xffffffffu) {
                 a[u] = rec_a[beg + pos[u]];
                 bb[u] = rec_b[beg + pos[u]];
@@ -799,7 +806,7 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
             const bool in = active[k] && x < (uint32_t)W && y < (uint32_t)H;
             pid[k] = in ? (uint32_t)W * y + x : 0u;
             done[k] = !in;
-            T_[k] = 1.0f;
+            T_[k] = (kSelF && !in) ? -1.0f : 1.0f;  // (kSelF: a finished pixel carries a negative T)
             C[k][0] = C[k][1] = C[k][2] = 0.f;
             last[k] = 0;
         }
@@ -817,7 +824,7 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
         for (uint32_t b0 = 0; b0 < cmax; b0 += kRgBatch) {
             bool any = false;
 #pragma unroll
-            for (int k = 0; k < kSlots; k++) any |= !done[k] && b0 < cnt;
+            for (int k = 0; k < kSlots; k++) any |= (kSelF ? T_[k] > 0.0f : !done[k]) && b0 < cnt;
             if (__ballot(any) == 0ull) break;  // every pixel saturated or its list exhausted
             __syncthreads();                     // single-wave workgroup: LDS fence only
 #pragma unroll
@@ -825,7 +832,7 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
                 s_a[h][l16 + 16 * u] = ra[u];
                 s_b[h][l16 + 16 * u] = rb[u];
                 s_c[h][l16 + 16 * u] = rc[u];
-                s_pos[h][l16 + 16 * u] = pos[u];
+                s_pos[h][l16 + 16 * u] = kSelF ? pos[u] + 1 : pos[u];  // (kSelF: the contributor index)
             }
             __syncthreads();
             // the next batch's records and the one after's positions, in flight
@@ -837,7 +844,70 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
             // entries of this batch: [0, m) for the group, [0, mw) for the wave
             const int m = (int)min((uint32_t)kRgBatch, cnt > b0 ? cnt - b0 : 0u);
             const int mw = (int)min((uint32_t)kRgBatch, cmax - b0);
-            if constexpr (kFold > 0) {
+            if constexpr (kFold > 0 && kSelF) {
+                // The fold of blend_one_sel2 (gs_blend.cuh): phase 1 turns each
+                // staged entry's alpha into its select-form value (0 when the
+                // reference skips the pair: power > 0 or alpha < 1/255; entries
+                // past the group's list are zero records), phase 2 folds them
+                // front to back with the finished state in T's sign -- no
+                // per-entry exec masks or bound tests, the same bits for every
+                // pixel still blending.
+#pragma unroll
+                for (int j0 = 0; j0 < kRgBatch; j0 += kFold) {
+                    float al[kFold][kSlots];
+                    float fr[kFold], fg[kFold], fb[kFold];
+                    uint32_t fp[kFold];
+#pragma unroll
+                    for (int e4 = 0; e4 < kFold; e4 += 4) {
+                        const float4 b4 = *reinterpret_cast<const float4*>(&s_c[h][j0 + e4]);
+                        const uint4 p4 = *reinterpret_cast<const uint4*>(&s_pos[h][j0 + e4]);
+                        fb[e4] = b4.x; fb[e4 + 1] = b4.y; fb[e4 + 2] = b4.z; fb[e4 + 3] = b4.w;
+                        fp[e4] = p4.x; fp[e4 + 1] = p4.y; fp[e4 + 2] = p4.z; fp[e4 + 3] = p4.w;
+                    }
+#pragma unroll
+                    for (int e = 0; e < kFold; e++) {
+                        const int j = j0 + e;
+                        const float4 a = s_a[h][j];
+                        const float4 co = s_b[h][j];
+                        fr[e] = a.z;
+                        fg[e] = a.w;
+#pragma unroll
+                        for (int k = 0; k < kSlots; k++) {
+                            if (kRounds > 1 && !active[k]) continue;  // wave-uniform (always on for one round)
+                            const float pw = splat_p2(a.x - pxx[k], a.y - pxy[k], co);
+                            float av = fminf(0.99f, co.w * splat_exp(pw));
+                            av = (pw > 0.0f) ? 0.0f : av;
+                            av = (av < 1.0f / 255.0f) ? 0.0f : av;
+                            al[e][k] = av;
+                        }
+                    }
+                    bool alive = false;
+#pragma unroll
+                    for (int e = 0; e < kFold; e++) {
+#pragma unroll
+                        for (int k = 0; k < kSlots; k++) {
+                            if (kRounds > 1 && !active[k]) continue;
+                            float av = al[e][k];
+                            const float test_T = T_[k] * (1.0f - av);
+                            const bool stop = test_T < 0.0001f;  // every finished pixel too (T < 0)
+                            av = stop ? 0.0f : av;
+                            const float w = av * T_[k];
+                            C[k][0] = __builtin_fmaf(fr[e], w, C[k][0]);
+                            C[k][1] = __builtin_fmaf(fg[e], w, C[k][1]);
+                            C[k][2] = __builtin_fmaf(fb[e], w, C[k][2]);
+                            T_[k] = stop ? -fabsf(T_[k]) : test_T;
+                            // (as a bit-field insert under an all-ones mask: written
+                            // as a select, the compiler sinks the move into an
+                            // exec-masked branch, 3 SALU + 1 VALU per entry)
+                            const uint32_t lm = av != 0.0f ? ~0u : 0u;
+                            last[k] = (fp[e] & lm) | (last[k] & ~lm);
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < kSlots; k++) alive |= T_[k] > 0.0f && j0 + kFold < m;
+                    if (j0 + kFold < kRgBatch && __ballot(alive) == 0ull) break;
+                }
+            } else if constexpr (kFold > 0) {
                 // Two phases per sub-batch of kFold entries.  The alpha of
                 // every staged entry does not depend on T, so phase 1
                 // evaluates them as independent chains (full issue rate even
@@ -982,6 +1052,7 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
             const uint32_t x = (uint32_t)pxx[k], y = (uint32_t)pxy[k];
             if (!active[k] || x >= (uint32_t)W || y >= (uint32_t)H) continue;
             const uint32_t pp = pid[k];
+            if (kSelF) T_[k] = fabsf(T_[k]);
             final_T[pp] = T_[k];
             n_contrib[pp] = last[k];
             const uint32_t lx = x - qx0, ly = y - qy0;
@@ -1009,6 +1080,9 @@ void set_amr_batch(int v) { g_amr_batch = v == 2 ? 2 : 1; }
 int g_amr_deep = 0;
 void set_amr_deep(int v) { g_amr_deep = v; }
 int g_amr_fold = 0x1e;
+// the progressive steps' fold in the select form (amr_region_render_kernel kSelF)
+int g_amr_sel = 1;
+void set_amr_sel(int v) { g_amr_sel = v; }
 int g_amr_fold_n = 8;
 void set_amr_fold(int v) {
     g_amr_fold = v & 0x1f;
@@ -1027,8 +1101,8 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
         const int T = tgx * tgy;
         const float* ov = (foveaStep > 0 && features != g.rgb) ? features : nullptr;
         const int nb = 32 * ((T + 7) / 8);  // b = 8 (4 (p / 8) + q) + p % 8
-#define GS_AMR_REGION(R, PER, FOLD)                                                                               \
-        hipLaunchKernelGGL((amr_region_render_kernel<R, PER, FOLD>), dim3(nb), dim3(64), 0, s, W, H, tgx, T,            \
+#define GS_AMR_REGION(R, PER, FOLD, ...)                                                                          \
+        hipLaunchKernelGGL((amr_region_render_kernel<R, PER, FOLD, ##__VA_ARGS__>), dim3(nb), dim3(64), 0, s, W, H, tgx, T,            \
                            img.tile_order,                                                                          \
                            img.ranges, ab.region_lists, img.region_count, levels, levels_last, ab.rec_a, ab.rec_b, \
                            ab.rec_c, b.point_list, ov, img.accum_alpha, img.n_contrib, bg, out_color, foveaStep,   \
@@ -1036,13 +1110,15 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
                            fused ? zero_radii : nullptr)
         if (foveaStep > 0) {
             const bool fold = (g_amr_fold >> foveaStep) & 1;
-            if (fold && ((g_amr_deep >> foveaStep) & 1)) GS_AMR_REGION(1, 2, 8);
+            if (fold && g_amr_sel) GS_AMR_REGION(1, 1, 8, true);
+            else if (fold && ((g_amr_deep >> foveaStep) & 1)) GS_AMR_REGION(1, 2, 8);
             else if (fold && g_amr_fold_n == 16) GS_AMR_REGION(1, 1, 16);
             else if (fold) GS_AMR_REGION(1, 1, 8);
             else if (g_amr_batch == 2) GS_AMR_REGION(1, 2, 0);
             else GS_AMR_REGION(1, 1, 0);
         } else {
-            if (g_amr_fold & 1) GS_AMR_REGION(4, 1, 4);
+            if ((g_amr_fold & 1) && g_amr_sel) GS_AMR_REGION(4, 1, 4, true);
+            else if (g_amr_fold & 1) GS_AMR_REGION(4, 1, 4);
             else if (g_amr_batch == 2) GS_AMR_REGION(4, 2, 0);
             else GS_AMR_REGION(4, 1, 0);
         }

@@ -1,6 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_parity_configs.py tests/test_gpu_cull.py -x -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/parf.log 2>&1 && \
-timeout -k 10 300 python tools/ab_tuning.py --key fwd_variant --values 3 5 --stage render > gpurun_out/abf_cfg2.log 2>&1 && \
-timeout -k 10 300 python tools/ab_tuning.py --key fwd_variant --values 3 5 --stage render --P 6100000 --W 1600 --H 1063 --rounds 4 > gpurun_out/abf_cfg4.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread -k "amr or AMR or config3 or fovea or once" > gpurun_out/para.log 2>&1 && \
+timeout -k 10 300 python tools/ab_tuning.py --key amr_sel --values 0 1 --stage amr_render --amr-once > gpurun_out/aba_once.log 2>&1
 echo rc=$?
