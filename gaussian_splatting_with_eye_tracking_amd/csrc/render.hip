@@ -1110,7 +1110,9 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
                            fused ? zero_radii : nullptr)
         if (foveaStep > 0) {
             const bool fold = (g_amr_fold >> foveaStep) & 1;
-            if (fold && g_amr_sel) GS_AMR_REGION(1, 1, 8, true);
+            if (fold && g_amr_sel && ((g_amr_deep >> foveaStep) & 1)) GS_AMR_REGION(1, 2, 8, true);
+            else if (fold && g_amr_sel && g_amr_fold_n == 16) GS_AMR_REGION(1, 1, 16, true);
+            else if (fold && g_amr_sel) GS_AMR_REGION(1, 1, 8, true);
             else if (fold && ((g_amr_deep >> foveaStep) & 1)) GS_AMR_REGION(1, 2, 8);
             else if (fold && g_amr_fold_n == 16) GS_AMR_REGION(1, 1, 16);
             else if (fold) GS_AMR_REGION(1, 1, 8);

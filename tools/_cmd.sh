@@ -1,5 +1,5 @@
 set -o pipefail
+export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread -k "amr or AMR or config3 or fovea or once" > gpurun_out/para.log 2>&1 && \
-timeout -k 10 300 python tools/ab_tuning.py --key amr_sel --values 0 1 --stage amr_render --amr-once > gpurun_out/aba_once.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/prof3t -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-sub --no-ext > gpurun_out/prof3t.log 2>&1
 echo rc=$?
