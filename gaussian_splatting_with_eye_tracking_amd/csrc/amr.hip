@@ -75,7 +75,17 @@ __device__ uint32_t block_select_kth(const uint32_t* __restrict__ ranges, int n,
 __global__ void __launch_bounds__(kLvlThreads) amr_levels_kernel(int T, const uint32_t* __restrict__ ranges,
                                                                  uint32_t* __restrict__ n_inter,
                                                                  uint32_t* __restrict__ pv,
-                                                                 uint32_t* __restrict__ levels) {
+                                                                 uint32_t* __restrict__ levels,
+                                                                 float4* __restrict__ zero4, int zero_n4) {
+    // blocks >= 1 (if any): foveaStep 0's zero image, grid-stride float4
+    // stores on the other CUs while block 0 -- one CU -- computes the levels
+    // (one launch instead of the levels kernel and a separate fill)
+    if (blockIdx.x > 0) {
+        for (int i = (int)((blockIdx.x - 1) * kLvlThreads + threadIdx.x); i < zero_n4;
+             i += (int)((gridDim.x - 1) * kLvlThreads))
+            zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
     __shared__ uint32_t hist[256];
     __shared__ uint32_t word[2];
     __shared__ uint32_t s_pv[3];
@@ -123,10 +133,14 @@ __global__ void __launch_bounds__(kLvlThreads) amr_levels_kernel(int T, const ui
     }
 }
 
-void launch_amr_levels(int T, const ImageView& img, hipStream_t s) {
+void launch_amr_levels(int T, const ImageView& img, hipStream_t s, float* zero_image, size_t zero_floats) {
     if (T == 0) return;
-    hipLaunchKernelGGL(amr_levels_kernel, dim3(1), dim3(kLvlThreads), 0, s, T, img.ranges, img.tile_count, img.pv,
-                       img.levels);
+    const int n4 = (zero_image && zero_floats % 4 == 0 && zero_floats / 4 <= (size_t)INT32_MAX) ? (int)(zero_floats / 4) : 0;
+    if (zero_image && n4 == 0 && zero_floats > 0)  // (an unaligned size: the plain fill)
+        (void)hipMemsetAsync(zero_image, 0, sizeof(float) * zero_floats, s);
+    const int zb = n4 > 0 ? std::min(512, (n4 + kLvlThreads * 8 - 1) / (kLvlThreads * 8)) : 0;
+    hipLaunchKernelGGL(amr_levels_kernel, dim3(1 + zb), dim3(kLvlThreads), 0, s, T, img.ranges, img.tile_count, img.pv,
+                       img.levels, reinterpret_cast<float4*>(zero_image), n4);
 }
 
 // amr/cr/rasterizer_impl.cu:208-243 (setFoveaAMRLevelsKernel)

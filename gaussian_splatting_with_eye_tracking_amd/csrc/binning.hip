@@ -98,8 +98,17 @@ __device__ __forceinline__ void slot_cursors(uint32_t* __restrict__ count, uint3
 // mapped, coherent host memory (vector stores over the fabric) by the scan:
 // the forward's read-back then needs no copy kernel, only an event after the
 // scan.
-__device__ __forceinline__ void mirror_header(uint32_t* m, uint32_t K, uint32_t err, uint32_t maxc, uint32_t nlarge) {
+// token != 0 (the polled read-back): after the words, a system-scope fence and
+// the call's token in word 4 -- the host spins on the token instead of
+// waiting for an event after the scan, so the stream carries no marker packet
+// between the scan and the work behind it.
+__device__ __forceinline__ void mirror_header(uint32_t* m, uint32_t K, uint32_t err, uint32_t maxc, uint32_t nlarge,
+                                              uint32_t token) {
     *reinterpret_cast<uint4*>(m) = make_uint4(K, err, maxc, nlarge);  // kHdrNumRendered, kHdrError, kHdrMaxTileCount, kHdrNumLargeTiles
+    if (token) {
+        __threadfence_system();
+        __hip_atomic_store(m + 4, token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 
@@ -111,6 +120,7 @@ struct BandScan {
     uint32_t* start;  // nullptr: direct duplicate
     uint32_t* cursor;
     uint32_t gx;
+    uint32_t mirror_token;  // the polled header read-back's token (0: none; see mirror_header)
     __device__ __forceinline__ void emit(int i, uint32_t ex) const {
         if (!start || (uint32_t)i % gx) return;
         const uint32_t row = (uint32_t)i / gx;
@@ -187,7 +197,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, uint32_t
         hdr[kHdrMaxTileCount] = m;
         hdr[kHdrNumLargeTiles] = nlarge;
         hdr[kHdrT] = (uint32_t)T;
-        if (hdr_mirror) mirror_header(hdr_mirror, total, hdr[kHdrError], m, nlarge);
+        if (hdr_mirror) mirror_header(hdr_mirror, total, hdr[kHdrError], m, nlarge, band.mirror_token);
     }
 }
 
@@ -268,7 +278,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, u
         hdr[kHdrMaxTileCount] = m;
         hdr[kHdrNumLargeTiles] = nlarge;
         hdr[kHdrT] = (uint32_t)T;
-        if (hdr_mirror) mirror_header(hdr_mirror, run, hdr[kHdrError], m, nlarge);
+        if (hdr_mirror) mirror_header(hdr_mirror, run, hdr[kHdrError], m, nlarge, band.mirror_token);
     }
 }
 
@@ -276,8 +286,8 @@ int g_scan_slices = 1;  // set_tuning("scan_slices"): 0 = the thread-contiguous 
 void set_scan_slices(int v) { g_scan_slices = v; }
 
 void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror, int nslots,
-                      int gx, bool banded) {
-    BandScan band{nullptr, nullptr, (uint32_t)std::max(gx, 1)};
+                      int gx, bool banded, uint32_t mirror_token) {
+    BandScan band{nullptr, nullptr, (uint32_t)std::max(gx, 1), mirror_token};
     if (banded) {
         band.start = img.band_start;
         band.cursor = img.band_cursor;

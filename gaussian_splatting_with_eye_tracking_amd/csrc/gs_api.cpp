@@ -16,6 +16,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -123,12 +124,15 @@ uint32_t* pinned_words() {
 
 // Mapped, coherent host words the tile scan writes the header into (no copy
 // kernel): thread-local like pinned_words; (host pointer, device pointer).
-int g_hdr_mirror = -1;  // set_tuning("hdr_mirror"); -1: GSAMD_HDR_MIRROR (default 0)
+// 0: copy + event; 1: scan-stored words + event; 2 (default): scan-stored
+// words + token, polled by the host (config 3 frame 0.575 -> 0.536 ms, config 2
+// 0.971 -> 0.965 ms per step, profiles/r03m_ab_hdr_mirror.log)
+int g_hdr_mirror = -1;  // set_tuning("hdr_mirror"); -1: GSAMD_HDR_MIRROR (default 2)
 
 bool hdr_mirror_on() {
     if (g_hdr_mirror < 0) {
         const char* e = std::getenv("GSAMD_HDR_MIRROR");
-        g_hdr_mirror = e ? std::atoi(e) : 0;
+        g_hdr_mirror = e ? std::atoi(e) : 2;
     }
     return g_hdr_mirror != 0;
 }
@@ -186,9 +190,18 @@ SideStream& side_stream() {
 // more than the ~6 us dispatch gap they remove)
 int g_side_copy = -1;  // set_tuning("side_copy"); -1: GSAMD_SIDE_COPY (default 0)
 
+// hdr_mirror 2: the scan also stores a per-call token after the words
+// (system-scope release) and the host spins on it -- no event or copy in the
+// stream between the scan and the work enqueued behind it.
+thread_local uint32_t t_mirror_token = 0;
+uint32_t next_mirror_token() {
+    t_mirror_token = t_mirror_token + 1u ? t_mirror_token + 1u : 1u;
+    return t_mirror_token;
+}
+
 void begin_header_read(const uint32_t* hdr_dev, hipStream_t s, const uint32_t* mirror = nullptr) {
     if (mirror) {  // the scan stores the words into host memory itself
-        GS_HIP(hipEventRecord(side_stream().done, s));
+        if (g_hdr_mirror != 2) GS_HIP(hipEventRecord(side_stream().done, s));
         return;
     }
     if (g_side_copy < 0) {
@@ -207,7 +220,23 @@ void begin_header_read(const uint32_t* hdr_dev, hipStream_t s, const uint32_t* m
     GS_HIP(hipEventRecord(ss.done, ss.s));
 }
 
-void finish_header_read(uint32_t out[4], const uint32_t* mirror = nullptr) {
+void finish_header_read(uint32_t out[4], const uint32_t* mirror = nullptr, hipStream_t s = nullptr) {
+    if (mirror && g_hdr_mirror == 2) {
+        const volatile uint32_t* m = mirror;
+        const auto t0 = std::chrono::steady_clock::now();
+        uint64_t spins = 0;
+        while (__atomic_load_n(const_cast<const uint32_t*>(mirror) + 4, __ATOMIC_ACQUIRE) != t_mirror_token) {
+            // a stream that faulted or was never run: wait for it, then re-check once
+            if ((++spins & 0xffff) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+                GS_HIP(hipStreamSynchronize(s));
+                if (__atomic_load_n(const_cast<const uint32_t*>(mirror) + 4, __ATOMIC_ACQUIRE) != t_mirror_token)
+                    throw GsError("header read-back: the tile scan did not publish its token");
+                break;
+            }
+        }
+        for (int i = 0; i < 4; i++) out[i] = m[i];
+        return;
+    }
     GS_HIP(hipEventSynchronize(side_stream().done));
     if (mirror) {
         const volatile uint32_t* m = mirror;
@@ -408,7 +437,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     stage_check(debug, s, "count_tiles");
     const std::pair<uint32_t*, uint32_t*> mirror =
         (r.T > 0 && hdr_mirror_on()) ? mirror_words() : std::pair<uint32_t*, uint32_t*>{nullptr, nullptr};
-    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second, bin_slots_for(in.P, gx, gy, tile), gx, dup_banded(gx, gy, tile)); }
+    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second, bin_slots_for(in.P, gx, gy, tile), gx, dup_banded(gx, gy, tile), (mirror.second && g_hdr_mirror == 2) ? next_mirror_token() : 0u); }
     stage_check(debug, s, "tile_scan");
     uint32_t hdr[4];
     const bool amr = tile == 32;  // the AMR layout appends records and region lists
@@ -425,17 +454,17 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     if (before_k) {
         begin_header_read(r.g.hdr, s, mirror.first);
         before_k(r);
-        finish_header_read(hdr, mirror.first);
+        finish_header_read(hdr, mirror.first, s);
     } else if (cap > 0) {
         begin_header_read(r.g.hdr, s, mirror.first);
         char* sbase = call_resize(binning, carve_binning(nullptr, cap, nullptr), "binning");
         carve_binning(sbase, cap, &r.b);
         { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, (uint32_t)cap, r.g.hdr, (uint32_t)cap); }
-        finish_header_read(hdr, mirror.first);
+        finish_header_read(hdr, mirror.first, s);
         dup_done = hdr[kHdrNumRendered] <= cap;
     } else if (mirror.first) {
         begin_header_read(r.g.hdr, s, mirror.first);
-        finish_header_read(hdr, mirror.first);
+        finish_header_read(hdr, mirror.first, s);
     } else {
         read_header(r.g.hdr, hdr, s);
     }
@@ -899,11 +928,13 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
         // the counts), the step's level schedule, the tile order (by list
         // length) and step 0's zero image.
         auto before_k = [&](Binned& r) {
-            { StageTimer _t(kAmrLevels, s); launch_amr_levels(r.T, r.img, s); }
+            // (variant 4 writes the zeros of the pixels it does not render;
+            // otherwise, and at foveaStep 0, the levels launch zeroes the image)
+            const bool zero_img = foveaStep == 0 || g_amr_variant != 4;
+            { StageTimer _t(kAmrLevels, s);
+              launch_amr_levels(r.T, r.img, s, zero_img ? out_color : nullptr, zero_img ? 3 * (size_t)W * H : 0); }
             stage_check(dbg, s, "amr_levels");
             if (g_amr_variant >= 3) launch_order_tiles(r.T, r.img, false, s);
-            if (foveaStep == 0 || g_amr_variant != 4)  // (variant 4 writes the zeros of the pixels it does not render)
-                GS_HIP(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)W * H, s));
             if (foveaStep != 0) launch_fovea_levels(foveaStep, r.T, r.img, s);
         };
         Binned r = preprocess_and_bin(in, geometry, binning, image, radii, tile, dbg, s, before_k);

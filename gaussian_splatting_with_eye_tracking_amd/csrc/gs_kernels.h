@@ -49,7 +49,7 @@ void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, c
 // hdr_mirror: device address of 16 mapped host bytes that receive header
 // words 0..3 (K, error, max tile count, large tiles) when the scan finishes.
 void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror, int nslots,
-                      int gx, bool banded);
+                      int gx, bool banded, uint32_t mirror_token = 0);
 // spec_hdr: a speculative launch into a buffer of spec_cap keys, enqueued
 // before the host knows K; it does nothing when the header's K > spec_cap.
 // n_keys: the instance capacity the binning buffer was carved for (K, or the
@@ -205,7 +205,8 @@ void launch_eye_preprocess(const uint8_t* gray, int H, int W, const uint8_t* gam
                            int limit, float* luts, float* out, hipStream_t s);
 
 // AMR (amr/cr/rasterizer_impl.cu:181-243, amr/cr/forward.cu:261-648).
-void launch_amr_levels(int T, const ImageView& img, hipStream_t s);
+// zero_image (optional): foveaStep 0's zero image, written by the same launch
+void launch_amr_levels(int T, const ImageView& img, hipStream_t s, float* zero_image = nullptr, size_t zero_floats = 0);
 // The 16x16 quadrant sub-lists of the sorted 32-px tile lists (render.hip).
 void launch_amr_quad_lists(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g, int K,
                            hipStream_t s);
