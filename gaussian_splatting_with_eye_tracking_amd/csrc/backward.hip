@@ -657,66 +657,24 @@ struct ShRowPtr {
 template <typename SH>
 __device__ __forceinline__ void sh_backward_terms(int deg, const float* campos, float mx, float my, float mz,
                                                   const SH& s, uint8_t cb, const float* acc,
-                                                  float (&dsh_c)[16], float (&dRGB)[3], float (&dmean)[3]) {
+                                                  float (&dsh_c)[16], float (&dRGB)[3], float (&dmean)[3],
+                                                  const float* drgb9 = nullptr) {
     const float dox = mx - campos[0], doy = my - campos[1], doz = mz - campos[2];
     const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
     const float x = dox / len, y = doy / len, z = doz / len;
 #pragma unroll
     for (int c = 0; c < 3; c++) dRGB[c] = acc[c] * (((cb >> c) & 1) ? 0.0f : 1.0f);
-    float dx3[3] = {0, 0, 0}, dy3[3] = {0, 0, 0}, dz3[3] = {0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 16; k++) dsh_c[k] = 0.f;
-    dsh_c[0] = SH_C0;
-    if (deg > 0) {
-        dsh_c[1] = -SH_C1 * y;
-        dsh_c[2] = SH_C1 * z;
-        dsh_c[3] = -SH_C1 * x;
+    float dx3[3], dy3[3], dz3[3];
+    sh_basis(deg, x, y, z, dsh_c);
+    if (drgb9) {  // the forward's derivatives (sh_ddir on the same operands: the same bits)
 #pragma unroll
         for (int c = 0; c < 3; c++) {
-            dx3[c] = -SH_C1 * s[3][c];
-            dy3[c] = -SH_C1 * s[1][c];
-            dz3[c] = SH_C1 * s[2][c];
+            dx3[c] = drgb9[c];
+            dy3[c] = drgb9[3 + c];
+            dz3[c] = drgb9[6 + c];
         }
-        if (deg > 1) {
-            const float xx = x * x, yy = y * y, zz = z * z;
-            const float xy = x * y, yz = y * z, xz = x * z;
-            dsh_c[4] = SH_C2_0 * xy;
-            dsh_c[5] = SH_C2_1 * yz;
-            dsh_c[6] = SH_C2_2 * (2.f * zz - xx - yy);
-            dsh_c[7] = SH_C2_3 * xz;
-            dsh_c[8] = SH_C2_4 * (xx - yy);
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                dx3[c] += SH_C2_0 * y * s[4][c] + SH_C2_2 * 2.f * -x * s[6][c] + SH_C2_3 * z * s[7][c] +
-                          SH_C2_4 * 2.f * x * s[8][c];
-                dy3[c] += SH_C2_0 * x * s[4][c] + SH_C2_1 * z * s[5][c] + SH_C2_2 * 2.f * -y * s[6][c] +
-                          SH_C2_4 * 2.f * -y * s[8][c];
-                dz3[c] += SH_C2_1 * y * s[5][c] + SH_C2_2 * 2.f * 2.f * z * s[6][c] + SH_C2_3 * x * s[7][c];
-            }
-            if (deg > 2) {
-                dsh_c[9] = SH_C3_0 * y * (3.f * xx - yy);
-                dsh_c[10] = SH_C3_1 * xy * z;
-                dsh_c[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
-                dsh_c[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                dsh_c[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
-                dsh_c[14] = SH_C3_5 * z * (xx - yy);
-                dsh_c[15] = SH_C3_6 * x * (xx - 3.f * yy);
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    dx3[c] += (SH_C3_0 * s[9][c] * 3.f * 2.f * xy + SH_C3_1 * s[10][c] * yz +
-                               SH_C3_2 * s[11][c] * -2.f * xy + SH_C3_3 * s[12][c] * -3.f * 2.f * xz +
-                               SH_C3_4 * s[13][c] * (-3.f * xx + 4.f * zz - yy) + SH_C3_5 * s[14][c] * 2.f * xz +
-                               SH_C3_6 * s[15][c] * 3.f * (xx - yy));
-                    dy3[c] += (SH_C3_0 * s[9][c] * 3.f * (xx - yy) + SH_C3_1 * s[10][c] * xz +
-                               SH_C3_2 * s[11][c] * (-3.f * yy + 4.f * zz - xx) +
-                               SH_C3_3 * s[12][c] * -3.f * 2.f * yz + SH_C3_4 * s[13][c] * -2.f * xy +
-                               SH_C3_5 * s[14][c] * -2.f * yz + SH_C3_6 * s[15][c] * -3.f * 2.f * xy);
-                    dz3[c] += (SH_C3_1 * s[10][c] * xy + SH_C3_2 * s[11][c] * 4.f * 2.f * yz +
-                               SH_C3_3 * s[12][c] * 3.f * (2.f * zz - xx - yy) + SH_C3_4 * s[13][c] * 4.f * 2.f * xz +
-                               SH_C3_5 * s[14][c] * (xx - yy));
-                }
-            }
-        }
+    } else {
+        sh_ddir(deg, s, x, y, z, dx3, dy3, dz3);
     }
     const float ddx = dot3(dx3[0], dx3[1], dx3[2], dRGB[0], dRGB[1], dRGB[2]);
     const float ddy = dot3(dy3[0], dy3[1], dy3[2], dRGB[0], dRGB[1], dRGB[2]);
@@ -734,11 +692,11 @@ __device__ __forceinline__ void sh_backward_terms(int deg, const float* campos, 
 template <bool kSH16>
 __device__ __forceinline__ void sh_backward(const BackwardGaussArgs& a, int idx, float mx, float my, float mz,
                                             const float (&s)[16][3], uint8_t cb, const float* acc,
-                                            float (&dmean)[3], float* lrow = nullptr) {
+                                            float (&dmean)[3], float* lrow = nullptr, const float* drgb9 = nullptr) {
     const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
     float* dsh = a.dL_dsh + (size_t)idx * a.M * 3;
     float dsh_c[16], dRGB[3];
-    sh_backward_terms(a.D, a.campos, mx, my, mz, s, cb, acc, dsh_c, dRGB, dmean);
+    sh_backward_terms(a.D, a.campos, mx, my, mz, s, cb, acc, dsh_c, dRGB, dmean, drgb9);
     if (kSH16) {
         float o[48];
 #pragma unroll
@@ -977,8 +935,16 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     }
     float s[16][3];
     uint8_t cb = 0;
+    // the forward's d(rgb)/d(dir) when it stored them: no SH coefficients read
+    const bool use_drgb = kHasSH && a.drgb && a.hdr[kHdrDrgb] == 1u;  // uniform
+    float d9[9];
     if (kHasSH) {
-        load_sh_rows<kSH16>(a, idx, s, lrow);
+        if (use_drgb) {
+#pragma unroll
+            for (int i = 0; i < 9; i++) d9[i] = a.drgb[(size_t)i * a.P + idx];
+        } else {
+            load_sh_rows<kSH16>(a, idx, s, lrow);
+        }
         cb = clamped_bits[idx];
     }
     const Mat4 V = load_mat4(a.viewmatrix);
@@ -998,7 +964,8 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     proj_backward(mx, my, mz, Pm, acc[3], acc[4], dmean);
 
     // ---- computeColorFromSH backward (backward.cu:20-139)
-    if (kHasSH) sh_backward<kSH16>(a, idx, mx, my, mz, s, cb, acc, dmean, kSH16 ? lrow : nullptr);
+    if (kHasSH) sh_backward<kSH16>(a, idx, mx, my, mz, s, cb, acc, dmean, kSH16 ? lrow : nullptr,
+                                   use_drgb ? d9 : nullptr);
 #pragma unroll
     for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = dmean[i];
 
@@ -1030,7 +997,9 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
     constexpr bool kStage = kHasSH && kSH16;
     __shared__ float s_dsh[kStage ? 256 * kShRow : 1];
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if constexpr (kStage) {  // the workgroup's 256 SH rows in, wave-contiguous
+    // (not needed when the forward stored d(rgb)/d(dir): the SH coefficients
+    // are then never read)
+    if (kStage && !(a.drgb && a.hdr[kHdrDrgb] == 1u)) {  // the workgroup's 256 SH rows in, wave-contiguous
         const int g0 = blockIdx.x * blockDim.x;
         const int n = min(256, a.P - g0);
         const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)g0 * 12;

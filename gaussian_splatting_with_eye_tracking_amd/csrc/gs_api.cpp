@@ -385,6 +385,7 @@ PreprocessArgs make_pp(const ForwardIn& in, int tile) {
     a.block = tile;
     a.prefiltered = in.prefiltered;
     a.store_cov3d = g_store_cov3d;
+    a.store_drgb = g_sh_drgb;
     a.zero_words = nullptr;
     a.zero_n = 0;
     a.err_token = 0;
@@ -571,6 +572,8 @@ int rasterizer_backward_impl(int amr_mode, int P, int D, int M, int R, const flo
         a.tan_fovx = tan_fovx;
         a.tan_fovy = tan_fovy;
         a.has_cov_precomp = cov3D_precomp != nullptr;
+        a.drgb = g_sh_drgb ? g.drgb : nullptr;
+        a.hdr = g.hdr;
         a.dL_dmean2D = dL_dmean2D;
         a.dL_dconic = dL_dconic;
         a.dL_dopacity = dL_dopacity;
@@ -1105,6 +1108,10 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "amr_batch") == 0) {
         set_amr_batch(value);
+        return 0;
+    }
+    if (std::strcmp(key, "sh_drgb") == 0) {  // the preprocess stores d(rgb)/d(dir) for the SH backward
+        g_sh_drgb = value;
         return 0;
     }
     if (std::strcmp(key, "store_cov3d") == 0) {

@@ -32,6 +32,84 @@ __device__ constexpr float SH_C3_4 = -0.4570457994644658f;
 __device__ constexpr float SH_C3_5 = 1.445305721320277f;
 __device__ constexpr float SH_C3_6 = -0.5900435899266435f;
 
+// computeColorFromSH backward (base/cr/backward.cu:20-139), split in two:
+// sh_basis -- the per-coefficient factors (dL_dsh[k][c] = basis[k] dL_drgb[c]),
+// a function of the view direction alone -- and sh_ddir -- d(rgb)/d(dir)
+// (dx3, dy3, dz3 per channel), which needs the coefficients.  The forward's
+// preprocess stores sh_ddir for the backward (GeomView::drgb), so the
+// backward reads 36 B per visible Gaussian instead of the 192-B SH row.
+__device__ __forceinline__ void sh_basis(int deg, float x, float y, float z, float (&dsh_c)[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) dsh_c[k] = 0.f;
+    dsh_c[0] = SH_C0;
+    if (deg > 0) {
+        dsh_c[1] = -SH_C1 * y;
+        dsh_c[2] = SH_C1 * z;
+        dsh_c[3] = -SH_C1 * x;
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            dsh_c[4] = SH_C2_0 * xy;
+            dsh_c[5] = SH_C2_1 * yz;
+            dsh_c[6] = SH_C2_2 * (2.f * zz - xx - yy);
+            dsh_c[7] = SH_C2_3 * xz;
+            dsh_c[8] = SH_C2_4 * (xx - yy);
+            if (deg > 2) {
+                dsh_c[9] = SH_C3_0 * y * (3.f * xx - yy);
+                dsh_c[10] = SH_C3_1 * xy * z;
+                dsh_c[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
+                dsh_c[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                dsh_c[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
+                dsh_c[14] = SH_C3_5 * z * (xx - yy);
+                dsh_c[15] = SH_C3_6 * x * (xx - 3.f * yy);
+            }
+        }
+    }
+}
+
+template <typename SH>
+__device__ __forceinline__ void sh_ddir(int deg, const SH& s, float x, float y, float z, float (&dx3)[3],
+                                        float (&dy3)[3], float (&dz3)[3]) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) dx3[c] = dy3[c] = dz3[c] = 0.f;
+    if (deg > 0) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            dx3[c] = -SH_C1 * s[3][c];
+            dy3[c] = -SH_C1 * s[1][c];
+            dz3[c] = SH_C1 * s[2][c];
+        }
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                dx3[c] += SH_C2_0 * y * s[4][c] + SH_C2_2 * 2.f * -x * s[6][c] + SH_C2_3 * z * s[7][c] +
+                          SH_C2_4 * 2.f * x * s[8][c];
+                dy3[c] += SH_C2_0 * x * s[4][c] + SH_C2_1 * z * s[5][c] + SH_C2_2 * 2.f * -y * s[6][c] +
+                          SH_C2_4 * 2.f * -y * s[8][c];
+                dz3[c] += SH_C2_1 * y * s[5][c] + SH_C2_2 * 2.f * 2.f * z * s[6][c] + SH_C2_3 * x * s[7][c];
+            }
+            if (deg > 2) {
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    dx3[c] += (SH_C3_0 * s[9][c] * 3.f * 2.f * xy + SH_C3_1 * s[10][c] * yz +
+                               SH_C3_2 * s[11][c] * -2.f * xy + SH_C3_3 * s[12][c] * -3.f * 2.f * xz +
+                               SH_C3_4 * s[13][c] * (-3.f * xx + 4.f * zz - yy) + SH_C3_5 * s[14][c] * 2.f * xz +
+                               SH_C3_6 * s[15][c] * 3.f * (xx - yy));
+                    dy3[c] += (SH_C3_0 * s[9][c] * 3.f * (xx - yy) + SH_C3_1 * s[10][c] * xz +
+                               SH_C3_2 * s[11][c] * (-3.f * yy + 4.f * zz - xx) +
+                               SH_C3_3 * s[12][c] * -3.f * 2.f * yz + SH_C3_4 * s[13][c] * -2.f * xy +
+                               SH_C3_5 * s[14][c] * -2.f * yz + SH_C3_6 * s[15][c] * -3.f * 2.f * xy);
+                    dz3[c] += (SH_C3_1 * s[10][c] * xy + SH_C3_2 * s[11][c] * 4.f * 2.f * yz +
+                               SH_C3_3 * s[12][c] * 3.f * (2.f * zz - xx - yy) + SH_C3_4 * s[13][c] * 4.f * 2.f * xz +
+                               SH_C3_5 * s[14][c] * (xx - yy));
+                }
+            }
+        }
+    }
+}
+
 // Column-major 3x3 (glm convention: m[c][r]).
 struct Mat3 {
     float m[3][3];

@@ -28,6 +28,7 @@ struct PreprocessArgs {
     int block;  // tile edge in pixels (16 base, 32 AMR)
     int prefiltered;
     int store_cov3d;  // write the geometry buffer's cov3D (nothing in the path reads it back)
+    int store_drgb;   // write d(rgb)/d(dir) of the SH colours for the backward (GeomView::drgb)
     // Words the launch zeroes before anything reads them (the binning's tile
     // histogram: no separate memset launch), and the value a prefiltered
     // violation stores in the header's error word (a per-call token, so that
@@ -112,6 +113,7 @@ void set_amr_deep(int v);
 void set_amr_lists_per(int v);
 void set_store_cov3d(int v);
 extern int g_store_cov3d;
+extern int g_sh_drgb;
 void set_sort_wide(int v);
 void set_amr_scramble(int v);
 void set_ritnet_mfma(int v);
@@ -140,6 +142,8 @@ struct BackwardGaussArgs {
     const float* campos;
     float focal_x, focal_y, tan_fovx, tan_fovy;
     int has_cov_precomp;
+    const float* drgb;      // the forward's d(rgb)/d(dir) [9][P] (nullptr: from the SH coefficients)
+    const uint32_t* hdr;    // the geometry header (kHdrDrgb says whether drgb was written)
     // outputs (every element written; no memsets needed)
     float* dL_dmean2D;
     float* dL_dconic;

@@ -117,6 +117,9 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
         }
     }
     for (int i = idx; i < a.zero_n; i += (int)(gridDim.x * blockDim.x)) a.zero_words[i] = 0u;
+    // whether the backward may take d(rgb)/d(dir) from g.drgb (every visible
+    // Gaussian's row is written below)
+    if (idx == 0) g.hdr[kHdrDrgb] = (kHasSH && a.store_drgb) ? 1u : 0u;
     if (idx >= a.P) return;
     // AMR: the geometry buffer keeps its own copy of the radii (the progressive
     // steps return zero radii, their backward reads these); base: the caller's
@@ -228,6 +231,17 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
         dx = dx / len; dy = dy / len; dz = dz / len;
         uint8_t cbits;
         const float3 rgb = eval_sh_color(a.D, shc, dx, dy, dz, cbits);
+        if (a.store_drgb) {  // the SH backward's d(rgb)/d(dir), from the coefficients already in registers
+            float dx3[3], dy3[3], dz3[3];
+            sh_ddir(a.D, shc, dx, dy, dz, dx3, dy3, dz3);
+            const size_t P = (size_t)a.P;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                g.drgb[c * P + idx] = dx3[c];
+                g.drgb[(3 + c) * P + idx] = dy3[c];
+                g.drgb[(6 + c) * P + idx] = dz3[c];
+            }
+        }
         g.rgb[3 * idx + 0] = rgb.x;
         g.rgb[3 * idx + 1] = rgb.y;
         g.rgb[3 * idx + 2] = rgb.z;
@@ -279,6 +293,10 @@ static void launch_pp(const PreprocessArgs& a, const GeomView& g, int* radii, ui
 }
 
 int g_store_cov3d = 0;  // set_tuning("store_cov3d"): the parity tests read the geometry buffer's cov3D
+// set_tuning("sh_drgb"): the preprocess stores d(rgb)/d(dir) of the SH colours
+// (GeomView::drgb, 36 B per visible Gaussian) and the backward reads them
+// instead of the 192-B SH rows
+int g_sh_drgb = 1;
 void set_store_cov3d(int v) { g_store_cov3d = v; }
 
 void launch_preprocess(const PreprocessArgs& a, const GeomView& g, int* radii, uint32_t* tile_count,

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_AMD_ABI_VERSION 2
+#define GSPLAT_AMD_ABI_VERSION 3
 
 /* Resize the caller-owned byte buffer `ctx` to `nbytes` and return its
  * (device, >=256-B aligned) base pointer, or NULL on failure.
@@ -295,6 +295,7 @@ typedef struct {
     float* rgb;           /* [P][3] */
     float* cov3D;         /* [P][6] */
     uint8_t* clamped;     /* [P] bit c = channel c clamped */
+    float* drgb;          /* [9][P] d(rgb)/d(view dir) of the SH colours (hdr[7] = 1: written) -- ABI 3 */
     uint32_t* tiles_touched;
     float* grad_accum; /* [P][16] */
 } gs_geom_view;

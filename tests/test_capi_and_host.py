@@ -45,16 +45,16 @@ def test_host_layout_helpers():
     lib.gs_image_bytes.restype = ctypes.c_size_t
     lib.gs_binning_bytes.restype = ctypes.c_size_t
     lib.gs_knn_workspace_bytes.restype = ctypes.c_size_t
-    assert lib.gs_abi_version() == 2  # 2: gs_image_view gained the band arrays
+    assert lib.gs_abi_version() == 3  # 2: gs_image_view gained the band arrays; 3: gs_geom_view gained drgb
     g1, g2 = lib.gs_geom_bytes(1000), lib.gs_geom_bytes(2000)
-    assert g2 > g1 > 1000 * (4 + 4 + 8 + 16 + 12 + 24 + 1 + 4 + 64)
+    assert g2 > g1 > 1000 * (4 + 4 + 8 + 16 + 12 + 24 + 1 + 36 + 4 + 64)
     assert lib.gs_image_bytes(1920, 1080, 16) >= 1920 * 1080 * 8 + 120 * 68 * 8
     assert lib.gs_binning_bytes(4096) >= 4096 * 20
     assert lib.gs_knn_workspace_bytes(10000) > 10000 * 16
     # views carve 256-B aligned arrays out of a base pointer (no device access)
     class GeomView(ctypes.Structure):
         _fields_ = [(n, ctypes.c_void_p) for n in ("hdr", "depths", "radii", "means2D", "conic_opacity", "rgb",
-                                                   "cov3D", "clamped", "tiles_touched", "grad_accum")]
+                                                   "cov3D", "clamped", "drgb", "tiles_touched", "grad_accum")]
     v = GeomView()
     base = 1 << 20
     assert lib.gs_geom_view_of(ctypes.c_void_p(base), 1000, ctypes.byref(v)) == 0
@@ -93,7 +93,7 @@ def test_torch_extension_surface():
     for n in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "amr_rasterize_gaussians",
               "distCUDA2", "parse_buffers", "profile_enable", "profile_read", "set_tuning"):
         assert hasattr(_C, n), n
-    assert _C.abi_version() == 2
+    assert _C.abi_version() == 3
     assert all(os.path.exists(p) and p.startswith(ROOT) for p in native_library_paths())
 
 

@@ -1,10 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_readback.py -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/readback.log 2>&1 && \
-GSAMD_HDR_MIRROR=0 timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-sub --no-profile > gpurun_out/b_m0.log 2>&1 && \
-GSAMD_HDR_MIRROR=2 timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-sub --no-profile > gpurun_out/b_m2.log 2>&1 && \
-GSAMD_HDR_MIRROR=0 timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-sub --no-profile > gpurun_out/b_m0b.log 2>&1 && \
-GSAMD_HDR_MIRROR=2 timeout -k 10 300 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-sub --no-profile > gpurun_out/b_m2b.log 2>&1 && \
-GSAMD_HDR_MIRROR=0 timeout -k 10 300 python bench.py --config cfg3_amr_1080p_1M --steps 50 --warmup 5 --no-cpu-baseline --no-sub --no-profile --no-ext > gpurun_out/b3_m0.log 2>&1 && \
-GSAMD_HDR_MIRROR=2 timeout -k 10 300 python bench.py --config cfg3_amr_1080p_1M --steps 50 --warmup 5 --no-cpu-baseline --no-sub --no-profile --no-ext > gpurun_out/b3_m2.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && \
+timeout -k 10 300 python tools/ab_tuning.py --key sh_drgb --values 0 1 --stage bwd_gauss --backward --rounds 6 > gpurun_out/ab_drgb_bg2.log 2>&1 && \
+timeout -k 10 300 python tools/ab_tuning.py --key sh_drgb --values 0 1 --stage preprocess --backward --rounds 6 > gpurun_out/ab_drgb_pp2.log 2>&1 && \
+timeout -k 10 400 python tools/ab_tuning.py --key sh_drgb --values 0 1 --stage bwd_gauss --backward --P 6100000 --W 1600 --H 1063 --rounds 4 > gpurun_out/ab_drgb_bg4.log 2>&1 && \
+timeout -k 10 400 python tools/ab_tuning.py --key sh_drgb --values 0 1 --stage preprocess --backward --P 6100000 --W 1600 --H 1063 --rounds 4 > gpurun_out/ab_drgb_pp4.log 2>&1
 echo rc=$?
