@@ -940,8 +940,10 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     float d9[9];
     if (kHasSH) {
         if (use_drgb) {
-#pragma unroll
-            for (int i = 0; i < 9; i++) d9[i] = a.drgb[(size_t)i * a.P + idx];
+            const float4* row = reinterpret_cast<const float4*>(a.drgb) + 3 * (size_t)idx;
+            const float4 r0 = row[0], r1 = row[1], r2 = row[2];
+            d9[0] = r0.x; d9[1] = r0.y; d9[2] = r0.z; d9[3] = r0.w;
+            d9[4] = r1.x; d9[5] = r1.y; d9[6] = r1.z; d9[7] = r1.w; d9[8] = r2.x;
         } else {
             load_sh_rows<kSH16>(a, idx, s, lrow);
         }

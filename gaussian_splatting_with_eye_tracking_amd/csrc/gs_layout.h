@@ -59,7 +59,7 @@ struct GeomView {
     float* rgb;            // [P][3]
     float* cov3D;          // [P][6]
     uint8_t* clamped;      // [P] bit c = channel c clamped
-    float* drgb;           // [9][P] d(rgb)/d(dir): (x, y, z) x (r, g, b), SH colours, visible Gaussians
+    float* drgb;           // [P][12] d(rgb)/d(dir): (x, y, z) x (r, g, b) + 3 pad, SH colours, visible Gaussians
     uint32_t* tiles_touched;
     float* grad_accum;  // [P][kGradRow]
 };
@@ -76,7 +76,7 @@ inline size_t carve_geom(char* base, size_t P, GeomView* v) {
     g.rgb = carve<float>(base, off, 3 * P);
     g.cov3D = carve<float>(base, off, 6 * P);
     g.clamped = carve<uint8_t>(base, off, P);
-    g.drgb = carve<float>(base, off, 9 * P);
+    g.drgb = carve<float>(base, off, 12 * P);
     g.tiles_touched = carve<uint32_t>(base, off, P);
     g.grad_accum = carve<float>(base, off, (size_t)kGradRow * P);
     if (v) *v = g;

@@ -234,13 +234,11 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
         if (a.store_drgb) {  // the SH backward's d(rgb)/d(dir), from the coefficients already in registers
             float dx3[3], dy3[3], dz3[3];
             sh_ddir(a.D, shc, dx, dy, dz, dx3, dy3, dz3);
-            const size_t P = (size_t)a.P;
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                g.drgb[c * P + idx] = dx3[c];
-                g.drgb[(3 + c) * P + idx] = dy3[c];
-                g.drgb[(6 + c) * P + idx] = dz3[c];
-            }
+            // one 48-B row: three 16-B stores from one address
+            float4* row = reinterpret_cast<float4*>(g.drgb) + 3 * (size_t)idx;
+            row[0] = make_float4(dx3[0], dx3[1], dx3[2], dy3[0]);
+            row[1] = make_float4(dy3[1], dy3[2], dz3[0], dz3[1]);
+            row[2] = make_float4(dz3[2], 0.f, 0.f, 0.f);
         }
         g.rgb[3 * idx + 0] = rgb.x;
         g.rgb[3 * idx + 1] = rgb.y;

@@ -295,7 +295,7 @@ typedef struct {
     float* rgb;           /* [P][3] */
     float* cov3D;         /* [P][6] */
     uint8_t* clamped;     /* [P] bit c = channel c clamped */
-    float* drgb;          /* [9][P] d(rgb)/d(view dir) of the SH colours (hdr[7] = 1: written) -- ABI 3 */
+    float* drgb;          /* [P][12] d(rgb)/d(view dir) of the SH colours, (x, y, z) x (r, g, b) + 3 pad (hdr[7] = 1: written) -- ABI 3 */
     uint32_t* tiles_touched;
     float* grad_accum; /* [P][16] */
 } gs_geom_view;

@@ -47,7 +47,7 @@ def test_host_layout_helpers():
     lib.gs_knn_workspace_bytes.restype = ctypes.c_size_t
     assert lib.gs_abi_version() == 3  # 2: gs_image_view gained the band arrays; 3: gs_geom_view gained drgb
     g1, g2 = lib.gs_geom_bytes(1000), lib.gs_geom_bytes(2000)
-    assert g2 > g1 > 1000 * (4 + 4 + 8 + 16 + 12 + 24 + 1 + 36 + 4 + 64)
+    assert g2 > g1 > 1000 * (4 + 4 + 8 + 16 + 12 + 24 + 1 + 48 + 4 + 64)
     assert lib.gs_image_bytes(1920, 1080, 16) >= 1920 * 1080 * 8 + 120 * 68 * 8
     assert lib.gs_binning_bytes(4096) >= 4096 * 20
     assert lib.gs_knn_workspace_bytes(10000) > 10000 * 16
