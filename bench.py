@@ -137,6 +137,20 @@ def algorithmic_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: in
     return 0.0
 
 
+def design_bytes(stage: str, P: int, V: int):
+    """This design's own compulsory bytes where they differ from the reference
+    stage's (`algorithmic_bytes`), else None.  Since r03n the preprocess stores
+    each visible Gaussian's SH direction derivatives (one 48-B row) and
+    bwd_gauss reads that row instead of the 192-B SH coefficients (DESIGN.md
+    §4): fewer bytes per view in total, but bwd_gauss's reference-stage figure
+    then counts 144 B per V it no longer moves."""
+    if stage == "preprocess":
+        return 20.0 * P + 337.0 * V
+    if stage == "bwd_gauss":
+        return 304.0 * P + 149.0 * V
+    return None
+
+
 def stream_read_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: int, views: int = 1):
     """Bytes of one launch of `stage` read as wave-contiguous streams, or None
     when (nearly) all its reads are streams.  profiles/r02n_pmc_calib.json
@@ -214,7 +228,7 @@ def load_raw_kib(stage: str, key: dict):
 
 
 def make_roofline(stage: str, by: float, avg_ms: float, key: dict, src: str, per: float = 1.0,
-                  stream_read: float | None = None) -> dict:
+                  stream_read: float | None = None, design_by: float | None = None) -> dict:
     """`by` bytes in `avg_ms`; `per` = launches those cover (PMC values are per
     launch); `stream_read`: streamed read bytes per launch (stream_read_bytes)
     -- given, traffic uses the gather calibration instead of doubling every
@@ -230,6 +244,9 @@ def make_roofline(stage: str, by: float, avg_ms: float, key: dict, src: str, per
          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": calib if calib is not None else traffic,
          "traffic_source": tr[1] if tr else None, "algorithmic_bytes": by, "avg_ms": round(avg_ms, 4), "events": src,
          "build": build_digest()}
+    if design_by is not None:  # what this design's kernel must move (design_bytes)
+        r["design_bytes"] = design_by
+        r["design_frac"] = round(design_by / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     if calib is not None:
         r["traffic_note"] = ("FETCH + WRITE + streamed reads / 2 (gathers counted x1, streams x2: "
                              "profiles/r02n_pmc_calib.json)")
@@ -380,6 +397,9 @@ def stage_table(prof: dict, steps: int, P, ws, views=1, key: dict | None = None)
             st = {"avg_ms": ms / cnt, "launches": cnt, "ms_per_step": ms / steps}
             b = algorithmic_bytes(name, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"], views)
             st["algorithmic_GBps"] = round(b / (st["avg_ms"] * 1e-3) / 1e9, 1) if b else None
+            db = design_bytes(name, P, ws["V"]) if views == 1 else None
+            if db is not None:
+                st["design_GBps"] = round(db / (st["avg_ms"] * 1e-3) / 1e9, 1)
             sr = stream_read_bytes(name, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"], views)
             raw = load_raw_kib(name, key) if key is not None and sr is not None and b else None
             if raw is not None:  # the blend kernels: gather-calibrated traffic (make_roofline)
@@ -453,7 +473,8 @@ def run_fwd_bwd(cfg_name: str, ctx: Ctx, steps: int, warmup: int) -> dict:
         avg_ms, src = (ms_t / cnt_t, "timed region") if cnt_t else (stages[dom]["avg_ms"], "stage-profile pass")
         by = algorithmic_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"])
         roofline = make_roofline(dom, by, avg_ms, config_key(P, W, H, 16), src,
-                                 stream_read=stream_read_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"]))
+                                 stream_read=stream_read_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"]),
+                                 design_by=design_bytes(dom, P, ws["V"]))
     res.update({
         "config": {"workload": f"{cfg_name}: {P} Gaussians, {W}x{H}, 16x16 tiles, forward+backward, 1 view per "
                                f"GPU per step", "P": P, "width": W, "height": H, "views_per_gpu_per_step": 1,
