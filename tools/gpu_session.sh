@@ -71,6 +71,8 @@ for step in "$@"; do
     pmc_bwd_a) run pmc_bwd_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_bwd_a -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_bwd_b) run pmc_bwd_b 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_bwd_b -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
     pmc_ql2) run pmc_ql2 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_ql2 -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 3 --warmup 1 --no-profile --no-ext --no-cpu-baseline ;;
+    pmc_issue2) run pmc_issue2 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace -d gpurun_out/pmc_issue2 -o run --output-format csv -- python3 bench.py --config cfg2_1080p_1M --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
+    pmc_issue4) run pmc_issue4 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace -d gpurun_out/pmc_issue4 -o run --output-format csv -- python3 bench.py --config cfg4_bicycle_6M --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
     pmc_fwd_a) run pmc_fwd_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_fwd_a -o run --output-format csv -- python3 tools/ab_tuning.py --key fwd_variant --values 2 --rounds 1 --iters 2 --stage render ;;
     pmc_fwd_b) run pmc_fwd_b 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_WAVES SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_fwd_b -o run --output-format csv -- python3 tools/ab_tuning.py --key fwd_variant --values 2 --rounds 1 --iters 2 --stage render ;;
     mv) run pytest_mv 400 python -m pytest tests/test_gpu_multiview.py tests/test_gpu_dist_views.py -q -m gpu -p no:cacheprovider --timeout 300 -rf &&
