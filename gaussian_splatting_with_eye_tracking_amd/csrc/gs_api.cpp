@@ -359,6 +359,20 @@ uint32_t next_error_token() {
     return t ? t : 1u;
 }
 
+// set_tuning("fwd_no_grad", 1): the NEXT forward on this thread is known to
+// need no backward (the autograd wrappers under no_grad / with no input
+// requiring a gradient): its preprocess skips the SH-derivative rows only the
+// backward reads (the header flag kHdrDrgb then says so, and a backward would
+// fall back to the SH coefficients).  One-shot: every forward entry consumes it.
+thread_local int t_fwd_no_grad = 0;
+int g_fwd_hint = 1;  // set_tuning("fwd_hint", 0): ignore the hint (A/B)
+bool take_fwd_no_grad() {
+    const bool v = t_fwd_no_grad != 0 && g_fwd_hint;
+    t_fwd_no_grad = 0;
+    return v;
+}
+thread_local bool t_store_drgb = true;  // this forward's choice (take_fwd_no_grad)
+
 PreprocessArgs make_pp(const ForwardIn& in, int tile) {
     PreprocessArgs a;
     a.P = in.P;
@@ -385,7 +399,7 @@ PreprocessArgs make_pp(const ForwardIn& in, int tile) {
     a.block = tile;
     a.prefiltered = in.prefiltered;
     a.store_cov3d = g_store_cov3d;
-    a.store_drgb = g_sh_drgb;
+    a.store_drgb = g_sh_drgb && t_store_drgb;
     a.zero_words = nullptr;
     a.zero_n = 0;
     a.err_token = 0;
@@ -500,6 +514,7 @@ int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image
                           float scale_modifier, const float* rotations, const float* cov3D_precomp,
                           const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
                           float tan_fovy, int prefiltered, float* out_color, int* radii, int debug, void* stream) {
+    t_store_drgb = !take_fwd_no_grad();
     return guarded([&]() -> int {
         if (P <= 0) return 0;
         hipStream_t s = static_cast<hipStream_t>(stream);
@@ -877,6 +892,7 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
                                  int foveaStep, const float* out_color_precomp, char* geom_buffer_precomp,
                                  char* binning_buffer_precomp, char* image_buffer_precomp, float* out_color,
                                  int* radii, int interpolate_image, int debug, int num_rendered_hint, void* stream) {
+    t_store_drgb = !take_fwd_no_grad();
     return guarded([&]() -> int {
         if (P <= 0) return 0;
         hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1112,6 +1128,14 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "sh_drgb") == 0) {  // the preprocess stores d(rgb)/d(dir) for the SH backward
         g_sh_drgb = value;
+        return 0;
+    }
+    if (std::strcmp(key, "fwd_no_grad") == 0) {  // one-shot hint for the next forward (make_pp)
+        t_fwd_no_grad = value;
+        return 0;
+    }
+    if (std::strcmp(key, "fwd_hint") == 0) {
+        g_fwd_hint = value;
         return 0;
     }
     if (std::strcmp(key, "store_cov3d") == 0) {

@@ -48,7 +48,20 @@ def _call(fn, args, debug: bool, dump: str, what: str):
         raise ex
 
 
+def _hint_forward_only(tensors) -> None:
+    """No backward can follow this call (grad mode off, or no input requires a
+    gradient): tell the next native forward, which then skips what only the
+    backward reads (the SH-derivative rows)."""
+    if not (torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in tensors)):
+        _C.set_tuning("fwd_no_grad", 1)
+
+
 class _RasterizeGaussians(torch.autograd.Function):
+    @classmethod
+    def apply(cls, *args):
+        _hint_forward_only(args[:8])
+        return super().apply(*args)
+
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                 raster_settings):
