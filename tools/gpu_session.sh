@@ -61,6 +61,9 @@ for step in "$@"; do
                run ab_chunk4_cnt 400 python tools/ab_tuning.py --key bin_chunk --values 4096 8192 16384 32768 --stage count_tiles --P 6100000 --W 1600 --H 1063 --rounds 3 ;;
     ab_dup) run ab_dup2 400 python tools/ab_tuning.py --key bin_two_phase --values 0 1 0 1 --stage duplicate &&
             run ab_dup4 400 python tools/ab_tuning.py --key bin_two_phase --values 0 1 0 1 --stage duplicate --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
+    ab_band) run ab_band_split4 400 python tools/ab_tuning.py --key band_split --values 0 16 32 128 256 --stage duplicate --P 6100000 --W 1600 --H 1063 --rounds 4 &&
+             run ab_band_thr4 400 python tools/ab_tuning.py --key band_threads --values 513 514 512 1024 --stage duplicate --P 6100000 --W 1600 --H 1063 --rounds 4 &&
+             run ab_band_split2 400 python tools/ab_tuning.py --key band_split --values 0 16 32 128 256 --stage duplicate --rounds 4 ;;
     ab_fold) run ab_fold 400 python tools/ab_tuning.py --key amr_fold --values 0 30 62 --stage amr_render --amr &&
              run ab_fold_once 400 python tools/ab_tuning.py --key amr_fold --values 0 1 --stage amr_render --amr-once ;;
     ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 3 4 3 4 --stage amr_render --amr ;;
