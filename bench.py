@@ -179,17 +179,24 @@ def _pmc_files():
 _DIGEST = None
 
 
+def _build_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_gsamd_build_digest", os.path.join(ROOT, "gaussian_splatting_with_eye_tracking_amd", "build.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
 def build_digest() -> str:
-    """Digest of the native sources + flags the library is built from
-    (gaussian_splatting_with_eye_tracking_amd/build.py: source_digest)."""
+    """gs_build_digest() of the loaded libgsplat_amd.so, checked against the
+    digest of the tree's native sources + flags (build.py source_digest,
+    check_loaded_digest): a library built from other sources is refused, so a
+    summary or bench line that carries this digest was measured on exactly
+    these sources."""
     global _DIGEST
     if _DIGEST is None:
-        import importlib.util
-        spec = importlib.util.spec_from_file_location(
-            "_gsamd_build_digest", os.path.join(ROOT, "gaussian_splatting_with_eye_tracking_amd", "build.py"))
-        m = importlib.util.module_from_spec(spec)
-        spec.loader.exec_module(m)
-        _DIGEST = m.source_digest()
+        _DIGEST = _build_module().check_loaded_digest()
     return _DIGEST
 
 
@@ -843,6 +850,7 @@ def main(argv=None):
     if args.launcher_dry_run:
         return dry_run(world, rank)
 
+    build_digest()  # refuse a native library built from other sources than this tree's
     import torch
     import torch.distributed as dist
     distributed = world > 1

@@ -57,27 +57,87 @@ def _headers() -> list[str]:
     return hs + [os.path.join(INCLUDE, "gsplat_amd.h")]
 
 
+DIGEST_STAMP = os.path.join(BUILD, "digest.txt")
+
+
+def _read(path: str) -> str:
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return ""
+
+
+def _object_digest(src: str, digest: str) -> str:
+    """What one object is built from: its source, every header, the flags
+    (and, for gs_api.cpp, the library digest it embeds)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in [os.path.join(CSRC, src)] + sorted(_headers()):
+        with open(f, "rb") as fh:
+            h.update(os.path.basename(f).encode() + fh.read())
+    h.update(" ".join(f for f in HIP_FLAGS if not f.startswith("-I")).encode())
+    if src == "gs_api.cpp":
+        h.update(digest.encode())
+    return h.hexdigest()[:16]
+
+
 def build_hip_lib(jobs: int = 8, verbose: bool = False) -> str:
+    """Compile every HIP source and link libgsplat_amd.so.  Rebuild rule:
+    content digests, not file times -- each object is rebuilt when the digest
+    of its source + headers + flags differs from the stamp written next to it
+    (_build/<src>.o.digest), and gs_api.cpp compiles the library digest
+    (source_digest) in as gs_build_digest() (-DGSAMD_DIGEST), so a loaded
+    library reports exactly the sources it was built from
+    (check_loaded_digest)."""
     os.makedirs(BUILD, exist_ok=True)
-    heads = _headers()
+    digest = source_digest()
     objs = []
     todo = []
     for src in HIP_SOURCES:
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, src + ".o")
         objs.append(o)
-        if _stale(o, [s] + heads):
-            lang = ["-x", "hip"] if src.endswith(".hip") else ["-x", "hip"]
-            todo.append([HIPCC] + HIP_FLAGS + lang + ["-c", s, "-o", o])
+        od = _object_digest(src, digest)
+        if not os.path.exists(o) or _read(o + ".digest") != od:
+            extra = [f"-DGSAMD_DIGEST=\"{digest}\""] if src == "gs_api.cpp" else []
+            todo.append((o, od, [HIPCC] + HIP_FLAGS + extra + ["-x", "hip", "-c", s, "-o", o]))
     if todo:
+        def one(t):
+            o, od, cmd = t
+            _run(cmd)
+            with open(o + ".digest", "w") as f:
+                f.write(od + "\n")
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-            for f in [ex.submit(_run, c) for c in todo]:
+            for f in [ex.submit(one, t) for t in todo]:
                 f.result()
-    if _stale(LIB, objs):
+    if todo or _stale(LIB, objs) or _read(DIGEST_STAMP) != digest:
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs)
+        with open(DIGEST_STAMP, "w") as f:
+            f.write(digest + "\n")
     if verbose:
-        print("built", LIB)
+        print("built", LIB, "digest", digest)
     return LIB
+
+
+def loaded_digest() -> str:
+    """gs_build_digest() of the libgsplat_amd.so this process loads (ctypes on
+    the in-tree file: the same object the torch binding links)."""
+    import ctypes
+    lib = ctypes.CDLL(LIB)
+    lib.gs_build_digest.restype = ctypes.c_char_p
+    return lib.gs_build_digest().decode()
+
+
+def check_loaded_digest() -> str:
+    """Refuse a library built from other sources than the tree's: returns the
+    digest when gs_build_digest() of the loaded library equals source_digest(),
+    raises otherwise."""
+    got, want = loaded_digest(), source_digest()
+    if got != want:
+        raise RuntimeError(f"libgsplat_amd.so was built from sources with digest {got}, the tree's is {want}: "
+                           "rebuild (python gaussian_splatting_with_eye_tracking_amd/build.py)")
+    return got
 
 
 def _torch_flags():

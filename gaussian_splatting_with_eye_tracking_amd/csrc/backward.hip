@@ -1174,6 +1174,13 @@ void launch_pack_view_grads(int P, const GeomView& g, const int* radii, bool has
 // backward runs once.  Optional densification statistics (train.py:111-113)
 // are accumulated view by view: accum += ||dL/dmean2D.xy||, denom += 1,
 // max_radii = max(max_radii, radius) for every view that sees the Gaussian.
+__device__ __forceinline__ const float* mv_row(const MultiViewArgs& a, int v) {
+    return a.table ? a.table[v] : a.rows[v];
+}
+__device__ __forceinline__ const float* mv_cam(const MultiViewArgs& a, int v) {
+    return a.table ? a.table[a.V + v] : a.cams[v];
+}
+
 template <bool kHasSH, bool kSH16>
 __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a) {
     // SH16: the workgroup's 256 SH rows staged in LDS (coalesced in, and the
@@ -1201,7 +1208,7 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
     const size_t roff = (size_t)local * kViewRow;
     bool any = false;
     if (live)
-        for (int v = 0; v < a.V; v++) any |= __float_as_uint(a.rows[v][roff + 9]) != 0u;
+        for (int v = 0; v < a.V; v++) any |= __float_as_uint(mv_row(a, v)[roff + 9]) != 0u;
     if (live && !any) {
 #pragma unroll
         for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = 0.f;
@@ -1234,7 +1241,7 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
                 st_max = a.max_radii[idx];
             }
             for (int v = 0; v < a.V; v++) {
-                const float* row = a.rows[v] + roff;
+                const float* row = mv_row(a, v) + roff;
                 const uint32_t w9 = __float_as_uint(row[9]);
                 if (w9 == 0u) continue;  // not visible in view v: no terms (the reference's radii > 0 filter)
                 // mean2D.y, conic x, y, w (rows are 40 B: 8-B aligned only)
@@ -1242,7 +1249,7 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
                 const float2 r1b = *reinterpret_cast<const float2*>(row + 6);
                 const float4 r1 = make_float4(r1a.x, r1a.y, r1b.x, r1b.y);
                 const float gx = row[3], dop_v = row[8];
-                const float* cam = a.cams[v];
+                const float* cam = mv_cam(a, v);
                 const Mat4 V = load_mat4(cam);
                 const Mat4 Pm = load_mat4(cam + 16);
                 const float tan_fovx = cam[37], tan_fovy = cam[38];
@@ -1293,12 +1300,12 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
             }
             float ddir[3] = {0.f, 0.f, 0.f};
             for (int v = 0; v < a.V; v++) {
-                const float* row = a.rows[v] + roff;
+                const float* row = mv_row(a, v) + roff;
                 const uint32_t w9 = __float_as_uint(row[9]);
                 if (w9 == 0u) continue;
                 const float acc[3] = {row[0], row[1], row[2]};
                 const uint8_t cb = (uint8_t)(w9 >> 24);
-                const float* cam = a.cams[v];
+                const float* cam = mv_cam(a, v);
                 float dsh_c[16], dRGB[3];
                 if constexpr (kStage) {
                     sh_backward_terms(a.D, cam + 32, mx, my, mz, ShRowPtr{lrow}, cb, acc, dsh_c, dRGB, ddir);

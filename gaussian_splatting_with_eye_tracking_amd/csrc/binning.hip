@@ -21,6 +21,8 @@
 // Per instance this moves ~20 B instead of the ~200 B of a 6-pass 64-bit
 // radix sort.
 #include <algorithm>
+#include <atomic>
+#include <stdexcept>
 
 #include "gs_blend.cuh"
 #include "gs_device.cuh"
@@ -389,9 +391,10 @@ constexpr int kBandBins = 1024;  // bins of one coalesced append round (rows, or
 // at 1080p, ~2.2 instances per Gaussian) the direct duplicate is cheaper
 // (46 vs 56 us at config 3, profiles/r03h_ab_amr_band.json); g_dup_band = 2
 // forces it for any grid (tests).
+bool band_lds_fits();  // (below: the banded kernels' dynamic LDS fits the current device)
 bool dup_banded(int gx, int gy, int block) {
     if (g_dup_band <= 0 || gx * gy > kLdsTiles || gx > kBandBins || gy > kBandBins) return false;
-    return block == 16 || g_dup_band == 2;
+    return (block == 16 || g_dup_band == 2) && band_lds_fits();
 }
 void set_bin_slots(int v) { g_bin_slots = std::max(0, std::min(kBinSlots, v)); }
 // Measured (profiles/r03b_ab_bin_slots*): the sub-buckets save ~30 us of the
@@ -670,6 +673,28 @@ struct BandLds {
     SourceLds<kNT * kSPT> src;
 };
 
+// The banded kernels need more than 64 KiB of dynamic LDS (65.6 KB for
+// <1024, 2, 1>): fine on gfx950's 160 KB, not on 64-KiB parts.  Checked per
+// device, once; a device where it does not fit keeps the direct duplicate
+// (dup_banded false, so the bin-slot policy follows too).
+constexpr size_t kBandLdsMax = std::max({sizeof(BandLds<1024, 2, 1>), sizeof(BandLds<512, 2, 2>),
+                                         sizeof(BandLds<512, 4, 2>), sizeof(BandLds<512, 2, 1>)});
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_band_fits[kMaxDevices];  // 0 unknown, 1 fits, 2 does not
+bool band_lds_fits() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return false;
+    int v = g_band_fits[dev].load(std::memory_order_relaxed);
+    if (v == 0) {
+        int cap = 0;
+        const bool ok = hipDeviceGetAttribute(&cap, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
+                        (size_t)cap >= kBandLdsMax;
+        v = ok ? 1 : 2;
+        g_band_fits[dev].store(v, std::memory_order_relaxed);
+    }
+    return v == 1;
+}
+
 template <int kNT, int kRound, int kSPT>
 __global__ void __launch_bounds__(kNT) band_stage_kernel(int P, const float* __restrict__ means2D,
                                                          const float* __restrict__ depths,
@@ -771,13 +796,18 @@ void launch_banded(int P, const GeomView& g, const int* radii, int block, uint32
                    const ImageView& img, const BinningView& b, hipStream_t s, uint32_t n_keys,
                    const uint32_t* spec_hdr, uint32_t spec_cap) {
     using Lds = BandLds<kNT, kR, kSPT>;
-    static bool attr = false;
-    if (!attr) {  // > 64 KiB of dynamic LDS
-        (void)hipFuncSetAttribute((const void*)band_stage_kernel<kNT, kR, kSPT>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Lds));
-        (void)hipFuncSetAttribute((const void*)band_split_kernel<kNT, kR, kSPT>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Lds));
-        attr = true;
+    // > 64 KiB of dynamic LDS: the attribute once per device (and variant)
+    static std::atomic<int> attr[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
+        throw std::runtime_error("launch_banded: no current device");
+    if (attr[dev].load(std::memory_order_acquire) == 0) {
+        if (hipFuncSetAttribute((const void*)band_stage_kernel<kNT, kR, kSPT>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Lds)) != hipSuccess ||
+            hipFuncSetAttribute((const void*)band_split_kernel<kNT, kR, kSPT>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(Lds)) != hipSuccess)
+            throw std::runtime_error("launch_banded: hipFuncSetAttribute(MaxDynamicSharedMemorySize) failed");
+        attr[dev].store(1, std::memory_order_release);
     }
     hipLaunchKernelGGL((band_stage_kernel<kNT, kR, kSPT>), dim3((P + kStageChunk - 1) / kStageChunk), dim3(kNT),
                        sizeof(Lds), s, P, g.means2D, g.depths, radii, block, gx, gy, img.band_cursor, b.scratch,

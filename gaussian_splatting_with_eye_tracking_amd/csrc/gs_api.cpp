@@ -220,21 +220,34 @@ void begin_header_read(const uint32_t* hdr_dev, hipStream_t s, const uint32_t* m
     GS_HIP(hipEventRecord(ss.done, ss.s));
 }
 
-void finish_header_read(uint32_t out[4], const uint32_t* mirror = nullptr, hipStream_t s = nullptr) {
+void finish_header_read(uint32_t out[4], const uint32_t* mirror = nullptr, hipStream_t s = nullptr,
+                        const uint32_t* hdr_dev = nullptr) {
     if (mirror && g_hdr_mirror == 2) {
         const volatile uint32_t* m = mirror;
+        auto token = [&]() { return __atomic_load_n(const_cast<const uint32_t*>(mirror) + 4, __ATOMIC_ACQUIRE); };
         const auto t0 = std::chrono::steady_clock::now();
         uint64_t spins = 0;
-        while (__atomic_load_n(const_cast<const uint32_t*>(mirror) + 4, __ATOMIC_ACQUIRE) != t_mirror_token) {
+        while (token() != t_mirror_token) {
+            __builtin_ia32_pause();  // (a spin-wait hint: the wait is ~10-50 us)
             // a stream that faulted or was never run: wait for it, then re-check once
             if ((++spins & 0xffff) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
                 GS_HIP(hipStreamSynchronize(s));
-                if (__atomic_load_n(const_cast<const uint32_t*>(mirror) + 4, __ATOMIC_ACQUIRE) != t_mirror_token)
+                if (token() != t_mirror_token)
                     throw GsError("header read-back: the tile scan did not publish its token");
                 break;
             }
         }
         for (int i = 0; i < 4; i++) out[i] = m[i];
+        // seqlock check: the words and the token share this thread's slot, so a
+        // scan of an earlier call that is still queued on another stream (its
+        // caller never finished, e.g. an exception in between) could rewrite
+        // them after the token test above.  Then the token is no longer ours:
+        // fall back to the device's own header words, after this stream.
+        if (token() != t_mirror_token) {
+            if (!hdr_dev) throw GsError("header read-back: the mirror slot was overwritten");
+            GS_HIP(hipStreamSynchronize(s));
+            GS_HIP(hipMemcpy(out, hdr_dev, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        }
         return;
     }
     GS_HIP(hipEventSynchronize(side_stream().done));
@@ -469,17 +482,17 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     if (before_k) {
         begin_header_read(r.g.hdr, s, mirror.first);
         before_k(r);
-        finish_header_read(hdr, mirror.first, s);
+        finish_header_read(hdr, mirror.first, s, r.g.hdr);
     } else if (cap > 0) {
         begin_header_read(r.g.hdr, s, mirror.first);
         char* sbase = call_resize(binning, carve_binning(nullptr, cap, nullptr), "binning");
         carve_binning(sbase, cap, &r.b);
         { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, (uint32_t)cap, r.g.hdr, (uint32_t)cap); }
-        finish_header_read(hdr, mirror.first, s);
+        finish_header_read(hdr, mirror.first, s, r.g.hdr);
         dup_done = hdr[kHdrNumRendered] <= cap;
     } else if (mirror.first) {
         begin_header_read(r.g.hdr, s, mirror.first);
-        finish_header_read(hdr, mirror.first, s);
+        finish_header_read(hdr, mirror.first, s, r.g.hdr);
     } else {
         read_header(r.g.hdr, hdr, s);
     }
@@ -505,6 +518,12 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
 extern "C" {
 
 int gs_abi_version(void) { return GSPLAT_AMD_ABI_VERSION; }
+
+// build.py passes -DGSAMD_DIGEST="<source_digest()>" for this file
+#ifndef GSAMD_DIGEST
+#define GSAMD_DIGEST "unstamped"
+#endif
+const char* gs_build_digest(void) { return GSAMD_DIGEST; }
 
 const char* gs_last_error(void) { return g_err.c_str(); }
 
@@ -692,7 +711,7 @@ int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* c
                    float* dL_drotations, float* grad_norm_accum, float* denom, float* max_radii, void* stream) {
     return guarded([&]() -> int {
         if (P <= 0 || count == 0) return 0;
-        if (V <= 0 || V > kMaxViews) throw GsError("gs_backward_gaussians_multiview: V must be in [1, 64]");
+        if (V <= 0) throw GsError("gs_backward_gaussians_multiview: V must be >= 1");
         if (g0 < 0 || count < 0 || g0 + count > P) throw GsError("gs_backward_gaussians_multiview: bad range");
         if (!scales || !rotations)
             throw GsError("gs_backward_gaussians_multiview: scales and rotations are required (no cov3D_precomp)");
@@ -704,10 +723,28 @@ int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* c
         a.P = P; a.D = D; a.M = M; a.V = V;
         a.g0 = g0;
         a.count = count;
-        for (int v = 0; v < V; v++) {
+        for (int v = 0; v < V; v++)
             if (!rows[v] || !cams[v]) throw GsError("gs_backward_gaussians_multiview: null view row / camera");
-            a.rows[v] = rows[v];
-            a.cams[v] = cams[v];
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        // up to kMaxViews views travel in the kernel arguments; more in a device
+        // table (same kernel, same view order: bit-identical sums)
+        void* table = nullptr;
+        if (V <= kMaxViews) {
+            for (int v = 0; v < V; v++) {
+                a.rows[v] = rows[v];
+                a.cams[v] = cams[v];
+            }
+        } else {
+            std::vector<const float*> host(2 * (size_t)V);
+            for (int v = 0; v < V; v++) {
+                host[v] = rows[v];
+                host[(size_t)V + v] = cams[v];
+            }
+            GS_HIP(hipMallocAsync(&table, host.size() * sizeof(const float*), s));
+            GS_HIP(hipMemcpyAsync(table, host.data(), host.size() * sizeof(const float*), hipMemcpyHostToDevice, s));
+            // (the host vector dies here: the pageable source must be consumed first)
+            GS_HIP(hipStreamSynchronize(s));
+            a.table = static_cast<const float* const*>(table);
         }
         a.means3D = means3D;
         a.shs = shs;
@@ -722,8 +759,8 @@ int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* c
         a.grad_norm_accum = grad_norm_accum;
         a.denom = denom;
         a.max_radii = max_radii;
-        hipStream_t s = static_cast<hipStream_t>(stream);
         { StageTimer _t(kMultiView, s); launch_multiview_backward(a, s); }
+        if (table) GS_HIP(hipFreeAsync(table, s));
         stage_check(false, s, "multiview_backward");
         return 0;
     });
@@ -735,17 +772,12 @@ int multiview_strided(int P, int g0, int count, int D, int M, int V, const float
                       const float* scales, const float* rotations, float scale_modifier, float* dL_dmeans3D,
                       float* dL_dsh, float* dL_dopacity, float* dL_dscales, float* dL_drotations,
                       float* grad_norm_accum, float* denom, float* max_radii, void* stream) {
-    const float* rp[kMaxViews] = {};
-    const float* cp[kMaxViews] = {};
-    if (V > kMaxViews) {
-        g_err = "gs_backward_gaussians_multiview: V must be in [1, 64]";
-        return -1;
-    }
+    std::vector<const float*> rp(V > 0 ? V : 0), cp(V > 0 ? V : 0);
     for (int v = 0; v < V; v++) {
         rp[v] = rows + (size_t)v * row_view_stride;
         cp[v] = cams + (size_t)v * cam_stride;
     }
-    return multiview_impl(P, g0, count, D, M, V, rp, cp, means3D, shs, scales, rotations, scale_modifier,
+    return multiview_impl(P, g0, count, D, M, V, rp.data(), cp.data(), means3D, shs, scales, rotations, scale_modifier,
                           dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations, grad_norm_accum, denom,
                           max_radii, stream);
 }

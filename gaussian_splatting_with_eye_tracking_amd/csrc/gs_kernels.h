@@ -168,6 +168,9 @@ struct MultiViewArgs {
     int g0, count;                  // this launch: Gaussians [g0, g0 + count)
     const float* rows[kMaxViews];   // view v's row of Gaussian g0 ([kViewRow] words per Gaussian), summed in v order
     const float* cams[kMaxViews];   // view v's camera ([kCamWords])
+    // V > kMaxViews: the same two pointer arrays in device memory (rows at
+    // [0, V), cams at [V, 2V)); null otherwise
+    const float* const* table;
     const float* means3D;
     const float* shs;  // nullable (colors precomputed: no SH gradient)
     const float* scales;

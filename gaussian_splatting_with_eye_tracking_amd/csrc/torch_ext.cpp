@@ -446,7 +446,7 @@ void BackwardGaussiansMultiviewViews(const std::vector<Tensor>& rows, const std:
                                      Tensor dL_drotations, Tensor grad_norm_accum, Tensor denom, Tensor max_radii) {
     const int P = (int)means3D_in.size(0);
     const int V = (int)rows.size();
-    TORCH_CHECK(V >= 1 && V <= 64 && (int)cams.size() == V, "1 to 64 views, one camera each");
+    TORCH_CHECK(V >= 1 && (int)cams.size() == V, "at least one view, one camera each");
     TORCH_CHECK(rows[0].dim() == 1 && rows[0].numel() % 10 == 0, "rows[v] must be a 1-D [count * 10] slice");
     const int count = (int)(rows[0].numel() / 10);
     TORCH_CHECK(g0 >= 0 && g0 + count <= P, "Gaussian range out of bounds");

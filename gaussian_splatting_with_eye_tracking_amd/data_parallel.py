@@ -181,7 +181,7 @@ class ViewExchange:
         # every gather lands in its own contiguous [world, n] buffer (one
         # all_gather_into_tensor on RCCL, no flatten copy); the multi-view
         # kernel then reads view (r, j) through a per-view row pointer
-        self.full: List[torch.Tensor] = []        # views 0 .. v-2: [world, RL]
+        self.full: List[torch.Tensor] = [None] * max(0, self.v - 1)  # views 0 .. v-2: [world, RL], by index
         self.pending: List[object] = []
         self.last: List[Tuple[int, int, torch.Tensor, object]] = []  # (a, b, [world, (b-a)*10], work)
         self.cam_stage = None
@@ -197,15 +197,23 @@ class ViewExchange:
         return out, w
 
     def add(self, j: int, rec: torch.Tensor) -> None:
+        """View j's record (any order; each j in [0, v) exactly once)."""
+        if not 0 <= j < self.v:
+            raise ValueError(f"ViewExchange.add: view {j} outside [0, {self.v})")
         if self.world == 1:
             self.buf[j].copy_(rec)
             return
         P = self.P
         if j < self.v - 1 or P == 0:
+            if j < self.v - 1 and self.full[j] is not None:
+                raise ValueError(f"ViewExchange.add: view {j} added twice")
             out, w = self._gather(rec)
-            self.full.append(out)
+            if j < self.v - 1:
+                self.full[j] = out
             self.pending.append(w)
             return
+        if self.cam_stage is not None:
+            raise ValueError(f"ViewExchange.add: view {j} added twice")
         self.cam_stage, self.cam_work = self._gather(rec[P * VIEW_ROW:])
         step = max(1, -(-P // self.chunks))
         for a in range(0, P, step):
@@ -251,6 +259,8 @@ class ViewExchange:
             return multiview_param_grads(self.buf, means3D, shs, settings.sh_degree, scales, rotations,
                                          settings.scale_modifier, stats)
         from . import _C
+        if self.cam_work is None or any(f is None for f in self.full):
+            raise ValueError("ViewExchange.finish: not every view was added")
         for w in self.pending:
             w.wait()
         self.cam_work.wait()

@@ -48,19 +48,32 @@ def _call(fn, args, debug: bool, dump: str, what: str):
         raise ex
 
 
-def _hint_forward_only(tensors) -> None:
+def _hint_forward_only(tensors) -> bool:
     """No backward can follow this call (grad mode off, or no input requires a
     gradient): tell the next native forward, which then skips what only the
-    backward reads (the SH-derivative rows)."""
+    backward reads (the SH-derivative rows).  Returns whether
+    the one-shot hint was set; the caller clears it once the call is over
+    (_clear_hint), so a forward that raised before consuming it cannot hand
+    it to a later training forward."""
     if not (torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in tensors)):
         _C.set_tuning("fwd_no_grad", 1)
+        return True
+    return False
+
+
+def _clear_hint(hinted: bool) -> None:
+    if hinted:
+        _C.set_tuning("fwd_no_grad", 0)
 
 
 class _RasterizeGaussians(torch.autograd.Function):
     @classmethod
     def apply(cls, *args):
-        _hint_forward_only(args[:8])
-        return super().apply(*args)
+        hinted = _hint_forward_only(args[:8])
+        try:
+            return super().apply(*args)
+        finally:
+            _clear_hint(hinted)
 
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,

@@ -36,7 +36,7 @@ import torch
 import torch.nn as nn
 
 from . import _C
-from .rasterization import GaussianRasterizationSettings, _check_exactly_one, _hint_forward_only, _or_empty  # noqa: F401
+from .rasterization import GaussianRasterizationSettings, _check_exactly_one, _clear_hint, _hint_forward_only, _or_empty  # noqa: F401
 
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
@@ -59,9 +59,11 @@ class _RasterizeGaussians(torch.autograd.Function):
             raise RuntimeError("the AMR backward differentiates interpolate_image only for render_once "
                                "(foveaStep < 0); run foveaStep >= 1 with interpolate_image=False or under "
                                "torch.no_grad()")
-        if int(args[8]) <= 0:  # the steps >= 1 run no preprocess
-            _hint_forward_only(args[:8])
-        return super().apply(*args)
+        hinted = int(args[8]) <= 0 and _hint_forward_only(args[:8])  # (the steps >= 1 run no preprocess)
+        try:
+            return super().apply(*args)
+        finally:
+            _clear_hint(hinted)
 
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, foveaStep,

@@ -42,6 +42,11 @@ typedef struct {
 } gs_buffer;
 
 int gs_abi_version(void);
+/* Digest of the sources + compiler flags this library was built from
+ * (build.py source_digest(); not part of any reference interface: the
+ * benchmark and smoke test refuse a library whose digest differs from the
+ * tree's). */
+const char* gs_build_digest(void);
 const char* gs_last_error(void);
 
 /* Replaces CudaRasterizer::Rasterizer::forward
@@ -118,10 +123,13 @@ int gs_backward_gaussians_multiview_range(int P, int g0, int count, int D, int M
                                           float* dL_drotations, float* grad_norm_accum, float* denom,
                                           float* max_radii, void* stream);
 
-/* The same over V <= 64 views whose rows need not share a stride: rows[v]
+/* The same over V views whose rows need not share a stride: rows[v]
  * (host array of device pointers) is view v's row of Gaussian g0, cams[v]
  * its 40-word camera; views are summed in v order.  Lets every all-gathered
- * piece stay in its own contiguous [world, n] buffer (no flatten copies). */
+ * piece stay in its own contiguous [world, n] buffer (no flatten copies).
+ * Any V >= 1: up to 64 views the pointers travel as kernel arguments, beyond
+ * that in a stream-ordered device table (one host synchronisation for its
+ * upload); the sums are the same either way. */
 int gs_backward_gaussians_multiview_views(int P, int g0, int count, int D, int M, int V, const float* const* rows,
                                           const float* const* cams, const float* means3D, const float* shs,
                                           const float* scales, const float* rotations, float scale_modifier,

@@ -39,6 +39,21 @@ def test_library_exports_every_declared_symbol():
     assert not missing, missing
 
 
+def test_library_carries_the_tree_digest():
+    """build.py compiles source_digest() into the library (gs_build_digest);
+    check_loaded_digest refuses a library built from other sources."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "_b", os.path.join(ROOT, "gaussian_splatting_with_eye_tracking_amd", "build.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    lib = ctypes.CDLL(LIB)
+    lib.gs_build_digest.restype = ctypes.c_char_p
+    d = lib.gs_build_digest().decode()
+    assert re.fullmatch(r"[0-9a-f]{16}", d)
+    assert d == b.source_digest() == b.check_loaded_digest()
+
+
 def test_host_layout_helpers():
     lib = ctypes.CDLL(LIB)
     lib.gs_geom_bytes.restype = ctypes.c_size_t

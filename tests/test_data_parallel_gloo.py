@@ -202,7 +202,7 @@ def test_view_record_gather_several_views_per_rank_and_empty_model():
         assert outs[r][1] == [(0, 3), (0, 16, 3), (0, 1), (0, 3), (0, 4)]
 
 
-def _pipelined_worker(rank, world, port, q):
+def _pipelined_worker(rank, world, port, q, order=(0, 1, 2)):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -212,29 +212,39 @@ def _pipelined_worker(rank, world, port, q):
         P, v = 37, 3
         n = DP.view_record_numel(P)
         ex = DP.ViewExchange(P, v, "cpu", chunks=4)
-        for j in range(v):  # record of (rank, view j): its values say whose it is
+        for j in order:  # record of (rank, view j): its values say whose it is
             ex.add(j, torch.arange(n, dtype=torch.float32) + 1000.0 * (rank * v + j))
-        q.put((rank, ex.records().numpy().copy()))
+        try:
+            ex.add(0, torch.zeros(n))
+            dup = False
+        except ValueError:
+            dup = True
+        q.put((rank, ex.records().numpy().copy(), dup))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(300)
-def test_pipelined_view_gather_order():
+@pytest.mark.parametrize("order", [(0, 1, 2), (1, 2, 0)])
+def test_pipelined_view_gather_order(order):
     """data_parallel.ViewExchange (per-view asynchronous gathers, the last view
     in Gaussian chunks) lands every record in rank-then-view order, the order
-    exchange_view_records sums in, on every rank (world size 2, 3 views each)."""
+    exchange_view_records sums in, on every rank (world size 2, 3 views each),
+    whatever order the views are added in (every rank adding in the same
+    order: the gathers are collectives); a view added twice is refused."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, q, order)) for r in range(world)]
     for p in procs:
         p.start()
-    outs = dict(q.get(timeout=240) for _ in range(world))
+    got = [q.get(timeout=240) for _ in range(world)]
+    outs = {r: rec for r, rec, _dup in got}
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    assert all(dup for _r, _rec, dup in got)
     from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
     n = DP.view_record_numel(37)
     want = np.stack([np.arange(n, dtype=np.float32) + 1000.0 * k for k in range(world * 3)])

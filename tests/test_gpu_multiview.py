@@ -108,3 +108,47 @@ def test_view_record_layout():
     np.testing.assert_array_equal(cam[32:35], s.campos.cpu().numpy())
     assert cam[35] == W and cam[36] == H
     assert cam[37] == np.float32(s.tanfovx) and cam[38] == np.float32(s.tanfovy)
+
+
+def test_multiview_more_than_64_views():
+    """V > 64 views (e.g. 16 ranks x 8 views) through both C
+    entries -- the strided record stack and the per-view pointer lists that
+    ViewExchange.finish uses.  Beyond 64 the pointers go through a device
+    table; the sums are the same: the 70-view result equals the two 35-view
+    halves added (atomic-free per-Gaussian sums: only the halves' rounding
+    differs), and the two entries agree bit for bit."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    P, W, H = 6000, 128, 96
+    sc, cams = _views(P, W, H, (-6.0, 0.0, 7.0))
+    t = G.scene_tensors(sc)
+    base = []
+    for v, cam in enumerate(cams):
+        s = G.torch_settings(cam)
+        dpix = torch.from_numpy(S.make_cotangent(H, W, 30 + v)).cuda()
+        fwd = _forward(C, s, t)
+        base.append(DP.view_record(s, fwd[2], fwd[3], fwd[0], fwd[4], fwd[5], dpix))
+    V = 70
+    views = torch.stack([base[v % 3] for v in range(V)]).contiguous()
+    args = (t["means3D"], t["shs"], 3, t["scales"], t["rotations"], 1.0)
+    got = DP.multiview_param_grads(views, *args)
+    h1 = DP.multiview_param_grads(views[:35].contiguous(), *args)
+    h2 = DP.multiview_param_grads(views[35:].contiguous(), *args)
+    torch.cuda.synchronize()
+    for a, b1, b2 in zip(got, h1, h2):
+        want = (b1.double() + b2.double()).cpu().numpy()
+        assert np.isfinite(a.cpu().numpy()).all()
+        assert G.rel_err(a.cpu().numpy(), want) < REL
+    # the per-view pointer entry (ViewExchange.finish's) over the same 70 views
+    e = torch.empty(0, device="cuda")
+    M = t["shs"].shape[1]
+    outs = (torch.empty((P, 3), device="cuda"), torch.empty((P, M, 3), device="cuda"),
+            torch.empty((P, 1), device="cuda"), torch.empty((P, 3), device="cuda"), torch.empty((P, 4), device="cuda"))
+    rows = [views[v, :P * DP.VIEW_ROW] for v in range(V)]
+    cams_ = [views[v, P * DP.VIEW_ROW:] for v in range(V)]
+    C.backward_gaussians_multiview_views(rows, cams_, 0, t["means3D"], t["shs"], 3, t["scales"], t["rotations"], 1.0,
+                                         *outs, e, e, e)
+    torch.cuda.synchronize()
+    for a, b in zip(got, outs):
+        assert torch.equal(a.reshape(-1), b.reshape(-1))

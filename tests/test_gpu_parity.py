@@ -1015,3 +1015,29 @@ def test_forward_only_hint_from_autograd_wrapper():
     torch.cuda.synchronize()
     geom = out[3]
     assert int(C.parse_buffers(geom, out[4], out[5], P, 0, W, H, 16)["hdr"][7].item()) == 1
+
+
+def test_forward_only_hint_cleared_when_the_forward_raises():
+    """a forward-only call whose native forward raises before it
+    consumes the one-shot hint must not leave it for the next (training)
+    forward: that forward still stores the SH-derivative rows."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from diff_gaussian_rasterization import GaussianRasterizer
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    W, H, P = 128, 96, 3000
+    cam = S.make_camera(W, H)
+    sc = S.make_scene(P, cam, seed=1)
+    s = G.torch_settings(cam)
+    t = G.scene_tensors(sc)
+    r = GaussianRasterizer(s)
+    with torch.no_grad(), pytest.raises(Exception):
+        bad = t["means3D"][:, :2].contiguous()  # not [P, 3]: the native forward refuses it
+        r(means3D=bad, means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"], shs=t["shs"],
+          scales=t["scales"], rotations=t["rotations"])
+    e = torch.empty(0, device="cuda")
+    out = C.rasterize_gaussians(s.bg, t["means3D"], e, t["opacities"], t["scales"], t["rotations"],
+                                s.scale_modifier, e, s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy,
+                                s.image_height, s.image_width, t["shs"], s.sh_degree, s.campos, s.prefiltered,
+                                s.debug)
+    torch.cuda.synchronize()
+    assert int(C.parse_buffers(out[3], out[4], out[5], P, 0, W, H, 16)["hdr"][7].item()) == 1
