@@ -108,46 +108,56 @@ def launch_ranks(n: int, argv: list[str]) -> int:
 
 # ------------------------------------------------------------- roofline ---
 def algorithmic_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: int, views: int = 1) -> float:
-    """Compulsory HBM bytes of one launch of `stage`: the bytes
-    the reference algorithm must read or write once, whatever the kernel.
-    P Gaussians, V visible, K instances, Kb instances up to each tile's last
-    contributor (what any blend must read), N pixels, T tiles."""
-    if stage == "preprocess":   # means 12 + radii 4 + tiles_touched 4 per P; per V: scales 12, rot 16,
-        return 20.0 * P + 289.0 * V  # opacity 4, SH 192 in; depth 4, xy 8, conic 16, rgb 12, cov 24, clamped 1 out
-    if stage == "render":       # per entry: id 4 + xy 8 + conic/opacity 16 + rgb 12; per pixel: colour 12,
-        # final T 4, n_contrib 4; per tile: range 8 + max_contrib 4; + the backward's 64-B accumulator
-        # rows, zeroed by this launch since r02p (the former zero_accum memset)
-        return 40.0 * Kb + 20.0 * N + 12.0 * T + 64.0 * P
-    if stage == "render_bwd":   # per entry: the same 40 B + 9 accumulated floats 36; per pixel: dL/dpix 12,
-        return 76.0 * Kb + 20.0 * N + 12.0 * T  # final T 4, n_contrib 4; per tile 12
+    """SURVEY.md §8(d)'s algorithmic bytes of the reference stage this kernel
+    replaces: the compulsory I/O of that stage, counted once (DESIGN.md §7
+    maps kernel -> reference stage).  P Gaussians, V visible, K instances, N
+    pixels, T tiles (Kb unused: the survey's blend rows read all K)."""
+    if stage == "preprocess":   # fwd preprocess
+        return 20.0 * P + 291.0 * V
+    if stage == "count_tiles":  # the reference's scan: tiles_touched in, offsets out
+        return 8.0 * P
+    if stage == "tile_scan":    # identifyTileRanges + the ranges memset
+        return 8.0 * K + 16.0 * T
+    if stage == "duplicate":    # duplicateWithKeys
+        return 4.0 * P + 16.0 * V + 12.0 * K
+    if stage == "sort_tiles":   # the radix sort
+        return 24.0 * K
+    if stage == "render":       # blend fwd
+        return 40.0 * K + 20.0 * N + 8.0 * T
+    if stage == "render_bwd":   # blend bwd
+        return 40.0 * K + 20.0 * N + 8.0 * T + 36.0 * V
+    if stage == "bwd_gauss":    # bwd zero-init of outputs 300P + cov2D bwd 4P + 84V + preprocess bwd 4P + 523V
+        return 308.0 * P + 607.0 * V
+    if stage == "multiview_bwd":  # per view 40-B records; params in (means 12, SH 192, scales 12, rot 16),
+        return 40.0 * views * P + 232.0 * P + 236.0 * P  # 59 gradient floats out (no reference stage)
+    return 0.0
+
+
+def design_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: int):
+    """What THIS design's kernel must move once, where it differs from the
+    reference stage (algorithmic_bytes), else None:
+    the blends read only the Kb entries before each tile's last contributor
+    and the render zeroes the backward's 64-B accumulator rows; the
+    backward's per-entry 36 B are its 64-B atomic rows; the preprocess also
+    writes a 48-B SH-derivative row per visible Gaussian that bwd_gauss reads
+    instead of the 192-B coefficients; the binning stages move keys per tile
+    bucket (no global radix passes)."""
+    if stage == "preprocess":
+        return 20.0 * P + 337.0 * V
+    if stage == "render":       # per entry: id 4 + xy 8 + conic/opacity 16 + rgb 12; per pixel 20; per tile
+        return 40.0 * Kb + 20.0 * N + 12.0 * T + 64.0 * P  # range + max_contrib 12; the 64-B accumulator rows
+    if stage == "render_bwd":   # per entry: the same 40 B + 9 accumulated floats 36; per pixel 20; per tile 12
+        return 76.0 * Kb + 20.0 * N + 12.0 * T
     if stage == "bwd_gauss":    # radii 4 + all 75 gradient floats 300 per P; per V: accum 36, means 12,
-        return 304.0 * P + 293.0 * V  # cov3D 24, scales 12, rot 16, SH 192, clamped 1
+        return 304.0 * P + 149.0 * V  # scales 12, rot 16, SH-derivative row 48, clamped 1, + opacity etc.
     if stage == "duplicate":    # per V: xy 8, radius 4, depth 4; per instance: one 8-B key
         return 16.0 * V + 8.0 * K
     if stage == "count_tiles":  # radius per P, xy per V in; T counts out
         return 4.0 * P + 8.0 * V + 4.0 * T
     if stage == "sort_tiles":   # per instance: key in 8, point_list out 4; per tile: range 8
         return 12.0 * K + 8.0 * T
-    if stage == "zero_accum":   # the 64-B accumulator rows (this design's own buffer)
-        return 64.0 * P
     if stage == "tile_scan":    # count in, range + cursor + max_contrib out
         return 28.0 * T
-    if stage == "multiview_bwd":  # per view 40-B records; params in (means 12, SH 192, scales 12, rot 16),
-        return 40.0 * views * P + 232.0 * P + 236.0 * P  # 59 gradient floats out
-    return 0.0
-
-
-def design_bytes(stage: str, P: int, V: int):
-    """This design's own compulsory bytes where they differ from the reference
-    stage's (`algorithmic_bytes`), else None.  Since r03n the preprocess stores
-    each visible Gaussian's SH direction derivatives (one 48-B row) and
-    bwd_gauss reads that row instead of the 192-B SH coefficients (DESIGN.md
-    §4): fewer bytes per view in total, but bwd_gauss's reference-stage figure
-    then counts 144 B per V it no longer moves."""
-    if stage == "preprocess":
-        return 20.0 * P + 337.0 * V
-    if stage == "bwd_gauss":
-        return 304.0 * P + 149.0 * V
     return None
 
 
@@ -234,12 +244,32 @@ def load_raw_kib(stage: str, key: dict):
     return None
 
 
-def make_roofline(stage: str, by: float, avg_ms: float, key: dict, src: str, per: float = 1.0,
+def load_kernel_avg_us(stage: str, key: dict):
+    """rocprofv3 --kernel-trace --stats mean duration (us) of one invocation
+    of `stage` from the newest summary of this configuration AND build, or
+    None."""
+    for f, d in _matching_summaries(key):
+        v = d.get("kernel_avg_us", {}).get(stage)
+        if v is not None:
+            return float(v), os.path.relpath(f, ROOT)
+    return None
+
+
+def make_roofline(stage: str, by: float, events_ms: float, key: dict, src: str, per: float = 1.0,
                   stream_read: float | None = None, design_by: float | None = None) -> dict:
-    """`by` bytes in `avg_ms`; `per` = launches those cover (PMC values are per
-    launch); `stream_read`: streamed read bytes per launch (stream_read_bytes)
-    -- given, traffic uses the gather calibration instead of doubling every
-    fetched byte."""
+    """`by` = SURVEY §8(d) algorithmic bytes (algorithmic_bytes) of `per`
+    launches of `stage`.  The duration is the rocprofv3 kernel-trace mean of
+    the SAME build and configuration (profiles/*pmc_summary.json
+    kernel_avg_us, x per) when one is committed -- so frac = bytes / that
+    mean / 8 TB/s can be reproduced from profiles/ alone -- else this run's
+    HIP-event mean; both timings are in the line.  `stream_read`: streamed
+    read bytes per launch (stream_read_bytes) -- given, traffic uses the
+    gather calibration instead of doubling every fetched byte."""
+    rp = load_kernel_avg_us(stage, key)
+    if rp is not None:
+        avg_ms, avg_src = rp[0] * 1e-3 * per, f"rocprofv3 kernel trace, {rp[1]}"
+    else:
+        avg_ms, avg_src = events_ms, f"HIP events ({src}); no rocprofv3 summary of this build"
     ach = by / (avg_ms * 1e-3) / 1e9
     tr = load_pmc(stage, key, "per_launch_hbm_bytes")
     traffic = tr[0] * per if tr else None
@@ -249,8 +279,9 @@ def make_roofline(stage: str, by: float, avg_ms: float, key: dict, src: str, per
         calib = (1024.0 * (raw[0] + raw[1]) + 0.5 * stream_read) * per
     r = {"kernel": stage, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": calib if calib is not None else traffic,
-         "traffic_source": tr[1] if tr else None, "algorithmic_bytes": by, "avg_ms": round(avg_ms, 4), "events": src,
-         "build": build_digest()}
+         "traffic_source": tr[1] if tr else None, "algorithmic_bytes": by,
+         "bytes_definition": "SURVEY.md §8(d) reference-stage bytes", "avg_ms": round(avg_ms, 4),
+         "avg_ms_source": avg_src, "avg_ms_events": round(events_ms, 4), "events": src, "build": build_digest()}
     if design_by is not None:  # what this design's kernel must move (design_bytes)
         r["design_bytes"] = design_by
         r["design_frac"] = round(design_by / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
@@ -300,6 +331,8 @@ def cpu_baselines(sc, cam) -> dict:
             "sample": f"one full {W}x{H} view, {P} Gaussians, fwd+bwd, CPU oracle (C, OpenMP, {n} threads): "
                       f"{dtn:.2f} s",
             "host_cpus": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "cores_note": ("all the cores this job may use: the GPU pool gives a one-GPU job 16 host CPUs "
+                           "(OMP_NUM_THREADS=16 there) although its affinity mask lists the whole host"),
             "single_thread": {"value": v1, "cores": 1, "seconds": round(dt1, 2)}}
 
 
@@ -404,7 +437,7 @@ def stage_table(prof: dict, steps: int, P, ws, views=1, key: dict | None = None)
             st = {"avg_ms": ms / cnt, "launches": cnt, "ms_per_step": ms / steps}
             b = algorithmic_bytes(name, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"], views)
             st["algorithmic_GBps"] = round(b / (st["avg_ms"] * 1e-3) / 1e9, 1) if b else None
-            db = design_bytes(name, P, ws["V"]) if views == 1 else None
+            db = design_bytes(name, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"]) if views == 1 else None
             if db is not None:
                 st["design_GBps"] = round(db / (st["avg_ms"] * 1e-3) / 1e9, 1)
             sr = stream_read_bytes(name, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"], views)
@@ -481,7 +514,7 @@ def run_fwd_bwd(cfg_name: str, ctx: Ctx, steps: int, warmup: int) -> dict:
         by = algorithmic_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"])
         roofline = make_roofline(dom, by, avg_ms, config_key(P, W, H, 16), src,
                                  stream_read=stream_read_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"]),
-                                 design_by=design_bytes(dom, P, ws["V"]))
+                                 design_by=design_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"]))
     res.update({
         "config": {"workload": f"{cfg_name}: {P} Gaussians, {W}x{H}, 16x16 tiles, forward+backward, 1 view per "
                                f"GPU per step", "P": P, "width": W, "height": H, "views_per_gpu_per_step": 1,

@@ -26,6 +26,7 @@
 // reference's dL_dmeans2D / dL_dconic / dL_dopacity / dL_dcolors layout from
 // grad_accum, and writes every output element (zeros included).
 #include <algorithm>
+#include <type_traits>
 
 #include "gs_blend.cuh"
 #include "gs_device.cuh"
@@ -50,6 +51,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const uint32_t* __restrict__ bucket_list, const uint8_t* __restrict__ hit_codes, const uint32_t* __restrict__ hdr) {
 #pragma clang fp contract(fast)
     static_assert(!kSel || (kWaves == 1 && kSwap), "the select form is the 1-wave transposed-sum geometry");
+    constexpr bool kStaged = kSel >= 2;  // staged sums (kSel 2, 3)
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
     // (x, y, r, g) and the scaled conic / opacity as two b128 reads, b as one
@@ -62,7 +64,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // the flush; 4 row partials would double the LDS footprint and cost
     // workgroups per CU); several waves add into one row with LDS atomics
     constexpr int kRowsPerG = (kWaves == 1 && !kSwap) ? 2 : 1;
-    __shared__ float s_acc[kB * kRowsPerG * kAccRow + (kSel == 2 ? 1 : 0)];  // (+ a dummy entry: kSel == 2)
+    __shared__ float s_acc[kB * kRowsPerG * kAccRow + (kStaged ? 1 : 0)];  // (+ a dummy entry: staged sums)
     __shared__ uint64_t s_bal[4 * kWaves];
     // kSel == 2: the per-Gaussian sums are finished in groups of 7 Gaussians --
     // each visit parks its two transposed registers (16 column partials of
@@ -75,7 +77,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // A g8 lane's 4 partials are its first float4; its other three stay zero.
     constexpr int kStageSlots = 7;
     constexpr int kStagePitch = 272;
-    __shared__ __attribute__((aligned(16))) float s_stage[kSel == 2 ? 3 * kStagePitch + 256 : 1];
+    __shared__ __attribute__((aligned(16))) float s_stage[kStaged ? 3 * kStagePitch + 256 : 1];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -195,6 +197,21 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         for (int off = 32; off >= 1; off >>= 1) g = max(g, (uint32_t)__shfl_xor((int)g, off, 64));
         group_last[k] = __builtin_amdgcn_readfirstlane((int)g);
     }
+    // kSel 3: the smallest n_contrib of each row group's image pixels (pixels
+    // outside the image count as started: their T and dL/dpix are 0, so any
+    // finite alpha leaves their terms 0).  Entries with contributor below it
+    // are taken by every pixel of the group: no per-pixel contributor test.
+    uint32_t min_last = 0xffffffffu;
+    if constexpr (kSel == 3) {
+#pragma unroll
+        for (int k = 0; k < kPPL; k++) {
+            uint32_t g = px.inside[k] ? last[k] : 0xffffffffu;
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) g = min(g, (uint32_t)__shfl_xor((int)g, off, 64));
+            min_last = min(min_last, g);
+        }
+        min_last = (uint32_t)__builtin_amdgcn_readfirstlane((int)min_last);
+    }
     // AMR: no per-tile max_contrib was recorded for the sub-lattice; with one
     // wave per block (the only AMR instantiation) the wave max is the block's
     if constexpr (kAMR) {
@@ -240,7 +257,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // reduce output: row jj's entry st_q; lane 63 (no slot) sums zeros into a
     // dummy row, so a full group's pass needs no lane mask
     const int st_mul = lane == 63 ? 0 : kAccRow, st_base = lane == 63 ? kB * kAccRow : st_q;
-    if constexpr (kSel == 2) {
+    if constexpr (kStaged) {
         for (int i = lane; i < 3 * kStagePitch + 256; i += 64) s_stage[i] = 0.f;
     }
     // writer lane: row r = lane / 16 of za / zb holds values swap_sum_slot(r) /
@@ -253,12 +270,16 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         const int cnt = min(kB, top);
         __syncthreads();
         uint32_t gm = 0;
+        bool fastg = false;  // kSel 3: p2 <= 0 at every pixel of the tile, provably (below)
         if (tid < cnt) {
             const float2 xy = nxy;
             const float4 co = nco;
+            const float4 pc = splat_coef(co);
             s_a[tid] = make_float4(xy.x, xy.y, nrgb[0], nrgb[1]);
-            s_co[tid] = splat_coef(co);
+            s_co[tid] = pc;
             s_b[tid].x = nrgb[2];
+            if constexpr (kSel == 3)  // the reference's `power > 0` skip cannot fire (gs_blend.cuh)
+                fastg = splat_form_safe(pc, fabsf(xy.x - (float)ox), fabsf(xy.y - (float)oy));
             gm = use_codes ? (uint32_t)hit_codes[range.x + top - 1 - tid]
                  : cull ? splat_group_mask(xy, co, (float)ox, (float)oy, (float)pstride) : 0xfu;
         }
@@ -266,6 +287,10 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         const bool has_next = ntop > 0 && tid < min(kB, ntop);
         if (has_next) nid = point_list[range.x + ntop - 1 - tid];
         publish_group_masks<kWaves>(gm, s_bal);
+        const uint64_t fast_mask = kSel == 3 ? uniform_u64(__ballot(fastg)) : 0ull;  // (kWaves == 1: slot = lane)
+        // every contributor of this batch (<= top - 1) below every row group's
+        // smallest n_contrib: all pixels take its entries
+        const bool bstarted = kSel == 3 && (uint32_t)(top - 1) < min_last;
         if (kWaves > 1)
             for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
         uint64_t written = 0;  // kWaves == 1: batch slots whose partial rows were stored
@@ -309,7 +334,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
           // wave's pixels.  (Reading the next set bit's record ahead, in two
           // register sets used in turn, measured no faster: the 4 waves per
           // SIMD already hide the LDS latency.)
-          auto visit = [&](const int cbit, const float2 xy, const float4 pc, const float4 cf) {
+          auto visit = [&](const int cbit, const float2 xy, const float4 pc, const float4 cf, auto kFastT,
+                           auto kStartedT) {
+            constexpr bool kFast = decltype(kFastT)::value, kStarted = decltype(kStartedT)::value;
             const int j = 64 * c + cbit;
             const uint32_t contributor = (uint32_t)(top - 1 - j);
             const float dx = xy.x - px.x;
@@ -320,9 +347,48 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             // so it sums s0 = sum t, s1 = sum t dy, s2 = sum t dy^2 and forms
             // the six moments (s0, dx s0, s1, dx^2 s0, dx s1, s2) once; the flush
             // applies o, the conic and the constants.
-            float c0 = 0.f, c1 = 0.f, c2 = 0.f, s0 = 0.f, s1 = 0.f, s2 = 0.f;
+            // (-0: x + -0 == x for every x, so the first visited row group's
+            // fma(a, b, -0) / -0 + t fold to a plain v_mul / move instead of a
+            // 3-operand fma with an inline 0)
+            float c0 = -0.f, c1 = -0.f, c2 = -0.f, s0 = -0.f, s1 = -0.f, s2 = -0.f;
             bool any = false;
-            if constexpr (kSel) {
+            if constexpr (kSel == 3) {
+                // kSel 2 with the selects on an SGPR-pair mask (gs_sel2_zero_v) and
+                // only the compares the entry needs: alpha >= 1/255 always;
+                // contributor < n_contrib unless the batch is started for every
+                // pixel; power > 0 only for Gaussians not provably negative
+                // definite (fast_mask).
+#pragma unroll
+                for (int k = 0; k < kPPL; k++) {
+                    if (!((mk[k] >> cbit) & 1ull)) continue;  // wave-uniform
+                    const float dy = xy.y - (py0 + (float)(4 * k * (int)pstride));
+                    const float p2 = splat_p2(pa, pb, dy, pc);
+                    const float Gr = splat_exp(p2);
+                    const float ar = fminf(0.99f, pc.w * Gr);
+                    uint64_t msk = __builtin_amdgcn_fcmpf(ar, 1.0f / 255.0f, kFcmpUGE);
+                    if (!kFast || !kStarted) msk &= __builtin_amdgcn_uicmp(contributor, last[k], kIcmpULT);
+                    if (!kFast) msk &= __builtin_amdgcn_fcmpf(p2, 0.0f, kFcmpULE);
+                    float G, alpha;
+                    gs_sel2_zero_v(msk, Gr, ar, G, alpha);
+                    const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
+                    T[k] = T[k] * rinv;
+                    const float dchannel_dcolor = alpha * T[k];
+                    const float diff = __builtin_fmaf(cf.z, dpx[k][2],
+                                                      __builtin_fmaf(cf.y, dpx[k][1],
+                                                                     __builtin_fmaf(cf.x, dpx[k][0], -acc_dot[k])));
+                    const float dL_dalpha = diff * T[k];
+                    acc_dot[k] = __builtin_fmaf(alpha, diff, acc_dot[k]);
+                    c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
+                    c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
+                    c2 = __builtin_fmaf(dchannel_dcolor, dpx[k][2], c2);
+                    const float t = G * dL_dalpha;
+                    const float tdy = t * dy;
+                    s0 += t;
+                    s1 += tdy;
+                    s2 = __builtin_fmaf(tdy, dy, s2);
+                }
+                any = true;
+            } else if constexpr (kSel) {
                 // Select form: a rejected pixel takes alpha = G = 0, i.e.
                 // rinv = 1 (T unchanged), dchannel = t = 0 and acc_dot += 0 --
                 // the same bits as the branchy form for every accepted pixel, no
@@ -406,7 +472,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             g[7] = dx * s1;
             g[8] = s2;
             if (kSel ? any : __ballot(any) != 0ull) {  // wave-uniform
-                if constexpr (kSel == 2) {
+                if constexpr (kStaged) {
                     float za, zb;
                     swap_rows8_pk(g, za, zb);
                     float* st = &s_stage[st_dst + 36 * nst];
@@ -457,15 +523,28 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 }
             }
           };
+          using T1 = std::integral_constant<bool, true>;
+          using T0 = std::integral_constant<bool, false>;
           while (todo) {
             const int cbit = __builtin_ctzll(todo);
             todo &= todo - 1;
             const int j = 64 * c + cbit;
             const float4 a4 = s_a[j];
-            visit(cbit, make_float2(a4.x, a4.y), s_co[j], make_float4(a4.z, a4.w, s_b[j].x, 0.f));
+            const float2 xy = make_float2(a4.x, a4.y);
+            const float4 pc = s_co[j], cf = make_float4(a4.z, a4.w, s_b[j].x, 0.f);
+            if constexpr (kSel == 3) {
+                if ((fast_mask >> cbit) & 1ull) {  // wave-uniform
+                    if (bstarted) visit(cbit, xy, pc, cf, T1{}, T1{});
+                    else visit(cbit, xy, pc, cf, T1{}, T0{});
+                } else {
+                    visit(cbit, xy, pc, cf, T0{}, T0{});
+                }
+            } else {
+                visit(cbit, xy, pc, cf, T0{}, T0{});
+            }
           }
         }
-        if constexpr (kSel == 2) {
+        if constexpr (kStaged) {
             if (nst) stage_reduce(nst);
         }
         __syncthreads();
@@ -582,6 +661,7 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         case 5: GS_BWD_LAUNCH(4, 1, 5, true); break;  // 96 VGPRs: 5 waves per SIMD
         case 6: GS_BWD_LAUNCH(4, 1, 4, true, false, 1); break;  // select form
         case 7: GS_BWD_LAUNCH(4, 1, 4, true, false, 2); break;  // select form, staged sums
+        case 8: GS_BWD_LAUNCH(4, 1, 4, true, false, 3); break;  // 7 + SGPR-mask selects, per-entry compares
         default: GS_BWD_LAUNCH(4, 1, 4, true); break;
     }
 #undef GS_BWD_LAUNCH

@@ -686,9 +686,12 @@ bool band_lds_fits() {
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return false;
     int v = g_band_fits[dev].load(std::memory_order_relaxed);
     if (v == 0) {
+        // the opt-in maximum (what hipFuncSetAttribute may grant), not the
+        // 64-KiB default per-block figure
         int cap = 0;
-        const bool ok = hipDeviceGetAttribute(&cap, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
-                        (size_t)cap >= kBandLdsMax;
+        if (hipDeviceGetAttribute(&cap, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess || cap <= 0)
+            cap = 0;
+        const bool ok = (size_t)cap >= kBandLdsMax;
         v = ok ? 1 : 2;
         g_band_fits[dev].store(v, std::memory_order_relaxed);
     }

@@ -60,6 +60,60 @@ __device__ __forceinline__ float splat_p2(float dx, float dy, float4 pc) {
 // few ulp).
 __device__ __forceinline__ float splat_exp(float p2) { return __builtin_amdgcn_exp2f(p2); }
 
+// ---------------------------------------------------- SGPR-mask selects
+// The compiler's selects take their condition in VCC (VOP2 v_cndmask_b32);
+// on gfx950 that form issues at ~15.5 cycles per wave instruction, the e64
+// form with the lane mask in an SGPR pair at ~4.3 (tools/valu_rate.hip,
+// profiles/r04a_valu_rate.log).  These helpers select on a 64-bit lane mask
+// from __builtin_amdgcn_fcmpf / _uicmp (v_cmp_*_e64 into an SGPR pair).  The
+// "_v" forms start with s_nop 1: a mask written by a VALU compare and read as
+// a lane mask by a VALU needs 2 wait states on gfx950 (the compiler inserts
+// them for its own selects, but cannot see into the asm).  Masks made by SALU
+// (s_and / s_andn2 of compare masks) need none.
+constexpr int kFcmpOLT = 4, kFcmpUGE = 11, kFcmpULE = 13, kIcmpULT = 36;
+
+__device__ __forceinline__ float gs_sel_v(uint64_t m, float t, float f) {  // m ? t : f
+    float r;
+    asm("s_nop 1\n\tv_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(t), "v"(f), "s"(m));
+    return r;
+}
+__device__ __forceinline__ float gs_sel_s(uint64_t m, float t, float f) {  // (mask from SALU)
+    float r;
+    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(t), "v"(f), "s"(m));
+    return r;
+}
+__device__ __forceinline__ uint32_t gs_sel_s_u32(uint64_t m, uint32_t t, uint32_t f) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(t), "v"(f), "s"(m));
+    return r;
+}
+// m ? -|x| : t (the select form's "finished" transmittance)
+__device__ __forceinline__ float gs_sel_v_negabs(uint64_t m, float x, float t) {
+    float r;
+    asm("s_nop 1\n\tv_cndmask_b32_e64 %0, %2, -|%1|, %3" : "=v"(r) : "v"(x), "v"(t), "s"(m));
+    return r;
+}
+// (m ? x : 0, m ? y : 0)
+__device__ __forceinline__ void gs_sel2_zero_v(uint64_t m, float x, float y, float& rx, float& ry) {
+    asm("s_nop 1\n\t"
+        "v_cndmask_b32_e64 %0, 0, %2, %4\n\t"
+        "v_cndmask_b32_e64 %1, 0, %3, %4"
+        : "=&v"(rx), "=&v"(ry)
+        : "v"(x), "v"(y), "s"(m));
+}
+
+// p2 <= 0 at every pixel, provably: the scaled form hx dx^2 + ny dx dy + hz
+// dy^2 (pc = splat_coef) is negative definite when hx, hz < 0 and ny^2 <
+// 0.998 * 4 hx hz; then its exact value is <= -(1 - 0.999) (|hx| dx^2 + |hz|
+// dy^2) while the rounding of its evaluation (two fmas after two products)
+// is < 1e-6 of that sum -- the computed p2 is never > 0, so the reference's
+// `power > 0` skip cannot fire.  Coefficients and the offset to the block
+// (ax, ay) bounded: every term < 1e19, nothing overflows.
+__device__ __forceinline__ bool splat_form_safe(float4 pc, float ax, float ay) {
+    return pc.x < 0.f && pc.z < 0.f && pc.y * pc.y < 0.998f * 4.0f * (pc.x * pc.z) && pc.x > -1e6f &&
+           pc.z > -1e6f && fabsf(pc.y) < 1e6f && ax < 1e6f && ay < 1e6f;
+}
+
 // 16x16 block at (ox, oy) with pixel stride `st` (1 = base, 2 = AMR sub-lattice).
 template <int kPPL, int kWaves>
 __device__ __forceinline__ PixelSetT<kPPL> make_pixels_t(int W, int H, uint32_t ox, uint32_t oy, uint32_t st) {
@@ -318,7 +372,35 @@ __device__ __forceinline__ bool blend_one_sel2(float2 xy, float4 co, float4 f, f
     return blended;
 }
 
-template <int kPPL, int kWaves, bool kSel = false>
+// blend_one_sel2 with every select on an SGPR-pair lane mask and only the
+// tests the entry needs (`safe`: splat_form_safe, no `power > 0` test).  The
+// stop test and "blended" come out as masks: blended = accepted & !stop (the
+// same lanes as blend_one_sel2's a != 0 -- an accepted alpha is >= 1/255 and
+// never NaN: fminf returns the number).  Returns the blended mask.
+__device__ __forceinline__ uint64_t blend_one_msk(float2 xy, float4 co, float4 f, float pxx, float pxy, uint32_t lo,
+                                                  float& T, float (&C)[3], uint32_t& last_lo, bool safe) {
+    const float dx = xy.x - pxx, dy = xy.y - pxy;
+    const float p = splat_p2(dx, dy, co);
+    const float ar = fminf(0.99f, co.w * splat_exp(p));
+    uint64_t acc = __builtin_amdgcn_fcmpf(ar, 1.0f / 255.0f, kFcmpUGE);  // !(alpha < 1/255)
+    if (!safe) acc &= __builtin_amdgcn_fcmpf(p, 0.0f, kFcmpULE);         // !(power > 0)
+    const float a1 = gs_sel_v(acc, ar, 0.0f);
+    const float test_T = T * (1.0f - a1);
+    const uint64_t stop = __builtin_amdgcn_fcmpf(test_T, 0.0001f, kFcmpOLT);  // true for every finished pixel
+    const uint64_t blended = acc & ~stop;
+    const float w = gs_sel_s(blended, a1, 0.0f) * T;
+    C[0] = __builtin_fmaf(f.x, w, C[0]);
+    C[1] = __builtin_fmaf(f.y, w, C[1]);
+    C[2] = __builtin_fmaf(f.z, w, C[2]);
+    T = gs_sel_v_negabs(stop, T, test_T);
+    last_lo = gs_sel_s_u32(blended, lo, last_lo);
+    return blended;
+}
+
+// kSel: 0 branchy, 1 select form (blend_one_sel2), 2 SGPR-mask select form
+// (blend_one_msk; s_bal then holds kWaves more words: the batch's per-64-slot
+// masks of splat_form_safe Gaussians at s_bal[4 kWaves + c])
+template <int kPPL, int kWaves, int kSel = 0>
 __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const PixelSetT<kPPL>& px, float ox, float oy,
                                                           float st, const uint32_t* __restrict__ point_list,
                                                           const float2* __restrict__ means2D,
@@ -372,6 +454,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
         }
         if (rec && b0 > 0) flush_codes(b0 - kB);  // the previous batch's codes (s_hit rewritten after the next barrier)
         uint32_t gm = 0;
+        bool safe = false;
         if (b0 + tid < n) {
             const uint32_t id = point_list[range.x + b0 + tid];
             const float2 xy = means2D[id];
@@ -382,8 +465,13 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
             s_co[tid] = splat_coef(co);
             s_b[tid * (kSel ? 4 : 1)] = features[3 * id + 2];  // (kSel: at a 16-B stride, one address for all reads)
             gm = cull ? splat_group_mask(xy, co, ox, oy, st) : 0xfu;
+            if (kSel == 2) safe = splat_form_safe(splat_coef(co), fabsf(xy.x - ox), fabsf(xy.y - oy));
         }
         publish_group_masks<kWaves>(gm, s_bal);
+        if (kSel == 2) {
+            const uint64_t sb = __ballot(safe);
+            if ((tid & 63) == 0) s_bal[4 * kWaves + (tid >> 6)] = sb;
+        }
         __syncthreads();
         if (rec && (tid & 63) == 0)
 #pragma unroll
@@ -398,6 +486,45 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
             for (int k = 0; k < kPPL; k++) {
                 mk[k] = uniform_u64(s_bal[c * 4 + wave * kPPL + k]);
                 todo |= mk[k];
+            }
+            if constexpr (kPPL == 1 && kSel == 2) {
+                // SGPR-mask select form (blend_one_msk), two Gaussians per
+                // iteration, as the kSel 1 loop below
+                const uint64_t safe_m = uniform_u64(s_bal[4 * kWaves + c]);
+                uint64_t hits = 0;
+                uint32_t last_lo = ~0u;
+                const char* sa = reinterpret_cast<const char*>(s_a);
+                const char* sco = reinterpret_cast<const char*>(s_co);
+                const char* sb = reinterpret_cast<const char*>(s_b);
+                while (todo) {
+                    const uint32_t bA = (uint32_t)__builtin_ctzll(todo);
+                    todo &= todo - 1;
+                    const bool two = todo != 0;  // wave-uniform
+                    const uint32_t bB = two ? (uint32_t)__builtin_ctzll(todo) : bA;
+                    if (two) todo &= todo - 1;
+                    const uint32_t loA = (c * 64 + bA) * 16, loB = (c * 64 + bB) * 16;
+                    const float4 sA = *reinterpret_cast<const float4*>(sa + loA);
+                    const float4 sB = *reinterpret_cast<const float4*>(sa + loB);
+                    const float4 coA = *reinterpret_cast<const float4*>(sco + loA);
+                    const float4 coB = *reinterpret_cast<const float4*>(sco + loB);
+                    const float bAc = *reinterpret_cast<const float*>(sb + loA);
+                    const float bBc = *reinterpret_cast<const float*>(sb + loB);
+                    const uint64_t hA = blend_one_msk(make_float2(sA.x, sA.y), coA, make_float4(sA.z, sA.w, bAc, 0.f),
+                                                      px.x, px.y[0], loA, st_.T[0], st_.C[0], last_lo,
+                                                      (safe_m >> bA) & 1ull);
+                    if (kRec) hits |= hA != 0ull ? 1ull << bA : 0ull;
+                    if (two) {
+                        const uint64_t hB = blend_one_msk(make_float2(sB.x, sB.y), coB,
+                                                          make_float4(sB.z, sB.w, bBc, 0.f), px.x, px.y[0], loB,
+                                                          st_.T[0], st_.C[0], last_lo, (safe_m >> bB) & 1ull);
+                        if (kRec) hits |= hB != 0ull ? 1ull << bB : 0ull;
+                    }
+                }
+                if (last_lo != ~0u) st_.last[0] = b0 + (last_lo >> 4) + 1;
+                if (rec && (tid & 63) == 0) s_hit[c * kWaves + wave] = hits;
+                done[0] = st_.T[0] < 0.0f;
+                if (__ballot(!done[0]) == 0ull) wave_alive = false;
+                continue;
             }
             if constexpr (kPPL == 1 && kSel) {
                 // select form (blend_one_sel2), two Gaussians per iteration; the

@@ -43,7 +43,7 @@ __device__ __forceinline__ void write_pixels(const PixelSetT<kPPL>& px, const Bl
 }
 
 // One 16x16 tile per workgroup of kWaves waves (kPPL pixels per lane).
-template <int kPPL, int kWaves, int kMinWaves = 1, bool kSel = false>
+template <int kPPL, int kWaves, int kMinWaves = 1, int kSel = 0>
 __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
                                                                  const uint32_t* __restrict__ point_list,
                                                                  const float2* __restrict__ means2D,
@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
     __shared__ float4 s_a[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
     __shared__ __attribute__((aligned(16))) float s_b[64 * kWaves * (kSel ? 4 : 1)];  // (kSel: 16-B stride)
-    __shared__ uint64_t s_bal[4 * kWaves];
+    __shared__ uint64_t s_bal[(kSel == 2 ? 5 : 4) * kWaves];  // (kSel 2: + the safe-form masks)
     __shared__ uint64_t s_hit[kWaves * kWaves];
     __shared__ uint32_t s_max;
     if (kWaves > 1 && threadIdx.x == 0) s_max = 0;
@@ -154,8 +154,9 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
         case 2: GS_FWD_LAUNCH(1, 4); break;
         case 3: GS_FWD_LAUNCH(1, 4, 8); break;  // <= 64 VGPRs: 8 waves per SIMD
         case 4: GS_FWD_LAUNCH(1, 4, 6); break;
-        case 6: GS_FWD_LAUNCH(1, 4, 1, true); break;
-        default: GS_FWD_LAUNCH(1, 4, 8, true); break;  // 5: 3 + the select-form blend
+        case 6: GS_FWD_LAUNCH(1, 4, 1, 1); break;
+        case 7: GS_FWD_LAUNCH(1, 4, 8, 2); break;  // 5 with SGPR-mask selects (gs_blend.cuh blend_one_msk)
+        default: GS_FWD_LAUNCH(1, 4, 8, 1); break;  // 5: 3 + the select-form blend
     }
 #undef GS_FWD_LAUNCH
     return zero_n4 > 0;

@@ -667,6 +667,11 @@ py::dict ParseBuffers(const Tensor& geomBuffer, const Tensor& binningBuffer, con
     }
     if (K > 0) {
         d["point_list"] = view(b.point_list, {K}, i32);
+        // the forward's per-instance row-group hit codes (base grid; valid when hdr[kHdrHitCodes] == 1)
+        // (gs_layout.h hit_codes_at: right after point_list, 256-B aligned)
+        if (tile == 16)
+            d["hit_codes"] = view(reinterpret_cast<uint8_t*>(b.point_list) + ((sizeof(uint32_t) * (size_t)K + 255) & ~(size_t)255),
+                                  {K}, o.dtype(torch::kUInt8));
         Tensor keys = torch::empty({K}, o.dtype(torch::kInt64));
         check(gs_reconstruct_keys(reinterpret_cast<char*>(geomBuffer.data_ptr()),
                                   reinterpret_cast<char*>(binningBuffer.data_ptr()),

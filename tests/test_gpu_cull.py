@@ -140,3 +140,57 @@ def test_cull_is_exact_amr_render_once():
     finally:
         C.set_tuning("cull", 1)
     np.testing.assert_array_equal(imgs[0], imgs[1])
+
+
+@pytest.mark.parametrize("P,W,H,seed", [(6000, 256, 192, 1), (30000, 320, 200, 2)])
+def test_sgpr_mask_backward_matches_select_form(P, W, H, seed):
+    """Backward variant 8 (SGPR-mask selects; the power > 0 test dropped for
+    Gaussians whose form is provably negative definite; the contributor test
+    dropped in batches every pixel has started) against variant 7 on the
+    adversarial scene (huge thin splats, near-degenerate conics): the blend
+    sums agree to float-atomic ordering noise."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    sc, cam = _adversarial_scene(P, W, H, seed)
+    dpix = torch.from_numpy(S.make_cotangent(H, W, seed + 1)).cuda()
+    res = {}
+    try:
+        for v in (7, 8):
+            s, t, out, _bufs = _forward(sc, cam, 5)
+            res[v] = _backward(s, t, out, dpix, v)
+    finally:
+        C.set_tuning("fwd_variant", -1)
+        C.set_tuning("bwd_variant", -1)
+    for i in range(3):  # dL_dmeans2D, dL_dcolors, dL_dopacity
+        assert G.rel_err(res[8][0][i], res[7][0][i]) < 5e-6, i
+    assert G.rel_err(res[8][1], res[7][1]) < 5e-6
+
+
+@pytest.mark.parametrize("P,W,H,seed,adv", [(6000, 256, 192, 1, True), (30000, 320, 200, 2, True),
+                                            (10000, 256, 256, 0, False)])
+def test_sgpr_mask_forward_bit_identical(P, W, H, seed, adv):
+    """Forward variant 7 (SGPR-mask selects, no power > 0 test for provably
+    negative-definite forms) against variant 5 (the select form): image,
+    final T, n_contrib, max_contrib and the backward's hit codes bit for bit,
+    on the adversarial scene (huge thin splats, opacities at 1/255) and the
+    default one."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    if adv:
+        sc, cam = _adversarial_scene(P, W, H, seed)
+    else:
+        cam = S.make_camera(W, H)
+        sc = S.make_scene(P, cam, seed=seed)
+    res = {}
+    try:
+        for v in (5, 7):
+            s, t, out, bufs = _forward(sc, cam, v)
+            K = int(out[0])
+            codes = C.parse_buffers(out[3], out[4], out[5], P, K, W, H, 16)["hit_codes"]
+            res[v] = (out[1].cpu().numpy(), {k: b.cpu().numpy() for k, b in bufs.items()}, codes.cpu().numpy())
+    finally:
+        C.set_tuning("fwd_variant", -1)
+    np.testing.assert_array_equal(res[5][0], res[7][0])
+    for k in res[5][1]:
+        np.testing.assert_array_equal(res[5][1][k], res[7][1][k], err_msg=k)
+    np.testing.assert_array_equal(res[5][2], res[7][2])

@@ -63,6 +63,13 @@
 #define OP_MUL_SALU(i) "v_mul_f32 %" #i ", %" #i ", %16\ns_add_u32 s42, s42, 1\n"
 #define OP_MUL_2SALU(i) "v_mul_f32 %" #i ", %" #i ", %16\ns_add_u32 s42, s42, 1\ns_and_b64 s[40:41], s[40:41], vcc\n"
 
+#define OP_CNDE(i) "v_cndmask_b32_e64 %" #i ", %" #i ", %16, vcc\n"
+#define OP_MINK(i) "v_min_f32 %" #i ", 0x3f7d70a4, %" #i "\n"
+#define OP_MAX(i) "v_max_f32 %" #i ", %" #i ", %16\n"
+#define OP_SUBR(i) "v_sub_f32 %" #i ", 1.0, %" #i "\n"
+// the kernels' pattern: one compare feeding two selects
+#define OP_CMP_CND2(i) "v_cmp_lt_f32 vcc, %" #i ", %16\nv_cndmask_b32 %" #i ", 0, %" #i ", vcc\nv_cndmask_b32 v41, 0, %" #i ", vcc\n"
+#define OP_CMP_CND2S(i) "v_cmp_lt_f32_e64 s[40:41], %" #i ", %16\nv_cndmask_b32_e64 %" #i ", 0, %" #i ", s[40:41]\nv_cndmask_b32_e64 v41, 0, %" #i ", s[40:41]\n"
 #define PRE "v_mov_b32 v40, 1.0\nv_mov_b32 v41, 1.0\ns_mov_b32 s44, 0.5\n"
 // (each body twice per iteration: 32 instructions against the loop's 3 SALU)
 #define TWICE(OP) PRE R16(OP) R16(OP)
@@ -86,6 +93,12 @@ BODY_KERNEL(k_cnd_salu, PRE "s_mov_b64 vcc, -1\n" R16(OP_CND) R16(OP_CND), 32)
 BODY_KERNEL(k_cmp, TWICE(OP_CMP), 32)
 BODY_KERNEL(k_cmps, TWICE(OP_CMPS), 32)
 BODY_KERNEL(k_dpp, TWICE(OP_DPP), 32)
+BODY_KERNEL(k_cnde, PRE "v_cmp_lt_f32 vcc, %16, v40\n" R16(OP_CNDE) R16(OP_CNDE), 32)
+BODY_KERNEL(k_mink, TWICE(OP_MINK), 32)
+BODY_KERNEL(k_max, TWICE(OP_MAX), 32)
+BODY_KERNEL(k_subr, TWICE(OP_SUBR), 32)
+BODY_KERNEL(k_cmpcnd2, PRE R16(OP_CMP_CND2), 48)
+BODY_KERNEL(k_cmpcnd2s, PRE R16(OP_CMP_CND2S), 48)
 BODY_KERNEL(k_fma_salu, TWICE(OP_FMA_SALU), 32)
 BODY_KERNEL(k_mul_salu, TWICE(OP_MUL_SALU), 32)
 BODY_KERNEL(k_mul_2salu, PRE "s_mov_b64 vcc, -1\n" R16(OP_MUL_2SALU) R16(OP_MUL_2SALU), 32)
@@ -131,6 +144,9 @@ static const Body kBodies[] = {
     {"v_cndmask_b32 (vcc from v_cmp)", k_cnd, 34}, {"v_cndmask_b32_e64 (sgpr from v_cmp)", k_cnds, 34},
     {"v_cndmask_b32 (vcc from s_mov)", k_cnd_salu, 34}, {"v_cmp_lt_f32 (vcc)", k_cmp, 34},
     {"v_cmp_lt_f32 (sgpr)", k_cmps, 34},  {"v_add_f32_dpp row_shr", k_dpp, 34},
+    {"v_cndmask_b32_e64 (vcc from v_cmp)", k_cnde, 34}, {"v_min_f32 literal", k_mink, 34},
+    {"v_max_f32", k_max, 34},             {"v_sub_f32 1.0 - v", k_subr, 34},
+    {"v_cmp (vcc) + 2 v_cndmask_b32 (vcc)", k_cmpcnd2, 50}, {"v_cmp (sgpr) + 2 v_cndmask_b32_e64 (sgpr)", k_cmpcnd2s, 50},
     {"v_pk_fma_f32", k_pkfma, 32},        {"v_pk_mul_f32", k_pkmul, 32},       {"v_pk_add_f32", k_pkadd, 32},
     {"v_fma_f32 + s_add (1:1)", k_fma_salu, 34}, {"v_mul_f32 + s_add (1:1)", k_mul_salu, 34},
     {"v_mul_f32 + 2 SALU (1:2)", k_mul_2salu, 34},
