@@ -646,7 +646,7 @@ void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningVi
 // given colors_precomp): colours from it through point_list instead of the
 // step-0 records.
 // kPer: entries each lane stages per batch (a group stages 16 kPer)
-template <int kRounds, int kPer, int kFold = 0, bool kSelF = false>
+template <int kRounds, int kPer, int kFold = 0, int kSelF = 0>
 __global__ void __launch_bounds__(64) amr_region_render_kernel(
     int W, int H, int tgx, int T, const uint32_t* __restrict__ order, const uint32_t* __restrict__ ranges,
     const uint32_t* __restrict__ lists, const uint32_t* __restrict__ region_count,
@@ -768,6 +768,9 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
             pos[u] = i < cnt ? list[i] : 0xffffffffu;
         }
     };
+    // kSelF 2: whether every staged entry of the wave's batch has a provably
+    // negative-definite form (splat_form_safe: no power > 0 test needed)
+    const float tox = (float)((tile % tgx) * 32), toy = (float)((tile / tgx) * 32);
     auto load_rec = [&](const uint32_t (&pos)[kPer], float4 (&a)[kPer], float4 (&bb)[kPer], float (&c)[kPer]) {
 #pragma unroll
         for (int u = 0; u < kPer; u++) {
@@ -835,6 +838,15 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
                 s_c[h][l16 + 16 * u] = rc[u];
                 s_pos[h][l16 + 16 * u] = kSelF ? pos[u] + 1 : pos[u];  // (kSelF: the contributor index)
             }
+            bool batch_safe = false;
+            if constexpr (kSelF == 2) {
+                bool unsafe = false;
+#pragma unroll
+                for (int u = 0; u < kPer; u++)  // (past-the-list zero records: p = 0, alpha 0 -- no test needed)
+                    unsafe |= pos[u] != 0xffffffffu &&
+                              !splat_form_safe(rb[u], fabsf(ra[u].x - tox), fabsf(ra[u].y - toy));
+                batch_safe = __ballot(unsafe) == 0ull;
+            }
             __syncthreads();
             // the next batch's records and the one after's positions, in flight
             // while this batch is blended
@@ -845,7 +857,65 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
             // entries of this batch: [0, m) for the group, [0, mw) for the wave
             const int m = (int)min((uint32_t)kRgBatch, cnt > b0 ? cnt - b0 : 0u);
             const int mw = (int)min((uint32_t)kRgBatch, cmax - b0);
-            if constexpr (kFold > 0 && kSelF) {
+            if constexpr (kFold > 0 && kSelF == 2) {
+                // kSelF 1 with every select on an SGPR-pair lane mask
+                // (gs_blend.cuh gs_sel_*): phase 1 keeps each entry's accept mask
+                // (alpha >= 1/255, and power <= 0 unless the batch is all
+                // provably negative definite), phase 2 the stop mask; blended =
+                // accept & !stop -- the lanes of kSelF 1's av != 0.
+#pragma unroll
+                for (int j0 = 0; j0 < kRgBatch; j0 += kFold) {
+                    float al[kFold][kSlots];
+                    uint64_t accm[kFold][kSlots];
+                    float fr[kFold], fg[kFold], fb[kFold];
+                    uint32_t fp[kFold];
+#pragma unroll
+                    for (int e4 = 0; e4 < kFold; e4 += 4) {
+                        const float4 b4 = *reinterpret_cast<const float4*>(&s_c[h][j0 + e4]);
+                        const uint4 p4 = *reinterpret_cast<const uint4*>(&s_pos[h][j0 + e4]);
+                        fb[e4] = b4.x; fb[e4 + 1] = b4.y; fb[e4 + 2] = b4.z; fb[e4 + 3] = b4.w;
+                        fp[e4] = p4.x; fp[e4 + 1] = p4.y; fp[e4 + 2] = p4.z; fp[e4 + 3] = p4.w;
+                    }
+#pragma unroll
+                    for (int e = 0; e < kFold; e++) {
+                        const int j = j0 + e;
+                        const float4 a = s_a[h][j];
+                        const float4 co = s_b[h][j];
+                        fr[e] = a.z;
+                        fg[e] = a.w;
+#pragma unroll
+                        for (int k = 0; k < kSlots; k++) {
+                            if (kRounds > 1 && !active[k]) continue;  // wave-uniform (always on for one round)
+                            const float pw = splat_p2(a.x - pxx[k], a.y - pxy[k], co);
+                            const float av = fminf(0.99f, co.w * splat_exp(pw));
+                            uint64_t am = __builtin_amdgcn_fcmpf(av, 1.0f / 255.0f, kFcmpUGE);
+                            if (!batch_safe) am &= __builtin_amdgcn_fcmpf(pw, 0.0f, kFcmpULE);
+                            accm[e][k] = am;
+                            al[e][k] = gs_sel_v(am, av, 0.0f);
+                        }
+                    }
+                    bool alive = false;
+#pragma unroll
+                    for (int e = 0; e < kFold; e++) {
+#pragma unroll
+                        for (int k = 0; k < kSlots; k++) {
+                            if (kRounds > 1 && !active[k]) continue;
+                            const float test_T = T_[k] * (1.0f - al[e][k]);
+                            const uint64_t stop = __builtin_amdgcn_fcmpf(test_T, 0.0001f, kFcmpOLT);
+                            const uint64_t blended = accm[e][k] & ~stop;
+                            const float w = gs_sel_s(blended, al[e][k], 0.0f) * T_[k];
+                            C[k][0] = __builtin_fmaf(fr[e], w, C[k][0]);
+                            C[k][1] = __builtin_fmaf(fg[e], w, C[k][1]);
+                            C[k][2] = __builtin_fmaf(fb[e], w, C[k][2]);
+                            T_[k] = gs_sel_v_negabs(stop, T_[k], test_T);
+                            last[k] = gs_sel_s_u32(blended, fp[e], last[k]);
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < kSlots; k++) alive |= T_[k] > 0.0f && j0 + kFold < m;
+                    if (j0 + kFold < kRgBatch && __ballot(alive) == 0ull) break;
+                }
+            } else if constexpr (kFold > 0 && kSelF) {
                 // The fold of blend_one_sel2 (gs_blend.cuh): phase 1 turns each
                 // staged entry's alpha into its select-form value (0 when the
                 // reference skips the pair: power > 0 or alpha < 1/255; entries
@@ -1081,7 +1151,8 @@ void set_amr_batch(int v) { g_amr_batch = v == 2 ? 2 : 1; }
 int g_amr_deep = 0;
 void set_amr_deep(int v) { g_amr_deep = v; }
 int g_amr_fold = 0x1e;
-// the progressive steps' fold in the select form (amr_region_render_kernel kSelF)
+// the fold in the select form (amr_region_render_kernel kSelF): 1 compiler
+// selects, 2 SGPR-mask selects (gs_blend.cuh gs_sel_*)
 int g_amr_sel = 1;
 void set_amr_sel(int v) { g_amr_sel = v; }
 int g_amr_fold_n = 8;
@@ -1111,7 +1182,8 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
                            fused ? zero_radii : nullptr)
         if (foveaStep > 0) {
             const bool fold = (g_amr_fold >> foveaStep) & 1;
-            if (fold && g_amr_sel && ((g_amr_deep >> foveaStep) & 1)) GS_AMR_REGION(1, 2, 8, true);
+            if (fold && g_amr_sel == 2 && g_amr_fold_n == 8 && !((g_amr_deep >> foveaStep) & 1)) GS_AMR_REGION(1, 1, 8, 2);
+            else if (fold && g_amr_sel && ((g_amr_deep >> foveaStep) & 1)) GS_AMR_REGION(1, 2, 8, true);
             else if (fold && g_amr_sel && g_amr_fold_n == 16) GS_AMR_REGION(1, 1, 16, true);
             else if (fold && g_amr_sel) GS_AMR_REGION(1, 1, 8, true);
             else if (fold && ((g_amr_deep >> foveaStep) & 1)) GS_AMR_REGION(1, 2, 8);
@@ -1120,7 +1192,8 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
             else if (g_amr_batch == 2) GS_AMR_REGION(1, 2, 0);
             else GS_AMR_REGION(1, 1, 0);
         } else {
-            if ((g_amr_fold & 1) && g_amr_sel) GS_AMR_REGION(4, 1, 4, true);
+            if ((g_amr_fold & 1) && g_amr_sel == 2) GS_AMR_REGION(4, 1, 4, 2);
+            else if ((g_amr_fold & 1) && g_amr_sel) GS_AMR_REGION(4, 1, 4, true);
             else if (g_amr_fold & 1) GS_AMR_REGION(4, 1, 4);
             else if (g_amr_batch == 2) GS_AMR_REGION(4, 2, 0);
             else GS_AMR_REGION(4, 1, 0);

@@ -680,6 +680,7 @@ def test_amr_forced_banded_duplicate(name, P, W, H, seed):
 
 
 DEFAULT_AMR_LISTS_PER = 2  # render.hip g_amr_lists_per
+DEFAULT_AMR_SEL = 1  # render.hip g_amr_sel
 
 
 @pytest.mark.parametrize("P,W,H,seed", [(10000, 256, 256, 0), (60000, 160, 96, 4), (3000, 2112, 1056, 8)])
@@ -694,18 +695,21 @@ def test_amr_fold_phases_bit_identical(P, W, H, seed):
     out = {}
     # (amr_fold, amr_deep, amr_lists_per: entries per thread and pass of the
     # region-lists build -- the lists must not depend on it)
-    variants = {"loop": (0, 0, 4), "fold": (0x1e, 0, 4), "deep": (0x1e, 0x1e, 4), "lists2": (0x1e, 0, 2),
-                "lists5": (0x1e, 0, 5), "lists8": (0x1e, 0, 8)}
-    for name, (fold, deep, lper) in variants.items():
+    # (+ amr_sel: 1 the select-form fold, 2 its SGPR-mask form)
+    variants = {"loop": (0, 0, 4, 1), "fold": (0x1e, 0, 4, 1), "deep": (0x1e, 0x1e, 4, 1), "lists2": (0x1e, 0, 2, 1),
+                "lists5": (0x1e, 0, 5, 1), "lists8": (0x1e, 0, 8, 1), "mask": (0x1e, 0, 2, 2)}
+    for name, (fold, deep, lper, sel) in variants.items():
         C.set_tuning("amr_fold", fold)
         C.set_tuning("amr_deep", deep)
         C.set_tuning("amr_lists_per", lper)
+        C.set_tuning("amr_sel", sel)
         try:
             acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.2, 0.3))
         finally:
             C.set_tuning("amr_fold", 0x1e)
             C.set_tuning("amr_deep", 0)
             C.set_tuning("amr_lists_per", DEFAULT_AMR_LISTS_PER)
+            C.set_tuning("amr_sel", DEFAULT_AMR_SEL)
         d = C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)
         K = int(d["hdr"][0].item())
         d = C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
@@ -713,7 +717,7 @@ def test_amr_fold_phases_bit_identical(P, W, H, seed):
         lv = d["levels"].cpu().numpy().astype(np.uint32)
         rendered = torch.from_numpy((O.amr_pixel_rounds(W, H) <= O.amr_tile_levels_per_pixel(lv, W, H)).reshape(-1))
         out[name] = [s_.cpu() for s_ in steps] + [d["n_contrib"].cpu()[rendered], d["accum_alpha"].cpu()[rendered]]
-    for name in ("fold", "deep", "lists2", "lists5", "lists8"):
+    for name in ("fold", "deep", "lists2", "lists5", "lists8", "mask"):
         for a, b in zip(out["loop"], out[name]):
             assert torch.equal(a, b), name
 
@@ -754,6 +758,36 @@ def test_amr_render_once_interpolated(amr_variant):
     rcol, rrad, st = O.amr_render_once(os_, dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs,
                                                   scales=sc.scales, rotations=sc.rotations))
     assert G.image_l1(color.cpu().numpy(), rcol) < G.IMAGE_L1_TOL
+
+
+@pytest.mark.parametrize("P,W,H,seed", [(8000, 224, 160, 5), (60000, 160, 96, 4)])
+def test_amr_render_once_mask_select_bit_identical(P, W, H, seed):
+    """render_once (all rounds of a tile in one pass, kRounds 4) with the
+    SGPR-mask fold (amr_sel 2) against the select-form fold (amr_sel 1):
+    image, final T and n_contrib bit for bit."""
+    import oracle as O
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from diff_gaussian_rasterization_amr import GaussianRasterizer
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    s = G.torch_settings(cam, amr=True)
+    t = G.scene_tensors(sc)
+    out = {}
+    for sel in (1, 2):
+        C.set_tuning("amr_sel", sel)
+        try:
+            color, radii, gb, bb, ib = GaussianRasterizer(s)(
+                means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"],
+                shs=t["shs"], scales=t["scales"], rotations=t["rotations"], foveaStep=-2, interpolate_image=False)
+            torch.cuda.synchronize()
+        finally:
+            C.set_tuning("amr_sel", DEFAULT_AMR_SEL)
+        d = C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)
+        # pixels the call rendered (round <= level; the others are never written)
+        lv = d["levels"].cpu().numpy().astype(np.uint32)
+        rendered = torch.from_numpy((O.amr_pixel_rounds(W, H) <= O.amr_tile_levels_per_pixel(lv, W, H)).reshape(-1))
+        out[sel] = (color.cpu(), d["accum_alpha"].cpu()[rendered], d["n_contrib"].cpu()[rendered])
+    for a, b in zip(out[1], out[2]):
+        assert torch.equal(a, b)
 
 
 def test_amr_step4_interpolate():
