@@ -525,23 +525,29 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
           };
           using T1 = std::integral_constant<bool, true>;
           using T0 = std::integral_constant<bool, false>;
-          while (todo) {
-            const int cbit = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            const int j = 64 * c + cbit;
-            const float4 a4 = s_a[j];
-            const float2 xy = make_float2(a4.x, a4.y);
-            const float4 pc = s_co[j], cf = make_float4(a4.z, a4.w, s_b[j].x, 0.f);
-            if constexpr (kSel == 3) {
-                if ((fast_mask >> cbit) & 1ull) {  // wave-uniform
-                    if (bstarted) visit(cbit, xy, pc, cf, T1{}, T1{});
-                    else visit(cbit, xy, pc, cf, T1{}, T0{});
-                } else {
-                    visit(cbit, xy, pc, cf, T0{}, T0{});
-                }
-            } else {
-                visit(cbit, xy, pc, cf, T0{}, T0{});
+          // kSel 3: one copy of the loop per (all-safe, started) batch case,
+          // chosen once per batch -- per-entry branches between the visit
+          // variants made the register allocator shuffle the loop-carried
+          // pixel state (8 v_mov per entry) at every join
+          auto run = [&](auto kFastT, auto kStartedT) {
+            while (todo) {
+              const int cbit = __builtin_ctzll(todo);
+              todo &= todo - 1;
+              const int j = 64 * c + cbit;
+              const float4 a4 = s_a[j];
+              const float2 xy = make_float2(a4.x, a4.y);
+              const float4 pc = s_co[j], cf = make_float4(a4.z, a4.w, s_b[j].x, 0.f);
+              visit(cbit, xy, pc, cf, kFastT, kStartedT);
             }
+          };
+          if constexpr (kSel == 3) {
+              // every entry this wave visits has a provably negative-definite form
+              const bool bsafe = (todo & ~fast_mask) == 0ull;
+              if (bsafe && bstarted) run(T1{}, T1{});
+              else if (bsafe) run(T1{}, T0{});
+              else run(T0{}, T0{});
+          } else {
+              run(T0{}, T0{});
           }
         }
         if constexpr (kStaged) {
