@@ -178,8 +178,13 @@ def stream_read_bytes(stage: str, P: int, V: int, K: int, Kb: int, N: int, T: in
     return None
 
 
-def config_key(P: int, W: int, H: int, tile: int) -> dict:
-    return {"P": int(P), "W": int(W), "H": int(H), "tile": int(tile)}
+def config_key(P: int, W: int, H: int, tile: int, views: int = 1) -> dict:
+    """What a committed PMC summary must match: the scene, image and tile
+    size, and (config 5) the views per step."""
+    k = {"P": int(P), "W": int(W), "H": int(H), "tile": int(tile)}
+    if views != 1:
+        k["views"] = int(views)
+    return k
 
 
 def _pmc_files():
@@ -639,12 +644,13 @@ def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange
     if ctx.rank != 0:
         return res
     ws = workload_stats(views[0]["st"], params, P, W, H)
-    stages = stage_table(prof, steps, P, ws, G)
+    key5 = config_key(P, W, H, 16, G)
+    stages = stage_table(prof, steps, P, ws, G, key=key5)
     roofline = None
     if stages:
         dom = max(stages, key=lambda n: stages[n]["ms_per_step"])
         by = algorithmic_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"], G)
-        roofline = make_roofline(dom, by, stages[dom]["avg_ms"], config_key(P, W, H, 16), "stage-profile pass",
+        roofline = make_roofline(dom, by, stages[dom]["avg_ms"], key5, "stage-profile pass",
                                  stream_read=stream_read_bytes(dom, P, ws["V"], ws["K"], ws["Kb"], ws["N"], ws["T"]))
     res.update({
         "config": {"workload": f"cfg5_8view_1080p_1M: {P} Gaussians, {W}x{H}, 16x16 tiles, {G} views per step "

@@ -20,7 +20,7 @@ run() {  # name limit cmd...
   if fault "$rc"; then echo "[gpu_session] stopping after fault-type exit $rc in $name"; exit "$rc"; fi
   return 0
 }
-cfg_of() { case "$1" in *2) echo cfg2_1080p_1M;; *3) echo cfg3_amr_1080p_1M;; *4) echo cfg4_bicycle_6M;; esac; }
+cfg_of() { case "$1" in *2) echo cfg2_1080p_1M;; *3) echo cfg3_amr_1080p_1M;; *4) echo cfg4_bicycle_6M;; *5) echo cfg5_8view_1080p_1M;; esac; }
 for step in "$@"; do
   case "$step" in
     tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
@@ -85,9 +85,9 @@ for step in "$@"; do
     gputrain) run pytest_gpu_train 600 python -m pytest tests/test_gpu_training.py tests/test_loss.py -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     train) run bench_train 600 python tools/bench_train.py ;;
     proftrain) run rocprof_train 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_train -o run --output-format csv -- python3 tools/bench_train.py --reps 10 ;;
-    prof2|prof3|prof4)
+    prof2|prof3|prof4|prof5)
       c=$(cfg_of "$step"); run "rocprof_$c" 600 rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_$c" -o run --output-format csv -- python3 bench.py --config "$c" --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
-    pmc2|pmc3|pmc4)  # one counter per pass (separate runs), MI355X_MICROARCH.md HBM recipe
+    pmc2|pmc3|pmc4|pmc5)  # one counter per pass (separate runs), MI355X_MICROARCH.md HBM recipe
       c=$(cfg_of "$step")
       run "pmc_${c}_fetch" 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "gpurun_out/pmc_${c}_fetch" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext &&
       run "pmc_${c}_write" 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "gpurun_out/pmc_${c}_write" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext &&

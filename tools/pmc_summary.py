@@ -189,7 +189,7 @@ def main():
     dig_p = os.path.join(args.src, "build_digest.txt")
     res.update({"tag": args.tag, "units": "per stage invocation (launch-weighted sum over the stage's kernels)",
                 "fetch_correction": 2.0, "config_name": args.config,
-                "config": bench.config_key(c["P"], c["W"], c["H"], c["tile"]),
+                "config": bench.config_key(c["P"], c["W"], c["H"], c["tile"], c.get("views", 1)),
                 "build": open(dig_p).read().strip() if os.path.exists(dig_p) else bench.build_digest(),
                 "note": "per_launch_hbm_bytes = (2*FETCH_SIZE + WRITE_SIZE) KiB (MI355X_MICROARCH.md §HBM)"})
     name = args.config.split("_")[0]
