@@ -51,7 +51,13 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const uint32_t* __restrict__ bucket_list, const uint8_t* __restrict__ hit_codes, const uint32_t* __restrict__ hdr) {
 #pragma clang fp contract(fast)
     static_assert(!kSel || (kWaves == 1 && kSwap), "the select form is the 1-wave transposed-sum geometry");
-    constexpr bool kStaged = kSel >= 2;  // staged sums (kSel 2, 3)
+    constexpr bool kStaged = kSel >= 2;  // staged sums (kSel 2, 3, 4)
+    constexpr bool kMaskSel = kSel >= 3;  // SGPR-mask selects, per-batch compare sets (kSel 3, 4)
+    // kSel 4: s2 joins the 8-value transposition (g6 = dx^2 s0 leaves it) and
+    // g6's column partials are dx x g4's, formed after the transposition by
+    // the lanes that hold them (lane l's pixels are column l % 16, its dx that
+    // column's): no DPP row tree for a ninth value, no lane-15 store
+    constexpr bool kG6Post = kSel == 4;
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
     // (x, y, r, g) and the scaled conic / opacity as two b128 reads, b as one
@@ -202,7 +208,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // finite alpha leaves their terms 0).  Entries with contributor below it
     // are taken by every pixel of the group: no per-pixel contributor test.
     uint32_t min_last = 0xffffffffu;
-    if constexpr (kSel == 3) {
+    if constexpr (kMaskSel) {
 #pragma unroll
         for (int k = 0; k < kPPL; k++) {
             uint32_t g = px.inside[k] ? last[k] : 0xffffffffu;
@@ -265,6 +271,17 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // lane 16 r + 15 also holds g8's row-r sum, element r of value 8
     const int st_dst = ((lane & 15) >> 2) * kStagePitch + 4 * swap_sum_slot(lane >> 4) + (lane & 3);
     const int st_g8 = 32 + (lane >> 4);
+    // kG6Post: zb's value v = 4 + swap_sum_slot(r) of (g4, s1, s2, g7) goes to
+    // output q = v except s2 (v = 6) -> q = 8; g6 (q = 6) from lanes 0-15 (zb
+    // row 0 = g4), the other lanes' product into their dummy word
+    const int st_dst_b = [&] {
+        const int v = 4 + swap_sum_slot(lane >> 4);
+        return ((lane & 15) >> 2) * kStagePitch + 4 * (v == 6 ? 8 : v) + (lane & 3);
+    }();
+    // (the idle lanes 16-63 store into the 16-word pads of pitch rows 0-2,
+    // which the reduce never reads)
+    const int st_g6 = lane < 16 ? ((lane & 15) >> 2) * kStagePitch + 4 * 6 + (lane & 3)
+                                : ((lane - 16) >> 4) * kStagePitch + 256 + (lane & 15);
     int par = 0;
     for (int top = m; top > 0; top -= kB, par ^= 1) {  // entries [top-cnt, top), back to front
         const int cnt = min(kB, top);
@@ -278,7 +295,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             s_a[tid] = make_float4(xy.x, xy.y, nrgb[0], nrgb[1]);
             s_co[tid] = pc;
             s_b[tid].x = nrgb[2];
-            if constexpr (kSel == 3)  // the reference's `power > 0` skip cannot fire (gs_blend.cuh)
+            if constexpr (kMaskSel)  // the reference's `power > 0` skip cannot fire (gs_blend.cuh)
                 fastg = splat_form_safe(pc, fabsf(xy.x - (float)ox), fabsf(xy.y - (float)oy));
             gm = use_codes ? (uint32_t)hit_codes[range.x + top - 1 - tid]
                  : cull ? splat_group_mask(xy, co, (float)ox, (float)oy, (float)pstride) : 0xfu;
@@ -287,10 +304,10 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         const bool has_next = ntop > 0 && tid < min(kB, ntop);
         if (has_next) nid = point_list[range.x + ntop - 1 - tid];
         publish_group_masks<kWaves>(gm, s_bal);
-        const uint64_t fast_mask = kSel == 3 ? uniform_u64(__ballot(fastg)) : 0ull;  // (kWaves == 1: slot = lane)
+        const uint64_t fast_mask = kMaskSel ? uniform_u64(__ballot(fastg)) : 0ull;  // (kWaves == 1: slot = lane)
         // every contributor of this batch (<= top - 1) below every row group's
         // smallest n_contrib: all pixels take its entries
-        const bool bstarted = kSel == 3 && (uint32_t)(top - 1) < min_last;
+        const bool bstarted = kMaskSel && (uint32_t)(top - 1) < min_last;
         if (kWaves > 1)
             for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
         uint64_t written = 0;  // kWaves == 1: batch slots whose partial rows were stored
@@ -352,7 +369,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             // 3-operand fma with an inline 0)
             float c0 = -0.f, c1 = -0.f, c2 = -0.f, s0 = -0.f, s1 = -0.f, s2 = -0.f;
             bool any = false;
-            if constexpr (kSel == 3) {
+            if constexpr (kMaskSel) {
                 // kSel 2 with the selects on an SGPR-pair mask (gs_sel2_zero_v) and
                 // only the compares the entry needs: alpha >= 1/255 always;
                 // contributor < n_contrib unless the batch is started for every
@@ -468,11 +485,24 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             g[3] = s0;
             g[4] = dx * s0;
             g[5] = s1;
-            g[6] = dx * g[4];
+            g[6] = kG6Post ? s2 : dx * g[4];
             g[7] = dx * s1;
             g[8] = s2;
             if (kSel ? any : __ballot(any) != 0ull) {  // wave-uniform
-                if constexpr (kStaged) {
+                if constexpr (kG6Post) {
+                    float za, zb;
+                    swap_rows8_pk_t<false>(g, za, zb);
+                    const float w6 = dx * zb;  // lanes 0-15: dx_c x (g4's column-c partial)
+                    s_stage[st_dst + 36 * nst] = za;
+                    s_stage[st_dst_b + 36 * nst] = zb;
+                    s_stage[st_g6 + (lane < 16 ? 36 * nst : 0)] = w6;
+                    js |= (uint64_t)j << (6 * nst);
+                    written |= 1ull << j;
+                    const bool full = ++nst == kStageSlots;
+                    if (full) stage_reduce(kStageSlots);
+                    nst = full ? 0 : nst;
+                    js = full ? 0ull : js;
+                } else if constexpr (kStaged) {
                     float za, zb;
                     swap_rows8_pk(g, za, zb);
                     float* st = &s_stage[st_dst + 36 * nst];
@@ -540,7 +570,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
               visit(cbit, xy, pc, cf, kFastT, kStartedT);
             }
           };
-          if constexpr (kSel == 3) {
+          if constexpr (kMaskSel) {
               // every entry this wave visits has a provably negative-definite form
               const bool bsafe = (todo & ~fast_mask) == 0ull;
               if (bsafe && bstarted) run(T1{}, T1{});
@@ -667,7 +697,8 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         case 5: GS_BWD_LAUNCH(4, 1, 5, true); break;  // 96 VGPRs: 5 waves per SIMD
         case 6: GS_BWD_LAUNCH(4, 1, 4, true, false, 1); break;  // select form
         case 7: GS_BWD_LAUNCH(4, 1, 4, true, false, 2); break;  // select form, staged sums
-        case 8: GS_BWD_LAUNCH(4, 1, 4, true, false, 3); break;  // 7 + SGPR-mask selects, per-entry compares
+        case 8: GS_BWD_LAUNCH(4, 1, 4, true, false, 3); break;  // 7 + SGPR-mask selects, per-batch compare sets
+        case 9: GS_BWD_LAUNCH(4, 1, 4, true, false, 4); break;  // 8 + g6 after the transposition (no 9th-value tree)
         default: GS_BWD_LAUNCH(4, 1, 4, true); break;
     }
 #undef GS_BWD_LAUNCH

@@ -905,7 +905,8 @@ __device__ __forceinline__ float dpp_add(float e) {
     return e + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, e), kCtrl, kRowMask,
                                                                       0xf, kBound));
 }
-__device__ __forceinline__ void swap_rows8_pk(float (&g)[9], float& za, float& zb) {
+template <bool kG8>
+__device__ __forceinline__ void swap_rows8_pk_t(float (&g)[9], float& za, float& zb) {
     const gs_f2 p0 = pl_swap32(g[0], g[1]), p4 = pl_swap32(g[4], g[5]);
     const gs_f2 p2 = pl_swap32(g[2], g[3]), p6 = pl_swap32(g[6], g[7]);
     const gs_f2 abef = gs_f2{p0.x, p4.x} + gs_f2{p0.y, p4.y};
@@ -914,16 +915,19 @@ __device__ __forceinline__ void swap_rows8_pk(float (&g)[9], float& za, float& z
     const gs_f2 z = gs_f2{q0.x, q1.x} + gs_f2{q0.y, q1.y};
     za = z.x;
     zb = z.y;
-    // g8: the DPP row tree (compiler-scheduled, so it interleaves with the
-    // swaps above instead of waiting out its own hazards); lane 16 r + 15
-    // ends with row r's sum
-    float e = g[8];
-    e = dpp_add<0x111, 0xf, true>(e);   // row_shr:1
-    e = dpp_add<0x112, 0xf, true>(e);   // row_shr:2
-    e = dpp_add<0x114, 0xf, true>(e);   // row_shr:4
-    e = dpp_add<0x118, 0xf, true>(e);   // row_shr:8
-    g[8] = e;
+    if constexpr (kG8) {
+        // g8: the DPP row tree (compiler-scheduled, so it interleaves with the
+        // swaps above instead of waiting out its own hazards); lane 16 r + 15
+        // ends with row r's sum
+        float e = g[8];
+        e = dpp_add<0x111, 0xf, true>(e);   // row_shr:1
+        e = dpp_add<0x112, 0xf, true>(e);   // row_shr:2
+        e = dpp_add<0x114, 0xf, true>(e);   // row_shr:4
+        e = dpp_add<0x118, 0xf, true>(e);   // row_shr:8
+        g[8] = e;
+    }
 }
+__device__ __forceinline__ void swap_rows8_pk(float (&g)[9], float& za, float& zb) { swap_rows8_pk_t<true>(g, za, zb); }
 
 __device__ __forceinline__ void swap_sum9(float (&g)[9], float& za, float& zb) {
     const float ab = pl_add32(g[0], g[1]), cd = pl_add32(g[2], g[3]);

@@ -146,7 +146,8 @@ def test_cull_is_exact_amr_render_once():
 def test_sgpr_mask_backward_matches_select_form(P, W, H, seed):
     """Backward variant 8 (SGPR-mask selects; the power > 0 test dropped for
     Gaussians whose form is provably negative definite; the contributor test
-    dropped in batches every pixel has started) against variant 7 on the
+    dropped in batches every pixel has started) and 9 (8 + the dx^2 s0 sum
+    formed after the transposition) against variant 7 on the
     adversarial scene (huge thin splats, near-degenerate conics): the blend
     sums agree to float-atomic ordering noise."""
     import gaussian_splatting_with_eye_tracking_amd._C as C
@@ -155,15 +156,16 @@ def test_sgpr_mask_backward_matches_select_form(P, W, H, seed):
     dpix = torch.from_numpy(S.make_cotangent(H, W, seed + 1)).cuda()
     res = {}
     try:
-        for v in (7, 8):
+        for v in (7, 8, 9):
             s, t, out, _bufs = _forward(sc, cam, 5)
             res[v] = _backward(s, t, out, dpix, v)
     finally:
         C.set_tuning("fwd_variant", -1)
         C.set_tuning("bwd_variant", -1)
-    for i in range(3):  # dL_dmeans2D, dL_dcolors, dL_dopacity
-        assert G.rel_err(res[8][0][i], res[7][0][i]) < 5e-6, i
-    assert G.rel_err(res[8][1], res[7][1]) < 5e-6
+    for v in (8, 9):
+        for i in range(3):  # dL_dmeans2D, dL_dcolors, dL_dopacity
+            assert G.rel_err(res[v][0][i], res[7][0][i]) < 5e-6, (v, i)
+        assert G.rel_err(res[v][1], res[7][1]) < 5e-6, v
 
 
 @pytest.mark.parametrize("P,W,H,seed,adv", [(6000, 256, 192, 1, True), (30000, 320, 200, 2, True),

@@ -17,11 +17,11 @@ run() {  # name limit cmd...
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 run rates 150 ./tools/valu_rate
 run tests 600 python -u -m pytest -x -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread tests/test_gpu_readback.py tests/test_gpu_cull.py tests/test_gpu_multiview.py -k "readback or sgpr_mask or more_than_64 or cull_is_exact"
-run tests_par 600 python -u -m pytest -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "geometries_match_oracle and (8 or 7) or hint"
+run tests_par 600 python -u -m pytest -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "geometries_match_oracle and (8 or 7 or 9) or hint"
 run tests_amr 600 python -u -m pytest -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "fold_phases or mask_select"
 run ab_amr_sel 400 python tools/ab_tuning.py --key amr_sel --values 1 2 1 2 --stage amr_render --amr --rounds 6
-run ab_bwd2 400 python tools/ab_tuning.py --key bwd_variant --values 7 8 7 8 --stage render_bwd --backward --rounds 6
-run ab_bwd4 400 python tools/ab_tuning.py --key bwd_variant --values 7 8 7 8 --stage render_bwd --backward --P 6100000 --W 1600 --H 1063 --rounds 4
+run ab_bwd2 400 python tools/ab_tuning.py --key bwd_variant --values 7 8 9 7 8 9 --stage render_bwd --backward --rounds 6
+run ab_bwd4 400 python tools/ab_tuning.py --key bwd_variant --values 7 8 9 7 8 9 --stage render_bwd --backward --P 6100000 --W 1600 --H 1063 --rounds 4
 run ab_fwd2 400 python tools/ab_tuning.py --key fwd_variant --values 5 7 5 7 --stage render --rounds 6
 run ab_fwd4 400 python tools/ab_tuning.py --key fwd_variant --values 5 7 5 7 --stage render --P 6100000 --W 1600 --H 1063 --rounds 4
 run pmc_waves 120 rocprofv3 --pmc SQ_WAVES --kernel-trace -d $O/pmc_waves -o run --output-format csv -- python3 bench.py --config cfg2_1080p_1M --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext
