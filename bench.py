@@ -889,9 +889,9 @@ def main(argv=None):
     if args.launcher_dry_run:
         return dry_run(world, rank)
 
-    build_digest()  # refuse a native library built from other sources than this tree's
     import torch
     import torch.distributed as dist
+    build_digest()  # refuse a native library built from other sources than this tree's (after torch: its HIP runtime)
     distributed = world > 1
     # GS_BENCH_SHARE_DEVICE=1 / GS_BENCH_BACKEND=gloo only rehearse the N>1 path
     # on a one-GPU box (every rank on device 0); real runs use one GPU per rank

@@ -122,8 +122,13 @@ def build_hip_lib(jobs: int = 8, verbose: bool = False) -> str:
 
 def loaded_digest() -> str:
     """gs_build_digest() of the libgsplat_amd.so this process loads (ctypes on
-    the in-tree file: the same object the torch binding links)."""
+    the in-tree file: the same object the torch binding links).  torch is
+    imported first so the HIP runtime the library binds to is torch's own
+    (libamdhip64.so.7 is resolved by soname: whichever loads first serves the
+    process; a ctypes load ahead of torch would put /opt/rocm's runtime under
+    torch -- under rocprofv3 --pmc no kernel of ours was dispatched then)."""
     import ctypes
+    import torch  # noqa: F401
     lib = ctypes.CDLL(LIB)
     lib.gs_build_digest.restype = ctypes.c_char_p
     return lib.gs_build_digest().decode()

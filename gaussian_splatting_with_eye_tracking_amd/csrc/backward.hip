@@ -632,8 +632,12 @@ extern int g_cull;  // render.hip
 // 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave x 4 px with the
 // half-wave DPP-tree sums instead of the permlane transposition
 // (1 wave x 4 px capped at 5 or 6 waves per SIMD spills: measured slower)
-// 7: the select-form blend with staged sums (the default since round 3)
-constexpr int kDefaultBwdVariant = 7;
+// 7: the select-form blend with staged sums (round 3's default)
+// 8: 7 with SGPR-pair masks (v_cndmask_b32_e64), compare set chosen per batch
+// 9: 8 with s2 in the 8-value transposition and g6 formed after it (the
+//    default since round 4: cfg2 0.3512 vs 0.3707 ms for 7, cfg4 0.2722 vs
+//    0.2887, profiles/r04b_ab_bwd2.log / r04b_ab_bwd4.log)
+constexpr int kDefaultBwdVariant = 9;
 int g_bwd_variant = kDefaultBwdVariant;
 // Flush of the per-(tile, Gaussian) sums: 0 = memory-side atomics (the only
 // correct mode); 1 = plain stores of the same shape, 2 = no flush -- timing
