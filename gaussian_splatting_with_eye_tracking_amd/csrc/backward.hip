@@ -57,7 +57,12 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // g6's column partials are dx x g4's, formed after the transposition by
     // the lanes that hold them (lane l's pixels are column l % 16, its dx that
     // column's): no DPP row tree for a ninth value, no lane-15 store
-    constexpr bool kG6Post = kSel == 4;
+    constexpr bool kG6Post = kSel >= 4;
+    // kSel 5: the 7 staging slots of a round unrolled (slot = a compile-time
+    // constant: LDS offsets as immediates, no slot counter / address VALU per
+    // entry) and the visited bit cleared with one s_andn2 on the 1 << bit the
+    // row tests use
+    constexpr bool kSlotUnroll = kSel == 5;
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
     // (x, y, r, g) and the scaled conic / opacity as two b128 reads, b as one
@@ -352,8 +357,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
           // register sets used in turn, measured no faster: the 4 waves per
           // SIMD already hide the LDS latency.)
           auto visit = [&](const int cbit, const float2 xy, const float4 pc, const float4 cf, auto kFastT,
-                           auto kStartedT) {
+                           auto kStartedT, auto kSlotT) {
             constexpr bool kFast = decltype(kFastT)::value, kStarted = decltype(kStartedT)::value;
+            constexpr int kSlot = decltype(kSlotT)::value;  // kSlotUnroll: this entry's staging slot
             const int j = 64 * c + cbit;
             const uint32_t contributor = (uint32_t)(top - 1 - j);
             const float dx = xy.x - px.x;
@@ -489,7 +495,16 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             g[7] = dx * s1;
             g[8] = s2;
             if (kSel ? any : __ballot(any) != 0ull) {  // wave-uniform
-                if constexpr (kG6Post) {
+                if constexpr (kSlotUnroll) {
+                    float za, zb;
+                    swap_rows8_pk_t<false>(g, za, zb);
+                    const float w6 = dx * zb;
+                    s_stage[st_dst + 36 * kSlot] = za;
+                    s_stage[st_dst_b + 36 * kSlot] = zb;
+                    s_stage[st_g6 + (lane < 16 ? 36 * kSlot : 0)] = w6;
+                    js |= (uint64_t)j << (6 * kSlot);
+                    written |= 1ull << j;
+                } else if constexpr (kG6Post) {
                     float za, zb;
                     swap_rows8_pk_t<false>(g, za, zb);
                     const float w6 = dx * zb;  // lanes 0-15: dx_c x (g4's column-c partial)
@@ -559,7 +574,36 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
           // chosen once per batch -- per-entry branches between the visit
           // variants made the register allocator shuffle the loop-carried
           // pixel state (8 v_mov per entry) at every join
+          using S0 = std::integral_constant<int, 0>;
           auto run = [&](auto kFastT, auto kStartedT) {
+            if constexpr (kSlotUnroll) {
+              // rounds of 7 entries, one unrolled copy of the visit per slot
+              auto one = [&](auto kSlotT) {
+                if (!todo) return;  // wave-uniform
+                const int cbit = __builtin_ctzll(todo);
+                todo &= ~(1ull << cbit);
+                const int j = 64 * c + cbit;
+                const float4 a4 = s_a[j];
+                const float2 xy = make_float2(a4.x, a4.y);
+                const float4 pc = s_co[j], cf = make_float4(a4.z, a4.w, s_b[j].x, 0.f);
+                visit(cbit, xy, pc, cf, kFastT, kStartedT, kSlotT);
+                nst = decltype(kSlotT)::value + 1;
+              };
+              while (todo) {
+                one(S0{});
+                one(std::integral_constant<int, 1>{});
+                one(std::integral_constant<int, 2>{});
+                one(std::integral_constant<int, 3>{});
+                one(std::integral_constant<int, 4>{});
+                one(std::integral_constant<int, 5>{});
+                one(std::integral_constant<int, 6>{});
+                if (nst == kStageSlots) {
+                    stage_reduce(kStageSlots);
+                    nst = 0;
+                    js = 0ull;
+                }
+              }
+            } else {
             while (todo) {
               const int cbit = __builtin_ctzll(todo);
               todo &= todo - 1;
@@ -567,7 +611,8 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
               const float4 a4 = s_a[j];
               const float2 xy = make_float2(a4.x, a4.y);
               const float4 pc = s_co[j], cf = make_float4(a4.z, a4.w, s_b[j].x, 0.f);
-              visit(cbit, xy, pc, cf, kFastT, kStartedT);
+              visit(cbit, xy, pc, cf, kFastT, kStartedT, S0{});
+            }
             }
           };
           if constexpr (kMaskSel) {
@@ -634,10 +679,12 @@ extern int g_cull;  // render.hip
 // (1 wave x 4 px capped at 5 or 6 waves per SIMD spills: measured slower)
 // 7: the select-form blend with staged sums (round 3's default)
 // 8: 7 with SGPR-pair masks (v_cndmask_b32_e64), compare set chosen per batch
-// 9: 8 with s2 in the 8-value transposition and g6 formed after it (the
-//    default since round 4: cfg2 0.3512 vs 0.3707 ms for 7, cfg4 0.2722 vs
-//    0.2887, profiles/r04b_ab_bwd2.log / r04b_ab_bwd4.log)
-constexpr int kDefaultBwdVariant = 9;
+// 9: 8 with s2 in the 8-value transposition and g6 formed after it
+//    (cfg2 0.3512 vs 0.3707 ms for 7, cfg4 0.2722 vs 0.2887,
+//    profiles/r04b_ab_bwd2.log / r04b_ab_bwd4.log)
+// 10: 9 with the 7 staging slots unrolled (the default since round 4: cfg2
+//    0.3403 vs 0.3551 ms for 9, cfg4 0.2644 vs 0.2747, profiles/r04e_ab_bwd*)
+constexpr int kDefaultBwdVariant = 10;
 int g_bwd_variant = kDefaultBwdVariant;
 // Flush of the per-(tile, Gaussian) sums: 0 = memory-side atomics (the only
 // correct mode); 1 = plain stores of the same shape, 2 = no flush -- timing
@@ -703,6 +750,7 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         case 7: GS_BWD_LAUNCH(4, 1, 4, true, false, 2); break;  // select form, staged sums
         case 8: GS_BWD_LAUNCH(4, 1, 4, true, false, 3); break;  // 7 + SGPR-mask selects, per-batch compare sets
         case 9: GS_BWD_LAUNCH(4, 1, 4, true, false, 4); break;  // 8 + g6 after the transposition (no 9th-value tree)
+        case 10: GS_BWD_LAUNCH(4, 1, 4, true, false, 5); break;  // 9 with the 7 staging slots unrolled
         default: GS_BWD_LAUNCH(4, 1, 4, true); break;
     }
 #undef GS_BWD_LAUNCH

@@ -92,6 +92,16 @@ for step in "$@"; do
       run "pmc_${c}_fetch" 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "gpurun_out/pmc_${c}_fetch" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext &&
       run "pmc_${c}_write" 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "gpurun_out/pmc_${c}_write" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext &&
       run "pmc_${c}_valu" 300 rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace -d "gpurun_out/pmc_${c}_valu" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
+    trace3) run trace_cfg3 300 rocprofv3 --kernel-trace -d gpurun_out/trace_cfg3 -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-ext ;;
+    sqa2|sqa4|sqb2|sqb4)  # SQ issue / wait counters per kernel (two 8-counter sets)
+      c=$(cfg_of "$step")
+      case "$step" in
+        sqa*) cnt="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY" ;;
+        *) cnt="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_ANY SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" ;;
+      esac
+      run "${step}_$c" 300 rocprofv3 --pmc $cnt --kernel-trace -d "gpurun_out/${step}_$c" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
+    ab_pp4) run ab_pp4 400 python tools/ab_tuning.py --key pp_dma --values 1 0 1 0 --stage preprocess --P 6100000 --W 1600 --H 1063 --rounds 4 &&
+            run ab_drgb4 400 python tools/ab_tuning.py --key sh_drgb --values 1 0 1 0 --stage preprocess --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
