@@ -13,6 +13,8 @@
 //   * no FMA contraction (file compiled with -ffp-contract=off): depth,
 //     means2D and radius are bit-identical to the oracle, which makes the
 //     tile keys bit-exact.
+#include <algorithm>
+
 #include "gs_blend.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
@@ -97,58 +99,16 @@ __device__ __forceinline__ float3 eval_sh_color(int deg, const float (&c)[16][3]
 // the price of whole-line requests instead of 12 scattered 16-B loads per
 // thread.
 constexpr int kPpThreads = 256;
-template <bool kHasSH, bool kSH16, bool kCovPrecomp, bool kDma = false>
-__global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a, GeomView g, int* __restrict__ radii,
-                                                                uint32_t* __restrict__ tile_count) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    __shared__ __attribute__((aligned(16))) float s_sh[kDma ? kPpThreads * 48 : 1];
-    if constexpr (kDma) {
-        // wave w: rows [64 w, 64 w + 64) of the block; lane l's 16-B pieces l + 64 i
-        const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        const size_t row0 = (size_t)blockIdx.x * kPpThreads + 64 * w;
-        const size_t nfl = (size_t)a.P * 48;
-        const float* src = a.shs + row0 * 48;
-        float* dst = s_sh + 64 * 48 * w;
-#pragma unroll
-        for (int i = 0; i < 12; i++) {
-            const size_t f = (size_t)(64 * i + lane) * 4;
-            if (row0 * 48 + f < nfl)
-                __builtin_amdgcn_global_load_lds(src + f, dst + 256 * i, 16, 0, 0);
-        }
-    }
-    for (int i = idx; i < a.zero_n; i += (int)(gridDim.x * blockDim.x)) a.zero_words[i] = 0u;
-    // whether the backward may take d(rgb)/d(dir) from g.drgb (every visible
-    // Gaussian's row is written below)
-    if (idx == 0) g.hdr[kHdrDrgb] = (kHasSH && a.store_drgb) ? 1u : 0u;
-    if (idx >= a.P) return;
-    // AMR: the geometry buffer keeps its own copy of the radii (the progressive
-    // steps return zero radii, their backward reads these); base: the caller's
-    const bool radii_copy = a.block == 32 && radii != g.radii;
-    radii[idx] = 0;
-    if (radii_copy) g.radii[idx] = 0;
-    g.tiles_touched[idx] = 0;
 
-    // Every global load of this Gaussian is issued up front (one memory round
-    // trip per thread); the math below then overlaps other waves' loads.
-    const float mx = a.means3D[3 * idx + 0];
-    const float my = a.means3D[3 * idx + 1];
-    const float mz = a.means3D[3 * idx + 2];
-    float sc[3] = {0.f, 0.f, 0.f};
-    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-    float cov3D[6];
-    if (kCovPrecomp) {
-#pragma unroll
-        for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D_precomp[6 * idx + i];
-    } else {
-        sc[0] = a.scales[3 * idx + 0];
-        sc[1] = a.scales[3 * idx + 1];
-        sc[2] = a.scales[3 * idx + 2];
-        q = reinterpret_cast<const float4*>(a.rotations)[idx];
-    }
-    const float opacity = a.opacities[idx];
-    const Mat4 V = load_mat4(a.viewmatrix);
-    const Mat4 Pm = load_mat4(a.projmatrix);
-
+// Everything after the loads of one Gaussian (forward.cu:155-256): the cull,
+// cov2D, conic, radius / rect, SH colour (coefficients from load_shc, only for
+// survivors), the records.  radii / tiles_touched were zeroed by the caller.
+template <bool kHasSH, bool kCovPrecomp, typename ShFn>
+__device__ __forceinline__ void pp_gaussian(const PreprocessArgs& a, const GeomView& g, int* __restrict__ radii,
+                                            uint32_t* __restrict__ tile_count, int idx, bool radii_copy, float mx,
+                                            float my, float mz, const float (&sc)[3], float4 q, float (&cov3D)[6],
+                                            float opacity, const Mat4& V, const Mat4& Pm, ShFn&& load_shc,
+                                            float* stage) {
     // in_frustum (auxiliary.h:139-164): near plane only.
     const float3 p_view = transform_point_4x3(mx, my, mz, V);
     if (p_view.z <= 0.2f) {
@@ -210,21 +170,12 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
     const uint32_t area = (r.x1 - r.x0) * (r.y1 - r.y0);
     if (area == 0) return;
 
+    float3 rgbv = make_float3(0.f, 0.f, 0.f);
     if (kHasSH) {
         // SH only for Gaussians that survive the cull (computeColorFromSH runs
         // after the rect test in the reference too, forward.cu:240-247)
         float shc[16][3];
-        if constexpr (kDma) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA rows have landed
-            const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
-            const float* row = s_sh + 48 * threadIdx.x;
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-#pragma unroll
-                for (int ch = 0; ch < 3; ch++) shc[k][ch] = k < ncoef ? row[3 * k + ch] : 0.f;
-        } else {
-            load_sh<kSH16>(a.D, a.M, a.shs + (size_t)idx * a.M * 3, shc);
-        }
+        load_shc(shc);
         // computeColorFromSH: dir = normalize(mean - campos)
         float dx = mx - a.cam_pos[0], dy = my - a.cam_pos[1], dz = mz - a.cam_pos[2];
         const float len = sqrtf(dot3(dx, dy, dz, dx, dy, dz));
@@ -234,15 +185,24 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
         if (a.store_drgb) {  // the SH backward's d(rgb)/d(dir), from the coefficients already in registers
             float dx3[3], dy3[3], dz3[3];
             sh_ddir(a.D, shc, dx, dy, dz, dx3, dy3, dz3);
-            // one 48-B row: three 16-B stores from one address
-            float4* row = reinterpret_cast<float4*>(g.drgb) + 3 * (size_t)idx;
+            // one 48-B row: three 16-B stores from one address (or into the
+            // thread's LDS row, which its wave stores coalesced)
+            float4* row = stage ? reinterpret_cast<float4*>(stage)
+                                : reinterpret_cast<float4*>(g.drgb) + 3 * (size_t)idx;
             row[0] = make_float4(dx3[0], dx3[1], dx3[2], dy3[0]);
             row[1] = make_float4(dy3[1], dy3[2], dz3[0], dz3[1]);
             row[2] = make_float4(dz3[2], 0.f, 0.f, 0.f);
         }
-        g.rgb[3 * idx + 0] = rgb.x;
-        g.rgb[3 * idx + 1] = rgb.y;
-        g.rgb[3 * idx + 2] = rgb.z;
+        if (stage) {
+            stage[12] = rgb.x;
+            stage[13] = rgb.y;
+            stage[14] = rgb.z;
+        } else {
+            g.rgb[3 * idx + 0] = rgb.x;
+            g.rgb[3 * idx + 1] = rgb.y;
+            g.rgb[3 * idx + 2] = rgb.z;
+        }
+        rgbv = rgb;
         g.clamped[idx] = cbits;
     }
     g.depths[idx] = p_view.z;
@@ -258,11 +218,12 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
         // (x, y, r, g), the log2(e)-scaled conic + opacity, (b, raw conic).
         float r_, g_, b_;
         if (kHasSH) {
-            r_ = g.rgb[3 * idx]; g_ = g.rgb[3 * idx + 1]; b_ = g.rgb[3 * idx + 2];
+            r_ = rgbv.x; g_ = rgbv.y; b_ = rgbv.z;
         } else {
             r_ = a.colors_precomp[3 * idx]; g_ = a.colors_precomp[3 * idx + 1]; b_ = a.colors_precomp[3 * idx + 2];
         }
-        float4* row = reinterpret_cast<float4*>(g.grad_accum + (size_t)kGradRow * idx);
+        float4* row = stage ? reinterpret_cast<float4*>(stage + 16)
+                            : reinterpret_cast<float4*>(g.grad_accum + (size_t)kGradRow * idx);
         const float4 co = make_float4(conic_x, conic_y, conic_z, opacity);
         row[0] = make_float4(pix_x, pix_y, r_, g_);
         row[1] = splat_coef(co);
@@ -276,12 +237,159 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
             for (uint32_t x = r.x0; x < r.x1; x++) atomicAdd(&tile_count[y * gx + x], 1u);
 }
 
-int g_pp_dma = 1;  // set_tuning("pp_dma"): SH rows through LDS-DMA (kDma) for SH16
-void set_pp_dma(int v) { g_pp_dma = v; }
+// One Gaussian: zero its counters, issue its loads, pp_gaussian.  stage: the
+// thread's LDS row for the strided records (kStageOut) or nullptr.
+template <bool kHasSH, bool kSH16, bool kCovPrecomp, bool kDma>
+__device__ __forceinline__ void pp_thread(const PreprocessArgs& a, const GeomView& g, int* __restrict__ radii,
+                                          uint32_t* __restrict__ tile_count, int idx, const float* sh_row,
+                                          float* stage) {
+    // AMR: the geometry buffer keeps its own copy of the radii (the progressive
+    // steps return zero radii, their backward reads these); base: the caller's
+    const bool radii_copy = a.block == 32 && radii != g.radii;
+    radii[idx] = 0;
+    if (radii_copy) g.radii[idx] = 0;
+    g.tiles_touched[idx] = 0;
+
+    // Every global load of this Gaussian is issued up front (one memory round
+    // trip per thread); the math below then overlaps other waves' loads.
+    const float mx = a.means3D[3 * idx + 0];
+    const float my = a.means3D[3 * idx + 1];
+    const float mz = a.means3D[3 * idx + 2];
+    float sc[3] = {0.f, 0.f, 0.f};
+    float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+    float cov3D[6];
+    if (kCovPrecomp) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D_precomp[6 * idx + i];
+    } else {
+        sc[0] = a.scales[3 * idx + 0];
+        sc[1] = a.scales[3 * idx + 1];
+        sc[2] = a.scales[3 * idx + 2];
+        q = reinterpret_cast<const float4*>(a.rotations)[idx];
+    }
+    const float opacity = a.opacities[idx];
+    const Mat4 V = load_mat4(a.viewmatrix);
+    const Mat4 Pm = load_mat4(a.projmatrix);
+    pp_gaussian<kHasSH, kCovPrecomp>(a, g, radii, tile_count, idx, radii_copy, mx, my, mz, sc, q, cov3D, opacity,
+                                     V, Pm, [&](float (&shc)[16][3]) {
+        if constexpr (kDma) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA rows have landed
+            const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) shc[k][ch] = k < ncoef ? sh_row[3 * k + ch] : 0.f;
+        } else {
+            load_sh<kSH16>(a.D, a.M, a.shs + (size_t)idx * a.M * 3, shc);
+        }
+    }, stage);
+}
+
+// kStageOut (kDma): a visible Gaussian's d(rgb)/d(dir) row and rgb go into its
+// thread's LDS row (free once its SH coefficients are in registers), and each
+// wave then stores its 64 records as wave-contiguous 16-B pieces instead of
+// per-thread stores at a 48-B / 12-B stride (one store instruction covers
+// whole lines, not a third of each).  Rows of culled Gaussians carry stale
+// words, as their never-read records may.
+template <bool kHasSH, bool kSH16, bool kCovPrecomp, bool kDma = false, bool kStageOut = false>
+__global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a, GeomView g, int* __restrict__ radii,
+                                                                uint32_t* __restrict__ tile_count) {
+    static_assert(!kStageOut || (kDma && kHasSH), "staged records use the SH rows' LDS");
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ __attribute__((aligned(16))) float s_sh[kDma ? kPpThreads * 48 : 1];
+    if constexpr (kDma) {
+        // wave w: rows [64 w, 64 w + 64) of the block; lane l's 16-B pieces l + 64 i
+        const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        const size_t row0 = (size_t)blockIdx.x * kPpThreads + 64 * w;
+        const size_t nfl = (size_t)a.P * 48;
+        const float* src = a.shs + row0 * 48;
+        float* dst = s_sh + 64 * 48 * w;
+#pragma unroll
+        for (int i = 0; i < 12; i++) {
+            const size_t f = (size_t)(64 * i + lane) * 4;
+            if (row0 * 48 + f < nfl)
+                __builtin_amdgcn_global_load_lds(src + f, dst + 256 * i, 16, 0, 0);
+        }
+    }
+    for (int i = idx; i < a.zero_n; i += (int)(gridDim.x * blockDim.x)) a.zero_words[i] = 0u;
+    // whether the backward may take d(rgb)/d(dir) from g.drgb (every visible
+    // Gaussian's row is written below)
+    if (idx == 0) g.hdr[kHdrDrgb] = (kHasSH && a.store_drgb) ? 1u : 0u;
+    float* row = s_sh + (kDma ? 48 * threadIdx.x : 0);
+    if constexpr (kStageOut) {
+        // every lane of a wave takes part in its coalesced record stores below
+        const int wrow0 = (int)(blockIdx.x * kPpThreads) + (int)(threadIdx.x & ~63u);
+        if (wrow0 >= a.P) return;  // wave-uniform
+        if (idx < a.P) pp_thread<kHasSH, kSH16, kCovPrecomp, kDma>(a, g, radii, tile_count, idx, row, row);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int lane = threadIdx.x & 63;
+        const float* wl = s_sh + 48 * (threadIdx.x & ~63u);
+        const int nrow = min(64, a.P - wrow0);
+        if (a.store_drgb) {  // 64 rows x three 16-B pieces
+            float4* out = reinterpret_cast<float4*>(g.drgb) + 3 * (size_t)wrow0;
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                const int c = lane + 64 * i;
+                if (c < 3 * nrow) out[c] = *reinterpret_cast<const float4*>(wl + 48 * (c / 3) + 4 * (c % 3));
+            }
+        }
+        if (a.block == 32) {  // AMR blend rows: 64 x 64 B (the fourth piece of a row is unused: zeros)
+            float4* out = reinterpret_cast<float4*>(g.grad_accum + (size_t)kGradRow * wrow0);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const int c = lane + 64 * i;
+                if (c < 4 * nrow)
+                    out[c] = (c & 3) == 3 ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                          : *reinterpret_cast<const float4*>(wl + 48 * (c >> 2) + 16 + 4 * (c & 3));
+            }
+        }
+        // 64 x 3 rgb floats = 48 pieces of 4
+        const int nf = 3 * nrow;
+        if (4 * lane < nf) {
+            float v4[4];
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int f = min(4 * lane + e, nf - 1);
+                v4[e] = wl[48 * (f / 3) + 12 + f % 3];
+            }
+            float* out = g.rgb + 3 * (size_t)wrow0 + 4 * lane;
+            if (4 * lane + 4 <= nf) {
+                *reinterpret_cast<float4*>(out) = make_float4(v4[0], v4[1], v4[2], v4[3]);
+            } else {
+#pragma unroll
+                for (int e = 0; e < 3; e++)
+                    if (4 * lane + e < nf) out[e] = v4[e];
+            }
+        }
+        return;
+    }
+    if (idx >= a.P) return;
+    pp_thread<kHasSH, kSH16, kCovPrecomp, kDma>(a, g, radii, tile_count, idx, row, nullptr);
+}
+
+// set_tuning("pp_dma"): 0 per-thread SH loads; 1 SH rows through LDS-DMA
+// (kDma) for SH16; 3 = 1 with the strided records staged (kStageOut; the
+// default since round 4: config 4 0.503 -> 0.441 ms, config 3 0.084 -> 0.077,
+// config 2 equal, profiles/r04f_ab_pp*.log); < 0 the default.  (2, a persistent pipelined form -- one-wave workgroups walking
+// batches with the next batch's SH rows and geometry in flight -- measured
+// slower: 0.537 vs 0.502 ms at config 4, 0.095 vs 0.092 at config 2,
+// profiles/r04e_ab_pp*.log; removed)
+constexpr int kDefaultPpDma = 3;
+int g_pp_dma = kDefaultPpDma;
+void set_pp_dma(int v) { g_pp_dma = v < 0 ? kDefaultPpDma : v; }
 
 template <bool A, bool B, bool C>
 static void launch_pp(const PreprocessArgs& a, const GeomView& g, int* radii, uint32_t* tile_count, hipStream_t s) {
     const int blocks = (a.P + kPpThreads - 1) / kPpThreads;
+    if constexpr (A && B) {
+        if (g_pp_dma == 3) {
+            hipLaunchKernelGGL((preprocess_kernel<A, B, C, true, true>), dim3(blocks), dim3(kPpThreads), 0, s, a, g,
+                               radii, tile_count);
+            return;
+        }
+    }
     if (A && B && g_pp_dma)
         hipLaunchKernelGGL((preprocess_kernel<A, B, C, true>), dim3(blocks), dim3(kPpThreads), 0, s, a, g, radii,
                            tile_count);
