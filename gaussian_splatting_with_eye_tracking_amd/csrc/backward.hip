@@ -62,7 +62,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // constant: LDS offsets as immediates, no slot counter / address VALU per
     // entry) and the visited bit cleared with one s_andn2 on the 1 << bit the
     // row tests use
-    constexpr bool kSlotUnroll = kSel == 5;
+    constexpr bool kSlotUnroll = kSel >= 5;
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
     // (x, y, r, g) and the scaled conic / opacity as two b128 reads, b as one
@@ -684,6 +684,10 @@ extern int g_cull;  // render.hip
 //    profiles/r04b_ab_bwd2.log / r04b_ab_bwd4.log)
 // 10: 9 with the 7 staging slots unrolled (the default since round 4: cfg2
 //    0.3403 vs 0.3551 ms for 9, cfg4 0.2644 vs 0.2747, profiles/r04e_ab_bwd*)
+// (11, 10 with each entry's row-group bits taken by one v_readlane and tested
+//    as constant bits -- s_bitcmp + branch, one SALU fewer per row group --
+//    measured slower: 0.3434 vs 0.3404 ms, 0.2673 vs 0.2632,
+//    profiles/r04g_ab_bwd*; removed)
 constexpr int kDefaultBwdVariant = 10;
 int g_bwd_variant = kDefaultBwdVariant;
 // Flush of the per-(tile, Gaussian) sums: 0 = memory-side atomics (the only

@@ -156,6 +156,7 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
         case 4: GS_FWD_LAUNCH(1, 4, 6); break;
         case 6: GS_FWD_LAUNCH(1, 4, 1, 1); break;
         case 7: GS_FWD_LAUNCH(1, 4, 8, 2); break;  // 5 with SGPR-mask selects (gs_blend.cuh blend_one_msk)
+        case 8: GS_FWD_LAUNCH(1, 4, 8, 3); break;  // 5 with the scalar bookkeeping trimmed
         default: GS_FWD_LAUNCH(1, 4, 8, 1); break;  // 5: 3 + the select-form blend
     }
 #undef GS_FWD_LAUNCH
