@@ -21,6 +21,9 @@ namespace gsamd {
 
 constexpr int kLvlThreads = 1024;
 constexpr int kLvlSortMax = 2048;  // tile grids up to this size sort their counts in LDS
+// set_tuning("amr_levels_hist"): counts < 2^16 take the two-pass histogram
+// select (select3_u16) instead of the sort / the 4-pass radix select
+int g_amr_levels_hist = 1;
 
 // k-th smallest (0-based) of v[0..n) -- MSD radix select, one workgroup.
 // Counts are read straight from ranges (count = y - x) so no global value is
@@ -72,11 +75,86 @@ __device__ uint32_t block_select_kth(const uint32_t* __restrict__ ranges, int n,
     return prefix;
 }
 
+// The three order statistics k[0..2] of the T counts when every count is
+// below 65536: two 8-bit digit passes (high byte, then the low byte of the
+// values in each statistic's high bin), all three statistics in the same
+// passes -- ~8 barriers instead of the bitonic sort's 66.  hist: 768 words.
+__device__ void select3_u16(const uint32_t* __restrict__ ranges, int T, const uint32_t (&k)[3], uint32_t* hist,
+                            uint32_t* word, uint32_t (&out)[3]) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ uint32_t s_carry[12];
+    for (int i = tid; i < 256; i += kLvlThreads) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < T; i += kLvlThreads) atomicAdd(&hist[(ranges[2 * i + 1] - ranges[2 * i]) >> 8], 1u);
+    __syncthreads();
+    uint32_t h = 0, inc = 0;
+    if (tid < 256) {
+        h = hist[tid];
+        inc = h;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)inc, off, 64);
+            if (lane >= off) inc += t;
+        }
+        if (lane == 63) s_carry[wave] = inc;
+    }
+    __syncthreads();
+    if (tid < 256) {
+        uint32_t start = inc - h;
+        for (int w = 0; w < wave; w++) start += s_carry[w];
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+            if (h > 0 && start <= k[q] && k[q] < start + h) {  // exactly one bin per statistic
+                word[2 * q] = (uint32_t)tid;
+                word[2 * q + 1] = k[q] - start;
+            }
+    }
+    __syncthreads();
+    uint32_t b[3], r[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        b[q] = word[2 * q];
+        r[q] = word[2 * q + 1];
+    }
+    for (int i = tid; i < 768; i += kLvlThreads) hist[i] = 0;
+    __syncthreads();
+    for (int i = tid; i < T; i += kLvlThreads) {
+        const uint32_t x = ranges[2 * i + 1] - ranges[2 * i];
+#pragma unroll
+        for (int q = 0; q < 3; q++)
+            if ((x >> 8) == b[q]) atomicAdd(&hist[256 * q + (x & 255u)], 1u);
+    }
+    __syncthreads();
+    h = 0;
+    inc = 0;
+    if (tid < 768) {
+        h = hist[tid];
+        inc = h;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)inc, off, 64);
+            if (lane >= off) inc += t;
+        }
+        if (lane == 63) s_carry[wave] = inc;
+    }
+    __syncthreads();
+    if (tid < 768) {
+        const int q = tid >> 8;
+        uint32_t start = inc - h;
+        for (int w = 4 * q; w < wave; w++) start += s_carry[w];
+        if (h > 0 && start <= r[q] && r[q] < start + h) word[q] = (b[q] << 8) | (uint32_t)(tid & 255);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 3; q++) out[q] = word[q];
+}
+
 __global__ void __launch_bounds__(kLvlThreads) amr_levels_kernel(int T, const uint32_t* __restrict__ ranges,
                                                                  uint32_t* __restrict__ n_inter,
                                                                  uint32_t* __restrict__ pv,
                                                                  uint32_t* __restrict__ levels,
-                                                                 float4* __restrict__ zero4, int zero_n4) {
+                                                                 float4* __restrict__ zero4, int zero_n4,
+                                                                 int use_hist) {
     // blocks >= 1 (if any): foveaStep 0's zero image, grid-stride float4
     // stores on the other CUs while block 0 -- one CU -- computes the levels
     // (one launch instead of the levels kernel and a separate fill)
@@ -86,14 +164,26 @@ __global__ void __launch_bounds__(kLvlThreads) amr_levels_kernel(int T, const ui
             zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
         return;
     }
-    __shared__ uint32_t hist[256];
-    __shared__ uint32_t word[2];
+    __shared__ uint32_t hist[768];
+    __shared__ uint32_t word[6];
     __shared__ uint32_t s_pv[3];
     const int tid = threadIdx.x;
     // calculateIntersections (amr/cr/rasterizer_impl.cu:181-188)
-    for (int t = tid; t < T; t += kLvlThreads) n_inter[t] = ranges[2 * t + 1] - ranges[2 * t];
+    bool big = false;
+    for (int t = tid; t < T; t += kLvlThreads) {
+        const uint32_t x = ranges[2 * t + 1] - ranges[2 * t];
+        n_inter[t] = x;
+        big |= x >= 65536u;
+    }
     const float percentiles[3] = {0.25f, 0.5f, 0.9f};
-    if (T <= kLvlSortMax) {
+    if (use_hist && !__syncthreads_or(big)) {
+        // every count < 2^16: two digit passes for all three statistics
+        const uint32_t kq[3] = {(uint32_t)(int)(percentiles[0] * (float)T), (uint32_t)(int)(percentiles[1] * (float)T),
+                                (uint32_t)(int)(percentiles[2] * (float)T)};  // float32 index, :630
+        uint32_t v[3];
+        select3_u16(ranges, T, kq, hist, word, v);
+        if (tid < 3) s_pv[tid] = v[tid];
+    } else if (T <= kLvlSortMax) {
         // small grids (1080p: 2040 tiles): one LDS bitonic sort of the counts
         // (padded with UINT32_MAX), then the three order statistics directly --
         // 66 barrier-separated stages instead of 12 radix-select passes
@@ -133,6 +223,8 @@ __global__ void __launch_bounds__(kLvlThreads) amr_levels_kernel(int T, const ui
     }
 }
 
+void set_amr_levels_hist(int v) { g_amr_levels_hist = v; }
+
 void launch_amr_levels(int T, const ImageView& img, hipStream_t s, float* zero_image, size_t zero_floats) {
     if (T == 0) return;
     const int n4 = (zero_image && zero_floats % 4 == 0 && zero_floats / 4 <= (size_t)INT32_MAX) ? (int)(zero_floats / 4) : 0;
@@ -140,7 +232,7 @@ void launch_amr_levels(int T, const ImageView& img, hipStream_t s, float* zero_i
         (void)hipMemsetAsync(zero_image, 0, sizeof(float) * zero_floats, s);
     const int zb = n4 > 0 ? std::min(512, (n4 + kLvlThreads * 8 - 1) / (kLvlThreads * 8)) : 0;
     hipLaunchKernelGGL(amr_levels_kernel, dim3(1 + zb), dim3(kLvlThreads), 0, s, T, img.ranges, img.tile_count, img.pv,
-                       img.levels, reinterpret_cast<float4*>(zero_image), n4);
+                       img.levels, reinterpret_cast<float4*>(zero_image), n4, g_amr_levels_hist);
 }
 
 // amr/cr/rasterizer_impl.cu:208-243 (setFoveaAMRLevelsKernel)

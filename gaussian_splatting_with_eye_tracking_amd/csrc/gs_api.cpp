@@ -1174,6 +1174,10 @@ int gs_set_tuning(const char* key, int value) {
         set_store_cov3d(value);
         return 0;
     }
+    if (std::strcmp(key, "amr_levels_hist") == 0) {  // AMR percentiles by the two-pass histogram select
+        set_amr_levels_hist(value);
+        return 0;
+    }
     if (std::strcmp(key, "amr_lists_per") == 0) {
         set_amr_lists_per(value);
         return 0;

@@ -526,46 +526,6 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 if (__ballot(!done[0]) == 0ull) wave_alive = false;
                 continue;
             }
-            if constexpr (kPPL == 1 && kSel == 3) {
-                // kSel 1 with the scalar bookkeeping trimmed: each visited bit
-                // cleared by one s_andn2 on the 1 << b the hit set uses (the
-                // second unconditionally: b_B = b_A when there is no second)
-                uint64_t hits = 0;
-                uint32_t last_lo = ~0u;
-                const char* sa = reinterpret_cast<const char*>(s_a);
-                const char* sco = reinterpret_cast<const char*>(s_co);
-                const char* sb = reinterpret_cast<const char*>(s_b);
-                while (todo) {
-                    const uint32_t bA = (uint32_t)__builtin_ctzll(todo);
-                    const uint64_t mA = 1ull << bA;
-                    todo &= ~mA;
-                    const bool two = todo != 0;  // wave-uniform
-                    const uint32_t bB = two ? (uint32_t)__builtin_ctzll(todo) : bA;
-                    const uint64_t mB = 1ull << bB;
-                    todo &= ~mB;
-                    const uint32_t loA = (c * 64 + bA) * 16, loB = (c * 64 + bB) * 16;
-                    const float4 sA = *reinterpret_cast<const float4*>(sa + loA);
-                    const float4 sB = *reinterpret_cast<const float4*>(sa + loB);
-                    const float4 coA = *reinterpret_cast<const float4*>(sco + loA);
-                    const float4 coB = *reinterpret_cast<const float4*>(sco + loB);
-                    const float bAc = *reinterpret_cast<const float*>(sb + loA);
-                    const float bBc = *reinterpret_cast<const float*>(sb + loB);
-                    const bool hA = blend_one_sel2(make_float2(sA.x, sA.y), coA, make_float4(sA.z, sA.w, bAc, 0.f),
-                                                   px.x, px.y[0], loA, st_.T[0], st_.C[0], last_lo);
-                    if (kRec && __ballot(hA) != 0ull) hits |= mA;
-                    if (two) {
-                        const bool hB = blend_one_sel2(make_float2(sB.x, sB.y), coB,
-                                                       make_float4(sB.z, sB.w, bBc, 0.f), px.x, px.y[0], loB,
-                                                       st_.T[0], st_.C[0], last_lo);
-                        if (kRec && __ballot(hB) != 0ull) hits |= mB;
-                    }
-                }
-                if (last_lo != ~0u) st_.last[0] = b0 + (last_lo >> 4) + 1;
-                if (rec && (tid & 63) == 0) s_hit[c * kWaves + wave] = hits;
-                done[0] = st_.T[0] < 0.0f;
-                if (__ballot(!done[0]) == 0ull) wave_alive = false;
-                continue;
-            }
             if constexpr (kPPL == 1 && kSel) {
                 // select form (blend_one_sel2), two Gaussians per iteration; the
                 // wave's early exit is tested once per 64 batch slots.  A

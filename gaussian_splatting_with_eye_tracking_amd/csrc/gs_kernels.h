@@ -111,6 +111,7 @@ void set_amr_fold(int v);
 void set_amr_sel(int v);
 void set_amr_deep(int v);
 void set_amr_lists_per(int v);
+void set_amr_levels_hist(int v);
 void set_store_cov3d(int v);
 extern int g_store_cov3d;
 extern int g_sh_drgb;

@@ -126,6 +126,9 @@ void set_xcd_map(int v) { g_xcd_map = v; }
 // per SIMD: 0.307 -> 0.299 ms at config 2, profiles/r03c_ab_fwd_variant_cfg2.log); 5: 3 with the
 // select-form blend (gs_blend.cuh blend_one_sel: 0.305 -> 0.277 ms at config 2, 0.237 -> 0.223 ms at
 // config 4, profiles/r03d_ab_fwd_select_cfg{2,4}.log); 6: 5 at the default occupancy
+// (8, variant 5 with each visited bit cleared by s_andn2 on the hit bit,
+// measured equal: 0.2540 vs 0.2555 ms at config 2, 0.2235 vs 0.2227 at
+// config 4, profiles/r04h_ab_fwd*; removed)
 int g_fwd_variant = 5;
 
 void set_forward_variant(int v) { g_fwd_variant = v; }
@@ -156,7 +159,6 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
         case 4: GS_FWD_LAUNCH(1, 4, 6); break;
         case 6: GS_FWD_LAUNCH(1, 4, 1, 1); break;
         case 7: GS_FWD_LAUNCH(1, 4, 8, 2); break;  // 5 with SGPR-mask selects (gs_blend.cuh blend_one_msk)
-        case 8: GS_FWD_LAUNCH(1, 4, 8, 3); break;  // 5 with the scalar bookkeeping trimmed
         default: GS_FWD_LAUNCH(1, 4, 8, 1); break;  // 5: 3 + the select-form blend
     }
 #undef GS_FWD_LAUNCH
