@@ -50,16 +50,16 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# VALU issue peak, measured (tools/valu_rate.hip, profiles/r03g_valu_rate.log):
-# with 8 waves per SIMD, independent v_fma_f32 chains retire one wave64
-# instruction per 4.43 cycles per SIMD at the 2.4 GHz s_memtime clock
-# (0.2257 wave-instructions per SIMD-cycle: 5.55e11 per second over the
-# chip), v_pk_fma_f32 (two f32 FMAs per lane) per 4.8 -- so f32 runs at ~16
-# lanes per cycle unpacked and the 157 TF vector peak is the packed rate.
-# (Rounds 1-2 priced the blend kernels at 2 cycles per instruction, half the
-# real rate.)  A mix with cheaper ops (moves, selects) can retire faster than
-# this FMA-chain rate, so the fraction is a guide, not a bound.
-VALU_PEAK_WAVE_INSTR_PER_S = 0.2257 * 256 * 4 * 2.4e9
+# VALU issue peak, measured with exact instruction streams (round 4,
+# tools/valu_rate.hip inline-asm bodies, profiles/r04a_valu_rate.log): the
+# two-operand VOP1/VOP2 forms (v_mul / v_add / v_fmac / v_mov) issue one wave64
+# instruction per 2.3-2.6 SIMD-cycles with >= 2 waves per SIMD -- 2.4 taken as
+# the peak; VOP3 fma 2.6-3.9, compares / e64 selects / v_min ~4, exp / rcp 8,
+# so a real mix runs below this rate at full issue (the blends' mixes cost
+# ~3.3 and ~2.9 cycles per instruction).  (Round 3 priced every
+# instruction at a packed-FMA rate of 4.43 cycles: its probe's "v_fma" chain
+# had been SLP-packed.)
+VALU_PEAK_WAVE_INSTR_PER_S = 256 * 4 * 2.4e9 / 2.4
 METRIC = "rendered views/sec (fwd+bwd) at 1080p, 1M Gaussians; achieved HBM GB/s %"
 
 CONFIGS = {
@@ -299,7 +299,9 @@ def make_roofline(stage: str, by: float, events_ms: float, key: dict, src: str, 
         a_ = vi[0] * per / (avg_ms * 1e-3)
         r["valu_issue"] = {"instructions": vi[0] * per, "achieved": round(a_, 1),
                            "peak": VALU_PEAK_WAVE_INSTR_PER_S, "unit": "wave-instr/s",
-                           "frac": round(a_ / VALU_PEAK_WAVE_INSTR_PER_S, 4)}
+                           "frac": round(a_ / VALU_PEAK_WAVE_INSTR_PER_S, 4),
+                           "peak_definition": "one VOP2 wave64 instruction per 2.4 SIMD-cycles, 1024 SIMDs, "
+                                              "2.4 GHz (profiles/r04a_valu_rate.log)"}
     return r
 
 

@@ -922,27 +922,28 @@ __device__ __forceinline__ void cov2d_backward(float mx, float my, float mz, con
     const float bb = cov2D.m[0][1];
     const float cc = cov2D.m[1][1] += 0.3f;
     const float denom = aa * cc - bb * bb;
-    float dL_da = 0, dL_db = 0, dL_dc = 0;
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
     const auto& Tm = T.m;
     const auto& Vm = Vrk.m;
-    if (denom2inv != 0) {
-        dL_da = denom2inv * (-cc * cc * dcx + 2 * bb * cc * dcy + (denom - aa * cc) * dcz);
-        dL_dc = denom2inv * (-aa * aa * dcz + 2 * aa * bb * dcy + (denom - aa * cc) * dcx);
-        dL_db = denom2inv * 2 * (bb * cc * dcx - (denom + 2 * bb * bb) * dcy + aa * bb * dcz);
-        dcov[0] = (Tm[0][0] * Tm[0][0] * dL_da + Tm[0][0] * Tm[1][0] * dL_db + Tm[1][0] * Tm[1][0] * dL_dc);
-        dcov[3] = (Tm[0][1] * Tm[0][1] * dL_da + Tm[0][1] * Tm[1][1] * dL_db + Tm[1][1] * Tm[1][1] * dL_dc);
-        dcov[5] = (Tm[0][2] * Tm[0][2] * dL_da + Tm[0][2] * Tm[1][2] * dL_db + Tm[1][2] * Tm[1][2] * dL_dc);
-        dcov[1] = 2 * Tm[0][0] * Tm[0][1] * dL_da + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_db +
-                  2 * Tm[1][0] * Tm[1][1] * dL_dc;
-        dcov[2] = 2 * Tm[0][0] * Tm[0][2] * dL_da + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_db +
-                  2 * Tm[1][0] * Tm[1][2] * dL_dc;
-        dcov[4] = 2 * Tm[0][2] * Tm[0][1] * dL_da + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_db +
-                  2 * Tm[1][1] * Tm[1][2] * dL_dc;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 6; i++) dcov[i] = 0;
-    }
+    // (the reference's `if (denom2inv != 0)` as selects on the same
+    // expressions -- the same values; as a branch, the compiler sank the two
+    // paths' dcov stores into a pointer phi and kept dcov in scratch memory)
+    const bool ok = denom2inv != 0;
+    const float dL_da = ok ? denom2inv * (-cc * cc * dcx + 2 * bb * cc * dcy + (denom - aa * cc) * dcz) : 0.f;
+    const float dL_dc = ok ? denom2inv * (-aa * aa * dcz + 2 * aa * bb * dcy + (denom - aa * cc) * dcx) : 0.f;
+    const float dL_db = ok ? denom2inv * 2 * (bb * cc * dcx - (denom + 2 * bb * bb) * dcy + aa * bb * dcz) : 0.f;
+    dcov[0] = ok ? (Tm[0][0] * Tm[0][0] * dL_da + Tm[0][0] * Tm[1][0] * dL_db + Tm[1][0] * Tm[1][0] * dL_dc) : 0.f;
+    dcov[3] = ok ? (Tm[0][1] * Tm[0][1] * dL_da + Tm[0][1] * Tm[1][1] * dL_db + Tm[1][1] * Tm[1][1] * dL_dc) : 0.f;
+    dcov[5] = ok ? (Tm[0][2] * Tm[0][2] * dL_da + Tm[0][2] * Tm[1][2] * dL_db + Tm[1][2] * Tm[1][2] * dL_dc) : 0.f;
+    dcov[1] = ok ? 2 * Tm[0][0] * Tm[0][1] * dL_da + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_db +
+                       2 * Tm[1][0] * Tm[1][1] * dL_dc
+                 : 0.f;
+    dcov[2] = ok ? 2 * Tm[0][0] * Tm[0][2] * dL_da + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_db +
+                       2 * Tm[1][0] * Tm[1][2] * dL_dc
+                 : 0.f;
+    dcov[4] = ok ? 2 * Tm[0][2] * Tm[0][1] * dL_da + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_db +
+                       2 * Tm[1][1] * Tm[1][2] * dL_dc
+                 : 0.f;
     const float dL_dT00 = 2 * (Tm[0][0] * Vm[0][0] + Tm[0][1] * Vm[0][1] + Tm[0][2] * Vm[0][2]) * dL_da +
                           (Tm[1][0] * Vm[0][0] + Tm[1][1] * Vm[0][1] + Tm[1][2] * Vm[0][2]) * dL_db;
     const float dL_dT01 = 2 * (Tm[0][0] * Vm[1][0] + Tm[0][1] * Vm[1][1] + Tm[0][2] * Vm[1][2]) * dL_da +
@@ -1031,11 +1032,14 @@ __device__ __forceinline__ void cov3d_backward(float4 qrot, const float (&scl)[3
 
 // kSH16: SH with M = 16 coefficients (degree-3 models): compile-time loops,
 // 16-B loads and stores of the 192-B SH rows.
+// small: when given, the 3-float outputs (dL_dmeans2D, dL_dmeans3D,
+// dL_dscales, dL_dcolors at 0, 3, 6, 9) are returned there for the caller's
+// coalesced stores instead of stored per thread at a 12-B stride.
 template <bool kHasSH, bool kHasScales, bool kSH16>
 __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& a,
                                                        const float* __restrict__ grad_accum,
                                                        const uint8_t* __restrict__ clamped_bits, int idx,
-                                                       float* lrow) {
+                                                       float* lrow, float (*small)[12] = nullptr) {
     if (idx >= a.P) return;
     const bool vis = a.radii[idx] > 0;
     // Blend-stage gradients in the reference layout.
@@ -1053,21 +1057,35 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     // (dL_dcolor, dL_dconic, dL_dcov3D: NULL = not wanted -- the autograd
     // wrapper discards them unless the matching precomputed input was given;
     // the uniform tests cost nothing, the skipped stores 52 B per Gaussian)
-    if (a.dL_dcolor) {
-        a.dL_dcolor[3 * idx + 0] = acc[0];
-        a.dL_dcolor[3 * idx + 1] = acc[1];
-        a.dL_dcolor[3 * idx + 2] = acc[2];
+    if (small) {
+        (*small)[9] = acc[0];
+        (*small)[10] = acc[1];
+        (*small)[11] = acc[2];
+        (*small)[0] = acc[3];
+        (*small)[1] = acc[4];
+        (*small)[2] = 0.f;
+    } else {
+        if (a.dL_dcolor) {
+            a.dL_dcolor[3 * idx + 0] = acc[0];
+            a.dL_dcolor[3 * idx + 1] = acc[1];
+            a.dL_dcolor[3 * idx + 2] = acc[2];
+        }
+        a.dL_dmean2D[3 * idx + 0] = acc[3];
+        a.dL_dmean2D[3 * idx + 1] = acc[4];
+        a.dL_dmean2D[3 * idx + 2] = 0.f;
     }
-    a.dL_dmean2D[3 * idx + 0] = acc[3];
-    a.dL_dmean2D[3 * idx + 1] = acc[4];
-    a.dL_dmean2D[3 * idx + 2] = 0.f;
     if (a.dL_dconic) reinterpret_cast<float4*>(a.dL_dconic)[idx] = make_float4(acc[5], acc[6], 0.f, acc[7]);
     a.dL_dopacity[idx] = acc[8];
 
     const int ncoef_out = a.M;  // dL_dsh is [P, M, 3]
     if (!vis) {
+        if (small) {
 #pragma unroll
-        for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = 0.f;
+            for (int i = 3; i < 9; i++) (*small)[i] = 0.f;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = 0.f;
+        }
         if (a.dL_dcov3D) {
 #pragma unroll
             for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = 0.f;
@@ -1078,7 +1096,8 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
         } else if (kHasSH) {
             for (int i = 0; i < ncoef_out * 3; i++) a.dL_dsh[(size_t)idx * ncoef_out * 3 + i] = 0.f;
         }
-        for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = 0.f;
+        if (!small)
+            for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = 0.f;
         for (int i = 0; i < 4; i++) a.dL_drot[4 * idx + i] = 0.f;
         return;
     }
@@ -1139,22 +1158,39 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     proj_backward(mx, my, mz, Pm, acc[3], acc[4], dmean);
 
     // ---- computeColorFromSH backward (backward.cu:20-139)
-    if (kHasSH) sh_backward<kSH16>(a, idx, mx, my, mz, s, cb, acc, dmean, kSH16 ? lrow : nullptr,
-                                   use_drgb ? d9 : nullptr);
+    // (two calls with a constant pointer each: a run-time select of d9 or
+    // nullptr made the compiler keep d9 in scratch memory)
+    if (kHasSH) {
+        if (use_drgb) sh_backward<kSH16>(a, idx, mx, my, mz, s, cb, acc, dmean, kSH16 ? lrow : nullptr, d9);
+        else sh_backward<kSH16>(a, idx, mx, my, mz, s, cb, acc, dmean, kSH16 ? lrow : nullptr, nullptr);
+    }
 #pragma unroll
-    for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = dmean[i];
+    for (int i = 0; i < 3; i++) {
+        if (small) (*small)[3 + i] = dmean[i];
+        else a.dL_dmean3D[3 * idx + i] = dmean[i];
+    }
 
     // ---- computeCov3D backward (backward.cu:278-341)
     if (kHasScales) {
         float dscale[3];
         float4 dq;
         cov3d_backward(qrot, scl, a.scale_modifier, dcov, dscale, dq);
-        a.dL_dscale[3 * idx + 0] = dscale[0];
-        a.dL_dscale[3 * idx + 1] = dscale[1];
-        a.dL_dscale[3 * idx + 2] = dscale[2];
+        if (small) {
+            (*small)[6] = dscale[0];
+            (*small)[7] = dscale[1];
+            (*small)[8] = dscale[2];
+        } else {
+            a.dL_dscale[3 * idx + 0] = dscale[0];
+            a.dL_dscale[3 * idx + 1] = dscale[1];
+            a.dL_dscale[3 * idx + 2] = dscale[2];
+        }
         reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
     } else {
-        for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = 0.f;
+        if (small) {
+            (*small)[6] = (*small)[7] = (*small)[8] = 0.f;
+        } else {
+            for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = 0.f;
+        }
         for (int i = 0; i < 4; i++) a.dL_drot[4 * idx + i] = 0.f;
     }
 }
@@ -1166,10 +1202,11 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
 // against ~5.4 TB/s coalesced on MI355X (tools/membench.hip).
 constexpr int kShRow = 49;
 
-template <bool kHasSH, bool kHasScales, bool kSH16>
+template <bool kHasSH, bool kHasScales, bool kSH16, bool kSmall = false>
 __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussArgs a, const float* __restrict__ grad_accum,
                                                                  const uint8_t* __restrict__ clamped_bits, int stage_mlp) {
     constexpr bool kStage = kHasSH && kSH16;
+    static_assert(!kSmall || kStage, "the small outputs are staged in the SH rows' LDS");
     __shared__ float s_dsh[kStage ? 256 * kShRow : 1];
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     // (not needed when the forward stored d(rgb)/d(dir): the SH coefficients
@@ -1200,8 +1237,14 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
         }
         __syncthreads();
     }
+    // stage_small: the 3-float outputs too go out as the workgroup's
+    // contiguous 3 x 256 floats per array (stores at a 12-B stride write one
+    // 32-B granule per lane per instruction: ~+23 % write bytes at config 4,
+    // profiles/r04d_cfg4_pmc_summary.json)
+    float small[12];
     backward_gaussian_body<kHasSH, kHasScales, kSH16>(a, grad_accum, clamped_bits, idx,
-                                                      kStage ? s_dsh + threadIdx.x * kShRow : nullptr);
+                                                      kStage ? s_dsh + threadIdx.x * kShRow : nullptr,
+                                                      kSmall ? &small : nullptr);
     if constexpr (kStage) {
         __syncthreads();
         const int g0 = blockIdx.x * blockDim.x;
@@ -1210,6 +1253,27 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
         for (int f = threadIdx.x; f < n * 12; f += 256) {
             const float* r = s_dsh + (f / 12) * kShRow + 4 * (f % 12);
             out[f] = make_float4(r[0], r[1], r[2], r[3]);
+        }
+        if constexpr (kSmall) {
+            __syncthreads();  // the SH rows are out: the LDS holds the small arrays now
+            if (idx < a.P) {
+#pragma unroll
+                for (int i = 0; i < 12; i++) s_dsh[(i / 3) * 768 + 3 * threadIdx.x + i % 3] = small[i];
+            }
+            __syncthreads();
+            const int nf = 3 * n;
+            for (int f = threadIdx.x; f < 4 * 192; f += 256) {
+                const int q = f / 192, i = f - 192 * q;
+                float* d = q == 0 ? a.dL_dmean2D : q == 1 ? a.dL_dmean3D : q == 2 ? a.dL_dscale : a.dL_dcolor;
+                if (!d || 4 * i >= nf) continue;
+                const float* r = s_dsh + q * 768 + 4 * i;
+                float* o = d + 3 * (size_t)g0 + 4 * i;
+                if (4 * i + 4 <= nf) {
+                    *reinterpret_cast<float4*>(o) = make_float4(r[0], r[1], r[2], r[3]);
+                } else {
+                    for (int e = 0; e < 4 && 4 * i + e < nf; e++) o[e] = r[e];
+                }
+            }
         }
     }
 }
@@ -1244,8 +1308,13 @@ __global__ void __launch_bounds__(256) sh_backward_kernel(BackwardGaussArgs a, c
 
 int g_bwd_gauss_split = 0;
 void set_bwd_gauss_split(int v) { g_bwd_gauss_split = v; }
-int g_bg_stage_mlp = 1;  // set_tuning("bg_stage_mlp"): the SH staging loads issued back to back
-void set_bg_stage_mlp(int v) { g_bg_stage_mlp = v; }
+// set_tuning("bg_stage_mlp"): 1 the SH staging loads issued back to back; 2 =
+// 1 + the 3-float outputs stored coalesced through LDS (stage_small; the
+// default since round 4: 0.0848 -> 0.0828 ms at config 2, 0.529 -> 0.479 at
+// config 4, profiles/r04j_ab_bg*.log); < 0 the default
+constexpr int kDefaultBgStage = 2;
+int g_bg_stage_mlp = kDefaultBgStage;
+void set_bg_stage_mlp(int v) { g_bg_stage_mlp = v < 0 ? kDefaultBgStage : v; }
 
 void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hipStream_t s) {
     if (a.P == 0) return;
@@ -1263,7 +1332,10 @@ void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hi
         else hipLaunchKernelGGL((sh_backward_kernel<false>), grid, dim3(256), 0, s, a, g.clamped);
         return;
     }
-    if (sh16 && sc) GS_BG_LAUNCH(true, true, true);
+    if (sh16 && sc && g_bg_stage_mlp >= 2)
+        hipLaunchKernelGGL((backward_gaussians_kernel<true, true, true, true>), grid, dim3(256), 0, s, a, g.grad_accum,
+                           g.clamped, g_bg_stage_mlp);
+    else if (sh16 && sc) GS_BG_LAUNCH(true, true, true);
     else if (sh16) GS_BG_LAUNCH(true, false, true);
     else if (sh && sc) GS_BG_LAUNCH(true, true, false);
     else if (sh) GS_BG_LAUNCH(true, false, false);

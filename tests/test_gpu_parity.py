@@ -167,6 +167,20 @@ def test_backward_parity_preprocess_forms(pp_dma):
         C.set_tuning("pp_dma", -1)
 
 
+@pytest.mark.parametrize("stage", [1, 2])
+def test_backward_parity_gauss_store_forms(stage):
+    """bwd_gauss with the 3-float outputs stored per thread (1) or staged
+    through LDS and stored coalesced (2): both against the oracle."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    C.set_tuning("bg_stage_mlp", stage)
+    try:
+        test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
+        test_backward_parity("ragged_3k_250x130", 3000, 250, 130, 7, "sh")
+        test_backward_parity("g1_64_32x32", 64, 32, 32, 3, "sh")
+    finally:
+        C.set_tuning("bg_stage_mlp", -1)
+
+
 @pytest.mark.parametrize("slots", [1, 3, 8, 0])
 def test_bin_slots_bit_exact(slots):
     """The binning's per-slot sub-buckets (gs_layout.h kBinSlots) change only
