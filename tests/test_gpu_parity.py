@@ -51,7 +51,7 @@ def _oracle_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0
 
 @pytest.mark.parametrize("pp_dma", [1, 3])  # 3: records staged through LDS, stored coalesced
 @pytest.mark.parametrize("name,P,W,H,seed", CASES)
-def test_forward_buffers_bit_exact(name, P, W, H, seed, pp_dma):
+def test_forward_buffers_bit_exact(name, P, W, H, seed, pp_dma=-1):
     import gaussian_splatting_with_eye_tracking_amd._C as C
     sc, cam = G.scene_and_camera(P, W, H, seed)
     C.set_tuning("store_cov3d", 1)  # the geometry buffer's cov3D is written on request only
