@@ -63,6 +63,12 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // entry) and the visited bit cleared with one s_andn2 on the 1 << bit the
     // row tests use
     constexpr bool kSlotUnroll = kSel >= 5;
+    // kSel 6: the staging reduce finishes the reference's nine terms itself
+    // (lane 9 s + q holds accumulator entry q of slot s's Gaussian; entries 4
+    // and 5 -- sum t dx, sum t dy -- fetched by two lane shuffles) and adds
+    // them into grad_accum: no accumulator rows in LDS, no per-batch flush
+    // pass, one atomic instruction per 7 Gaussians
+    constexpr bool kFusedFlush = kSel >= 6;
     constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
     // (x, y, r, g) and the scaled conic / opacity as two b128 reads, b as one
@@ -75,7 +81,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // the flush; 4 row partials would double the LDS footprint and cost
     // workgroups per CU); several waves add into one row with LDS atomics
     constexpr int kRowsPerG = (kWaves == 1 && !kSwap) ? 2 : 1;
-    __shared__ float s_acc[kB * kRowsPerG * kAccRow + (kStaged ? 1 : 0)];  // (+ a dummy entry: staged sums)
+    __shared__ float s_acc[kFusedFlush ? 1 : kB * kRowsPerG * kAccRow + (kStaged ? 1 : 0)];  // (+ a dummy entry: staged sums)
     __shared__ uint64_t s_bal[4 * kWaves];
     // kSel == 2: the per-Gaussian sums are finished in groups of 7 Gaussians --
     // each visit parks its two transposed registers (16 column partials of
@@ -329,7 +335,29 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 const gs_f2 x2 = gs_f2{c.x, c.y} + gs_f2{d.x, d.y}, x3 = gs_f2{c.z, c.w} + gs_f2{d.z, d.w};
                 const gs_f2 y = (x0 + x1) + (x2 + x3);
                 const uint32_t jj = (uint32_t)(js >> (6 * st_slot)) & 63u;
-                s_acc[jj * st_mul + st_base] = y.x + y.y;
+                if constexpr (kFusedFlush) {
+                    // lane 9 s + q: output component fq of q (entries 0..2 colours,
+                    // 3 = sum t -> opacity (8), 4 = sum t dx -> mean x (3), 5 = sum t
+                    // dy -> mean y (4), 6..8 -> conic (5..7)); the flush's formula
+                    const float tot = y.x + y.y;
+                    const float g4 = __shfl(tot, 9 * st_slot + 4, 64), sy = __shfl(tot, 9 * st_slot + 5, 64);
+                    if (lane < 63) {
+                        const int fq = st_q < 3 ? st_q : st_q == 3 ? 8 : st_q - 1;
+                        const float qa = (fq == 3 || fq == 4) ? g4 : tot;
+                        const float4 pc = s_co[jj];
+                        const float o = pc.w;
+                        const float cx = pc.x * (-1.0f / kHalfLog2e), cy = pc.y * (-1.0f / kLog2e),
+                                    cz = pc.z * (-1.0f / kHalfLog2e);
+                        const float ka = fq == 3 ? -o * cx * ddelx_dx
+                                       : fq == 4 ? -o * cy * ddely_dy
+                                       : (fq >= 5 && fq <= 7) ? -0.5f * o : 1.0f;
+                        const float kb = fq == 3 ? -o * cy * ddelx_dx : fq == 4 ? -o * cz * ddely_dy : 0.0f;
+                        const float v = ka * qa + kb * sy;
+                        if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[par][jj] * kGradRow + fq], v);
+                    }
+                } else {
+                    s_acc[jj * st_mul + st_base] = y.x + y.y;
+                }
             }
         };
         __syncthreads();
@@ -502,8 +530,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                     s_stage[st_dst + 36 * kSlot] = za;
                     s_stage[st_dst_b + 36 * kSlot] = zb;
                     s_stage[st_g6 + (lane < 16 ? 36 * kSlot : 0)] = w6;
-                    js |= (uint64_t)j << (6 * kSlot);
-                    written |= 1ull << j;
+                    js |= (uint64_t)j << (6 * kSlot);  // (written: every todo bit, set before the loop)
                 } else if constexpr (kG6Post) {
                     float za, zb;
                     swap_rows8_pk_t<false>(g, za, zb);
@@ -577,6 +604,9 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
           using S0 = std::integral_constant<int, 0>;
           auto run = [&](auto kFastT, auto kStartedT) {
             if constexpr (kSlotUnroll) {
+              // every entry of todo is visited and staged (select form: a
+              // visited row group always sums), so the written set is todo
+              written |= todo;  // (kSel: kWaves == 1, c == 0)
               // rounds of 7 entries, one unrolled copy of the visit per slot
               auto one = [&](auto kSlotT) {
                 if (!todo) return;  // wave-uniform
@@ -639,7 +669,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         // (one 64-B memory-side atomic request per (tile, Gaussian)).  (A full
         // unroll lets the scheduler hoist all 64 LDS reads: 163 VGPRs.)
 #pragma unroll 4
-        for (int i = 0; i < kB / (4 * kWaves); i++) {
+        for (int i = 0; i < (kFusedFlush ? 0 : kB / (4 * kWaves)); i++) {
             const int r = (tid >> 4) + 4 * kWaves * i;
             bool live = r < cnt && comp < kNG;
             if (kWaves == 1) live = live && ((written >> (r & 63)) & 1ull);
@@ -682,13 +712,17 @@ extern int g_cull;  // render.hip
 // 9: 8 with s2 in the 8-value transposition and g6 formed after it
 //    (cfg2 0.3512 vs 0.3707 ms for 7, cfg4 0.2722 vs 0.2887,
 //    profiles/r04b_ab_bwd2.log / r04b_ab_bwd4.log)
-// 10: 9 with the 7 staging slots unrolled (the default since round 4: cfg2
-//    0.3403 vs 0.3551 ms for 9, cfg4 0.2644 vs 0.2747, profiles/r04e_ab_bwd*)
+// 10: 9 with the 7 staging slots unrolled (cfg2 0.3403 vs 0.3551 ms for 9,
+//    cfg4 0.2644 vs 0.2747, profiles/r04e_ab_bwd*)
+// 11: 10 with the flush fused into the staging reduce (the default since
+//    round 4: cfg2 0.3139 vs 0.3394 ms for 10, cfg4 0.2433 vs 0.2659,
+//    profiles/r04l_ab_bwd*_m.log; 11 under a 5-wave cap -- 96 VGPRs, 7
+//    spilled -- measured 0.3254 / 0.2502 and is not kept)
 // (11, 10 with each entry's row-group bits taken by one v_readlane and tested
 //    as constant bits -- s_bitcmp + branch, one SALU fewer per row group --
 //    measured slower: 0.3434 vs 0.3404 ms, 0.2673 vs 0.2632,
 //    profiles/r04g_ab_bwd*; removed)
-constexpr int kDefaultBwdVariant = 10;
+constexpr int kDefaultBwdVariant = 11;
 int g_bwd_variant = kDefaultBwdVariant;
 // Flush of the per-(tile, Gaussian) sums: 0 = memory-side atomics (the only
 // correct mode); 1 = plain stores of the same shape, 2 = no flush -- timing
@@ -755,6 +789,7 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
         case 8: GS_BWD_LAUNCH(4, 1, 4, true, false, 3); break;  // 7 + SGPR-mask selects, per-batch compare sets
         case 9: GS_BWD_LAUNCH(4, 1, 4, true, false, 4); break;  // 8 + g6 after the transposition (no 9th-value tree)
         case 10: GS_BWD_LAUNCH(4, 1, 4, true, false, 5); break;  // 9 with the 7 staging slots unrolled
+        case 11: GS_BWD_LAUNCH(4, 1, 4, true, false, 6); break;  // 10 with the flush fused into the staging reduce
         default: GS_BWD_LAUNCH(4, 1, 4, true); break;
     }
 #undef GS_BWD_LAUNCH

@@ -370,7 +370,12 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const float* __re
 //                inside the run with LDS atomics and writes the keys.
 // Slot order inside a bucket stays arbitrary; sort_tiles makes it exact.
 constexpr int kBinThreads = 1024;
-int g_bin_chunk = 4096;
+// Gaussians per binning workgroup (count_tiles and duplicate_lds must agree:
+// the chunk -> sub-bucket slot map); 0 = auto: 8192 from 4M Gaussians (config
+// 4 count_tiles 57.0 -> 52.4 us), else 4096 (config 2: 22.1 us vs 29.9 at
+// 8192), profiles/r04l_ab_chunk*.log
+int g_bin_chunk = 0;
+int bin_chunk_for(int P) { return g_bin_chunk ? g_bin_chunk : (P >= 4000000 ? 8192 : 4096); }
 int g_dup_diag = 0;
 // sub-bucket slots the LDS binning spreads its chunks over (1..kBinSlots;
 // the scan sums all kBinSlots, unused ones stay zero)
@@ -405,7 +410,7 @@ int bin_slots_for(int P, int gx, int gy, int block) {
     return g_bin_slots ? g_bin_slots : (P >= 2000000 ? kBinSlots : 1);
 }
 void set_dup_diag(int v) { g_dup_diag = v; }
-void set_bin_chunk(int v) { g_bin_chunk = max(kBinThreads, v); }
+void set_bin_chunk(int v) { g_bin_chunk = v <= 0 ? 0 : max(kBinThreads, v); }
 
 __device__ __forceinline__ bool gaussian_rect(int idx, const float* __restrict__ means2D,
                                               const int* __restrict__ radii, int block, uint32_t gx, uint32_t gy,
@@ -489,7 +494,7 @@ void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H
                         hipStream_t s) {
     const uint32_t gx = (uint32_t)((W + block - 1) / block), gy = (uint32_t)((H + block - 1) / block);
     if (P == 0 || gx * gy == 0) return;
-    const int chunk = g_bin_chunk;
+    const int chunk = bin_chunk_for(P);
     hipLaunchKernelGGL(count_tiles_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
                        sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, radii, block, gx, gy, img.tile_count,
                        (uint32_t)bin_slots_for(P, (int)gx, (int)gy, block));
@@ -839,7 +844,7 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
         return;
     }
     if (gx * gy <= (uint32_t)kLdsTiles) {
-        const int chunk = g_bin_chunk;
+        const int chunk = bin_chunk_for(P);
         hipLaunchKernelGGL(duplicate_lds_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
                            sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, g.depths, radii, block, gx, gy,
                            img.tile_cursor, b.pair_keys, spec_hdr, spec_cap, g_dup_diag,

@@ -440,7 +440,9 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     const int gx = (W + tile - 1) / tile, gy = (H + tile - 1) / tile;
     r.T = gx * gy;
     const size_t N = (size_t)W * H;
-    char* gbase = call_resize(geometry, carve_geom(nullptr, in.P, nullptr), "geometry");
+    // the optional tail (gs_layout.h) only when this forward writes into it
+    const bool tail = g_store_cov3d || (in.colors_precomp == nullptr && g_sh_drgb && t_store_drgb);
+    char* gbase = call_resize(geometry, carve_geom(nullptr, in.P, nullptr, tail), "geometry");
     carve_geom(gbase, in.P, &r.g);
     set_accum_clean(r.g.grad_accum, false);  // this forward decides afresh
     char* ibase = call_resize(image, carve_image(nullptr, N, r.T, nullptr, tile), "image");

@@ -65,7 +65,13 @@ struct GeomView {
 };
 
 // base is 256-B aligned by the caller (torch allocations are).
-inline size_t carve_geom(char* base, size_t P, GeomView* v) {
+// The optional tail -- d(rgb)/d(dir) rows (written when the forward stores
+// them for an SH backward, header flag kHdrDrgb) and cov3D (written only on
+// request, set_tuning("store_cov3d")) -- comes last: a forward that writes
+// neither sizes its buffer without it (tail = false: 72 B per Gaussian less,
+// ~440 MB at 6.1M Gaussians); the pointers are carved either way and read
+// only when the header / the request says they were written.
+inline size_t carve_geom(char* base, size_t P, GeomView* v, bool tail = true) {
     size_t off = 0;
     GeomView g;
     g.hdr = carve<uint32_t>(base, off, kHdrWords);
@@ -74,13 +80,14 @@ inline size_t carve_geom(char* base, size_t P, GeomView* v) {
     g.means2D = carve<float>(base, off, 2 * P);
     g.conic_opacity = carve<float>(base, off, 4 * P);
     g.rgb = carve<float>(base, off, 3 * P);
-    g.cov3D = carve<float>(base, off, 6 * P);
     g.clamped = carve<uint8_t>(base, off, P);
-    g.drgb = carve<float>(base, off, 12 * P);
     g.tiles_touched = carve<uint32_t>(base, off, P);
     g.grad_accum = carve<float>(base, off, (size_t)kGradRow * P);
+    const size_t head = align_up(off);
+    g.drgb = carve<float>(base, off, 12 * P);
+    g.cov3D = carve<float>(base, off, 6 * P);
     if (v) *v = g;
-    return align_up(off);
+    return tail ? align_up(off) : head;
 }
 
 struct ImageView {

@@ -648,7 +648,8 @@ py::dict ParseBuffers(const Tensor& geomBuffer, const Tensor& binningBuffer, con
     d["means2D"] = view(g.means2D, {P, 2}, f32);
     d["conic_opacity"] = view(g.conic_opacity, {P, 4}, f32);
     d["rgb"] = view(g.rgb, {P, 3}, f32);
-    d["cov3D"] = view(g.cov3D, {P, 6}, f32);
+    if ((size_t)geomBuffer.numel() >= gs_geom_bytes((int)P))  // (the optional tail: a forward that wrote it)
+        d["cov3D"] = view(g.cov3D, {P, 6}, f32);
     d["clamped_bits"] = view(g.clamped, {P}, o.dtype(torch::kUInt8));
     d["tiles_touched"] = view(g.tiles_touched, {P}, i32);
     d["grad_accum"] = view(g.grad_accum, {P, 16}, f32);
@@ -831,6 +832,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("activate", &Activate);
     m.def("activation_backward", &ActivationBackward);
     m.def("abi_version", []() { return gs_abi_version(); });
+    m.def("geom_bytes", [](int P) { return gs_geom_bytes(P); },
+          "geometry-buffer bytes with the optional tail (the upper bound a forward asks for)");
     m.def("profile_enable", [](bool on) { gs_profile_enable(on ? 1 : 0); });
     m.def("profile_stages", [](const std::vector<std::string>& names) {
         // [] = all stages

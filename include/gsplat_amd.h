@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define GSPLAT_AMD_ABI_VERSION 3
+#define GSPLAT_AMD_ABI_VERSION 4  /* 4: drgb / cov3D moved to an optional tail of the geometry buffer */
 
 /* Resize the caller-owned byte buffer `ctx` to `nbytes` and return its
  * (device, >=256-B aligned) base pointer, or NULL on failure.
@@ -301,9 +301,9 @@ typedef struct {
     float* means2D;       /* [P][2] */
     float* conic_opacity; /* [P][4] */
     float* rgb;           /* [P][3] */
-    float* cov3D;         /* [P][6] */
+    float* cov3D;         /* [P][6], in the optional tail (written on request only) -- ABI 4 */
     uint8_t* clamped;     /* [P] bit c = channel c clamped */
-    float* drgb;          /* [P][12] d(rgb)/d(view dir) of the SH colours, (x, y, z) x (r, g, b) + 3 pad (hdr[7] = 1: written) -- ABI 3 */
+    float* drgb;          /* [P][12] d(rgb)/d(view dir) of the SH colours, (x, y, z) x (r, g, b) + 3 pad (hdr[7] = 1: written), in the optional tail -- ABI 3 / 4 */
     uint32_t* tiles_touched;
     float* grad_accum; /* [P][16] */
 } gs_geom_view;
@@ -336,6 +336,11 @@ typedef struct {
     uint64_t* scratch;
 } gs_binning_view;
 
+/* Upper bound: the geometry buffer with its optional tail (d(rgb)/d(dir)
+ * rows and cov3D, csrc/gs_layout.h); a forward that writes neither asks its
+ * resize callback for 72 B per Gaussian less, and gs_geom_view_of's drgb /
+ * cov3D pointers are then past the end of that buffer (read them only when
+ * header word kHdrDrgb / the store_cov3d request says they were written). */
 size_t gs_geom_bytes(int P);
 size_t gs_image_bytes(int width, int height, int tile);
 size_t gs_binning_bytes(int K);

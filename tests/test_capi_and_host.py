@@ -60,7 +60,9 @@ def test_host_layout_helpers():
     lib.gs_image_bytes.restype = ctypes.c_size_t
     lib.gs_binning_bytes.restype = ctypes.c_size_t
     lib.gs_knn_workspace_bytes.restype = ctypes.c_size_t
-    assert lib.gs_abi_version() == 3  # 2: gs_image_view gained the band arrays; 3: gs_geom_view gained drgb
+    # 2: gs_image_view gained the band arrays; 3: gs_geom_view gained drgb;
+    # 4: drgb and cov3D moved to an optional tail of the geometry buffer
+    assert lib.gs_abi_version() == 4
     g1, g2 = lib.gs_geom_bytes(1000), lib.gs_geom_bytes(2000)
     assert g2 > g1 > 1000 * (4 + 4 + 8 + 16 + 12 + 24 + 1 + 48 + 4 + 64)
     assert lib.gs_image_bytes(1920, 1080, 16) >= 1920 * 1080 * 8 + 120 * 68 * 8
@@ -74,8 +76,11 @@ def test_host_layout_helpers():
     base = 1 << 20
     assert lib.gs_geom_view_of(ctypes.c_void_p(base), 1000, ctypes.byref(v)) == 0
     ptrs = [getattr(v, f[0]) for f in GeomView._fields_]
-    assert ptrs[0] == base and all(p % 256 == 0 for p in ptrs) and ptrs == sorted(ptrs)
-    assert v.grad_accum + 1000 * 64 - base <= g1
+    assert ptrs[0] == base and all(p % 256 == 0 for p in ptrs) and len(set(ptrs)) == len(ptrs)
+    # the optional tail (drgb, cov3D) follows everything else
+    head = [p for f, p in zip(GeomView._fields_, ptrs) if f[0] not in ("drgb", "cov3D")]
+    assert head == sorted(head) and v.grad_accum < v.drgb < v.cov3D
+    assert v.cov3D + 1000 * 24 - base <= g1
 
 
 @pytest.mark.parametrize("prefix", ["gs_binning", "gs_amr_binning"])
@@ -108,7 +113,7 @@ def test_torch_extension_surface():
     for n in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "amr_rasterize_gaussians",
               "distCUDA2", "parse_buffers", "profile_enable", "profile_read", "set_tuning"):
         assert hasattr(_C, n), n
-    assert _C.abi_version() == 3
+    assert _C.abi_version() == 4
     assert all(os.path.exists(p) and p.startswith(ROOT) for p in native_library_paths())
 
 

@@ -156,13 +156,13 @@ def test_sgpr_mask_backward_matches_select_form(P, W, H, seed):
     dpix = torch.from_numpy(S.make_cotangent(H, W, seed + 1)).cuda()
     res = {}
     try:
-        for v in (7, 8, 9, 10):
+        for v in (7, 8, 9, 10, 11):
             s, t, out, _bufs = _forward(sc, cam, 5)
             res[v] = _backward(s, t, out, dpix, v)
     finally:
         C.set_tuning("fwd_variant", -1)
         C.set_tuning("bwd_variant", -1)
-    for v in (8, 9, 10):
+    for v in (8, 9, 10, 11):
         for i in range(3):  # dL_dmeans2D, dL_dcolors, dL_dopacity
             assert G.rel_err(res[v][0][i], res[7][0][i]) < 5e-6, (v, i)
         assert G.rel_err(res[v][1], res[7][1]) < 5e-6, v

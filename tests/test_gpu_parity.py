@@ -51,7 +51,11 @@ def _oracle_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0
 
 @pytest.mark.parametrize("pp_dma", [1, 3])  # 3: records staged through LDS, stored coalesced
 @pytest.mark.parametrize("name,P,W,H,seed", CASES)
-def test_forward_buffers_bit_exact(name, P, W, H, seed, pp_dma=-1):
+def test_forward_buffers_bit_exact(name, P, W, H, seed, pp_dma):
+    _forward_buffers_bit_exact(name, P, W, H, seed, pp_dma)
+
+
+def _forward_buffers_bit_exact(name, P, W, H, seed, pp_dma=-1):
     import gaussian_splatting_with_eye_tracking_amd._C as C
     sc, cam = G.scene_and_camera(P, W, H, seed)
     C.set_tuning("store_cov3d", 1)  # the geometry buffer's cov3D is written on request only
@@ -403,7 +407,7 @@ def test_config2_full_size_parity_and_psnr():
         assert G.rel_err(g.cpu().numpy(), rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(g.cpu().numpy(), rg[n]))
 
 
-@pytest.mark.parametrize("bwd_variant", [0, 1, 2, 3, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("bwd_variant", [0, 1, 2, 3, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("fwd_variant", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
     """Every forward / backward blend geometry (gs_set_tuning) against the oracle."""
@@ -466,7 +470,7 @@ def test_thread_contiguous_tile_scan_matches_oracle(name, P, W, H, seed):
     import gaussian_splatting_with_eye_tracking_amd._C as C
     try:
         C.set_tuning("scan_slices", 0)
-        test_forward_buffers_bit_exact(name, P, W, H, seed)
+        _forward_buffers_bit_exact(name, P, W, H, seed)
     finally:
         C.set_tuning("scan_slices", 1)
 
@@ -1107,7 +1111,11 @@ def test_forward_only_hint_from_autograd_wrapper():
              tt["rotations"], e)
         c_, _r, gb, bb, ib = _RasterizeGaussians.apply(*a, 0, e, u8, u8, u8, False, st)
         torch.cuda.synchronize()
-        return int(C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)["hdr"][7].item())
+        flag = int(C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)["hdr"][7].item())
+        # the geometry buffer's optional tail (d(rgb)/d(dir) + cov3D, 72 B per
+        # Gaussian) is allocated exactly when the rows are written
+        assert (gb.numel() == C.geom_bytes(P)) == (flag == 1), (gb.numel(), C.geom_bytes(P), flag)
+        return flag
 
     with torch.no_grad():
         assert step0(False) == 0
