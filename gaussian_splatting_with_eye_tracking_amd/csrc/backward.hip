@@ -1070,11 +1070,15 @@ __device__ __forceinline__ void cov3d_backward(float4 qrot, const float (&scl)[3
 // small: when given, the 3-float outputs (dL_dmeans2D, dL_dmeans3D,
 // dL_dscales, dL_dcolors at 0, 3, 6, 9) are returned there for the caller's
 // coalesced stores instead of stored per thread at a 12-B stride.
-template <bool kHasSH, bool kHasScales, bool kSH16>
+// kDrgb: the host knows the forward stored d(rgb)/d(dir) (no SH coefficient
+// path compiled: 114 instead of 164 VGPRs); the SH basis and dL/drgb are
+// returned in sh19 (16 + 3) for the caller's staged dL_dsh stores.
+template <bool kHasSH, bool kHasScales, bool kSH16, bool kDrgb = false>
 __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& a,
                                                        const float* __restrict__ grad_accum,
                                                        const uint8_t* __restrict__ clamped_bits, int idx,
-                                                       float* lrow, float (*small)[12] = nullptr) {
+                                                       float* lrow, float (*small)[12] = nullptr,
+                                                       float (*sh19)[19] = nullptr) {
     if (idx >= a.P) return;
     const bool vis = a.radii[idx] > 0;
     // Blend-stage gradients in the reference layout.
@@ -1125,7 +1129,10 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
 #pragma unroll
             for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = 0.f;
         }
-        if (kHasSH && kSH16) {
+        if (kDrgb) {
+#pragma unroll
+            for (int i = 0; i < 19; i++) (*sh19)[i] = 0.f;
+        } else if (kHasSH && kSH16) {
 #pragma unroll
             for (int i = 0; i < 48; i++) lrow[i] = 0.f;
         } else if (kHasSH) {
@@ -1163,7 +1170,7 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     float s[16][3];
     uint8_t cb = 0;
     // the forward's d(rgb)/d(dir) when it stored them: no SH coefficients read
-    const bool use_drgb = kHasSH && a.drgb && a.hdr[kHdrDrgb] == 1u;  // uniform
+    const bool use_drgb = kDrgb || (kHasSH && a.drgb && a.hdr[kHdrDrgb] == 1u);  // uniform
     float d9[9];
     if (kHasSH) {
         if (use_drgb) {
@@ -1171,7 +1178,7 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
             const float4 r0 = row[0], r1 = row[1], r2 = row[2];
             d9[0] = r0.x; d9[1] = r0.y; d9[2] = r0.z; d9[3] = r0.w;
             d9[4] = r1.x; d9[5] = r1.y; d9[6] = r1.z; d9[7] = r1.w; d9[8] = r2.x;
-        } else {
+        } else if constexpr (!kDrgb) {
             load_sh_rows<kSH16>(a, idx, s, lrow);
         }
         cb = clamped_bits[idx];
@@ -1195,7 +1202,14 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     // ---- computeColorFromSH backward (backward.cu:20-139)
     // (two calls with a constant pointer each: a run-time select of d9 or
     // nullptr made the compiler keep d9 in scratch memory)
-    if (kHasSH) {
+    if constexpr (kDrgb) {
+        float dsh_c[16], dRGB[3];
+        sh_backward_terms(a.D, a.campos, mx, my, mz, s, cb, acc, dsh_c, dRGB, dmean, d9);
+#pragma unroll
+        for (int k = 0; k < 16; k++) (*sh19)[k] = dsh_c[k];
+#pragma unroll
+        for (int c = 0; c < 3; c++) (*sh19)[16 + c] = dRGB[c];
+    } else if (kHasSH) {
         if (use_drgb) sh_backward<kSH16>(a, idx, mx, my, mz, s, cb, acc, dmean, kSH16 ? lrow : nullptr, d9);
         else sh_backward<kSH16>(a, idx, mx, my, mz, s, cb, acc, dmean, kSH16 ? lrow : nullptr, nullptr);
     }
@@ -1313,6 +1327,61 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
     }
 }
 
+// The drgb-known form (the training path: the forward stored d(rgb)/d(dir)):
+// no SH-coefficient path (114 VGPRs: 4 waves per SIMD instead of 3) and the
+// 192-B dL_dsh rows staged through a half-size LDS area in two rounds of 128
+// Gaussians (25 KB, recomputed from the 16 basis values and dL/drgb each
+// thread keeps), then the small outputs as in backward_gaussians_kernel.
+__global__ void __launch_bounds__(256) backward_gaussians_drgb_kernel(BackwardGaussArgs a,
+                                                                      const float* __restrict__ grad_accum,
+                                                                      const uint8_t* __restrict__ clamped_bits) {
+    __shared__ float s_half[128 * kShRow];
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    float small[12], sh19[19];
+    backward_gaussian_body<true, true, true, true>(a, grad_accum, clamped_bits, idx, nullptr, &small, &sh19);
+    const int g0 = blockIdx.x * blockDim.x;
+    const int n = min(256, a.P - g0);
+    const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
+#pragma unroll 1
+    for (int h = 0; h < 2; h++) {
+        const int gh = g0 + 128 * h, nh = min(128, n - 128 * h);
+        if (nh <= 0) break;  // block-uniform
+        if (h) __syncthreads();  // the previous round's stores have read the area
+        if ((int)(threadIdx.x >> 7) == h && idx < a.P) {
+            float* r = s_half + (threadIdx.x & 127) * kShRow;
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) r[3 * k + c] = k < ncoef ? sh19[k] * sh19[16 + c] : 0.f;
+        }
+        __syncthreads();
+        float4* out = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)gh * 12;
+        for (int f = threadIdx.x; f < nh * 12; f += 256) {
+            const float* r = s_half + (f / 12) * kShRow + 4 * (f % 12);
+            out[f] = make_float4(r[0], r[1], r[2], r[3]);
+        }
+    }
+    __syncthreads();  // the SH rows are out: the area holds the small arrays now
+    if (idx < a.P) {
+#pragma unroll
+        for (int i = 0; i < 12; i++) s_half[(i / 3) * 768 + 3 * threadIdx.x + i % 3] = small[i];
+    }
+    __syncthreads();
+    const int nf = 3 * n;
+    for (int f = threadIdx.x; f < 4 * 192; f += 256) {
+        const int q = f / 192, i = f - 192 * q;
+        float* d = q == 0 ? a.dL_dmean2D : q == 1 ? a.dL_dmean3D : q == 2 ? a.dL_dscale : a.dL_dcolor;
+        if (!d || 4 * i >= nf) continue;
+        const float* r = s_half + q * 768 + 4 * i;
+        float* o = d + 3 * (size_t)g0 + 4 * i;
+        if (4 * i + 4 <= nf) {
+            *reinterpret_cast<float4*>(o) = make_float4(r[0], r[1], r[2], r[3]);
+        } else {
+            for (int e = 0; e < 4 && 4 * i + e < nf; e++) o[e] = r[e];
+        }
+    }
+}
+
 // Split mode, second kernel: the SH part alone (its ~50 live SH registers no
 // longer limit the occupancy of the geometry part).  Reads dL_dcolor and the
 // partial dL_dmeans3D the geometry kernel wrote, adds the SH term, writes
@@ -1346,7 +1415,8 @@ void set_bwd_gauss_split(int v) { g_bwd_gauss_split = v; }
 // set_tuning("bg_stage_mlp"): 1 the SH staging loads issued back to back; 2 =
 // 1 + the 3-float outputs stored coalesced through LDS (stage_small; the
 // default since round 4: 0.0848 -> 0.0828 ms at config 2, 0.529 -> 0.479 at
-// config 4, profiles/r04j_ab_bg*.log); < 0 the default
+// config 4, profiles/r04j_ab_bg*.log); 3 = 2 + the drgb-known kernel when
+// the host knows the forward stored d(rgb)/d(dir); < 0 the default
 constexpr int kDefaultBgStage = 2;
 int g_bg_stage_mlp = kDefaultBgStage;
 void set_bg_stage_mlp(int v) { g_bg_stage_mlp = v < 0 ? kDefaultBgStage : v; }
@@ -1367,7 +1437,9 @@ void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hi
         else hipLaunchKernelGGL((sh_backward_kernel<false>), grid, dim3(256), 0, s, a, g.clamped);
         return;
     }
-    if (sh16 && sc && g_bg_stage_mlp >= 2)
+    if (sh16 && sc && a.drgb && a.drgb_known && g_bg_stage_mlp >= 3)
+        hipLaunchKernelGGL(backward_gaussians_drgb_kernel, grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
+    else if (sh16 && sc && g_bg_stage_mlp >= 2)
         hipLaunchKernelGGL((backward_gaussians_kernel<true, true, true, true>), grid, dim3(256), 0, s, a, g.grad_accum,
                            g.clamped, g_bg_stage_mlp);
     else if (sh16 && sc) GS_BG_LAUNCH(true, true, true);

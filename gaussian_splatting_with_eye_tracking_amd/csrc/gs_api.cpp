@@ -267,6 +267,21 @@ void finish_header_read(uint32_t out[4], const uint32_t* mirror = nullptr, hipSt
 std::mutex g_clean_mu;
 std::unordered_set<const float*> g_accum_clean;
 
+// Geometry buffers whose forward stored d(rgb)/d(dir) (keyed by the rows'
+// address; set or cleared by every forward): the backward then launches the
+// drgb-known bwd_gauss kernel (no SH-coefficient path compiled in).
+std::mutex g_drgb_mu;
+std::unordered_set<const float*> g_drgb_rows;
+void set_drgb_written(const float* rows, bool w) {
+    std::lock_guard<std::mutex> l(g_drgb_mu);
+    if (w) g_drgb_rows.insert(rows);
+    else g_drgb_rows.erase(rows);
+}
+bool drgb_written(const float* rows) {
+    std::lock_guard<std::mutex> l(g_drgb_mu);
+    return g_drgb_rows.count(rows) > 0;
+}
+
 void set_accum_clean(const float* rows, bool clean) {
     std::lock_guard<std::mutex> l(g_clean_mu);
     if (clean) g_accum_clean.insert(rows);
@@ -286,6 +301,10 @@ void zero_accum_unless_clean(const GeomView& g, int P, hipStream_t s) {
 
 // Capacity for the speculative duplicate: the last base forward's K plus
 // 1/8 (0 before the first call, or when speculation is switched off).
+// set_tuning("fwd_zero"): 1 (default) the forward render zeroes the
+// backward's accumulator rows behind the blend when a backward can follow;
+// 0: never (the backward memsets them)
+int g_fwd_zero = 1;
 int g_spec_dup = 1;  // set_tuning("spec_dup")
 // The speculative duplicate's capacity, remembered per (device, W, H, P):
 // workloads that alternate render sizes or scenes (train 1080p / eval
@@ -457,6 +476,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     if (r.T > 0 && !lds_bin) GS_HIP(hipMemsetAsync(r.img.tile_count, 0, sizeof(uint32_t) * kBinSlots * r.T, s));
     PreprocessArgs pa = make_pp(in, tile);
     pa.err_token = next_error_token();
+    set_drgb_written(r.g.drgb, pa.store_drgb && in.colors_precomp == nullptr);
     if (r.T > 0 && lds_bin) {
         pa.zero_words = r.img.tile_count;
         pa.zero_n = kBinSlots * r.T;
@@ -546,8 +566,12 @@ int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image
         bool zeroed;
         {
             StageTimer _t(kRender, s);
+            // the accumulator rows are zeroed behind the blend only when a
+            // backward can follow (not under the forward-only hint: a later
+            // backward of this forward then zeroes them itself)
+            const bool zero = g_fwd_zero && t_store_drgb;
             zeroed = launch_render_forward(width, height, r.img, r.b, r.g, feats, background, out_color, s,
-                                           r.g.grad_accum, (size_t)kGradRow * (size_t)P,
+                                           zero ? r.g.grad_accum : nullptr, zero ? (size_t)kGradRow * (size_t)P : 0,
                                            hit_codes_at(r.b.point_list, (size_t)r.K));
         }
         if (zeroed) set_accum_clean(r.g.grad_accum, true);
@@ -609,6 +633,7 @@ int rasterizer_backward_impl(int amr_mode, int P, int D, int M, int R, const flo
         a.tan_fovy = tan_fovy;
         a.has_cov_precomp = cov3D_precomp != nullptr;
         a.drgb = g_sh_drgb ? g.drgb : nullptr;
+        a.drgb_known = a.drgb != nullptr && drgb_written(g.drgb);
         a.hdr = g.hdr;
         a.dL_dmean2D = dL_dmean2D;
         a.dL_dconic = dL_dconic;
@@ -1174,6 +1199,10 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "store_cov3d") == 0) {
         set_store_cov3d(value);
+        return 0;
+    }
+    if (std::strcmp(key, "fwd_zero") == 0) {
+        g_fwd_zero = value;
         return 0;
     }
     if (std::strcmp(key, "amr_levels_hist") == 0) {  // AMR percentiles by the two-pass histogram select

@@ -145,6 +145,7 @@ struct BackwardGaussArgs {
     int has_cov_precomp;
     const float* drgb;      // the forward's d(rgb)/d(dir) [9][P] (nullptr: from the SH coefficients)
     const uint32_t* hdr;    // the geometry header (kHdrDrgb says whether drgb was written)
+    int drgb_known;         // the host knows this geometry buffer's forward wrote drgb (gs_api registry)
     // outputs (every element written; no memsets needed)
     float* dL_dmean2D;
     float* dL_dconic;

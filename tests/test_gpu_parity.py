@@ -171,10 +171,25 @@ def test_backward_parity_preprocess_forms(pp_dma):
         C.set_tuning("pp_dma", -1)
 
 
-@pytest.mark.parametrize("stage", [1, 2])
+def test_backward_parity_without_forward_zeroing():
+    """fwd_zero 0: the forward leaves the accumulator rows alone and the
+    backward zeroes them itself (the path a forward under the forward-only
+    hint takes): gradients against the oracle."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    C.set_tuning("fwd_zero", 0)
+    try:
+        test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
+        test_backward_parity("ragged_3k_250x130", 3000, 250, 130, 7, "colors_precomp")
+    finally:
+        C.set_tuning("fwd_zero", 1)
+
+
+@pytest.mark.parametrize("stage", [1, 2, 3])
 def test_backward_parity_gauss_store_forms(stage):
-    """bwd_gauss with the 3-float outputs stored per thread (1) or staged
-    through LDS and stored coalesced (2): both against the oracle."""
+    """bwd_gauss with the 3-float outputs stored per thread (1), staged
+    through LDS and stored coalesced (2), and the drgb-known kernel (3: the
+    forward stored d(rgb)/d(dir), dL_dsh in two half-size LDS rounds): all
+    against the oracle."""
     import gaussian_splatting_with_eye_tracking_amd._C as C
     C.set_tuning("bg_stage_mlp", stage)
     try:
