@@ -1416,10 +1416,13 @@ void set_bwd_gauss_split(int v) { g_bwd_gauss_split = v; }
 // 1 + the 3-float outputs stored coalesced through LDS (stage_small; the
 // default since round 4: 0.0848 -> 0.0828 ms at config 2, 0.529 -> 0.479 at
 // config 4, profiles/r04j_ab_bg*.log); 3 = 2 + the drgb-known kernel when
-// the host knows the forward stored d(rgb)/d(dir); < 0 the default
-constexpr int kDefaultBgStage = 2;
-int g_bg_stage_mlp = kDefaultBgStage;
-void set_bg_stage_mlp(int v) { g_bg_stage_mlp = v < 0 ? kDefaultBgStage : v; }
+// the host knows the forward stored d(rgb)/d(dir) (config 2 0.0825 -> 0.0747
+// ms, config 4 0.465 -> 0.486: 4 waves per SIMD help the latency-bound small
+// scene, the two staging rounds cost the HBM-bound large one,
+// profiles/r04n_ab_bg*.log); < 0: auto -- 3 below 4M Gaussians, else 2
+int g_bg_stage_mlp = -1;
+void set_bg_stage_mlp(int v) { g_bg_stage_mlp = v < 0 ? -1 : v; }
+int bg_stage_for(int P) { return g_bg_stage_mlp >= 0 ? g_bg_stage_mlp : (P < 4000000 ? 3 : 2); }
 
 void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hipStream_t s) {
     if (a.P == 0) return;
@@ -1427,9 +1430,10 @@ void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hi
     const bool sh = a.shs != nullptr;
     const bool sh16 = sh && a.M == 16;
     const bool sc = a.scales != nullptr;
+    const int stage = bg_stage_for(a.P);
 #define GS_BG_LAUNCH(A, B, C) \
     hipLaunchKernelGGL((backward_gaussians_kernel<A, B, C>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped, \
-                       g_bg_stage_mlp)
+                       stage)
     if (sh && g_bwd_gauss_split && a.dL_dcolor) {  // (the split SH pass reads dL_dcolor back)
         if (sc) GS_BG_LAUNCH(false, true, false);
         else GS_BG_LAUNCH(false, false, false);
@@ -1437,11 +1441,11 @@ void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hi
         else hipLaunchKernelGGL((sh_backward_kernel<false>), grid, dim3(256), 0, s, a, g.clamped);
         return;
     }
-    if (sh16 && sc && a.drgb && a.drgb_known && g_bg_stage_mlp >= 3)
+    if (sh16 && sc && a.drgb && a.drgb_known && stage >= 3)
         hipLaunchKernelGGL(backward_gaussians_drgb_kernel, grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
-    else if (sh16 && sc && g_bg_stage_mlp >= 2)
+    else if (sh16 && sc && stage >= 2)
         hipLaunchKernelGGL((backward_gaussians_kernel<true, true, true, true>), grid, dim3(256), 0, s, a, g.grad_accum,
-                           g.clamped, g_bg_stage_mlp);
+                           g.clamped, stage);
     else if (sh16 && sc) GS_BG_LAUNCH(true, true, true);
     else if (sh16) GS_BG_LAUNCH(true, false, true);
     else if (sh && sc) GS_BG_LAUNCH(true, true, false);

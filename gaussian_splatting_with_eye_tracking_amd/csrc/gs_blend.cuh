@@ -352,12 +352,15 @@ __device__ __forceinline__ bool blend_one_sel(float2 xy, float4 co, float4 f, fl
 // last contributor is tracked as the entry's LDS byte offset (lo, the VGPR the
 // record reads already use) and converted once per 64 entries.  Bits for
 // every pixel still blending are those of blend_one_sel.
+template <bool kSafe = false>
 __device__ __forceinline__ bool blend_one_sel2(float2 xy, float4 co, float4 f, float pxx, float pxy, uint32_t lo,
                                                float& T, float (&C)[3], uint32_t& last_lo) {
     const float dx = xy.x - pxx, dy = xy.y - pxy;
     const float p = splat_p2(dx, dy, co);
     float a = fminf(0.99f, co.w * splat_exp(p));
-    a = (p > 0.0f) ? 0.0f : a;           // power > 0: skipped
+    // power > 0: skipped (kSafe: splat_form_safe -- the computed power is
+    // never > 0 over the tile, so the test cannot fire)
+    if (!kSafe) a = (p > 0.0f) ? 0.0f : a;
     a = (a < 1.0f / 255.0f) ? 0.0f : a;  // alpha < 1/255: skipped
     const float test_T = T * (1.0f - a);
     const bool stop = test_T < 0.0001f;  // false whenever a == 0 and T >= 1e-4; true for every finished pixel
@@ -465,10 +468,10 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
             s_co[tid] = splat_coef(co);
             s_b[tid * (kSel ? 4 : 1)] = features[3 * id + 2];  // (kSel: at a 16-B stride, one address for all reads)
             gm = cull ? splat_group_mask(xy, co, ox, oy, st) : 0xfu;
-            if (kSel == 2) safe = splat_form_safe(splat_coef(co), fabsf(xy.x - ox), fabsf(xy.y - oy));
+            if (kSel >= 2) safe = splat_form_safe(splat_coef(co), fabsf(xy.x - ox), fabsf(xy.y - oy));
         }
         publish_group_masks<kWaves>(gm, s_bal);
-        if (kSel == 2) {
+        if (kSel >= 2) {
             const uint64_t sb = __ballot(safe);
             if ((tid & 63) == 0) s_bal[4 * kWaves + (tid >> 6)] = sb;
         }
@@ -520,6 +523,52 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                         if (kRec) hits |= hB != 0ull ? 1ull << bB : 0ull;
                     }
                 }
+                if (last_lo != ~0u) st_.last[0] = b0 + (last_lo >> 4) + 1;
+                if (rec && (tid & 63) == 0) s_hit[c * kWaves + wave] = hits;
+                done[0] = st_.T[0] < 0.0f;
+                if (__ballot(!done[0]) == 0ull) wave_alive = false;
+                continue;
+            }
+            if constexpr (kPPL == 1 && kSel == 3) {
+                // kSel 1 with the `power > 0` test dropped for 64-slot chunks
+                // whose visited entries are all provably negative definite
+                // over the tile (splat_form_safe, published as with kSel 2):
+                // one loop copy per case, chosen per chunk (the same bits)
+                const uint64_t safe_m = uniform_u64(s_bal[4 * kWaves + c]);
+                uint64_t hits = 0;
+                uint32_t last_lo = ~0u;
+                const char* sa = reinterpret_cast<const char*>(s_a);
+                const char* sco = reinterpret_cast<const char*>(s_co);
+                const char* sb = reinterpret_cast<const char*>(s_b);
+                auto loop = [&](auto kSafeT) {
+                    constexpr bool kSafe = decltype(kSafeT)::value;
+                    while (todo) {
+                        const uint32_t bA = (uint32_t)__builtin_ctzll(todo);
+                        todo &= todo - 1;
+                        const bool two = todo != 0;  // wave-uniform
+                        const uint32_t bB = two ? (uint32_t)__builtin_ctzll(todo) : bA;
+                        if (two) todo &= todo - 1;
+                        const uint32_t loA = (c * 64 + bA) * 16, loB = (c * 64 + bB) * 16;
+                        const float4 sA = *reinterpret_cast<const float4*>(sa + loA);
+                        const float4 sB = *reinterpret_cast<const float4*>(sa + loB);
+                        const float4 coA = *reinterpret_cast<const float4*>(sco + loA);
+                        const float4 coB = *reinterpret_cast<const float4*>(sco + loB);
+                        const float bAc = *reinterpret_cast<const float*>(sb + loA);
+                        const float bBc = *reinterpret_cast<const float*>(sb + loB);
+                        const bool hA = blend_one_sel2<kSafe>(make_float2(sA.x, sA.y), coA,
+                                                              make_float4(sA.z, sA.w, bAc, 0.f), px.x, px.y[0], loA,
+                                                              st_.T[0], st_.C[0], last_lo);
+                        if (kRec) hits |= __ballot(hA) != 0ull ? 1ull << bA : 0ull;
+                        if (two) {
+                            const bool hB = blend_one_sel2<kSafe>(make_float2(sB.x, sB.y), coB,
+                                                                  make_float4(sB.z, sB.w, bBc, 0.f), px.x, px.y[0],
+                                                                  loB, st_.T[0], st_.C[0], last_lo);
+                            if (kRec) hits |= __ballot(hB) != 0ull ? 1ull << bB : 0ull;
+                        }
+                    }
+                };
+                if ((todo & ~safe_m) == 0ull) loop(std::integral_constant<bool, true>{});
+                else loop(std::integral_constant<bool, false>{});
                 if (last_lo != ~0u) st_.last[0] = b0 + (last_lo >> 4) + 1;
                 if (rec && (tid & 63) == 0) s_hit[c * kWaves + wave] = hits;
                 done[0] = st_.T[0] < 0.0f;

@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
     __shared__ float4 s_a[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
     __shared__ __attribute__((aligned(16))) float s_b[64 * kWaves * (kSel ? 4 : 1)];  // (kSel: 16-B stride)
-    __shared__ uint64_t s_bal[(kSel == 2 ? 5 : 4) * kWaves];  // (kSel 2: + the safe-form masks)
+    __shared__ uint64_t s_bal[(kSel >= 2 ? 5 : 4) * kWaves];  // (kSel 2, 3: + the safe-form masks)
     __shared__ uint64_t s_hit[kWaves * kWaves];
     __shared__ uint32_t s_max;
     if (kWaves > 1 && threadIdx.x == 0) s_max = 0;
@@ -159,6 +159,7 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
         case 4: GS_FWD_LAUNCH(1, 4, 6); break;
         case 6: GS_FWD_LAUNCH(1, 4, 1, 1); break;
         case 7: GS_FWD_LAUNCH(1, 4, 8, 2); break;  // 5 with SGPR-mask selects (gs_blend.cuh blend_one_msk)
+        case 8: GS_FWD_LAUNCH(1, 4, 8, 3); break;  // 5 without the power > 0 test in all-safe chunks
         default: GS_FWD_LAUNCH(1, 4, 8, 1); break;  // 5: 3 + the select-form blend
     }
 #undef GS_FWD_LAUNCH
