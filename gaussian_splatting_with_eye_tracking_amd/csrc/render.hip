@@ -126,12 +126,16 @@ void set_xcd_map(int v) { g_xcd_map = v; }
 // per SIMD: 0.307 -> 0.299 ms at config 2, profiles/r03c_ab_fwd_variant_cfg2.log); 5: 3 with the
 // select-form blend (gs_blend.cuh blend_one_sel: 0.305 -> 0.277 ms at config 2, 0.237 -> 0.223 ms at
 // config 4, profiles/r03d_ab_fwd_select_cfg{2,4}.log); 6: 5 at the default occupancy
-// (8, variant 5 with each visited bit cleared by s_andn2 on the hit bit,
-// measured equal: 0.2540 vs 0.2555 ms at config 2, 0.2235 vs 0.2227 at
-// config 4, profiles/r04h_ab_fwd*; removed)
-int g_fwd_variant = 5;
+// (an earlier variant 8, variant 5 with each visited bit cleared by s_andn2
+// on the hit bit, measured equal: 0.2540 vs 0.2555 ms at config 2, 0.2235 vs
+// 0.2227 at config 4, profiles/r04h_ab_fwd*; removed)
+// 8 (default since round 4): 5 without the `power > 0` test in 64-slot
+// chunks whose visited entries are all splat_form_safe: 0.2511 -> 0.2441 ms
+// at config 2, 0.1872 -> 0.1824 at config 4 (profiles/r04o_ab_fwd*.log)
+constexpr int kDefaultFwdVariant = 8;
+int g_fwd_variant = kDefaultFwdVariant;
 
-void set_forward_variant(int v) { g_fwd_variant = v; }
+void set_forward_variant(int v) { g_fwd_variant = v < 0 ? kDefaultFwdVariant : v; }
 
 bool launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                            const float* features, const float* bg, float* out_color, hipStream_t s,
@@ -159,8 +163,8 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
         case 4: GS_FWD_LAUNCH(1, 4, 6); break;
         case 6: GS_FWD_LAUNCH(1, 4, 1, 1); break;
         case 7: GS_FWD_LAUNCH(1, 4, 8, 2); break;  // 5 with SGPR-mask selects (gs_blend.cuh blend_one_msk)
-        case 8: GS_FWD_LAUNCH(1, 4, 8, 3); break;  // 5 without the power > 0 test in all-safe chunks
-        default: GS_FWD_LAUNCH(1, 4, 8, 1); break;  // 5: 3 + the select-form blend
+        case 5: GS_FWD_LAUNCH(1, 4, 8, 1); break;  // 3 + the select-form blend
+        default: GS_FWD_LAUNCH(1, 4, 8, 3); break;  // 8
     }
 #undef GS_FWD_LAUNCH
     return zero_n4 > 0;

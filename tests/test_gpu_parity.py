@@ -443,7 +443,7 @@ def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
                                                s.campos, geom, K, binning, img, False)
         torch.cuda.synchronize()
     finally:
-        C.set_tuning("fwd_variant", 2)
+        C.set_tuning("fwd_variant", -1)
         C.set_tuning("bwd_variant", -1)
     os_, ref, kw = _oracle_forward(sc, cam, bg=(0.2, 0.1, 0.05))
     assert G.image_l1(color.cpu().numpy(), ref.color) < G.IMAGE_L1_TOL
