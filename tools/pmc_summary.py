@@ -53,6 +53,7 @@ STAGES = [
     ("duplicate_kernel", "duplicate"),
     ("count_tiles_kernel", "count_tiles"),
     ("backward_gaussians_kernel", "bwd_gauss"),
+    ("backward_gaussians_drgb_kernel", "bwd_gauss"),
     ("sh_backward_kernel", "bwd_gauss"),
     ("preprocess_kernel", "preprocess"),
     ("sort_tiles_small_kernel", "sort_tiles"),
