@@ -1217,6 +1217,10 @@ int gs_set_tuning(const char* key, int value) {
         set_amr_deep(value);
         return 0;
     }
+    if (std::strcmp(key, "amr_lists_order") == 0) {
+        set_amr_lists_order(value);
+        return 0;
+    }
     if (std::strcmp(key, "amr_sel") == 0) {
         set_amr_sel(value);
         return 0;

@@ -109,6 +109,7 @@ void set_amr_variant(int v);
 void set_amr_batch(int v);
 void set_amr_fold(int v);
 void set_amr_sel(int v);
+void set_amr_lists_order(int v);
 void set_amr_deep(int v);
 void set_amr_lists_per(int v);
 void set_amr_levels_hist(int v);

@@ -516,6 +516,12 @@ constexpr int kRlThreads = 256;
 // 4 -> 0.083, 8 -> 0.083: occupancy beats per-thread memory parallelism)
 int g_amr_lists_per = 2;
 void set_amr_lists_per(int v) { g_amr_lists_per = v; }
+// 1: workgroup b builds the lists of tile_order[b] (the steps' heaviest-first
+// order, computed before the K copy) instead of tile b -- the heavy tiles'
+// serial passes no longer start last (0.0792 -> 0.0758 ms at config 3,
+// profiles/r04q_ab_lorder.log)
+int g_amr_lists_order = 1;
+void set_amr_lists_order(int v) { g_amr_lists_order = v; }
 // Region mask of one entry: the exact ellipse test (splat_rect_hit) on the
 // four 16x16 quadrants, refined to the 8x8 regions by the alpha >= 1/255
 // ellipse's bounding box (both conservative).  Bit g = 4 row + col.
@@ -556,13 +562,14 @@ __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, c
                                                                       float* __restrict__ rec_c,
                                                                       uint32_t* __restrict__ lists,
                                                                       uint32_t* __restrict__ region_count,
-                                                                      uint32_t* __restrict__ tile_done) {
+                                                                      uint32_t* __restrict__ tile_done,
+                                                                      const uint32_t* __restrict__ order) {
     constexpr int kW = kRlThreads / 64;
     // per pass: hits of (slot e, region g, wave w), then their exclusive
     // offsets in the pass's (e, w) order, per region
     __shared__ uint32_t s_cnt[16][kRlPer * kW];
     __shared__ uint32_t s_base[16];  // entries written per region by earlier passes
-    const int tile = blockIdx.x;
+    const int tile = order ? (int)order[blockIdx.x] : (int)blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t beg = ranges[2 * tile];
     const int n = (int)(ranges[2 * tile + 1] - beg);
@@ -634,7 +641,8 @@ void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningVi
 #define GS_RL_LAUNCH(PER)                                                                                       \
     hipLaunchKernelGGL(amr_region_lists_kernel<PER>, dim3(tgx * tgy), dim3(kRlThreads), 0, s, tgx, img.ranges,     \
                        b.point_list, reinterpret_cast<const float4*>(g.grad_accum), ab.rec_a, ab.rec_b, ab.rec_c,  \
-                       ab.region_lists, img.region_count, img.tile_done)
+                       ab.region_lists, img.region_count, img.tile_done,                                  \
+                       g_amr_lists_order ? img.tile_order : nullptr)
     switch (g_amr_lists_per) {
         case 2: GS_RL_LAUNCH(2); break;
         case 5: GS_RL_LAUNCH(5); break;
@@ -930,7 +938,9 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
                 // past the group's list are zero records), phase 2 folds them
                 // front to back with the finished state in T's sign -- no
                 // per-entry exec masks or bound tests, the same bits for every
-                // pixel still blending.
+                // pixel still blending.  (Dropping the power > 0 select in
+                // provably safe batches, the forward's variant 8 form, measured
+                // equal here: 0.0583 ms either way, profiles/r04q_ab_sel.log.)
 #pragma unroll
                 for (int j0 = 0; j0 < kRgBatch; j0 += kFold) {
                     float al[kFold][kSlots];

@@ -10,6 +10,8 @@ performs when it skips whole pixel groups with no live pixel --
   strip:  4 rows x 16 columns (the current row groups, 64 px)
   quad:   8 x 8 quadrants (64 px)
   half:   2 rows x 16 columns / 4 x 8 (32 px, a half-wave group)
+and for the forward (a wave per group, entries below the group's largest
+n_contrib whose alpha >= 1/255 ellipse reaches the group): fstrip / fquad.
 usage: python tools/cull_stats.py [--P 1000000 --W 1920 --H 1080]
 """
 from __future__ import annotations
@@ -52,7 +54,7 @@ def main() -> None:
     quad = ((py // 8) * 2 + px // 8).reshape(-1)
     half = (py // 2).reshape(-1)  # 8 groups of 2 rows x 16
     half8 = ((py // 4) * 2 + px // 8).reshape(-1)  # 8 groups of 4 rows x 8
-    tot = dict(live=0, none=0, strip=0, quad=0, half=0, half8=0, entries=0)
+    tot = dict(live=0, none=0, strip=0, quad=0, half=0, half8=0, entries=0, fstrip=0, fquad=0)
     step = max(1, a.tiles)
     for t in range(0, gx * gy, step):
         tx, ty = t % gx, t // gx
@@ -74,6 +76,16 @@ def main() -> None:
         power = -0.5 * (c[:, 0:1] * dx * dx + c[:, 2:3] * dy * dy) - c[:, 1:2] * dx * dy
         alpha = np.minimum(0.99, c[:, 3:4] * np.exp(power))
         live = (power <= 0) & (alpha >= 1.0 / 255.0) & (np.arange(last)[:, None] < ncp[None, :]) & inside[None, :]
+        # the forward: wave g evaluates the entries below the largest
+        # n_contrib of its pixels whose alpha >= 1/255 ellipse reaches the group
+        geo = (power <= 0) & (alpha >= 1.0 / 255.0) & inside[None, :]
+        for name, grp in (("fstrip", strip), ("fquad", quad)):
+            for k in range(4):
+                sel = grp == k
+                if not inside[sel].any():
+                    continue
+                mx = int(ncp[sel].max())
+                tot[name] += int(geo[:mx, sel].any(axis=1).sum()) * 64
         tot["live"] += int(live.sum())
         tot["entries"] += last
         tot["none"] += last * 256
@@ -83,7 +95,7 @@ def main() -> None:
                 any_g[:, k] = live[:, grp == k].any(axis=1)
             tot[name] += int(any_g.sum()) * (256 // n)
     print(tot)
-    for k in ("none", "strip", "quad", "half", "half8"):
+    for k in ("none", "strip", "quad", "half", "half8", "fstrip", "fquad"):
         print(f"{k:6s} evaluations {tot[k] / 1e6:9.1f} M  per live pair {tot[k] / max(1, tot['live']):.2f}")
 
 
