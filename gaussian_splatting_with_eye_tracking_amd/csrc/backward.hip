@@ -14,8 +14,9 @@
 //      reduction therefore serves 256 pixels,
 //   2. lane 63 parks the 9 sums in an LDS row,
 //   3. at the end of each 64-Gaussian batch the wave flushes each Gaussian's
-//      9 sums as a single 64-B row of grad_accum[P][16] (16 lanes per row, 4
-//      rows per wave instruction): one memory-side request per (tile, Gaussian).
+//      9 sums into its grad_accum[P][kGradRow] row (16 lanes per row, 4 rows
+//      per wave instruction; variant 11 adds them from the staging reduce
+//      itself, one atomic instruction per 7 Gaussians).
 // The backward also starts each tile at max(n_contrib) of its pixels
 // (recorded by the forward) instead of the end of the range: entries past it
 // are skipped by every pixel in the reference too.

@@ -21,11 +21,17 @@
 #include <stdint.h>
 
 #include <hip/hip_runtime.h>  // float4
+#include "gsplat_amd.h"  // GSPLAT_AMD_GRAD_ROW
 
 namespace gsamd {
 
 constexpr size_t kAlign = 256;
-constexpr int kGradRow = 16;  // floats per grad_accum row (9 used)
+// floats per grad_accum row: the blend's 9 sums, or the AMR forward's blend
+// record (three float4s); 48 B keeps every row 16-B aligned for float4 access
+// (64-B rows cost the forward's zeroing and the Gaussian backward's read 33 %
+// more bytes: 390 MB each per launch at config 4)
+constexpr int kGradRow = 12;
+static_assert(kGradRow == GSPLAT_AMD_GRAD_ROW, "the public layout constant");
 
 // Header words (geom buffer, device side).
 enum HdrWord : int {

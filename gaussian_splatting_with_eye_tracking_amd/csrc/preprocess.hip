@@ -212,7 +212,7 @@ __device__ __forceinline__ void pp_gaussian(const PreprocessArgs& a, const GeomV
     reinterpret_cast<float4*>(g.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     g.tiles_touched[idx] = area;
     if (a.block == 32) {
-        // AMR: the blend record of this Gaussian as ONE 64-B row of the
+        // AMR: the blend record of this Gaussian as ONE 48-B row of the
         // (forward-idle) grad_accum buffer, so foveaStep 0's region-list pass
         // (render.hip) gathers one line per instance instead of three:
         // (x, y, r, g), the log2(e)-scaled conic + opacity, (b, raw conic).
@@ -335,14 +335,13 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
                 if (c < 3 * nrow) out[c] = *reinterpret_cast<const float4*>(wl + 48 * (c / 3) + 4 * (c % 3));
             }
         }
-        if (a.block == 32) {  // AMR blend rows: 64 x 64 B (the fourth piece of a row is unused: zeros)
+        if (a.block == 32) {  // AMR blend rows: 64 x 48 B
+            static_assert(kGradRow == 12, "an AMR blend row is three float4s");
             float4* out = reinterpret_cast<float4*>(g.grad_accum + (size_t)kGradRow * wrow0);
 #pragma unroll
-            for (int i = 0; i < 4; i++) {
+            for (int i = 0; i < 3; i++) {
                 const int c = lane + 64 * i;
-                if (c < 4 * nrow)
-                    out[c] = (c & 3) == 3 ? make_float4(0.f, 0.f, 0.f, 0.f)
-                                          : *reinterpret_cast<const float4*>(wl + 48 * (c >> 2) + 16 + 4 * (c & 3));
+                if (c < 3 * nrow) out[c] = *reinterpret_cast<const float4*>(wl + 48 * (c / 3) + 16 + 4 * (c % 3));
             }
         }
         // 64 x 3 rgb floats = 48 pieces of 4

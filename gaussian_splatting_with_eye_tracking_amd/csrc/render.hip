@@ -551,7 +551,7 @@ __device__ __forceinline__ uint32_t region_mask(float2 xy, float4 co, float ox, 
     return m;
 }
 
-// rows: the per-Gaussian 64-B blend rows the AMR preprocess wrote into
+// rows: the per-Gaussian 48-B blend rows the AMR preprocess wrote into
 // grad_accum (preprocess.hip): (x, y, r, g), splat_coef, (b, raw conic).
 template <int kRlPer>
 __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, const uint32_t* __restrict__ ranges,
@@ -587,7 +587,8 @@ __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, c
             m[e] = 0;
             if (i < n) {
                 const uint32_t id = point_list[beg + i];
-                const float4 ra = rows[4 * (size_t)id], rb = rows[4 * (size_t)id + 1], rc = rows[4 * (size_t)id + 2];
+                const float4* rr = rows + (size_t)(kGradRow / 4) * id;
+                const float4 ra = rr[0], rb = rr[1], rc = rr[2];
                 rec_a[beg + i] = ra;
                 rec_b[beg + i] = rb;
                 rec_c[beg + i] = rc.x;

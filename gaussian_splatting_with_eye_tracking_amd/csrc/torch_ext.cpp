@@ -652,7 +652,7 @@ py::dict ParseBuffers(const Tensor& geomBuffer, const Tensor& binningBuffer, con
         d["cov3D"] = view(g.cov3D, {P, 6}, f32);
     d["clamped_bits"] = view(g.clamped, {P}, o.dtype(torch::kUInt8));
     d["tiles_touched"] = view(g.tiles_touched, {P}, i32);
-    d["grad_accum"] = view(g.grad_accum, {P, 16}, f32);
+    d["grad_accum"] = view(g.grad_accum, {P, GSPLAT_AMD_GRAD_ROW}, f32);
     d["accum_alpha"] = view(im.accum_alpha, {N}, f32);
     d["n_contrib"] = view(im.n_contrib, {N}, i32);
     d["ranges"] = view(im.ranges, {T, 2}, i32);

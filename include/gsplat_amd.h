@@ -28,7 +28,10 @@
 extern "C" {
 #endif
 
-#define GSPLAT_AMD_ABI_VERSION 4  /* 4: drgb / cov3D moved to an optional tail of the geometry buffer */
+#define GSPLAT_AMD_ABI_VERSION 5  /* 4: drgb / cov3D moved to an optional tail of the geometry buffer;
+                                     5: grad_accum rows of GSPLAT_AMD_GRAD_ROW = 12 floats (were 16) */
+/* floats per grad_accum row of the geometry buffer (gs_geom_view.grad_accum) */
+#define GSPLAT_AMD_GRAD_ROW 12
 
 /* Resize the caller-owned byte buffer `ctx` to `nbytes` and return its
  * (device, >=256-B aligned) base pointer, or NULL on failure.
@@ -305,7 +308,7 @@ typedef struct {
     uint8_t* clamped;     /* [P] bit c = channel c clamped */
     float* drgb;          /* [P][12] d(rgb)/d(view dir) of the SH colours, (x, y, z) x (r, g, b) + 3 pad (hdr[7] = 1: written), in the optional tail -- ABI 3 / 4 */
     uint32_t* tiles_touched;
-    float* grad_accum; /* [P][16] */
+    float* grad_accum; /* [P][GSPLAT_AMD_GRAD_ROW] */
 } gs_geom_view;
 
 typedef struct {

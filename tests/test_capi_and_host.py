@@ -61,10 +61,11 @@ def test_host_layout_helpers():
     lib.gs_binning_bytes.restype = ctypes.c_size_t
     lib.gs_knn_workspace_bytes.restype = ctypes.c_size_t
     # 2: gs_image_view gained the band arrays; 3: gs_geom_view gained drgb;
-    # 4: drgb and cov3D moved to an optional tail of the geometry buffer
-    assert lib.gs_abi_version() == 4
+    # 4: drgb and cov3D moved to an optional tail of the geometry buffer;
+    # 5: 48-B grad_accum rows
+    assert lib.gs_abi_version() == 5
     g1, g2 = lib.gs_geom_bytes(1000), lib.gs_geom_bytes(2000)
-    assert g2 > g1 > 1000 * (4 + 4 + 8 + 16 + 12 + 24 + 1 + 48 + 4 + 64)
+    assert g2 > g1 > 1000 * (4 + 4 + 8 + 16 + 12 + 24 + 1 + 48 + 4 + 48)
     assert lib.gs_image_bytes(1920, 1080, 16) >= 1920 * 1080 * 8 + 120 * 68 * 8
     assert lib.gs_binning_bytes(4096) >= 4096 * 20
     assert lib.gs_knn_workspace_bytes(10000) > 10000 * 16
@@ -113,7 +114,7 @@ def test_torch_extension_surface():
     for n in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "amr_rasterize_gaussians",
               "distCUDA2", "parse_buffers", "profile_enable", "profile_read", "set_tuning"):
         assert hasattr(_C, n), n
-    assert _C.abi_version() == 4
+    assert _C.abi_version() == 5
     assert all(os.path.exists(p) and p.startswith(ROOT) for p in native_library_paths())
 
 
