@@ -1420,7 +1420,11 @@ void set_bwd_gauss_split(int v) { g_bwd_gauss_split = v; }
 // the host knows the forward stored d(rgb)/d(dir) (config 2 0.0825 -> 0.0747
 // ms, config 4 0.465 -> 0.486: 4 waves per SIMD help the latency-bound small
 // scene, the two staging rounds cost the HBM-bound large one,
-// profiles/r04n_ab_bg*.log); < 0: auto -- 3 below 4M Gaussians, else 2
+// profiles/r04n_ab_bg*.log; again with 48-B rows: 0.4617 vs 0.4703,
+// r04y_ab_bg4.log); < 0: auto -- 3 below 4M Gaussians, else 2.  (3 staging
+// the 19 factors -- basis, dL/drgb -- in one round and forming each 16-B
+// dL_dsh piece from them measured slower: 0.0722 -> 0.0806 ms at config 2,
+// 0.447 -> 0.479 at config 4, profiles/r04z1_ab_bg*_stage4.log; removed)
 int g_bg_stage_mlp = -1;
 void set_bg_stage_mlp(int v) { g_bg_stage_mlp = v < 0 ? -1 : v; }
 int bg_stage_for(int P) { return g_bg_stage_mlp >= 0 ? g_bg_stage_mlp : (P < 4000000 ? 3 : 2); }
