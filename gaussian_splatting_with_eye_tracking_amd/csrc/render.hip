@@ -519,8 +519,11 @@ void set_amr_lists_per(int v) { g_amr_lists_per = v; }
 // 1: workgroup b builds the lists of tile_order[b] (the steps' heaviest-first
 // order, computed before the K copy) instead of tile b -- the heavy tiles'
 // serial passes no longer start last (0.0792 -> 0.0758 ms at config 3,
-// profiles/r04q_ab_lorder.log)
-int g_amr_lists_order = 1;
+// profiles/r04q_ab_lorder.log); 2 (default): XCD-compact strips
+// (gs_blend.cuh xcd_block_tile: neighbouring tiles, which gather the same
+// Gaussians' rows, share an XCD's L2): 0.0789 (1) -> 0.0765 ms with 48-B
+// rows, tile order 0.0818 (profiles/r04z2_ab_lorder.log)
+int g_amr_lists_order = 2;
 void set_amr_lists_order(int v) { g_amr_lists_order = v; }
 // Region mask of one entry: the exact ellipse test (splat_rect_hit) on the
 // four 16x16 quadrants, refined to the 8x8 regions by the alpha >= 1/255
@@ -563,13 +566,14 @@ __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, c
                                                                       uint32_t* __restrict__ lists,
                                                                       uint32_t* __restrict__ region_count,
                                                                       uint32_t* __restrict__ tile_done,
-                                                                      const uint32_t* __restrict__ order) {
+                                                                      const uint32_t* __restrict__ order, int xcd,
+                                                                      int tgy) {
     constexpr int kW = kRlThreads / 64;
     // per pass: hits of (slot e, region g, wave w), then their exclusive
     // offsets in the pass's (e, w) order, per region
     __shared__ uint32_t s_cnt[16][kRlPer * kW];
     __shared__ uint32_t s_base[16];  // entries written per region by earlier passes
-    const int tile = order ? (int)order[blockIdx.x] : (int)blockIdx.x;
+    const int tile = order ? (int)order[blockIdx.x] : xcd ? xcd_block_tile((int)blockIdx.x, tgx, tgy) : (int)blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t beg = ranges[2 * tile];
     const int n = (int)(ranges[2 * tile + 1] - beg);
@@ -643,7 +647,7 @@ void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningVi
     hipLaunchKernelGGL(amr_region_lists_kernel<PER>, dim3(tgx * tgy), dim3(kRlThreads), 0, s, tgx, img.ranges,     \
                        b.point_list, reinterpret_cast<const float4*>(g.grad_accum), ab.rec_a, ab.rec_b, ab.rec_c,  \
                        ab.region_lists, img.region_count, img.tile_done,                                  \
-                       g_amr_lists_order ? img.tile_order : nullptr)
+                       g_amr_lists_order == 1 ? img.tile_order : nullptr, g_amr_lists_order == 2 ? 1 : 0, tgy)
     switch (g_amr_lists_per) {
         case 2: GS_RL_LAUNCH(2); break;
         case 5: GS_RL_LAUNCH(5); break;

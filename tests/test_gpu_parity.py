@@ -773,7 +773,7 @@ def test_amr_forced_banded_duplicate(name, P, W, H, seed):
 
 DEFAULT_AMR_LISTS_PER = 2  # render.hip g_amr_lists_per
 DEFAULT_AMR_SEL = 1  # render.hip g_amr_sel
-DEFAULT_AMR_LISTS_ORDER = 1  # render.hip g_amr_lists_order
+DEFAULT_AMR_LISTS_ORDER = 2  # render.hip g_amr_lists_order
 
 
 @pytest.mark.parametrize("P,W,H,seed", [(10000, 256, 256, 0), (60000, 160, 96, 4), (3000, 2112, 1056, 8)])
@@ -791,9 +791,9 @@ def test_amr_fold_phases_bit_identical(P, W, H, seed):
     # (+ amr_sel: 1 the select-form fold, 2 its SGPR-mask form)
     variants = {"loop": (0, 0, 4, 1), "fold": (0x1e, 0, 4, 1), "deep": (0x1e, 0x1e, 4, 1), "lists2": (0x1e, 0, 2, 1),
                 "lists5": (0x1e, 0, 5, 1), "lists8": (0x1e, 0, 8, 1), "mask": (0x1e, 0, 2, 2),
-                "order": (0x1e, 0, 2, 1, 0)}
+                "order": (0x1e, 0, 2, 1, 0), "heavy": (0x1e, 0, 2, 1, 1)}
     # (+ amr_lists_order: 0 the lists built in tile-index order instead of the
-    # steps' heaviest-first order)
+    # XCD-compact strips, 1 in the steps' heaviest-first order)
     for name, (fold, deep, lper, sel, *lord) in variants.items():
         C.set_tuning("amr_fold", fold)
         C.set_tuning("amr_deep", deep)
@@ -815,7 +815,7 @@ def test_amr_fold_phases_bit_identical(P, W, H, seed):
         lv = d["levels"].cpu().numpy().astype(np.uint32)
         rendered = torch.from_numpy((O.amr_pixel_rounds(W, H) <= O.amr_tile_levels_per_pixel(lv, W, H)).reshape(-1))
         out[name] = [s_.cpu() for s_ in steps] + [d["n_contrib"].cpu()[rendered], d["accum_alpha"].cpu()[rendered]]
-    for name in ("fold", "deep", "lists2", "lists5", "lists8", "mask", "order"):
+    for name in ("fold", "deep", "lists2", "lists5", "lists8", "mask", "order", "heavy"):
         for a, b in zip(out["loop"], out[name]):
             assert torch.equal(a, b), name
 
