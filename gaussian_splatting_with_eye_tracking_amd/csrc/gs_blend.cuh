@@ -529,11 +529,15 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 if (__ballot(!done[0]) == 0ull) wave_alive = false;
                 continue;
             }
-            if constexpr (kPPL == 1 && kSel == 3) {
+            if constexpr (kPPL == 1 && kSel >= 3) {
                 // kSel 1 with the `power > 0` test dropped for 64-slot chunks
                 // whose visited entries are all provably negative definite
                 // over the tile (splat_form_safe, published as with kSel 2):
-                // one loop copy per case, chosen per chunk (the same bits)
+                // one loop copy per case, chosen per chunk (the same bits).
+                // kSel 4: the wave also leaves the chunk as soon as all its
+                // pixels have finished (one ballot per pair of entries instead
+                // of one per chunk: a saturating wave no longer runs out the
+                // rest of its chunk -- entries no pixel can blend any more)
                 const uint64_t safe_m = uniform_u64(s_bal[4 * kWaves + c]);
                 uint64_t hits = 0;
                 uint32_t last_lo = ~0u;
@@ -565,6 +569,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                                                                   loB, st_.T[0], st_.C[0], last_lo);
                             if (kRec) hits |= __ballot(hB) != 0ull ? 1ull << bB : 0ull;
                         }
+                        if (kSel >= 4 && __ballot(st_.T[0] > 0.0f) == 0ull) break;  // wave-uniform
                     }
                 };
                 if ((todo & ~safe_m) == 0ull) loop(std::integral_constant<bool, true>{});

@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
     __shared__ float4 s_a[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
     __shared__ __attribute__((aligned(16))) float s_b[64 * kWaves * (kSel ? 4 : 1)];  // (kSel: 16-B stride)
-    __shared__ uint64_t s_bal[(kSel >= 2 ? 5 : 4) * kWaves];  // (kSel 2, 3: + the safe-form masks)
+    __shared__ uint64_t s_bal[(kSel >= 2 ? 5 : 4) * kWaves];  // (kSel >= 2: + the safe-form masks)
     __shared__ uint64_t s_hit[kWaves * kWaves];
     __shared__ uint32_t s_max;
     if (kWaves > 1 && threadIdx.x == 0) s_max = 0;
@@ -129,10 +129,13 @@ void set_xcd_map(int v) { g_xcd_map = v; }
 // (an earlier variant 8, variant 5 with each visited bit cleared by s_andn2
 // on the hit bit, measured equal: 0.2540 vs 0.2555 ms at config 2, 0.2235 vs
 // 0.2227 at config 4, profiles/r04h_ab_fwd*; removed)
-// 8 (default since round 4): 5 without the `power > 0` test in 64-slot
-// chunks whose visited entries are all splat_form_safe: 0.2511 -> 0.2441 ms
-// at config 2, 0.1872 -> 0.1824 at config 4 (profiles/r04o_ab_fwd*.log)
-constexpr int kDefaultFwdVariant = 8;
+// 8: 5 without the `power > 0` test in 64-slot chunks whose visited entries
+// are all splat_form_safe: 0.2511 -> 0.2441 ms at config 2, 0.1872 -> 0.1824
+// at config 4 (profiles/r04o_ab_fwd*.log)
+// 9 (default since round 4): 8 with the wave's exit tested after every pair
+// of entries instead of every 64-slot chunk: config 2 equal (0.2456 /
+// 0.2458 ms), config 4 0.1819 -> 0.1755 (profiles/r04z3_ab_fwd*.log)
+constexpr int kDefaultFwdVariant = 9;
 int g_fwd_variant = kDefaultFwdVariant;
 
 void set_forward_variant(int v) { g_fwd_variant = v < 0 ? kDefaultFwdVariant : v; }
@@ -164,7 +167,8 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
         case 6: GS_FWD_LAUNCH(1, 4, 1, 1); break;
         case 7: GS_FWD_LAUNCH(1, 4, 8, 2); break;  // 5 with SGPR-mask selects (gs_blend.cuh blend_one_msk)
         case 5: GS_FWD_LAUNCH(1, 4, 8, 1); break;  // 3 + the select-form blend
-        default: GS_FWD_LAUNCH(1, 4, 8, 3); break;  // 8
+        case 8: GS_FWD_LAUNCH(1, 4, 8, 3); break;
+        default: GS_FWD_LAUNCH(1, 4, 8, 4); break;  // 9
     }
 #undef GS_FWD_LAUNCH
     return zero_n4 > 0;

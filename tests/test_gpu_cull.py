@@ -185,14 +185,16 @@ def test_sgpr_mask_forward_bit_identical(P, W, H, seed, adv):
         sc = S.make_scene(P, cam, seed=seed)
     res = {}
     try:
-        for v in (5, 7, 8):
+        for v in (5, 7, 8, 9):
             s, t, out, bufs = _forward(sc, cam, v)
             K = int(out[0])
             codes = C.parse_buffers(out[3], out[4], out[5], P, K, W, H, 16)["hit_codes"]
             res[v] = (out[1].cpu().numpy(), {k: b.cpu().numpy() for k, b in bufs.items()}, codes.cpu().numpy())
     finally:
         C.set_tuning("fwd_variant", -1)
-    for v in (7, 8):  # 8: variant 5 without the power > 0 test in all-safe chunks
+    # 8: variant 5 without the power > 0 test in all-safe chunks; 9: 8 leaving
+    # a chunk as soon as every pixel of the wave has finished
+    for v in (7, 8, 9):
         np.testing.assert_array_equal(res[5][0], res[v][0])
         for k in res[5][1]:
             np.testing.assert_array_equal(res[5][1][k], res[v][1][k], err_msg=(v, k))

@@ -423,7 +423,7 @@ def test_config2_full_size_parity_and_psnr():
 
 
 @pytest.mark.parametrize("bwd_variant", [0, 1, 2, 3, 5, 6, 7, 8, 9, 10, 11])
-@pytest.mark.parametrize("fwd_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8])
+@pytest.mark.parametrize("fwd_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
 def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
     """Every forward / backward blend geometry (gs_set_tuning) against the oracle."""
     import oracle as O
