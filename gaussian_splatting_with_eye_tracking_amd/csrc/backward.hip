@@ -1066,6 +1066,18 @@ __device__ __forceinline__ void cov3d_backward(float4 qrot, const float (&scl)[3
            4 * z * (Dm[1][1] + Dm[0][0]);
 }
 
+// A 16-B store of an output nothing in this pass reads back; nt: with the
+// non-temporal hint (the line is not kept in L2 for reuse).
+__device__ __forceinline__ void store_out4(float4* p, float4 v, bool nt) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    if (nt) __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
+    else *p = v;
+}
+__device__ __forceinline__ void store_out1(float* p, float v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // kSH16: SH with M = 16 coefficients (degree-3 models): compile-time loops,
 // 16-B loads and stores of the 192-B SH rows.
 // small: when given, the 3-float outputs (dL_dmeans2D, dL_dmeans3D,
@@ -1115,7 +1127,7 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
         a.dL_dmean2D[3 * idx + 2] = 0.f;
     }
     if (a.dL_dconic) reinterpret_cast<float4*>(a.dL_dconic)[idx] = make_float4(acc[5], acc[6], 0.f, acc[7]);
-    a.dL_dopacity[idx] = acc[8];
+    store_out1(&a.dL_dopacity[idx], acc[8], a.nt_out != 0);
 
     const int ncoef_out = a.M;  // dL_dsh is [P, M, 3]
     if (!vis) {
@@ -1225,6 +1237,7 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
         float dscale[3];
         float4 dq;
         cov3d_backward(qrot, scl, a.scale_modifier, dcov, dscale, dq);
+        store_out4(reinterpret_cast<float4*>(a.dL_drot) + idx, dq, a.nt_out != 0);
         if (small) {
             (*small)[6] = dscale[0];
             (*small)[7] = dscale[1];
@@ -1234,7 +1247,6 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
             a.dL_dscale[3 * idx + 1] = dscale[1];
             a.dL_dscale[3 * idx + 2] = dscale[2];
         }
-        reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
     } else {
         if (small) {
             (*small)[6] = (*small)[7] = (*small)[8] = 0.f;
@@ -1251,6 +1263,7 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
 // wave-contiguous 16-B stores: per-thread 192-B row stores measured ~3.5 TB/s
 // against ~5.4 TB/s coalesced on MI355X (tools/membench.hip).
 constexpr int kShRow = 49;
+
 
 template <bool kHasSH, bool kHasScales, bool kSH16, bool kSmall = false>
 __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussArgs a, const float* __restrict__ grad_accum,
@@ -1300,9 +1313,10 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
         const int g0 = blockIdx.x * blockDim.x;
         const int n = min(256, a.P - g0);
         float4* out = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)g0 * 12;
+        const bool nt = (stage_mlp & 16) != 0;
         for (int f = threadIdx.x; f < n * 12; f += 256) {
             const float* r = s_dsh + (f / 12) * kShRow + 4 * (f % 12);
-            out[f] = make_float4(r[0], r[1], r[2], r[3]);
+            store_out4(&out[f], make_float4(r[0], r[1], r[2], r[3]), nt);
         }
         if constexpr (kSmall) {
             __syncthreads();  // the SH rows are out: the LDS holds the small arrays now
@@ -1319,7 +1333,7 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
                 const float* r = s_dsh + q * 768 + 4 * i;
                 float* o = d + 3 * (size_t)g0 + 4 * i;
                 if (4 * i + 4 <= nf) {
-                    *reinterpret_cast<float4*>(o) = make_float4(r[0], r[1], r[2], r[3]);
+                    store_out4(reinterpret_cast<float4*>(o), make_float4(r[0], r[1], r[2], r[3]), a.nt_out != 0);
                 } else {
                     for (int e = 0; e < 4 && 4 * i + e < nf; e++) o[e] = r[e];
                 }
@@ -1335,7 +1349,8 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
 // thread keeps), then the small outputs as in backward_gaussians_kernel.
 __global__ void __launch_bounds__(256) backward_gaussians_drgb_kernel(BackwardGaussArgs a,
                                                                       const float* __restrict__ grad_accum,
-                                                                      const uint8_t* __restrict__ clamped_bits) {
+                                                                      const uint8_t* __restrict__ clamped_bits,
+                                                                      int nt) {
     __shared__ float s_half[128 * kShRow];
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     float small[12], sh19[19];
@@ -1359,7 +1374,7 @@ __global__ void __launch_bounds__(256) backward_gaussians_drgb_kernel(BackwardGa
         float4* out = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)gh * 12;
         for (int f = threadIdx.x; f < nh * 12; f += 256) {
             const float* r = s_half + (f / 12) * kShRow + 4 * (f % 12);
-            out[f] = make_float4(r[0], r[1], r[2], r[3]);
+            store_out4(&out[f], make_float4(r[0], r[1], r[2], r[3]), nt != 0);
         }
     }
     __syncthreads();  // the SH rows are out: the area holds the small arrays now
@@ -1376,7 +1391,7 @@ __global__ void __launch_bounds__(256) backward_gaussians_drgb_kernel(BackwardGa
         const float* r = s_half + q * 768 + 4 * i;
         float* o = d + 3 * (size_t)g0 + 4 * i;
         if (4 * i + 4 <= nf) {
-            *reinterpret_cast<float4*>(o) = make_float4(r[0], r[1], r[2], r[3]);
+            store_out4(reinterpret_cast<float4*>(o), make_float4(r[0], r[1], r[2], r[3]), a.nt_out != 0);
         } else {
             for (int e = 0; e < 4 && 4 * i + e < nf; e++) o[e] = r[e];
         }
@@ -1426,16 +1441,24 @@ void set_bwd_gauss_split(int v) { g_bwd_gauss_split = v; }
 // dL_dsh piece from them measured slower: 0.0722 -> 0.0806 ms at config 2,
 // 0.447 -> 0.479 at config 4, profiles/r04z1_ab_bg*_stage4.log; removed)
 int g_bg_stage_mlp = -1;
+// set_tuning("bg_nt"): bit 0 = the dL_dsh rows stored with the non-temporal
+// hint (the default: 0.0727 -> 0.0697 ms at config 2, 0.4582 -> 0.4393 at
+// config 4, profiles/r04z4_ab_nt*.log), bit 1 = the other outputs too
+// (0.0696 -> 0.0719 at config 2, config 4 equal: r04z5_ab_nt*.log)
+int g_bg_nt = 1;
+void set_bg_nt(int v) { g_bg_nt = v; }
 void set_bg_stage_mlp(int v) { g_bg_stage_mlp = v < 0 ? -1 : v; }
 int bg_stage_for(int P) { return g_bg_stage_mlp >= 0 ? g_bg_stage_mlp : (P < 4000000 ? 3 : 2); }
 
-void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hipStream_t s) {
-    if (a.P == 0) return;
+void launch_backward_gaussians(const BackwardGaussArgs& args, const GeomView& g, hipStream_t s) {
+    if (args.P == 0) return;
+    BackwardGaussArgs a = args;
     const dim3 grid((a.P + 255) / 256);
     const bool sh = a.shs != nullptr;
     const bool sh16 = sh && a.M == 16;
     const bool sc = a.scales != nullptr;
     const int stage = bg_stage_for(a.P);
+    a.nt_out = (g_bg_nt & 2) ? 1 : 0;
 #define GS_BG_LAUNCH(A, B, C) \
     hipLaunchKernelGGL((backward_gaussians_kernel<A, B, C>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped, \
                        stage)
@@ -1447,10 +1470,10 @@ void launch_backward_gaussians(const BackwardGaussArgs& a, const GeomView& g, hi
         return;
     }
     if (sh16 && sc && a.drgb && a.drgb_known && stage >= 3)
-        hipLaunchKernelGGL(backward_gaussians_drgb_kernel, grid, dim3(256), 0, s, a, g.grad_accum, g.clamped);
+        hipLaunchKernelGGL(backward_gaussians_drgb_kernel, grid, dim3(256), 0, s, a, g.grad_accum, g.clamped, g_bg_nt & 1);
     else if (sh16 && sc && stage >= 2)
         hipLaunchKernelGGL((backward_gaussians_kernel<true, true, true, true>), grid, dim3(256), 0, s, a, g.grad_accum,
-                           g.clamped, stage);
+                           g.clamped, stage | ((g_bg_nt & 1) ? 16 : 0));
     else if (sh16 && sc) GS_BG_LAUNCH(true, true, true);
     else if (sh16) GS_BG_LAUNCH(true, false, true);
     else if (sh && sc) GS_BG_LAUNCH(true, true, false);

@@ -1221,6 +1221,14 @@ int gs_set_tuning(const char* key, int value) {
         set_amr_lists_order(value);
         return 0;
     }
+    if (std::strcmp(key, "zero_nt") == 0) {
+        set_zero_nt(value);
+        return 0;
+    }
+    if (std::strcmp(key, "bg_nt") == 0) {
+        set_bg_nt(value);
+        return 0;
+    }
     if (std::strcmp(key, "amr_sel") == 0) {
         set_amr_sel(value);
         return 0;

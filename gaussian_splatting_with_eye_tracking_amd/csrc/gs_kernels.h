@@ -109,6 +109,8 @@ void set_amr_variant(int v);
 void set_amr_batch(int v);
 void set_amr_fold(int v);
 void set_amr_sel(int v);
+void set_bg_nt(int v);
+void set_zero_nt(int v);
 void set_amr_lists_order(int v);
 void set_amr_deep(int v);
 void set_amr_lists_per(int v);
@@ -147,6 +149,7 @@ struct BackwardGaussArgs {
     const float* drgb;      // the forward's d(rgb)/d(dir) [9][P] (nullptr: from the SH coefficients)
     const uint32_t* hdr;    // the geometry header (kHdrDrgb says whether drgb was written)
     int drgb_known;         // the host knows this geometry buffer's forward wrote drgb (gs_api registry)
+    int nt_out = 0;         // the outputs other than dL_dsh stored with the non-temporal hint (launcher)
     // outputs (every element written; no memsets needed)
     float* dL_dmean2D;
     float* dL_dconic;

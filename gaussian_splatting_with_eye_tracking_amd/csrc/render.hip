@@ -59,13 +59,17 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
                                                                  int zero_n4, uint32_t* __restrict__ bucket_count,
                                                                  uint32_t* __restrict__ bucket_list,
                                                                  uint8_t* __restrict__ hit_codes,
-                                                                 uint32_t* __restrict__ hdr) {
+                                                                 uint32_t* __restrict__ hdr, int zero_nt) {
     // The backward's per-Gaussian accumulator rows (grad_accum, idle in the
     // base forward) are zeroed here, behind the blend, instead of by a memset
     // on the backward's critical path: fire-and-forget stores in a kernel
-    // bound by VALU / LDS, not HBM (gs_api.cpp: accum_clean).
-    for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < zero_n4; i += (int)(gridDim.x * blockDim.x))
-        zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // bound by VALU / LDS, not HBM (gs_api.cpp: accum_clean).  zero_nt: with
+    // the non-temporal hint (the rows are next touched by the backward).
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    for (int i = (int)(blockIdx.x * blockDim.x + threadIdx.x); i < zero_n4; i += (int)(gridDim.x * blockDim.x)) {
+        if (zero_nt) __builtin_nontemporal_store(f4v{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f4v*>(zero4 + i));
+        else zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     __shared__ float4 s_a[64 * kWaves];
     __shared__ float4 s_co[64 * kWaves];
     __shared__ __attribute__((aligned(16))) float s_b[64 * kWaves * (kSel ? 4 : 1)];  // (kSel: 16-B stride)
@@ -109,6 +113,11 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
 }
 
 int g_cull = 1;         // row-group cull on (gs_blend.cuh); 0 only for the exactness A/B test
+// set_tuning("zero_nt"): the forward's grad_accum zeroing with the
+// non-temporal hint (default; fwd + bwd step equal at config 2, 2.552 ->
+// 2.540 ms at config 4 in the A/B tool, profiles/r04z5_ab_znt*.log)
+int g_zero_nt = 1;
+void set_zero_nt(int v) { g_zero_nt = v; }
 int g_hit_codes = 1;    // the forward records exact row-group hit codes for the backward (set_tuning("hit_codes"))
 void set_hit_codes(int v) { g_hit_codes = v; }
 void set_cull(int v) { g_cull = v; }
@@ -157,7 +166,7 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
                        b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
                        img.max_contrib, bg, out_color, g_cull, order, gx, g_xcd_map & 1, zero4, zero_n4,     \
-                       img.bucket_count, img.bucket_list, g_hit_codes ? hit_codes : nullptr, g.hdr)
+                       img.bucket_count, img.bucket_list, g_hit_codes ? hit_codes : nullptr, g.hdr, g_zero_nt)
     switch (g_fwd_variant) {
         case 0: GS_FWD_LAUNCH(4, 1); break;
         case 1: GS_FWD_LAUNCH(2, 2); break;

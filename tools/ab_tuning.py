@@ -4,6 +4,7 @@
 times from the library's profiler, median and min reported.
 
 usage: python tools/ab_tuning.py --key fwd_variant --values 0 1 2 --stage render [--backward]
+(--stage step: the whole call per run, events around the timed loop)
 """
 import argparse
 import json
@@ -119,15 +120,21 @@ def main():
                         print(f"WARNING variant {v}: {name} grad max rel diff {rel:.2e}")
             _C.profile_read(True)
             acc_steps = np.zeros(5)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
             for _ in range(args.iters):
                 run()
                 if args.amr and args.per_step:
                     torch.cuda.synchronize()
                     acc_steps += [evs[2 * k].elapsed_time(evs[2 * k + 1]) for k in range(5)]
+            e1.record()
             torch.cuda.synchronize()
             if args.amr and args.per_step:
                 step_ms[v].append(acc_steps / args.iters)
             prof = _C.profile_read(True)
+            if args.stage == "step":  # the whole forward (+ backward) per call, stream time
+                results[v].append(e0.elapsed_time(e1) / args.iters)
+                continue
             ms, cnt = prof[args.stage]
             results[v].append(ms / max(cnt, 1))
     _C.profile_enable(False)
