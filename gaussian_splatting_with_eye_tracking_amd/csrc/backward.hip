@@ -1444,7 +1444,10 @@ int g_bg_stage_mlp = -1;
 // set_tuning("bg_nt"): bit 0 = the dL_dsh rows stored with the non-temporal
 // hint (the default: 0.0727 -> 0.0697 ms at config 2, 0.4582 -> 0.4393 at
 // config 4, profiles/r04z4_ab_nt*.log), bit 1 = the other outputs too
-// (0.0696 -> 0.0719 at config 2, config 4 equal: r04z5_ab_nt*.log)
+// (0.0696 -> 0.0719 at config 2, config 4 equal: r04z5_ab_nt*.log).  (The
+// per-Gaussian input loads non-temporal measured slower: 0.0722 -> 0.0790 ms
+// at config 2, 0.426 -> 0.477 at config 4, profiles/r04z7_ab_bg*.log --
+// the three 4-B loads of a 12-B field each refetch the line; removed)
 int g_bg_nt = 1;
 void set_bg_nt(int v) { g_bg_nt = v; }
 void set_bg_stage_mlp(int v) { g_bg_stage_mlp = v < 0 ? -1 : v; }
@@ -1470,10 +1473,11 @@ void launch_backward_gaussians(const BackwardGaussArgs& args, const GeomView& g,
         return;
     }
     if (sh16 && sc && a.drgb && a.drgb_known && stage >= 3)
-        hipLaunchKernelGGL(backward_gaussians_drgb_kernel, grid, dim3(256), 0, s, a, g.grad_accum, g.clamped, g_bg_nt & 1);
+        hipLaunchKernelGGL(backward_gaussians_drgb_kernel, grid, dim3(256), 0, s, a, g.grad_accum, g.clamped,
+                           g_bg_nt & 1);
     else if (sh16 && sc && stage >= 2)
-        hipLaunchKernelGGL((backward_gaussians_kernel<true, true, true, true>), grid, dim3(256), 0, s, a, g.grad_accum,
-                           g.clamped, stage | ((g_bg_nt & 1) ? 16 : 0));
+        hipLaunchKernelGGL((backward_gaussians_kernel<true, true, true, true>), grid, dim3(256), 0, s, a,
+                           g.grad_accum, g.clamped, stage | ((g_bg_nt & 1) ? 16 : 0));
     else if (sh16 && sc) GS_BG_LAUNCH(true, true, true);
     else if (sh16) GS_BG_LAUNCH(true, false, true);
     else if (sh && sc) GS_BG_LAUNCH(true, true, false);

@@ -1221,6 +1221,10 @@ int gs_set_tuning(const char* key, int value) {
         set_amr_lists_order(value);
         return 0;
     }
+    if (std::strcmp(key, "pp_nt") == 0) {
+        set_pp_nt(value);
+        return 0;
+    }
     if (std::strcmp(key, "zero_nt") == 0) {
         set_zero_nt(value);
         return 0;

@@ -16,6 +16,24 @@ namespace gsamd {
 constexpr int kChannels = 3;
 constexpr int kWave = 64;
 
+// Loads of per-Gaussian inputs a pass reads exactly once; kNt: with the
+// non-temporal hint (the lines are not kept in L2 for reuse).
+template <bool kNt>
+__device__ __forceinline__ float ldg1(const float* p) {
+    if constexpr (kNt) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool kNt>
+__device__ __forceinline__ float4 ldg4(const float4* p) {
+    if constexpr (kNt) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+        return make_float4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
+
 // base/cr/auxiliary.h:22-39
 __device__ constexpr float SH_C0 = 0.28209479177387814f;
 __device__ constexpr float SH_C1 = 0.4886025119029199f;

@@ -36,6 +36,7 @@ struct PreprocessArgs {
     uint32_t* zero_words;
     int zero_n;
     uint32_t err_token;
+    int nt = 0;  // bit 0: the SH rows' LDS-DMA loads non-temporal; bit 1: the drgb rows' stores (launcher)
 };
 
 // base/cr/forward.cu:155-256 (+ the tile histogram the binning needs).
@@ -111,6 +112,7 @@ void set_amr_fold(int v);
 void set_amr_sel(int v);
 void set_bg_nt(int v);
 void set_zero_nt(int v);
+void set_pp_nt(int v);
 void set_amr_lists_order(int v);
 void set_amr_deep(int v);
 void set_amr_lists_per(int v);

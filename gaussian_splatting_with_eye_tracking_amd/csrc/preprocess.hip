@@ -239,7 +239,7 @@ __device__ __forceinline__ void pp_gaussian(const PreprocessArgs& a, const GeomV
 
 // One Gaussian: zero its counters, issue its loads, pp_gaussian.  stage: the
 // thread's LDS row for the strided records (kStageOut) or nullptr.
-template <bool kHasSH, bool kSH16, bool kCovPrecomp, bool kDma>
+template <bool kHasSH, bool kSH16, bool kCovPrecomp, bool kDma, bool kNtIn = false>
 __device__ __forceinline__ void pp_thread(const PreprocessArgs& a, const GeomView& g, int* __restrict__ radii,
                                           uint32_t* __restrict__ tile_count, int idx, const float* sh_row,
                                           float* stage) {
@@ -252,9 +252,11 @@ __device__ __forceinline__ void pp_thread(const PreprocessArgs& a, const GeomVie
 
     // Every global load of this Gaussian is issued up front (one memory round
     // trip per thread); the math below then overlaps other waves' loads.
-    const float mx = a.means3D[3 * idx + 0];
-    const float my = a.means3D[3 * idx + 1];
-    const float mz = a.means3D[3 * idx + 2];
+    // (kNtIn: non-temporal -- read once per pass, and the backward's re-read
+    // comes after far more traffic than the caches hold)
+    const float mx = ldg1<kNtIn>(a.means3D + 3 * idx + 0);
+    const float my = ldg1<kNtIn>(a.means3D + 3 * idx + 1);
+    const float mz = ldg1<kNtIn>(a.means3D + 3 * idx + 2);
     float sc[3] = {0.f, 0.f, 0.f};
     float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
     float cov3D[6];
@@ -262,12 +264,12 @@ __device__ __forceinline__ void pp_thread(const PreprocessArgs& a, const GeomVie
 #pragma unroll
         for (int i = 0; i < 6; i++) cov3D[i] = a.cov3D_precomp[6 * idx + i];
     } else {
-        sc[0] = a.scales[3 * idx + 0];
-        sc[1] = a.scales[3 * idx + 1];
-        sc[2] = a.scales[3 * idx + 2];
-        q = reinterpret_cast<const float4*>(a.rotations)[idx];
+        sc[0] = ldg1<kNtIn>(a.scales + 3 * idx + 0);
+        sc[1] = ldg1<kNtIn>(a.scales + 3 * idx + 1);
+        sc[2] = ldg1<kNtIn>(a.scales + 3 * idx + 2);
+        q = ldg4<kNtIn>(reinterpret_cast<const float4*>(a.rotations) + idx);
     }
-    const float opacity = a.opacities[idx];
+    const float opacity = ldg1<kNtIn>(a.opacities + idx);
     const Mat4 V = load_mat4(a.viewmatrix);
     const Mat4 Pm = load_mat4(a.projmatrix);
     pp_gaussian<kHasSH, kCovPrecomp>(a, g, radii, tile_count, idx, radii_copy, mx, my, mz, sc, q, cov3D, opacity,
@@ -291,7 +293,7 @@ __device__ __forceinline__ void pp_thread(const PreprocessArgs& a, const GeomVie
 // per-thread stores at a 48-B / 12-B stride (one store instruction covers
 // whole lines, not a third of each).  Rows of culled Gaussians carry stale
 // words, as their never-read records may.
-template <bool kHasSH, bool kSH16, bool kCovPrecomp, bool kDma = false, bool kStageOut = false>
+template <bool kHasSH, bool kSH16, bool kCovPrecomp, bool kDma = false, bool kStageOut = false, bool kNtIn = false>
 __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a, GeomView g, int* __restrict__ radii,
                                                                 uint32_t* __restrict__ tile_count) {
     static_assert(!kStageOut || (kDma && kHasSH), "staged records use the SH rows' LDS");
@@ -307,8 +309,10 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
 #pragma unroll
         for (int i = 0; i < 12; i++) {
             const size_t f = (size_t)(64 * i + lane) * 4;
-            if (row0 * 48 + f < nfl)
-                __builtin_amdgcn_global_load_lds(src + f, dst + 256 * i, 16, 0, 0);
+            if (row0 * 48 + f < nfl) {
+                if (a.nt & 1) __builtin_amdgcn_global_load_lds(src + f, dst + 256 * i, 16, 0, 2);  // (nt)
+                else __builtin_amdgcn_global_load_lds(src + f, dst + 256 * i, 16, 0, 0);
+            }
         }
     }
     for (int i = idx; i < a.zero_n; i += (int)(gridDim.x * blockDim.x)) a.zero_words[i] = 0u;
@@ -320,7 +324,7 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
         // every lane of a wave takes part in its coalesced record stores below
         const int wrow0 = (int)(blockIdx.x * kPpThreads) + (int)(threadIdx.x & ~63u);
         if (wrow0 >= a.P) return;  // wave-uniform
-        if (idx < a.P) pp_thread<kHasSH, kSH16, kCovPrecomp, kDma>(a, g, radii, tile_count, idx, row, row);
+        if (idx < a.P) pp_thread<kHasSH, kSH16, kCovPrecomp, kDma, kNtIn>(a, g, radii, tile_count, idx, row, row);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -332,7 +336,12 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
 #pragma unroll
             for (int i = 0; i < 3; i++) {
                 const int c = lane + 64 * i;
-                if (c < 3 * nrow) out[c] = *reinterpret_cast<const float4*>(wl + 48 * (c / 3) + 4 * (c % 3));
+                if (c < 3 * nrow) {
+                    const float4 v = *reinterpret_cast<const float4*>(wl + 48 * (c / 3) + 4 * (c % 3));
+                    typedef float f4v __attribute__((ext_vector_type(4)));
+                    if (a.nt & 2) __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(out + c));
+                    else out[c] = v;
+                }
             }
         }
         if (a.block == 32) {  // AMR blend rows: 64 x 48 B
@@ -377,12 +386,28 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
 // profiles/r04e_ab_pp*.log; removed)
 constexpr int kDefaultPpDma = 3;
 int g_pp_dma = kDefaultPpDma;
+// set_tuning("pp_nt"): bit 0 the SH rows' LDS-DMA loads non-temporal (0.0645
+// -> 0.0578 ms at config 2, 0.378 -> 0.356 at config 4, forward only;
+// profiles/r04z6_ab_pp*.log), bit 1 the drgb rows' stores (read once, by the
+// Gaussian backward, after more traffic than the caches hold; bits 0 + 1:
+// config-4 fwd + bwd step 2.544 -> 2.508 ms, r04z6_ab_ppstep4.log), bit 2
+// the geometry loads (pp_thread kNtIn: 0.394 -> 0.380 ms at config 4, config
+// 2 -1 %, r04z7_ab_pp*.log); default all three
+int g_pp_nt = 7;
+void set_pp_nt(int v) { g_pp_nt = v; }
 void set_pp_dma(int v) { g_pp_dma = v < 0 ? kDefaultPpDma : v; }
 
 template <bool A, bool B, bool C>
-static void launch_pp(const PreprocessArgs& a, const GeomView& g, int* radii, uint32_t* tile_count, hipStream_t s) {
+static void launch_pp(const PreprocessArgs& args, const GeomView& g, int* radii, uint32_t* tile_count, hipStream_t s) {
+    PreprocessArgs a = args;
+    a.nt = g_pp_nt;
     const int blocks = (a.P + kPpThreads - 1) / kPpThreads;
     if constexpr (A && B) {
+        if (g_pp_dma == 3 && (g_pp_nt & 4)) {
+            hipLaunchKernelGGL((preprocess_kernel<A, B, C, true, true, true>), dim3(blocks), dim3(kPpThreads), 0, s,
+                               a, g, radii, tile_count);
+            return;
+        }
         if (g_pp_dma == 3) {
             hipLaunchKernelGGL((preprocess_kernel<A, B, C, true, true>), dim3(blocks), dim3(kPpThreads), 0, s, a, g,
                                radii, tile_count);
