@@ -1735,13 +1735,15 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
         float4* out = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)(a.g0 + local0) * 12;
         for (int f = threadIdx.x; f < nblk * 12; f += 256) {
             const float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
-            out[f] = make_float4(r[0], r[1], r[2], r[3]);
+            store_out4(&out[f], make_float4(r[0], r[1], r[2], r[3]), a.nt != 0);
         }
     }
 }
 
-void launch_multiview_backward(const MultiViewArgs& a, hipStream_t s) {
-    if (a.count <= 0) return;
+void launch_multiview_backward(const MultiViewArgs& args, hipStream_t s) {
+    if (args.count <= 0) return;
+    MultiViewArgs a = args;
+    a.nt = g_bg_nt & 1;
     const dim3 grid((a.count + 255) / 256);
     const bool sh = a.shs != nullptr;
     if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward_kernel<true, true>), grid, dim3(256), 0, s, a);

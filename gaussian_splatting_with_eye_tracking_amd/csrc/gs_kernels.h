@@ -192,6 +192,7 @@ struct MultiViewArgs {
     float* grad_norm_accum;  // nullable: densification statistics, accumulated
     float* denom;
     float* max_radii;
+    int nt = 0;  // the dL_dsh rows stored with the non-temporal hint (launcher: bwd_gauss's bg_nt bit 0)
 };
 void launch_pack_view_grads(int P, const GeomView& g, const int* radii, bool has_sh, const float* viewmatrix,
                             const float* projmatrix, const float* campos, int width, int height, float tan_fovx,
