@@ -1581,10 +1581,26 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
     const int nblk = min(256, a.count - local0);
     if constexpr (kStage) {
         const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)(a.g0 + local0) * 12;
-        for (int f = threadIdx.x; f < nblk * 12; f += 256) {
-            const float4 v = in[f];
-            float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
-            r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+        if (nblk == 256) {
+            // a full workgroup: the 12 loads of each thread issued back to back
+            // (one memory round trip, as backward_gaussians_kernel's stage_mlp:
+            // multiview_bwd 0.3614 -> 0.3393 ms per 8-view step at config 5,
+            // profiles/r04ze_bench_cfg5.log against r04zz_bench.log)
+            float4 v[12];
+#pragma unroll
+            for (int k = 0; k < 12; k++) v[k] = in[threadIdx.x + 256 * k];
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                const int f = threadIdx.x + 256 * k;
+                float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
+                r[0] = v[k].x; r[1] = v[k].y; r[2] = v[k].z; r[3] = v[k].w;
+            }
+        } else {
+            for (int f = threadIdx.x; f < nblk * 12; f += 256) {
+                const float4 v = in[f];
+                float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
+                r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+            }
         }
         __syncthreads();
     }
