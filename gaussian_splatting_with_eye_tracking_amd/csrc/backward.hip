@@ -1183,7 +1183,10 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     float s[16][3];
     uint8_t cb = 0;
     // the forward's d(rgb)/d(dir) when it stored them: no SH coefficients read
-    const bool use_drgb = kDrgb || (kHasSH && a.drgb && a.hdr[kHdrDrgb] == 1u);  // uniform
+    // (the header word is checked in the drgb-known kernel too: the host picks
+    // that kernel from a registry keyed by the rows' address, which cannot see
+    // a geometry buffer no forward of this library wrote)
+    const bool use_drgb = kHasSH && a.drgb && a.hdr[kHdrDrgb] == 1u;  // uniform
     float d9[9];
     if (kHasSH) {
         if (use_drgb) {
@@ -1193,6 +1196,22 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
             d9[4] = r1.x; d9[5] = r1.y; d9[6] = r1.z; d9[7] = r1.w; d9[8] = r2.x;
         } else if constexpr (!kDrgb) {
             load_sh_rows<kSH16>(a, idx, s, lrow);
+        } else {
+            // drgb-known kernel, rows not written: the preprocess's derivatives
+            // from the coefficients (same operands as sh_backward_terms: the
+            // same bits), in a phase of their own before the body's peak
+            float c[16][3];
+            load_sh_rows<true>(a, idx, c);
+            const float dox = mx - a.campos[0], doy = my - a.campos[1], doz = mz - a.campos[2];
+            const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
+            float dx3[3], dy3[3], dz3[3];
+            sh_ddir(a.D, c, dox / len, doy / len, doz / len, dx3, dy3, dz3);
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                d9[k] = dx3[k];
+                d9[3 + k] = dy3[k];
+                d9[6 + k] = dz3[k];
+            }
         }
         cb = clamped_bits[idx];
     }

@@ -106,6 +106,14 @@ __device__ __forceinline__ void slot_cursors(uint32_t* __restrict__ count, uint3
 // between the scan and the work behind it.
 __device__ __forceinline__ void mirror_header(uint32_t* m, uint32_t K, uint32_t err, uint32_t maxc, uint32_t nlarge,
                                               uint32_t token) {
+    if (token) {
+        // seqlock: the slot's token is invalidated before the words change, so a
+        // reader that saw a token, copied the words and sees the same token
+        // again read words no later scan had started to rewrite
+        // (gs_api.cpp finish_header_read)
+        __hip_atomic_store(m + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+    }
     *reinterpret_cast<uint4*>(m) = make_uint4(K, err, maxc, nlarge);  // kHdrNumRendered, kHdrError, kHdrMaxTileCount, kHdrNumLargeTiles
     if (token) {
         __threadfence_system();

@@ -19,6 +19,8 @@
 #include <chrono>
 #include <cstring>
 #include <functional>
+#include <algorithm>
+#include <deque>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -270,16 +272,22 @@ std::unordered_set<const float*> g_accum_clean;
 // Geometry buffers whose forward stored d(rgb)/d(dir) (keyed by the rows'
 // address; set or cleared by every forward): the backward then launches the
 // drgb-known bwd_gauss kernel (no SH-coefficient path compiled in).
+// Bounded: the newest kDrgbEntries forwards' buffers (an entry older than that
+// only costs the drgb-known kernel; its device-side header check keeps a
+// stale entry correct either way).
+constexpr size_t kDrgbEntries = 64;
 std::mutex g_drgb_mu;
-std::unordered_set<const float*> g_drgb_rows;
+std::deque<const float*> g_drgb_rows;
 void set_drgb_written(const float* rows, bool w) {
     std::lock_guard<std::mutex> l(g_drgb_mu);
-    if (w) g_drgb_rows.insert(rows);
-    else g_drgb_rows.erase(rows);
+    g_drgb_rows.erase(std::remove(g_drgb_rows.begin(), g_drgb_rows.end(), rows), g_drgb_rows.end());
+    if (!w) return;
+    g_drgb_rows.push_back(rows);
+    if (g_drgb_rows.size() > kDrgbEntries) g_drgb_rows.pop_front();
 }
 bool drgb_written(const float* rows) {
     std::lock_guard<std::mutex> l(g_drgb_mu);
-    return g_drgb_rows.count(rows) > 0;
+    return std::find(g_drgb_rows.begin(), g_drgb_rows.end(), rows) != g_drgb_rows.end();
 }
 
 void set_accum_clean(const float* rows, bool clean) {
@@ -731,6 +739,45 @@ int gs_rasterizer_backward_view_grads(int P, int R, const float* background, int
 }
 
 namespace {
+// The view table of a call with more than kMaxViews views: pinned host staging
+// and a device copy, one pair per (thread, device), reused by every such call
+// -- no allocation, no stream synchronisation per call.  `done` (recorded
+// behind the kernel that reads the table) guards the reuse: the next call's
+// host writes wait for it, and its stream waits for it before the copy
+// overwrites the device table another stream's kernel may still read.
+struct ViewTable {
+    const float** host = nullptr;
+    const float** dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+};
+
+ViewTable& view_table(size_t n, hipStream_t s) {
+    thread_local std::vector<ViewTable> per_device;
+    int d = 0;
+    GS_HIP(hipGetDevice(&d));
+    if ((int)per_device.size() <= d) per_device.resize(d + 1);
+    ViewTable& t = per_device[d];
+    if (!t.done) GS_HIP(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
+    GS_HIP(hipEventSynchronize(t.done));  // the last use's copy and kernel are done (a fresh event: at once)
+    if (t.cap < n) {
+        if (t.host) GS_HIP(hipHostFree(t.host));
+        if (t.dev) GS_HIP(hipFree(t.dev));
+        t.host = nullptr;
+        t.dev = nullptr;
+        t.cap = 0;
+        void* h = nullptr;
+        void* dv = nullptr;
+        GS_HIP(hipHostMalloc(&h, n * sizeof(const float*), hipHostMallocDefault));
+        t.host = static_cast<const float**>(h);
+        GS_HIP(hipMalloc(&dv, n * sizeof(const float*)));
+        t.dev = static_cast<const float**>(dv);
+        t.cap = n;
+    }
+    GS_HIP(hipStreamWaitEvent(s, t.done, 0));
+    return t;
+}
+
 // rows[v] / cams[v]: view v's row of Gaussian g0 and its camera, summed in v order
 int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* const* rows, const float* const* cams,
                    const float* means3D, const float* shs, const float* scales, const float* rotations,
@@ -755,23 +802,20 @@ int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* c
         hipStream_t s = static_cast<hipStream_t>(stream);
         // up to kMaxViews views travel in the kernel arguments; more in a device
         // table (same kernel, same view order: bit-identical sums)
-        void* table = nullptr;
+        ViewTable* vt = nullptr;
         if (V <= kMaxViews) {
             for (int v = 0; v < V; v++) {
                 a.rows[v] = rows[v];
                 a.cams[v] = cams[v];
             }
         } else {
-            std::vector<const float*> host(2 * (size_t)V);
+            vt = &view_table(2 * (size_t)V, s);
             for (int v = 0; v < V; v++) {
-                host[v] = rows[v];
-                host[(size_t)V + v] = cams[v];
+                vt->host[v] = rows[v];
+                vt->host[(size_t)V + v] = cams[v];
             }
-            GS_HIP(hipMallocAsync(&table, host.size() * sizeof(const float*), s));
-            GS_HIP(hipMemcpyAsync(table, host.data(), host.size() * sizeof(const float*), hipMemcpyHostToDevice, s));
-            // (the host vector dies here: the pageable source must be consumed first)
-            GS_HIP(hipStreamSynchronize(s));
-            a.table = static_cast<const float* const*>(table);
+            GS_HIP(hipMemcpyAsync(vt->dev, vt->host, 2 * (size_t)V * sizeof(const float*), hipMemcpyHostToDevice, s));
+            a.table = vt->dev;
         }
         a.means3D = means3D;
         a.shs = shs;
@@ -787,7 +831,7 @@ int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* c
         a.denom = denom;
         a.max_radii = max_radii;
         { StageTimer _t(kMultiView, s); launch_multiview_backward(a, s); }
-        if (table) GS_HIP(hipFreeAsync(table, s));
+        if (vt) GS_HIP(hipEventRecord(vt->done, s));  // the staging and the table are free again after this
         stage_check(false, s, "multiview_backward");
         return 0;
     });

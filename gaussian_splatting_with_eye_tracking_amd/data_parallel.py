@@ -197,7 +197,14 @@ class ViewExchange:
         return out, w
 
     def add(self, j: int, rec: torch.Tensor) -> None:
-        """View j's record (any order; each j in [0, v) exactly once)."""
+        """View j's record; each j in [0, v) exactly once.
+
+        Every rank must add its views in the SAME order of j: add() issues
+        the step's collectives as it goes (a full-record all-gather for
+        j < v - 1; the cameras and the chunked row gathers for j = v - 1), and
+        collectives of different shapes issued in different orders on two
+        ranks mismatch (a hang or corrupted records).  With one rank any order
+        works."""
         if not 0 <= j < self.v:
             raise ValueError(f"ViewExchange.add: view {j} outside [0, {self.v})")
         if self.world == 1:

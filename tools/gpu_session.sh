@@ -2,10 +2,12 @@
 # Guarded GPU session for gpurun: every GPU step has its own time limit and
 # the script stops at the first fault-type exit (abort/segv/timeout).  A
 # pytest exit code of 1 (test failures) is not a fault and does not stop it.
-# usage: tools/gpu_session.sh <step> [<step> ...]   steps: tests smoke bench prof pmc
+# usage: [GS_TAG=r05a] tools/gpu_session.sh <step> [<step> ...]   steps: tests smoke bench prof pmc ...
+# logs go to gpurun_out/$GS_TAG/ (default gpurun_out/)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
+O=gpurun_out/${GS_TAG:-}
+mkdir -p "$O"
 export TMPDIR=/tmp
 # the digest of the native sources this session runs (tools/pmc_summary.py records it)
 python -c "import bench; print(bench.build_digest())" > gpurun_out/build_digest.txt
@@ -13,16 +15,19 @@ fault() { case "$1" in 0|1) return 1;; *) return 0;; esac; }
 run() {  # name limit cmd...
   local name=$1 lim=$2; shift 2
   echo "[gpu_session] $(date +%T) start $name"
-  timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+  timeout -k 10 "$lim" "$@" > "$O/$name.log" 2>&1
   local rc=$?
   echo "[gpu_session] $(date +%T) end $name rc=$rc"
-  tail -n 5 "gpurun_out/$name.log"
+  tail -n 5 "$O/$name.log"
   if fault "$rc"; then echo "[gpu_session] stopping after fault-type exit $rc in $name"; exit "$rc"; fi
   return 0
 }
 cfg_of() { case "$1" in *2) echo cfg2_1080p_1M;; *3) echo cfg3_amr_1080p_1M;; *4) echo cfg4_bicycle_6M;; *5) echo cfg5_8view_1080p_1M;; esac; }
 for step in "$@"; do
   case "$step" in
+    probe) run probe 60 bash -c 'echo "cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>&1)"; echo "cfs: $(cat /sys/fs/cgroup/cpu/cpu.cfs_quota_us 2>&1) / $(cat /sys/fs/cgroup/cpu/cpu.cfs_period_us 2>&1)"; echo "nproc $(nproc) OMP_NUM_THREADS=${OMP_NUM_THREADS:-unset}"; python3 -c "import bench; print(bench.cpu_share())"' ;;
+    gaptrace) run gaptrace 600 rocprofv3 --kernel-trace -d "$O/gaptrace" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sub ;;
+    benchns) run bench_ns 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sub ;;
     tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     configs) run pytest_configs 1100 python -u -m pytest tests/test_gpu_parity_configs.py tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf ;;
     amrtests) run pytest_amr 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_parity_configs.py tests/test_gpu_cull.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf -k "amr or config3 or cull" ;;
