@@ -21,9 +21,10 @@ namespace gsamd {
 
 constexpr int kLvlThreads = 1024;
 constexpr int kLvlSortMax = 2048;  // tile grids up to this size sort their counts in LDS
-// set_tuning("amr_levels_hist"): counts < 2^16 take the two-pass histogram
-// select (select3_u16) instead of the sort / the 4-pass radix select
-int g_amr_levels_hist = 1;
+// Counts < 2^16 take the two-pass histogram select (select3_u16: 19.2 ->
+// 13.5 us per frame at config 3, profiles/r04i_ab_lvl.log); a grid with a
+// larger count sorts its counts in LDS (<= kLvlSortMax tiles) or runs the
+// 4-pass radix select.
 
 // k-th smallest (0-based) of v[0..n) -- MSD radix select, one workgroup.
 // Counts are read straight from ranges (count = y - x) so no global value is
@@ -153,8 +154,7 @@ __global__ void __launch_bounds__(kLvlThreads) amr_levels_kernel(int T, const ui
                                                                  uint32_t* __restrict__ n_inter,
                                                                  uint32_t* __restrict__ pv,
                                                                  uint32_t* __restrict__ levels,
-                                                                 float4* __restrict__ zero4, int zero_n4,
-                                                                 int use_hist) {
+                                                                 float4* __restrict__ zero4, int zero_n4) {
     // blocks >= 1 (if any): foveaStep 0's zero image, grid-stride float4
     // stores on the other CUs while block 0 -- one CU -- computes the levels
     // (one launch instead of the levels kernel and a separate fill)
@@ -176,7 +176,7 @@ __global__ void __launch_bounds__(kLvlThreads) amr_levels_kernel(int T, const ui
         big |= x >= 65536u;
     }
     const float percentiles[3] = {0.25f, 0.5f, 0.9f};
-    if (use_hist && !__syncthreads_or(big)) {
+    if (!__syncthreads_or(big)) {
         // every count < 2^16: two digit passes for all three statistics
         const uint32_t kq[3] = {(uint32_t)(int)(percentiles[0] * (float)T), (uint32_t)(int)(percentiles[1] * (float)T),
                                 (uint32_t)(int)(percentiles[2] * (float)T)};  // float32 index, :630
@@ -223,8 +223,6 @@ __global__ void __launch_bounds__(kLvlThreads) amr_levels_kernel(int T, const ui
     }
 }
 
-void set_amr_levels_hist(int v) { g_amr_levels_hist = v; }
-
 void launch_amr_levels(int T, const ImageView& img, hipStream_t s, float* zero_image, size_t zero_floats) {
     if (T == 0) return;
     const int n4 = (zero_image && zero_floats % 4 == 0 && zero_floats / 4 <= (size_t)INT32_MAX) ? (int)(zero_floats / 4) : 0;
@@ -232,7 +230,7 @@ void launch_amr_levels(int T, const ImageView& img, hipStream_t s, float* zero_i
         (void)hipMemsetAsync(zero_image, 0, sizeof(float) * zero_floats, s);
     const int zb = n4 > 0 ? std::min(512, (n4 + kLvlThreads * 8 - 1) / (kLvlThreads * 8)) : 0;
     hipLaunchKernelGGL(amr_levels_kernel, dim3(1 + zb), dim3(kLvlThreads), 0, s, T, img.ranges, img.tile_count, img.pv,
-                       img.levels, reinterpret_cast<float4*>(zero_image), n4, g_amr_levels_hist);
+                       img.levels, reinterpret_cast<float4*>(zero_image), n4);
 }
 
 // amr/cr/rasterizer_impl.cu:208-243 (setFoveaAMRLevelsKernel)

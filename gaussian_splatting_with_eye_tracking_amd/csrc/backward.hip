@@ -8,15 +8,15 @@
 // are memory-side atomics at ~one 64-B request each, and 64 lanes hitting one
 // address serialise.  Here one wave64 owns a whole 16x16 tile (4 pixels per
 // lane, gs_blend.cuh) and, per Gaussian j of the LDS batch:
-//   1. each lane sums its 4 pixels' terms, then the wave sums its 64 lanes'
-//      9 values with DPP row_shr/row_bcast adds (no LDS traffic) -- skipped
-//      when no pixel of the tile contributes (a wave-uniform ballot); one
-//      reduction therefore serves 256 pixels,
-//   2. lane 63 parks the 9 sums in an LDS row,
-//   3. at the end of each 64-Gaussian batch the wave flushes each Gaussian's
-//      9 sums into its grad_accum[P][kGradRow] row (16 lanes per row, 4 rows
-//      per wave instruction; variant 11 adds them from the staging reduce
-//      itself, one atomic instruction per 7 Gaussians).
+//   1. each lane sums its 4 pixels' terms as moments (the lane's pixels share
+//      x), then the wave transposes the 64 lanes' values with permlane swaps
+//      down to 16 column partials per value, parked in an LDS staging slot;
+//   2. every 7 Gaussians, one 63-lane pass sums the staged partials (lane
+//      9 s + q = value q of slot s), forms the reference's nine terms and adds
+//      them into grad_accum[P][kGradRow] -- one atomic instruction per 7
+//      (tile, Gaussian) pairs.
+// (The fallback form sums by a full transposition into LDS rows and flushes
+// one 64-B atomic row per (tile, Gaussian) at the end of each batch.)
 // The backward also starts each tile at max(n_contrib) of its pixels
 // (recorded by the forward) instead of the end of the range: entries past it
 // are skipped by every pixel in the reference too.
@@ -37,40 +37,26 @@ namespace gsamd {
 
 constexpr int kNG = 9;      // gradient terms per (pixel, Gaussian)
 constexpr int kAccRow = 9;   // LDS accumulator row (floats; odd stride: 9 scalar stores per row)
+constexpr int kPPL = 4;      // pixels per lane: one wave64 covers the 16x16 tile (gs_blend.cuh mapping)
 
-// One 16x16 tile per workgroup of kWaves wave64s, kPPL pixels per lane
-// (kWaves * 64 * kPPL = 256; gs_blend.cuh mapping).  kMinWaves: waves per
-// SIMD the register allocation must allow.
-template <int kPPL, int kWaves, int kMinWaves, bool kSwap, bool kAMR = false, int kSel = 0>
-__global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
+// One 16x16 tile per single-wave workgroup, 4 pixels per lane (lane l: column
+// l % 16 of the 4 row groups).  kSel (the default): the select-form visit
+// with SGPR-mask selects and per-batch compare sets, staged transposed sums
+// and the flush fused into the staging reduce (below).  !kSel (the fallback,
+// and the AMR backward): the predicate form, full sums by transposition into
+// LDS rows, one 64-B atomic row per (tile, Gaussian) at the end of each batch.
+template <bool kSel, bool kAMR = false>
+__global__ void __launch_bounds__(64, 4) render_bwd_kernel(
     int W, int H, const uint32_t* __restrict__ ranges, const uint32_t* __restrict__ max_contrib,
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
     const float4* __restrict__ conic_opacity, const float* __restrict__ colors, const float* __restrict__ final_Ts,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ bg,
-    float* __restrict__ grad_accum, int cull, const uint32_t* __restrict__ order, int gx, int xcd,
-    int amr_mode, const uint32_t* __restrict__ levels, int flush_mode, const uint32_t* __restrict__ bucket_count,
-    const uint32_t* __restrict__ bucket_list, const uint8_t* __restrict__ hit_codes, const uint32_t* __restrict__ hdr) {
+    float* __restrict__ grad_accum, int cull, int gx, int amr_mode, const uint32_t* __restrict__ levels,
+    const uint32_t* __restrict__ bucket_count, const uint32_t* __restrict__ bucket_list,
+    const uint8_t* __restrict__ hit_codes, const uint32_t* __restrict__ hdr) {
 #pragma clang fp contract(fast)
-    static_assert(!kSel || (kWaves == 1 && kSwap), "the select form is the 1-wave transposed-sum geometry");
-    constexpr bool kStaged = kSel >= 2;  // staged sums (kSel 2, 3, 4)
-    constexpr bool kMaskSel = kSel >= 3;  // SGPR-mask selects, per-batch compare sets (kSel 3, 4)
-    // kSel 4: s2 joins the 8-value transposition (g6 = dx^2 s0 leaves it) and
-    // g6's column partials are dx x g4's, formed after the transposition by
-    // the lanes that hold them (lane l's pixels are column l % 16, its dx that
-    // column's): no DPP row tree for a ninth value, no lane-15 store
-    constexpr bool kG6Post = kSel >= 4;
-    // kSel 5: the 7 staging slots of a round unrolled (slot = a compile-time
-    // constant: LDS offsets as immediates, no slot counter / address VALU per
-    // entry) and the visited bit cleared with one s_andn2 on the 1 << bit the
-    // row tests use
-    constexpr bool kSlotUnroll = kSel >= 5;
-    // kSel 6: the staging reduce finishes the reference's nine terms itself
-    // (lane 9 s + q holds accumulator entry q of slot s's Gaussian; entries 4
-    // and 5 -- sum t dx, sum t dy -- fetched by two lane shuffles) and adds
-    // them into grad_accum: no accumulator rows in LDS, no per-batch flush
-    // pass, one atomic instruction per 7 Gaussians
-    constexpr bool kFusedFlush = kSel >= 6;
-    constexpr int kB = 64 * kWaves;  // Gaussians per LDS batch
+    static_assert(!(kSel && kAMR), "the AMR backward is the fallback form");
+    constexpr int kB = 64;  // Gaussians per LDS batch
     __shared__ uint32_t s_id[2][kB];  // double-buffered: the next batch's ids land while this one flushes
     // (x, y, r, g) and the scaled conic / opacity as two b128 reads, b as one
     // b32 (LDS cycles per wave-read: b128 4, b96 8, b64 / b32 2)
@@ -78,28 +64,23 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     __shared__ float4 s_co[kB];
     // (b at a 16-B stride: one LDS address serves all three record reads)
     __shared__ float4 s_b[kB];
-    // per-Gaussian sums: one wave parks its two half-wave partials (summed by
-    // the flush; 4 row partials would double the LDS footprint and cost
-    // workgroups per CU); several waves add into one row with LDS atomics
-    constexpr int kRowsPerG = (kWaves == 1 && !kSwap) ? 2 : 1;
-    __shared__ float s_acc[kFusedFlush ? 1 : kB * kRowsPerG * kAccRow + (kStaged ? 1 : 0)];  // (+ a dummy entry: staged sums)
-    __shared__ uint64_t s_bal[4 * kWaves];
-    // kSel == 2: the per-Gaussian sums are finished in groups of 7 Gaussians --
+    // !kSel: per-Gaussian sums, one row per batch slot, flushed per batch
+    __shared__ float s_acc[kSel ? 1 : kB * kAccRow];
+    __shared__ uint64_t s_bal[4];
+    // kSel: the per-Gaussian sums are finished in groups of 7 Gaussians --
     // each visit parks its two transposed registers (16 column partials of
-    // each of g0..g7, swap_rows8_pk) and g8's 4 row sums in a staging slot,
-    // and one pass over 7 slots sums them with 63 lanes at once (lane = 9 *
-    // slot + value) instead of 14 DPP adds per Gaussian.  Layout: reduce lane
-    // l's 16 partials are 4 float4s at l * 4 + i * kStagePitch (i = 0..3), so
-    // each b128 read is 64 consecutive dwords per 16 lanes; the pitch's
-    // 16-float pad spreads the writers' 4 column groups over all 64 banks.
-    // A g8 lane's 4 partials are its first float4; its other three stay zero.
+    // each of 8 values, swap_rows8_pk_t) in a staging slot, and one pass over
+    // 7 slots sums them with 63 lanes at once (lane = 9 * slot + value)
+    // instead of 14 DPP adds per Gaussian.  Layout: reduce lane l's 16
+    // partials are 4 float4s at l * 4 + i * kStagePitch (i = 0..3), so each
+    // b128 read is 64 consecutive dwords per 16 lanes; the pitch's 16-float pad
+    // spreads the writers' 4 column groups over all 64 banks.
     constexpr int kStageSlots = 7;
     constexpr int kStagePitch = 272;
-    __shared__ __attribute__((aligned(16))) float s_stage[kStaged ? 3 * kStagePitch + 256 : 1];
+    __shared__ __attribute__((aligned(16))) float s_stage[kSel ? 3 * kStagePitch + 256 : 1];
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const int wave = tid >> 6;
     // AMR mode (kAMR, amr_mode != 0; the foveated backward, an extension beyond
     // parity): block b = (32-px tile b / 4, sub-lattice (b & 1, (b >> 1) & 1)),
     // its 16 x 16 pixels at stride 2 -- the pixels amr_render_kernel blended
@@ -107,7 +88,6 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     // tiles with level >= k); < 0: render_once (rounds <= level).
     int tile;
     uint32_t ox, oy;
-    uint32_t gsel = 0xFu;  // row groups this block owns (a split heavy tile: a subset)
     // (a template parameter: run-time AMR branches cost the base kernel 12 %)
     constexpr uint32_t pstride = kAMR ? 2 : 1;
     if constexpr (kAMR) {
@@ -119,10 +99,10 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         ox = (uint32_t)(tile % gx) * 32 + sx;
         oy = (uint32_t)(tile / gx) * 32 + sy;
     } else {
-        if (kWaves == 1 && bucket_count) {
+        tile = (int)blockIdx.x;
+        if (bucket_count) {
             // rank blockIdx.x of the heaviest-first order: the bucket whose
-            // inclusive count first exceeds it (64 buckets, one per lane)
-            // (256 buckets: 4 per lane)
+            // inclusive count first exceeds it (256 buckets: 4 per lane)
             const uint4 c4 = reinterpret_cast<const uint4*>(bucket_count)[lane];
             const uint32_t c = c4.x + c4.y + c4.z + c4.w;
             uint32_t incl = c;
@@ -138,26 +118,18 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             // caller or size): every block takes the identity order instead,
             // so each tile is still processed exactly once
             const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-            if (total != gridDim.x || past == 0ull) {
-                tile = (int)blockIdx.x;
-            } else {
-            const int L = __builtin_ctzll(past);
-            uint32_t r = rank - (uint32_t)__builtin_amdgcn_readlane((int)(incl - c), L);
-            const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)c4.x, L),
-                           q1 = (uint32_t)__builtin_amdgcn_readlane((int)c4.y, L),
-                           q2 = (uint32_t)__builtin_amdgcn_readlane((int)c4.z, L);
-            int b = 4 * L;
-            if (r >= q0) { r -= q0; b++;
-                if (r >= q1) { r -= q1; b++;
-                    if (r >= q2) { r -= q2; b++; } } }
-            tile = (int)bucket_list[(size_t)b * gridDim.x + r];
+            if (total == gridDim.x && past != 0ull) {
+                const int L = __builtin_ctzll(past);
+                uint32_t r = rank - (uint32_t)__builtin_amdgcn_readlane((int)(incl - c), L);
+                const uint32_t q0 = (uint32_t)__builtin_amdgcn_readlane((int)c4.x, L),
+                               q1 = (uint32_t)__builtin_amdgcn_readlane((int)c4.y, L),
+                               q2 = (uint32_t)__builtin_amdgcn_readlane((int)c4.z, L);
+                int b = 4 * L;
+                if (r >= q0) { r -= q0; b++;
+                    if (r >= q1) { r -= q1; b++;
+                        if (r >= q2) { r -= q2; b++; } } }
+                tile = (int)bucket_list[(size_t)b * gridDim.x + r];
             }
-        } else if (order) {
-            const uint32_t u = order[blockIdx.x];
-            tile = (int)(u & 0x0FFFFFFFu);
-            if (kWaves == 1 && (u >> 28)) gsel = u >> 28;
-        } else {
-            tile = xcd ? xcd_block_tile((int)blockIdx.x, gx, (int)(gridDim.x / gx)) : (int)blockIdx.x;
         }
         ox = (uint32_t)(tile % gx) * 16;
         oy = (uint32_t)(tile / gx) * 16;
@@ -167,13 +139,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     int m = kAMR ? n : min(n, (int)max_contrib[tile]);
     if (m == 0) return;  // block-uniform
 
-    PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, pstride);
-    if constexpr (kWaves == 1) {
-        // a split unit's other row groups are somebody else's: no pixel there
-        // (last = 0, so every one of their entries is culled below)
-#pragma unroll
-        for (int k = 0; k < kPPL; k++) px.inside[k] = px.inside[k] && ((gsel >> k) & 1u);
-    }
+    const PixelSetT<kPPL> px = make_pixels_t<kPPL, 1>(W, H, ox, oy, pstride);
     const size_t plane = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
     // row group k's pixel y is py0 + 4 k stride: exact small-integer floats, the
@@ -215,12 +181,12 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         for (int off = 32; off >= 1; off >>= 1) g = max(g, (uint32_t)__shfl_xor((int)g, off, 64));
         group_last[k] = __builtin_amdgcn_readfirstlane((int)g);
     }
-    // kSel 3: the smallest n_contrib of each row group's image pixels (pixels
+    // kSel: the smallest n_contrib of each row group's image pixels (pixels
     // outside the image count as started: their T and dL/dpix are 0, so any
     // finite alpha leaves their terms 0).  Entries with contributor below it
     // are taken by every pixel of the group: no per-pixel contributor test.
     uint32_t min_last = 0xffffffffu;
-    if constexpr (kMaskSel) {
+    if constexpr (kSel) {
 #pragma unroll
         for (int k = 0; k < kPPL; k++) {
             uint32_t g = px.inside[k] ? last[k] : 0xffffffffu;
@@ -230,16 +196,10 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         }
         min_last = (uint32_t)__builtin_amdgcn_readfirstlane((int)min_last);
     }
-    // AMR: no per-tile max_contrib was recorded for the sub-lattice; with one
-    // wave per block (the only AMR instantiation) the wave max is the block's
-    if constexpr (kAMR) {
-        m = min(n, (int)wave_last);
-        if (m == 0) return;
-    } else if constexpr (kWaves == 1) {
-        // = max_contrib[tile] for a whole tile; a split unit's own, smaller max
-        m = min(m, __builtin_amdgcn_readfirstlane((int)wave_last));
-        if (m == 0) return;
-    }
+    // = max_contrib[tile] for a whole base tile; AMR: no per-tile max_contrib
+    // was recorded for the sub-lattice, the wave max is the block's
+    m = min(kAMR ? n : m, __builtin_amdgcn_readfirstlane((int)wave_last));
+    if (m == 0) return;
     // Row masks: the forward's exact hit codes when it left them (gs_blend.cuh
     // blend_tile_t: bit r = row group r has a pixel that blended the entry,
     // i.e. a pixel this backward takes it at), else the geometric cull.
@@ -247,7 +207,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
     const int comp = lane & 15;
-    // flush: the accumulator-row entry each output component starts from
+    // !kSel flush: the accumulator-row entry each output component starts from
     const int ia = comp < 3 ? comp : comp == 8 ? 3 : comp < 5 ? 4 : comp + 1;
 
     // Software pipeline over the batches (vector-memory counters retire in
@@ -267,25 +227,21 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         nrgb[0] = colors[3 * nid]; nrgb[1] = colors[3 * nid + 1]; nrgb[2] = colors[3 * nid + 2];
         s_id[0][tid] = nid;
     }
-    // kSel staging reduce: lane (slot = lane / 8, value q = lane % 8) sums the 16
-    // column partials of value q parked by slot's Gaussian (za rows hold values
-    // swap_sum_slot(r), zb rows 4 + swap_sum_slot(r); swap_sum_slot is its own
-    // inverse) and stores the total into that Gaussian's accumulator row.
+    // kSel staging reduce: lane (slot = lane / 9, value q = lane % 9) sums the
+    // 16 column partials of value q parked by slot's Gaussian (za rows hold
+    // values swap_sum_slot(r), zb rows 4 + swap_sum_slot(r); swap_sum_slot is
+    // its own inverse) and adds the reference's term into grad_accum.
     const int st_slot = lane / 9, st_q = lane - 9 * (lane / 9);
-    // reduce output: row jj's entry st_q; lane 63 (no slot) sums zeros into a
-    // dummy row, so a full group's pass needs no lane mask
-    const int st_mul = lane == 63 ? 0 : kAccRow, st_base = lane == 63 ? kB * kAccRow : st_q;
-    if constexpr (kStaged) {
+    if constexpr (kSel) {
         for (int i = lane; i < 3 * kStagePitch + 256; i += 64) s_stage[i] = 0.f;
     }
     // writer lane: row r = lane / 16 of za / zb holds values swap_sum_slot(r) /
-    // 4 + swap_sum_slot(r), column c = lane % 16 is element c of that sum;
-    // lane 16 r + 15 also holds g8's row-r sum, element r of value 8
+    // 4 + swap_sum_slot(r), column c = lane % 16 is element c of that sum.
+    // zb's value v = 4 + swap_sum_slot(r) of (g4, s1, s2, g7) goes to output
+    // q = v except s2 (v = 6) -> q = 8; g6 (q = 6) = dx x (g4's column
+    // partial), formed after the transposition by lanes 0-15 (zb row 0 = g4),
+    // the other lanes' product into their dummy word: no ninth-value DPP tree.
     const int st_dst = ((lane & 15) >> 2) * kStagePitch + 4 * swap_sum_slot(lane >> 4) + (lane & 3);
-    const int st_g8 = 32 + (lane >> 4);
-    // kG6Post: zb's value v = 4 + swap_sum_slot(r) of (g4, s1, s2, g7) goes to
-    // output q = v except s2 (v = 6) -> q = 8; g6 (q = 6) from lanes 0-15 (zb
-    // row 0 = g4), the other lanes' product into their dummy word
     const int st_dst_b = [&] {
         const int v = 4 + swap_sum_slot(lane >> 4);
         return ((lane & 15) >> 2) * kStagePitch + 4 * (v == 6 ? 8 : v) + (lane & 3);
@@ -299,7 +255,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         const int cnt = min(kB, top);
         __syncthreads();
         uint32_t gm = 0;
-        bool fastg = false;  // kSel 3: p2 <= 0 at every pixel of the tile, provably (below)
+        bool fastg = false;  // kSel: p2 <= 0 at every pixel of the tile, provably (below)
         if (tid < cnt) {
             const float2 xy = nxy;
             const float4 co = nco;
@@ -307,7 +263,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             s_a[tid] = make_float4(xy.x, xy.y, nrgb[0], nrgb[1]);
             s_co[tid] = pc;
             s_b[tid].x = nrgb[2];
-            if constexpr (kMaskSel)  // the reference's `power > 0` skip cannot fire (gs_blend.cuh)
+            if constexpr (kSel)  // the reference's `power > 0` skip cannot fire (gs_blend.cuh)
                 fastg = splat_form_safe(pc, fabsf(xy.x - (float)ox), fabsf(xy.y - (float)oy));
             gm = use_codes ? (uint32_t)hit_codes[range.x + top - 1 - tid]
                  : cull ? splat_group_mask(xy, co, (float)ox, (float)oy, (float)pstride) : 0xfu;
@@ -315,18 +271,21 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         const int ntop = top - kB;  // the next batch: entries [ntop - ncnt, ntop)
         const bool has_next = ntop > 0 && tid < min(kB, ntop);
         if (has_next) nid = point_list[range.x + ntop - 1 - tid];
-        publish_group_masks<kWaves>(gm, s_bal);
-        const uint64_t fast_mask = kMaskSel ? uniform_u64(__ballot(fastg)) : 0ull;  // (kWaves == 1: slot = lane)
+        publish_group_masks<1>(gm, s_bal);
+        const uint64_t fast_mask = kSel ? uniform_u64(__ballot(fastg)) : 0ull;
         // every contributor of this batch (<= top - 1) below every row group's
         // smallest n_contrib: all pixels take its entries
-        const bool bstarted = kMaskSel && (uint32_t)(top - 1) < min_last;
-        if (kWaves > 1)
-            for (int i = tid; i < kB * kAccRow; i += 64 * kWaves) s_acc[i] = 0.f;
-        uint64_t written = 0;  // kWaves == 1: batch slots whose partial rows were stored
-        int nst = 0;           // kSel == 2: staging slots in use (wave-uniform)
-        uint64_t js = 0;       // kSel == 2: batch slot j of staging slot s in bits [6 s, 6 s + 6)
-        auto stage_reduce = [&](const int n) {
-            if (n == kStageSlots || lane < 9 * n) {
+        const bool bstarted = kSel && (uint32_t)(top - 1) < min_last;
+        uint64_t written = 0;  // !kSel: batch slots whose sum rows were stored
+        int nst = 0;           // kSel: staging slots in use (wave-uniform)
+        uint64_t js = 0;       // kSel: batch slot j of staging slot s in bits [6 s, 6 s + 6)
+        // kSel: the staging reduce finishes the reference's nine terms itself
+        // (lane 9 s + q holds accumulator entry q of slot s's Gaussian; entries
+        // 4 and 5 -- sum t dx, sum t dy -- fetched by two lane shuffles) and
+        // adds them into grad_accum: no accumulator rows in LDS, no per-batch
+        // flush pass, one atomic instruction per 7 Gaussians
+        auto stage_reduce = [&](const int nslot) {
+            if (nslot == kStageSlots || lane < 9 * nslot) {
                 const float* src = &s_stage[4 * lane];
                 const float4 a = *reinterpret_cast<const float4*>(src);
                 const float4 b = *reinterpret_cast<const float4*>(src + kStagePitch);
@@ -336,28 +295,24 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                 const gs_f2 x2 = gs_f2{c.x, c.y} + gs_f2{d.x, d.y}, x3 = gs_f2{c.z, c.w} + gs_f2{d.z, d.w};
                 const gs_f2 y = (x0 + x1) + (x2 + x3);
                 const uint32_t jj = (uint32_t)(js >> (6 * st_slot)) & 63u;
-                if constexpr (kFusedFlush) {
-                    // lane 9 s + q: output component fq of q (entries 0..2 colours,
-                    // 3 = sum t -> opacity (8), 4 = sum t dx -> mean x (3), 5 = sum t
-                    // dy -> mean y (4), 6..8 -> conic (5..7)); the flush's formula
-                    const float tot = y.x + y.y;
-                    const float g4 = __shfl(tot, 9 * st_slot + 4, 64), sy = __shfl(tot, 9 * st_slot + 5, 64);
-                    if (lane < 63) {
-                        const int fq = st_q < 3 ? st_q : st_q == 3 ? 8 : st_q - 1;
-                        const float qa = (fq == 3 || fq == 4) ? g4 : tot;
-                        const float4 pc = s_co[jj];
-                        const float o = pc.w;
-                        const float cx = pc.x * (-1.0f / kHalfLog2e), cy = pc.y * (-1.0f / kLog2e),
-                                    cz = pc.z * (-1.0f / kHalfLog2e);
-                        const float ka = fq == 3 ? -o * cx * ddelx_dx
-                                       : fq == 4 ? -o * cy * ddely_dy
-                                       : (fq >= 5 && fq <= 7) ? -0.5f * o : 1.0f;
-                        const float kb = fq == 3 ? -o * cy * ddelx_dx : fq == 4 ? -o * cz * ddely_dy : 0.0f;
-                        const float v = ka * qa + kb * sy;
-                        if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[par][jj] * kGradRow + fq], v);
-                    }
-                } else {
-                    s_acc[jj * st_mul + st_base] = y.x + y.y;
+                // lane 9 s + q: output component fq of q (entries 0..2 colours,
+                // 3 = sum t -> opacity (8), 4 = sum t dx -> mean x (3), 5 = sum t
+                // dy -> mean y (4), 6..8 -> conic (5..7)); the flush's formula
+                const float tot = y.x + y.y;
+                const float g4 = __shfl(tot, 9 * st_slot + 4, 64), sy = __shfl(tot, 9 * st_slot + 5, 64);
+                if (lane < 63) {
+                    const int fq = st_q < 3 ? st_q : st_q == 3 ? 8 : st_q - 1;
+                    const float qa = (fq == 3 || fq == 4) ? g4 : tot;
+                    const float4 pc = s_co[jj];
+                    const float o = pc.w;
+                    const float cx = pc.x * (-1.0f / kHalfLog2e), cy = pc.y * (-1.0f / kLog2e),
+                                cz = pc.z * (-1.0f / kHalfLog2e);
+                    const float ka = fq == 3 ? -o * cx * ddelx_dx
+                                   : fq == 4 ? -o * cy * ddely_dy
+                                   : (fq >= 5 && fq <= 7) ? -0.5f * o : 1.0f;
+                    const float kb = fq == 3 ? -o * cy * ddelx_dx : fq == 4 ? -o * cz * ddely_dy : 0.0f;
+                    const float v = ka * qa + kb * sy;
+                    if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[par][jj] * kGradRow + fq], v);
                 }
             }
         };
@@ -367,29 +322,25 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
         // compiler cannot prove it; without this the bit-scan loop below is
         // compiled as a divergent VALU loop)
         const int j0 = __builtin_amdgcn_readfirstlane(max(0, top - (int)wave_last));
-#pragma unroll 1
-        for (int c = 0; c < kWaves; c++) {
-          if (64 * c + 64 <= j0) continue;
-          uint64_t mk[kPPL];
-          uint64_t todo = 0;
-          const uint64_t lo_cut = (j0 > 64 * c) ? ~0ull << (j0 - 64 * c) : ~0ull;
+        uint64_t mk[kPPL];
+        uint64_t todo = 0;
+        const uint64_t lo_cut = j0 >= 64 ? 0ull : j0 > 0 ? ~0ull << j0 : ~0ull;
 #pragma unroll
-          for (int k = 0; k < kPPL; k++) {
-              // slots j with contributor = top-1-j < group_last[k], i.e. j >= top - group_last[k]
-              const int jk = top - group_last[k] - 64 * c;
-              const uint64_t gcut = jk <= 0 ? ~0ull : (jk >= 64 ? 0ull : ~0ull << jk);
-              mk[k] = uniform_u64(s_bal[c * 4 + wave * kPPL + k]) & lo_cut & gcut;
-              todo |= mk[k];
-          }
-          // One Gaussian (batch slot j, record staged in LDS) against the
-          // wave's pixels.  (Reading the next set bit's record ahead, in two
-          // register sets used in turn, measured no faster: the 4 waves per
-          // SIMD already hide the LDS latency.)
-          auto visit = [&](const int cbit, const float2 xy, const float4 pc, const float4 cf, auto kFastT,
-                           auto kStartedT, auto kSlotT) {
+        for (int k = 0; k < kPPL; k++) {
+            // slots j with contributor = top-1-j < group_last[k], i.e. j >= top - group_last[k]
+            const int jk = top - group_last[k];
+            const uint64_t gcut = jk <= 0 ? ~0ull : (jk >= 64 ? 0ull : ~0ull << jk);
+            mk[k] = uniform_u64(s_bal[k]) & lo_cut & gcut;
+            todo |= mk[k];
+        }
+        // One Gaussian (batch slot j, record staged in LDS) against the wave's
+        // pixels.  (Reading the next set bit's record ahead, in two register
+        // sets used in turn, measured no faster: the 4 waves per SIMD already
+        // hide the LDS latency.)
+        auto visit = [&](const int j, const float2 xy, const float4 pc, const float4 cf, auto kFastT, auto kStartedT,
+                         auto kSlotT) {
             constexpr bool kFast = decltype(kFastT)::value, kStarted = decltype(kStartedT)::value;
-            constexpr int kSlot = decltype(kSlotT)::value;  // kSlotUnroll: this entry's staging slot
-            const int j = 64 * c + cbit;
+            constexpr int kSlot = decltype(kSlotT)::value;  // kSel: this entry's staging slot
             const uint32_t contributor = (uint32_t)(top - 1 - j);
             const float dx = xy.x - px.x;
             const float pa = (pc.x * dx) * dx, pb = pc.y * dx;  // the lane's pixels share x
@@ -404,15 +355,21 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             // 3-operand fma with an inline 0)
             float c0 = -0.f, c1 = -0.f, c2 = -0.f, s0 = -0.f, s1 = -0.f, s2 = -0.f;
             bool any = false;
-            if constexpr (kMaskSel) {
-                // kSel 2 with the selects on an SGPR-pair mask (gs_sel2_zero_v) and
-                // only the compares the entry needs: alpha >= 1/255 always;
-                // contributor < n_contrib unless the batch is started for every
-                // pixel; power > 0 only for Gaussians not provably negative
-                // definite (fast_mask).
+            if constexpr (kSel) {
+                // The select form: a rejected pixel takes alpha = G = 0, i.e.
+                // rinv = 1 (T unchanged), dchannel = t = 0 and acc_dot += 0 --
+                // the same bits as the predicate form for every accepted pixel,
+                // no exec-mask bookkeeping: a visited Gaussian is always summed
+                // (with the forward's hit codes a visited row group has a pixel
+                // that blended; under the geometric cull an all-rejected visit
+                // sums zeros, which the flush skips).  The selects take an
+                // SGPR-pair mask (gs_sel2_zero_v) and only the compares the
+                // entry needs: alpha >= 1/255 always; contributor < n_contrib
+                // unless the batch is started for every pixel; power > 0 only
+                // for Gaussians not provably negative definite (fast_mask).
 #pragma unroll
                 for (int k = 0; k < kPPL; k++) {
-                    if (!((mk[k] >> cbit) & 1ull)) continue;  // wave-uniform
+                    if (!((mk[k] >> j) & 1ull)) continue;  // wave-uniform
                     const float dy = xy.y - (py0 + (float)(4 * k * (int)pstride));
                     const float p2 = splat_p2(pa, pb, dy, pc);
                     const float Gr = splat_exp(p2);
@@ -422,42 +379,6 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                     if (!kFast) msk &= __builtin_amdgcn_fcmpf(p2, 0.0f, kFcmpULE);
                     float G, alpha;
                     gs_sel2_zero_v(msk, Gr, ar, G, alpha);
-                    const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
-                    T[k] = T[k] * rinv;
-                    const float dchannel_dcolor = alpha * T[k];
-                    const float diff = __builtin_fmaf(cf.z, dpx[k][2],
-                                                      __builtin_fmaf(cf.y, dpx[k][1],
-                                                                     __builtin_fmaf(cf.x, dpx[k][0], -acc_dot[k])));
-                    const float dL_dalpha = diff * T[k];
-                    acc_dot[k] = __builtin_fmaf(alpha, diff, acc_dot[k]);
-                    c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
-                    c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
-                    c2 = __builtin_fmaf(dchannel_dcolor, dpx[k][2], c2);
-                    const float t = G * dL_dalpha;
-                    const float tdy = t * dy;
-                    s0 += t;
-                    s1 += tdy;
-                    s2 = __builtin_fmaf(tdy, dy, s2);
-                }
-                any = true;
-            } else if constexpr (kSel) {
-                // Select form: a rejected pixel takes alpha = G = 0, i.e.
-                // rinv = 1 (T unchanged), dchannel = t = 0 and acc_dot += 0 --
-                // the same bits as the branchy form for every accepted pixel, no
-                // exec-mask bookkeeping and no ballot: a visited Gaussian is
-                // always summed (with the forward's hit codes a visited row
-                // group has a pixel that blended; under the geometric cull an
-                // all-rejected visit sums zeros, which the flush skips).
-#pragma unroll
-                for (int k = 0; k < kPPL; k++) {
-                    if (!((mk[k] >> cbit) & 1ull)) continue;  // wave-uniform
-                    const float dy = xy.y - (py0 + (float)(4 * k * (int)pstride));
-                    const float p2 = splat_p2(pa, pb, dy, pc);
-                    const float Gr = splat_exp(p2);
-                    const float ar = fminf(0.99f, pc.w * Gr);
-                    const bool ok = contributor < last[k] && !(p2 > 0.0f) && !(ar < 1.0f / 255.0f);
-                    const float G = ok ? Gr : 0.f;
-                    const float alpha = ok ? ar : 0.f;
                     const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
                     T[k] = T[k] * rinv;
                     const float dchannel_dcolor = alpha * T[k];
@@ -477,41 +398,42 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
                     s2 = __builtin_fmaf(tdy, dy, s2);
                 }
                 any = true;
-            } else
+            } else {
 #pragma unroll
-            for (int k = 0; k < kPPL; k++) {
-                if (!((mk[k] >> cbit) & 1ull)) continue;  // wave-uniform: culled for this row group
-                const float dy = xy.y - (py0 + (float)(4 * k * (int)pstride));
-                const float p2 = splat_p2(pa, pb, dy, pc);  // the forward's bits
-                const float G = splat_exp(p2);
-                const float alpha = fminf(0.99f, pc.w * G);
-                // The reference's three per-pixel `continue`s (backward.cu:466-482)
-                // as one predicate: only wave-uniform branches save SIMD time, and
-                // nested ones make the compiler re-zero g[] on every skip path.
-                // (contributor >= last also covers pixels outside the image.)
-                const bool ok = contributor < last[k] && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
-                if (!ok) continue;
-                any = true;
-                const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
-                T[k] = T[k] * rinv;
-                const float dchannel_dcolor = alpha * T[k];
-                // sum_ch (c - accum_rec) dL_dpix, with accum_rec . dL_dpix
-                // advanced by the reference's recurrence (backward.cu:500-507)
-                const float c_dot = cf.x * dpx[k][0] + cf.y * dpx[k][1] + cf.z * dpx[k][2];
-                // The reference advances accum_rec at the NEXT contributor from the
-                // stored (last_alpha, last_color); advancing it here with the same
-                // operands gives the same bits and needs no per-pixel "last" state.
-                const float diff = c_dot - acc_dot[k];
-                const float dL_dalpha = diff * T[k] + nbg[k] * rinv;
-                acc_dot[k] = __builtin_fmaf(alpha, diff, acc_dot[k]);
-                c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
-                c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
-                c2 = __builtin_fmaf(dchannel_dcolor, dpx[k][2], c2);
-                const float t = G * dL_dalpha;
-                const float tdy = t * dy;
-                s0 += t;
-                s1 += tdy;
-                s2 = __builtin_fmaf(tdy, dy, s2);
+                for (int k = 0; k < kPPL; k++) {
+                    if (!((mk[k] >> j) & 1ull)) continue;  // wave-uniform: culled for this row group
+                    const float dy = xy.y - (py0 + (float)(4 * k * (int)pstride));
+                    const float p2 = splat_p2(pa, pb, dy, pc);  // the forward's bits
+                    const float G = splat_exp(p2);
+                    const float alpha = fminf(0.99f, pc.w * G);
+                    // The reference's three per-pixel `continue`s (backward.cu:466-482)
+                    // as one predicate: only wave-uniform branches save SIMD time, and
+                    // nested ones make the compiler re-zero g[] on every skip path.
+                    // (contributor >= last also covers pixels outside the image.)
+                    const bool ok = contributor < last[k] && !(p2 > 0.0f) && !(alpha < 1.0f / 255.0f);
+                    if (!ok) continue;
+                    any = true;
+                    const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
+                    T[k] = T[k] * rinv;
+                    const float dchannel_dcolor = alpha * T[k];
+                    // sum_ch (c - accum_rec) dL_dpix, with accum_rec . dL_dpix
+                    // advanced by the reference's recurrence (backward.cu:500-507)
+                    const float c_dot = cf.x * dpx[k][0] + cf.y * dpx[k][1] + cf.z * dpx[k][2];
+                    // The reference advances accum_rec at the NEXT contributor from the
+                    // stored (last_alpha, last_color); advancing it here with the same
+                    // operands gives the same bits and needs no per-pixel "last" state.
+                    const float diff = c_dot - acc_dot[k];
+                    const float dL_dalpha = diff * T[k] + nbg[k] * rinv;
+                    acc_dot[k] = __builtin_fmaf(alpha, diff, acc_dot[k]);
+                    c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
+                    c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
+                    c2 = __builtin_fmaf(dchannel_dcolor, dpx[k][2], c2);
+                    const float t = G * dL_dalpha;
+                    const float tdy = t * dy;
+                    s0 += t;
+                    s1 += tdy;
+                    s2 = __builtin_fmaf(tdy, dy, s2);
+                }
             }
             float g[kNG];
             g[0] = c0;
@@ -520,144 +442,85 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             g[3] = s0;
             g[4] = dx * s0;
             g[5] = s1;
-            g[6] = kG6Post ? s2 : dx * g[4];
+            g[6] = kSel ? s2 : dx * g[4];
             g[7] = dx * s1;
             g[8] = s2;
-            if (kSel ? any : __ballot(any) != 0ull) {  // wave-uniform
-                if constexpr (kSlotUnroll) {
-                    float za, zb;
-                    swap_rows8_pk_t<false>(g, za, zb);
-                    const float w6 = dx * zb;
-                    s_stage[st_dst + 36 * kSlot] = za;
-                    s_stage[st_dst_b + 36 * kSlot] = zb;
-                    s_stage[st_g6 + (lane < 16 ? 36 * kSlot : 0)] = w6;
-                    js |= (uint64_t)j << (6 * kSlot);  // (written: every todo bit, set before the loop)
-                } else if constexpr (kG6Post) {
-                    float za, zb;
-                    swap_rows8_pk_t<false>(g, za, zb);
-                    const float w6 = dx * zb;  // lanes 0-15: dx_c x (g4's column-c partial)
-                    s_stage[st_dst + 36 * nst] = za;
-                    s_stage[st_dst_b + 36 * nst] = zb;
-                    s_stage[st_g6 + (lane < 16 ? 36 * nst : 0)] = w6;
-                    js |= (uint64_t)j << (6 * nst);
-                    written |= 1ull << j;
-                    const bool full = ++nst == kStageSlots;
-                    if (full) stage_reduce(kStageSlots);
-                    nst = full ? 0 : nst;
-                    js = full ? 0ull : js;
-                } else if constexpr (kStaged) {
-                    float za, zb;
-                    swap_rows8_pk(g, za, zb);
-                    float* st = &s_stage[st_dst + 36 * nst];
-                    st[0] = za;
-                    st[16] = zb;
-                    if ((lane & 15) == 15) s_stage[st_g8 + 36 * nst] = g[8];
-                    js |= (uint64_t)j << (6 * nst);
-                    written |= 1ull << j;
-                    // (the resets as selects outside the reduce's lane-masked
-                    // region: assigned inside it, the slot state would be
-                    // treated as divergent and kept in VGPRs)
-                    const bool full = ++nst == kStageSlots;
-                    if (full) stage_reduce(kStageSlots);
-                    nst = full ? 0 : nst;
-                    js = full ? 0ull : js;
-                } else if (kSwap) {  // full sums by transposition: 2 values per row leader + g8 in lane 63
-                    float za, zb;
-                    if constexpr (kSel == 1) swap_sum9_pk(g, za, zb);
-                    else swap_sum9(g, za, zb);
-                    if ((lane & 15) == 15) {
-                        float* row = &s_acc[j * kAccRow];
-                        const int q = swap_sum_slot(lane >> 4);
-                        if (kWaves == 1) {
-                            row[q] = za;
-                            row[4 + q] = zb;
-                            if (lane == 63) row[8] = g[8];
-                        } else {
-                            atomicAdd(&row[q], za);
-                            atomicAdd(&row[4 + q], zb);
-                            if (lane == 63) atomicAdd(&row[8], g[8]);
-                        }
-                    }
-                    written |= 1ull << j;
-                } else if (kWaves == 1) {  // half-wave sums, parked by lanes 31 and 63
-                    dpp_sum9_halves(g);
-                    if ((lane & 31) == 31) {
-                        float* row = &s_acc[(j * 2 + (lane >> 5)) * kAccRow];
-#pragma unroll
-                        for (int q = 0; q < kNG; q++) row[q] = g[q];
-                    }
-                    written |= 1ull << j;
-                } else {  // 16-lane row sums; the 4 row leaders add them into LDS
-                    dpp_sum9_rows(g);
-                    if ((lane & 15) == 15) {
-#pragma unroll
-                        for (int q = 0; q < kNG; q++) atomicAdd(&s_acc[j * kAccRow + q], g[q]);
+            if constexpr (kSel) {
+                // s2 rides in the 8-value transposition (g6 = dx^2 s0 leaves it;
+                // g6's column partials are dx x g4's, formed after it)
+                float za, zb;
+                swap_rows8_pk_t<false>(g, za, zb);
+                const float w6 = dx * zb;
+                s_stage[st_dst + 36 * kSlot] = za;
+                s_stage[st_dst_b + 36 * kSlot] = zb;
+                s_stage[st_g6 + (lane < 16 ? 36 * kSlot : 0)] = w6;
+                js |= (uint64_t)j << (6 * kSlot);
+            } else if (__ballot(any) != 0ull) {  // wave-uniform
+                // full sums by transposition: 2 values per row leader + g8 in lane 63
+                float za, zb;
+                swap_sum9(g, za, zb);
+                if ((lane & 15) == 15) {
+                    float* row = &s_acc[j * kAccRow];
+                    const int q = swap_sum_slot(lane >> 4);
+                    row[q] = za;
+                    row[4 + q] = zb;
+                    if (lane == 63) row[8] = g[8];
+                }
+                written |= 1ull << j;
+            }
+        };
+        using T1 = std::integral_constant<bool, true>;
+        using T0 = std::integral_constant<bool, false>;
+        using S0 = std::integral_constant<int, 0>;
+        if constexpr (kSel) {
+            // one copy of the loop per (all-safe, started) batch case, chosen
+            // once per batch -- per-entry branches between the visit variants
+            // made the register allocator shuffle the loop-carried pixel state
+            // (8 v_mov per entry) at every join.  Rounds of 7 entries, one
+            // unrolled copy of the visit per staging slot (slot offsets as
+            // immediates, no per-entry slot counter or address VALU, the
+            // visited bit cleared by one s_andn2)
+            auto run = [&](auto kFastT, auto kStartedT) {
+                auto one = [&](auto kSlotT) {
+                    if (!todo) return;  // wave-uniform
+                    const int j = __builtin_ctzll(todo);
+                    todo &= ~(1ull << j);
+                    const float4 a4 = s_a[j];
+                    const float2 xy = make_float2(a4.x, a4.y);
+                    const float4 pc = s_co[j], cf = make_float4(a4.z, a4.w, s_b[j].x, 0.f);
+                    visit(j, xy, pc, cf, kFastT, kStartedT, kSlotT);
+                    nst = decltype(kSlotT)::value + 1;
+                };
+                while (todo) {
+                    one(S0{});
+                    one(std::integral_constant<int, 1>{});
+                    one(std::integral_constant<int, 2>{});
+                    one(std::integral_constant<int, 3>{});
+                    one(std::integral_constant<int, 4>{});
+                    one(std::integral_constant<int, 5>{});
+                    one(std::integral_constant<int, 6>{});
+                    if (nst == kStageSlots) {
+                        stage_reduce(kStageSlots);
+                        nst = 0;
+                        js = 0ull;
                     }
                 }
-            }
-          };
-          using T1 = std::integral_constant<bool, true>;
-          using T0 = std::integral_constant<bool, false>;
-          // kSel 3: one copy of the loop per (all-safe, started) batch case,
-          // chosen once per batch -- per-entry branches between the visit
-          // variants made the register allocator shuffle the loop-carried
-          // pixel state (8 v_mov per entry) at every join
-          using S0 = std::integral_constant<int, 0>;
-          auto run = [&](auto kFastT, auto kStartedT) {
-            if constexpr (kSlotUnroll) {
-              // every entry of todo is visited and staged (select form: a
-              // visited row group always sums), so the written set is todo
-              written |= todo;  // (kSel: kWaves == 1, c == 0)
-              // rounds of 7 entries, one unrolled copy of the visit per slot
-              auto one = [&](auto kSlotT) {
-                if (!todo) return;  // wave-uniform
-                const int cbit = __builtin_ctzll(todo);
-                todo &= ~(1ull << cbit);
-                const int j = 64 * c + cbit;
+            };
+            // every entry this wave visits has a provably negative-definite form
+            const bool bsafe = (todo & ~fast_mask) == 0ull;
+            if (bsafe && bstarted) run(T1{}, T1{});
+            else if (bsafe) run(T1{}, T0{});
+            else run(T0{}, T0{});
+            if (nst) stage_reduce(nst);
+        } else {
+            while (todo) {
+                const int j = __builtin_ctzll(todo);
+                todo &= todo - 1;
                 const float4 a4 = s_a[j];
                 const float2 xy = make_float2(a4.x, a4.y);
                 const float4 pc = s_co[j], cf = make_float4(a4.z, a4.w, s_b[j].x, 0.f);
-                visit(cbit, xy, pc, cf, kFastT, kStartedT, kSlotT);
-                nst = decltype(kSlotT)::value + 1;
-              };
-              while (todo) {
-                one(S0{});
-                one(std::integral_constant<int, 1>{});
-                one(std::integral_constant<int, 2>{});
-                one(std::integral_constant<int, 3>{});
-                one(std::integral_constant<int, 4>{});
-                one(std::integral_constant<int, 5>{});
-                one(std::integral_constant<int, 6>{});
-                if (nst == kStageSlots) {
-                    stage_reduce(kStageSlots);
-                    nst = 0;
-                    js = 0ull;
-                }
-              }
-            } else {
-            while (todo) {
-              const int cbit = __builtin_ctzll(todo);
-              todo &= todo - 1;
-              const int j = 64 * c + cbit;
-              const float4 a4 = s_a[j];
-              const float2 xy = make_float2(a4.x, a4.y);
-              const float4 pc = s_co[j], cf = make_float4(a4.z, a4.w, s_b[j].x, 0.f);
-              visit(cbit, xy, pc, cf, kFastT, kStartedT, S0{});
+                visit(j, xy, pc, cf, T0{}, T0{}, S0{});
             }
-            }
-          };
-          if constexpr (kMaskSel) {
-              // every entry this wave visits has a provably negative-definite form
-              const bool bsafe = (todo & ~fast_mask) == 0ull;
-              if (bsafe && bstarted) run(T1{}, T1{});
-              else if (bsafe) run(T1{}, T0{});
-              else run(T0{}, T0{});
-          } else {
-              run(T0{}, T0{});
-          }
-        }
-        if constexpr (kStaged) {
-            if (nst) stage_reduce(nst);
         }
         __syncthreads();
         if (has_next) {  // gathers for the next batch, ahead of the flush atomics
@@ -666,38 +529,30 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
             nco = conic_opacity[nid];
             nrgb[0] = colors[3 * nid]; nrgb[1] = colors[3 * nid + 1]; nrgb[2] = colors[3 * nid + 2];
         }
-        // Flush: 16 lanes per Gaussian row, 4 rows per wave instruction
-        // (one 64-B memory-side atomic request per (tile, Gaussian)).  (A full
-        // unroll lets the scheduler hoist all 64 LDS reads: 163 VGPRs.)
+        if constexpr (!kSel) {
+            // Flush: 16 lanes per Gaussian row, 4 rows per wave instruction
+            // (one 64-B memory-side atomic request per (tile, Gaussian)).  (A full
+            // unroll lets the scheduler hoist all 64 LDS reads: 163 VGPRs.)
 #pragma unroll 4
-        for (int i = 0; i < (kFusedFlush ? 0 : kB / (4 * kWaves)); i++) {
-            const int r = (tid >> 4) + 4 * kWaves * i;
-            bool live = r < cnt && comp < kNG;
-            if (kWaves == 1) live = live && ((written >> (r & 63)) & 1ull);
-            if (live) {
-                // row sums (c0, c1, c2, s0, sx, sy, sxx, sxy, syy) -> the
-                // reference's nine terms: v = ka * row[ia] + kb * sy, with o and
-                // the conic from the staged log2(e)-scaled record
-                const float* row0 = &s_acc[r * kRowsPerG * kAccRow];
-                float qa = row0[ia], qb = row0[5];
-                if (kRowsPerG == 2) {
-                    qa += row0[kAccRow + ia];
-                    qb += row0[kAccRow + 5];
-                }
-                const float4 pc = s_co[r];
-                const float o = pc.w;
-                const float cx = pc.x * (-1.0f / kHalfLog2e), cy = pc.y * (-1.0f / kLog2e),
-                            cz = pc.z * (-1.0f / kHalfLog2e);
-                const float ka = comp == 3 ? -o * cx * ddelx_dx
-                               : comp == 4 ? -o * cy * ddely_dy
-                               : (comp >= 5 && comp <= 7) ? -0.5f * o : 1.0f;
-                const float kb = comp == 3 ? -o * cy * ddelx_dx : comp == 4 ? -o * cz * ddely_dy : 0.0f;
-                const float v = ka * qa + kb * qb;
-                float* dst = &grad_accum[(size_t)s_id[par][r] * kGradRow + comp];
-                if (flush_mode == 0) {
-                    if (v != 0.f) atomicAdd(dst, v);
-                } else if (flush_mode == 1) {  // diagnostic only (wrong sums): plain stores of the same shape
-                    *dst = v;
+            for (int i = 0; i < kB / 4; i++) {
+                const int r = (tid >> 4) + 4 * i;
+                const bool live = r < cnt && comp < kNG && ((written >> (r & 63)) & 1ull);
+                if (live) {
+                    // row sums (c0, c1, c2, s0, sx, sy, sxx, sxy, syy) -> the
+                    // reference's nine terms: v = ka * row[ia] + kb * sy, with o and
+                    // the conic from the staged log2(e)-scaled record
+                    const float* row0 = &s_acc[r * kAccRow];
+                    const float qa = row0[ia], qb = row0[5];
+                    const float4 pc = s_co[r];
+                    const float o = pc.w;
+                    const float cx = pc.x * (-1.0f / kHalfLog2e), cy = pc.y * (-1.0f / kLog2e),
+                                cz = pc.z * (-1.0f / kHalfLog2e);
+                    const float ka = comp == 3 ? -o * cx * ddelx_dx
+                                   : comp == 4 ? -o * cy * ddely_dy
+                                   : (comp >= 5 && comp <= 7) ? -0.5f * o : 1.0f;
+                    const float kb = comp == 3 ? -o * cy * ddelx_dx : comp == 4 ? -o * cz * ddely_dy : 0.0f;
+                    const float v = ka * qa + kb * qb;
+                    if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[par][r] * kGradRow + comp], v);
                 }
             }
         }
@@ -705,94 +560,37 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_bwd_kernel(
 }
 
 extern int g_cull;  // render.hip
-// 0: 1 wave x 4 px (<=128 VGPR), 1: 2 waves x 2 px, 2: 4 waves x 1 px, 3: 1 wave x 4 px with the
-// half-wave DPP-tree sums instead of the permlane transposition
-// (1 wave x 4 px capped at 5 or 6 waves per SIMD spills: measured slower)
-// 7: the select-form blend with staged sums (round 3's default)
-// 8: 7 with SGPR-pair masks (v_cndmask_b32_e64), compare set chosen per batch
-// 9: 8 with s2 in the 8-value transposition and g6 formed after it
-//    (cfg2 0.3512 vs 0.3707 ms for 7, cfg4 0.2722 vs 0.2887,
-//    profiles/r04b_ab_bwd2.log / r04b_ab_bwd4.log)
-// 10: 9 with the 7 staging slots unrolled (cfg2 0.3403 vs 0.3551 ms for 9,
-//    cfg4 0.2644 vs 0.2747, profiles/r04e_ab_bwd*)
-// 11: 10 with the flush fused into the staging reduce (the default since
-//    round 4: cfg2 0.3139 vs 0.3394 ms for 10, cfg4 0.2433 vs 0.2659,
-//    profiles/r04l_ab_bwd*_m.log; 11 under a 5-wave cap -- 96 VGPRs, 7
-//    spilled -- measured 0.3254 / 0.2502 and is not kept)
-// (11, 10 with each entry's row-group bits taken by one v_readlane and tested
-//    as constant bits -- s_bitcmp + branch, one SALU fewer per row group --
-//    measured slower: 0.3434 vs 0.3404 ms, 0.2673 vs 0.2632,
-//    profiles/r04g_ab_bwd*; removed)
-constexpr int kDefaultBwdVariant = 11;
+// Backward variants (set_tuning("bwd_variant")).  Default (round 4's variant
+// 11): the select form with SGPR-pair masks, per-batch compare sets, staged
+// sums and the flush fused into the staging reduce -- render_bwd 0.3707
+// (variant 7) -> 0.3634 (masks) -> 0.3512 (s2 in the transposition) ->
+// 0.3403 (unrolled slots) -> 0.3139 ms (fused flush) at config 2, 0.2887 ->
+// 0.2433 at config 4 (profiles/r04b_ab_bwd*.log, r04e_ab_bwd*.log,
+// r04l_ab_bwd*_m.log).  Fallback (0): the predicate form with full sums in
+// LDS rows (also the AMR backward's form).  Measured and removed (logs in
+// profiles/): 2 waves x 2 px and 4 x 1 geometries, half-wave DPP-tree sums,
+// a 5-wave occupancy cap (spills), the un-fused staged forms, the heavy-tile
+// split (r01h / DESIGN.md §8e), an XCD-compact tile order (r04u_ab_xcd*),
+// plain-store / no-flush timing diagnostics.
+constexpr int kDefaultBwdVariant = 1;
 int g_bwd_variant = kDefaultBwdVariant;
-// Flush of the per-(tile, Gaussian) sums: 0 = memory-side atomics (the only
-// correct mode); 1 = plain stores of the same shape, 2 = no flush -- timing
-// diagnostics for the A/B tool only (they produce wrong gradients).
-int g_bwd_flush = 0;
-void set_backward_flush(int v) { g_bwd_flush = v; }
-
-void set_backward_variant(int v) { g_bwd_variant = v < 0 ? kDefaultBwdVariant : v; }  // < 0: the default
-// Heavy-tile split of the backward blend: the heaviest T * g_bwd_split_permille
-// / 1000 tiles run as g_bwd_split_ways units (row-group subsets) each, so the
-// launch's tail is not one wave walking the longest list for all 256 pixels.
-// Pixels and their per-pixel arithmetic are unchanged; only the grouping of
-// the per-(unit, Gaussian) atomic sums differs.
-// Backward launch order from the forward render's 64 work buckets (no sort
-// kernel); 0: the one-workgroup counting sort (order_tiles_kernel).
-int g_bucket_order = 1;
-void set_bucket_order(int v) { g_bucket_order = v; }
-int g_bwd_split_ways = 1;
-int g_bwd_split_permille = 0;
-void set_backward_split(int ways, int permille) {
-    g_bwd_split_ways = ways;
-    g_bwd_split_permille = permille;
-}
+void set_backward_variant(int v) { g_bwd_variant = v == 0 ? 0 : kDefaultBwdVariant; }
 
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s, int K) {
     const size_t hit_codes_k = (size_t)(K > 0 ? K : 0);  // (the forward's instance count: where its codes are)
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return;
-    const uint32_t* order = nullptr;
-    const uint32_t *bcount = nullptr, *blist = nullptr;
-    int units = gx * gy;
-    const bool one_wave_v = g_bwd_variant == 0 || g_bwd_variant == 3 || g_bwd_variant >= 5;
-    if (tile_order_enabled() && g_bucket_order && one_wave_v && !(g_xcd_map & 2) &&
-        !(g_bwd_split_ways == 2 || g_bwd_split_ways == 4)) {
-        bcount = img.bucket_count;  // filled by this image buffer's forward render
-        blist = img.bucket_list;
-    } else if (tile_order_enabled()) {
-        const bool one_wave = g_bwd_variant == 0 || g_bwd_variant == 3 || g_bwd_variant >= 5;
-        const int ways = (one_wave && !(g_xcd_map & 2) && (g_bwd_split_ways == 2 || g_bwd_split_ways == 4))
-                             ? g_bwd_split_ways : 1;
-        const int heavy = ways > 1 ? std::min(gx * gy, (int)((long)gx * gy * g_bwd_split_permille / 1000)) : 0;
-        launch_order_tiles(gx * gy, img, true, s, gx, gy, heavy, heavy ? ways : 1);
-        order = img.tile_order;
-        units = gx * gy + (heavy ? (ways - 1) * heavy : 0);
-    }
-    // hit codes cover whole tiles: not with the heavy-tile split (its units
-    // own row-group subsets of a tile and the tile order word carries them)
-    const bool gsel_codes = units == gx * gy;
-#define GS_BWD_LAUNCH(PPL, WAVES, OCC, SWAP, ...)                                                               \
-    hipLaunchKernelGGL((render_bwd_kernel<PPL, WAVES, OCC, SWAP, ##__VA_ARGS__>), dim3(units), dim3(64 * WAVES), 0, s, \
-                       W, H,                                                                                      \
-                       img.ranges, img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),  \
-                       reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib, \
-                       dL_dpix, bg, g.grad_accum, g_cull, order, gx, (g_xcd_map >> 1) & 1, 0, nullptr, g_bwd_flush, \
-                       bcount, blist, gsel_codes ? hit_codes_at(b.point_list, hit_codes_k) : nullptr, g.hdr)
-    switch (g_bwd_variant) {
-        case 1: GS_BWD_LAUNCH(2, 2, 4, true); break;
-        case 2: GS_BWD_LAUNCH(1, 4, 4, true); break;
-        case 3: GS_BWD_LAUNCH(4, 1, 4, false); break;
-        case 5: GS_BWD_LAUNCH(4, 1, 5, true); break;  // 96 VGPRs: 5 waves per SIMD
-        case 6: GS_BWD_LAUNCH(4, 1, 4, true, false, 1); break;  // select form
-        case 7: GS_BWD_LAUNCH(4, 1, 4, true, false, 2); break;  // select form, staged sums
-        case 8: GS_BWD_LAUNCH(4, 1, 4, true, false, 3); break;  // 7 + SGPR-mask selects, per-batch compare sets
-        case 9: GS_BWD_LAUNCH(4, 1, 4, true, false, 4); break;  // 8 + g6 after the transposition (no 9th-value tree)
-        case 10: GS_BWD_LAUNCH(4, 1, 4, true, false, 5); break;  // 9 with the 7 staging slots unrolled
-        case 11: GS_BWD_LAUNCH(4, 1, 4, true, false, 6); break;  // 10 with the flush fused into the staging reduce
-        default: GS_BWD_LAUNCH(4, 1, 4, true); break;
-    }
+    // tiles heaviest first: the forward render filled this image buffer's 256
+    // work buckets (the kernel falls back to the identity order otherwise)
+#define GS_BWD_LAUNCH(SEL)                                                                                         \
+    hipLaunchKernelGGL((render_bwd_kernel<SEL>), dim3(gx * gy), dim3(64), 0, s, W, H, img.ranges, img.max_contrib, \
+                       b.point_list, reinterpret_cast<const float2*>(g.means2D),                                   \
+                       reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,    \
+                       dL_dpix, bg, g.grad_accum, g_cull, gx, 0, nullptr, img.bucket_count, img.bucket_list,       \
+                       hit_codes_at(b.point_list, hit_codes_k), g.hdr)
+    if (g_bwd_variant == 0) GS_BWD_LAUNCH(false);
+    else GS_BWD_LAUNCH(true);
 #undef GS_BWD_LAUNCH
 }
 
@@ -805,11 +603,10 @@ void launch_amr_render_backward(int W, int H, int mode, const ImageView& img, co
                                 hipStream_t s) {
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0 || mode == 0) return;
-    hipLaunchKernelGGL((render_bwd_kernel<4, 1, 4, true, true>), dim3(4 * tgx * tgy), dim3(64), 0, s, W, H, img.ranges,
+    hipLaunchKernelGGL((render_bwd_kernel<false, true>), dim3(4 * tgx * tgy), dim3(64), 0, s, W, H, img.ranges,
                        img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,
-                       dL_dpix, bg, g.grad_accum, g_cull, nullptr, tgx, 0, mode, img.levels, 0, nullptr, nullptr,
-                       nullptr, nullptr);
+                       dL_dpix, bg, g.grad_accum, g_cull, tgx, mode, img.levels, nullptr, nullptr, nullptr, nullptr);
 }
 
 // ------------------------------------------------------ per-Gaussian bwd ---
@@ -1282,11 +1079,12 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
 // wave-contiguous 16-B stores: per-thread 192-B row stores measured ~3.5 TB/s
 // against ~5.4 TB/s coalesced on MI355X (tools/membench.hip).
 constexpr int kShRow = 49;
+constexpr int kBgStageNt = 16;  // backward_gaussians_kernel stage flag: dL_dsh rows non-temporal
 
 
 template <bool kHasSH, bool kHasScales, bool kSH16, bool kSmall = false>
 __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussArgs a, const float* __restrict__ grad_accum,
-                                                                 const uint8_t* __restrict__ clamped_bits, int stage_mlp) {
+                                                                 const uint8_t* __restrict__ clamped_bits, int stage) {
     constexpr bool kStage = kHasSH && kSH16;
     static_assert(!kSmall || kStage, "the small outputs are staged in the SH rows' LDS");
     __shared__ float s_dsh[kStage ? 256 * kShRow : 1];
@@ -1297,7 +1095,7 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
         const int g0 = blockIdx.x * blockDim.x;
         const int n = min(256, a.P - g0);
         const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)g0 * 12;
-        if (n == 256 && stage_mlp) {
+        if (n == 256) {
             // a full workgroup: the 12 loads of each thread issued back to back
             // (one memory round trip; the loop below waits for each load before
             // its LDS write -- 12 round trips at 3 waves per SIMD)
@@ -1332,7 +1130,7 @@ __global__ void __launch_bounds__(256) backward_gaussians_kernel(BackwardGaussAr
         const int g0 = blockIdx.x * blockDim.x;
         const int n = min(256, a.P - g0);
         float4* out = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)g0 * 12;
-        const bool nt = (stage_mlp & 16) != 0;
+        const bool nt = (stage & kBgStageNt) != 0;
         for (int f = threadIdx.x; f < n * 12; f += 256) {
             const float* r = s_dsh + (f / 12) * kShRow + 4 * (f % 12);
             store_out4(&out[f], make_float4(r[0], r[1], r[2], r[3]), nt);
@@ -1417,61 +1215,19 @@ __global__ void __launch_bounds__(256) backward_gaussians_drgb_kernel(BackwardGa
     }
 }
 
-// Split mode, second kernel: the SH part alone (its ~50 live SH registers no
-// longer limit the occupancy of the geometry part).  Reads dL_dcolor and the
-// partial dL_dmeans3D the geometry kernel wrote, adds the SH term, writes
-// dL_dsh (zeros for culled Gaussians).
-template <bool kSH16>
-__global__ void __launch_bounds__(256) sh_backward_kernel(BackwardGaussArgs a, const uint8_t* __restrict__ clamped_bits) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
-    if (a.radii[idx] <= 0) {
-        if (kSH16) {
-#pragma unroll
-            for (int i = 0; i < 12; i++)
-                reinterpret_cast<float4*>(a.dL_dsh)[(size_t)idx * 12 + i] = make_float4(0.f, 0.f, 0.f, 0.f);
-        } else {
-            for (int i = 0; i < a.M * 3; i++) a.dL_dsh[(size_t)idx * a.M * 3 + i] = 0.f;
-        }
-        return;
-    }
-    const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
-    float acc[3] = {a.dL_dcolor[3 * idx], a.dL_dcolor[3 * idx + 1], a.dL_dcolor[3 * idx + 2]};
-    float dmean[3] = {a.dL_dmean3D[3 * idx], a.dL_dmean3D[3 * idx + 1], a.dL_dmean3D[3 * idx + 2]};
-    float s[16][3];
-    load_sh_rows<kSH16>(a, idx, s);
-    sh_backward<kSH16>(a, idx, mx, my, mz, s, clamped_bits[idx], acc, dmean);
-#pragma unroll
-    for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = dmean[i];
-}
-
-int g_bwd_gauss_split = 0;
-void set_bwd_gauss_split(int v) { g_bwd_gauss_split = v; }
-// set_tuning("bg_stage_mlp"): 1 the SH staging loads issued back to back; 2 =
-// 1 + the 3-float outputs stored coalesced through LDS (stage_small; the
-// default since round 4: 0.0848 -> 0.0828 ms at config 2, 0.529 -> 0.479 at
-// config 4, profiles/r04j_ab_bg*.log); 3 = 2 + the drgb-known kernel when
-// the host knows the forward stored d(rgb)/d(dir) (config 2 0.0825 -> 0.0747
-// ms, config 4 0.465 -> 0.486: 4 waves per SIMD help the latency-bound small
-// scene, the two staging rounds cost the HBM-bound large one,
-// profiles/r04n_ab_bg*.log; again with 48-B rows: 0.4617 vs 0.4703,
-// r04y_ab_bg4.log); < 0: auto -- 3 below 4M Gaussians, else 2.  (3 staging
-// the 19 factors -- basis, dL/drgb -- in one round and forming each 16-B
-// dL_dsh piece from them measured slower: 0.0722 -> 0.0806 ms at config 2,
-// 0.447 -> 0.479 at config 4, profiles/r04z1_ab_bg*_stage4.log; removed)
-int g_bg_stage_mlp = -1;
-// set_tuning("bg_nt"): bit 0 = the dL_dsh rows stored with the non-temporal
-// hint (the default: 0.0727 -> 0.0697 ms at config 2, 0.4582 -> 0.4393 at
-// config 4, profiles/r04z4_ab_nt*.log), bit 1 = the other outputs too
-// (0.0696 -> 0.0719 at config 2, config 4 equal: r04z5_ab_nt*.log).  (The
-// per-Gaussian input loads non-temporal measured slower: 0.0722 -> 0.0790 ms
-// at config 2, 0.426 -> 0.477 at config 4, profiles/r04z7_ab_bg*.log --
-// the three 4-B loads of a 12-B field each refetch the line; removed)
-int g_bg_nt = 1;
-void set_bg_nt(int v) { g_bg_nt = v; }
-void set_bg_stage_mlp(int v) { g_bg_stage_mlp = v < 0 ? -1 : v; }
-int bg_stage_for(int P) { return g_bg_stage_mlp >= 0 ? g_bg_stage_mlp : (P < 4000000 ? 3 : 2); }
-
+// The SH16 + scales kernel: the SH staging loads issued back to back and the
+// 3-float outputs stored coalesced through LDS (stage_small: 0.0848 -> 0.0828
+// ms at config 2, 0.529 -> 0.479 at config 4, profiles/r04j_ab_bg*.log); the
+// drgb-known kernel when the host knows the forward stored d(rgb)/d(dir),
+// below 4M Gaussians (config 2 0.0825 -> 0.0747 ms; at config 4 0.465 ->
+// 0.486: 4 waves per SIMD help the latency-bound small scene, the two staging
+// rounds cost the HBM-bound large one, profiles/r04n_ab_bg*.log, again with
+// 48-B rows: 0.4617 vs 0.4703, r04y_ab_bg4.log).  The dL_dsh rows are stored
+// with the non-temporal hint (0.0727 -> 0.0697 ms at config 2, 0.4582 ->
+// 0.4393 at config 4, profiles/r04z4_ab_nt*.log); the other outputs and the
+// input loads are not (+3 % / +9 %, r04z5_*, r04z7_*).  Measured and removed:
+// the SH backward as its own kernel, per-thread SH staging loads, one-round
+// drgb staging (r04z1_ab_bg*_stage4.log).
 void launch_backward_gaussians(const BackwardGaussArgs& args, const GeomView& g, hipStream_t s) {
     if (args.P == 0) return;
     BackwardGaussArgs a = args;
@@ -1479,25 +1235,14 @@ void launch_backward_gaussians(const BackwardGaussArgs& args, const GeomView& g,
     const bool sh = a.shs != nullptr;
     const bool sh16 = sh && a.M == 16;
     const bool sc = a.scales != nullptr;
-    const int stage = bg_stage_for(a.P);
-    a.nt_out = (g_bg_nt & 2) ? 1 : 0;
+    a.nt_out = 0;
 #define GS_BG_LAUNCH(A, B, C) \
-    hipLaunchKernelGGL((backward_gaussians_kernel<A, B, C>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped, \
-                       stage)
-    if (sh && g_bwd_gauss_split && a.dL_dcolor) {  // (the split SH pass reads dL_dcolor back)
-        if (sc) GS_BG_LAUNCH(false, true, false);
-        else GS_BG_LAUNCH(false, false, false);
-        if (sh16) hipLaunchKernelGGL((sh_backward_kernel<true>), grid, dim3(256), 0, s, a, g.clamped);
-        else hipLaunchKernelGGL((sh_backward_kernel<false>), grid, dim3(256), 0, s, a, g.clamped);
-        return;
-    }
-    if (sh16 && sc && a.drgb && a.drgb_known && stage >= 3)
-        hipLaunchKernelGGL(backward_gaussians_drgb_kernel, grid, dim3(256), 0, s, a, g.grad_accum, g.clamped,
-                           g_bg_nt & 1);
-    else if (sh16 && sc && stage >= 2)
+    hipLaunchKernelGGL((backward_gaussians_kernel<A, B, C>), grid, dim3(256), 0, s, a, g.grad_accum, g.clamped, 0)
+    if (sh16 && sc && a.drgb && a.drgb_known && a.P < 4000000)
+        hipLaunchKernelGGL(backward_gaussians_drgb_kernel, grid, dim3(256), 0, s, a, g.grad_accum, g.clamped, 1);
+    else if (sh16 && sc)
         hipLaunchKernelGGL((backward_gaussians_kernel<true, true, true, true>), grid, dim3(256), 0, s, a,
-                           g.grad_accum, g.clamped, stage | ((g_bg_nt & 1) ? 16 : 0));
-    else if (sh16 && sc) GS_BG_LAUNCH(true, true, true);
+                           g.grad_accum, g.clamped, kBgStageNt);
     else if (sh16) GS_BG_LAUNCH(true, false, true);
     else if (sh && sc) GS_BG_LAUNCH(true, true, false);
     else if (sh) GS_BG_LAUNCH(true, false, false);
@@ -1602,7 +1347,7 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
         const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)(a.g0 + local0) * 12;
         if (nblk == 256) {
             // a full workgroup: the 12 loads of each thread issued back to back
-            // (one memory round trip, as backward_gaussians_kernel's stage_mlp:
+            // (one memory round trip, as backward_gaussians_kernel's staging:
             // multiview_bwd 0.3614 -> 0.3393 ms per 8-view step at config 5,
             // profiles/r04ze_bench_cfg5.log against r04zz_bench.log)
             float4 v[12];
@@ -1778,7 +1523,7 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
 void launch_multiview_backward(const MultiViewArgs& args, hipStream_t s) {
     if (args.count <= 0) return;
     MultiViewArgs a = args;
-    a.nt = g_bg_nt & 1;
+    a.nt = 1;  // the dL_dsh rows non-temporal (as backward_gaussians_kernel's)
     const dim3 grid((a.count + 255) / 256);
     const bool sh = a.shs != nullptr;
     if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward_kernel<true, true>), grid, dim3(256), 0, s, a);

@@ -307,9 +307,6 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, u
     }
 }
 
-int g_scan_slices = 1;  // set_tuning("scan_slices"): 0 = the thread-contiguous scan
-void set_scan_slices(int v) { g_scan_slices = v; }
-
 void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror, int nslots,
                       int gx, bool banded, uint32_t mirror_token) {
     BandScan band{nullptr, nullptr, (uint32_t)std::max(gx, 1), mirror_token};
@@ -317,7 +314,7 @@ void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s,
         band.start = img.band_start;
         band.cursor = img.band_cursor;
     }
-    if (g_scan_slices) {
+    {  // T <= 8192 (1080p at 16 px: 8160): the wave-contiguous slices; larger grids below
         const int slices = (T + kScanThreads - 1) / kScanThreads;
 #define GS_SLICE_LAUNCH(S)                                                                                        \
     hipLaunchKernelGGL(tile_scan_slices_kernel<S>, dim3(1), dim3(kScanThreads), 0, s, T, img.tile_count,         \
@@ -384,7 +381,7 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const float* __re
 // when scattered (MI355X_MICROARCH.md "Global float atomics"): 4.4M per-pair
 // histogram increments plus 4.4M returning cursor bumps at config 2 cost
 // ~0.2 ms apiece.  Instead a workgroup of kBinThreads threads takes a chunk
-// of g_bin_chunk consecutive Gaussians and counts its (Gaussian, tile) pairs
+// of bin_chunk_for(P) consecutive Gaussians and counts its (Gaussian, tile) pairs
 // in an LDS histogram over all T tiles, then
 //   count_tiles: adds the histogram to tile_count with consecutive-tile
 //                (coalesced, no-return) atomics, one per non-empty tile;
@@ -394,46 +391,33 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const float* __re
 // Slot order inside a bucket stays arbitrary; sort_tiles makes it exact.
 constexpr int kBinThreads = 1024;
 // Gaussians per binning workgroup (count_tiles and duplicate_lds must agree:
-// the chunk -> sub-bucket slot map); 0 = auto: 8192 from 4M Gaussians (config
-// 4 count_tiles 57.0 -> 52.4 us), else 4096 (config 2: 22.1 us vs 29.9 at
-// 8192), profiles/r04l_ab_chunk*.log
-int g_bin_chunk = 0;
-int bin_chunk_for(int P) { return g_bin_chunk ? g_bin_chunk : (P >= 4000000 ? 8192 : 4096); }
-int g_dup_diag = 0;
-// sub-bucket slots the LDS binning spreads its chunks over (1..kBinSlots;
-// the scan sums all kBinSlots, unused ones stay zero)
-int g_bin_slots = 0;  // 0: auto (bin_slots_for)
-int g_dup_band = 1;  // set_tuning("dup_band"): 1 = row-banded duplicate (16-px grids), 2 = any grid, 0 = direct
-// set_tuning("band_threads"): the banded duplicate's workgroup shape (0 auto;
-// 512: 512 threads x 1 source; 513: 512 x 2 sources per thread; 514: 512 x 2
-// sources, 4 items per round; 1024: 1024 x 1).  Measured
-// (profiles/r03h_ab_threads_cfg*.json): 1024 best at config 2 (77.6 us, direct
-// duplicate 87.3), 513 at config 4 (282 us, direct 318).
-int g_band_threads = 0;
-int g_band_split = 0;  // set_tuning("band_split"): workgroups per tile row in the split pass (0: auto)
-void set_dup_band(int v) { g_dup_band = v; }
-void set_band_split(int v) { g_band_split = std::max(0, v); }
-void set_band_threads(int v) { g_band_threads = v; }
+// the chunk -> sub-bucket slot map): 8192 from 4M Gaussians (config 4
+// count_tiles 57.0 -> 52.4 us), else 4096 (config 2: 22.1 us vs 29.9 at
+// 8192; 2048 / 1024: 27.4 / 42.4 us), profiles/r04l_ab_chunk*.log,
+// r04zh_chunk_*.log
+int bin_chunk_for(int P) { return P >= 4000000 ? 8192 : 4096; }
+// The banded duplicate's workgroup shape: 1024 threads x 1 source below 2M
+// Gaussians (config 2: 77.6 us, direct duplicate 87.3), 512 x 2 sources per
+// thread above (config 4: 282 us, direct 318; profiles/r03h_ab_threads_cfg*.json,
+// the other shapes removed).
 constexpr int kBandBins = 1024;  // bins of one coalesced append round (rows, or the tiles of a row)
 // Banded only on the base 16-px grid: on the AMR 32-px grid (34 tile rows
 // at 1080p, ~2.2 instances per Gaussian) the direct duplicate is cheaper
-// (46 vs 56 us at config 3, profiles/r03h_ab_amr_band.json); g_dup_band = 2
-// forces it for any grid (tests).
+// (46 vs 56 us at config 3, profiles/r03h_ab_amr_band.json).
 bool band_lds_fits();  // (below: the banded kernels' dynamic LDS fits the current device)
 bool dup_banded(int gx, int gy, int block) {
-    if (g_dup_band <= 0 || gx * gy > kLdsTiles || gx > kBandBins || gy > kBandBins) return false;
-    return (block == 16 || g_dup_band == 2) && band_lds_fits();
+    if (gx * gy > kLdsTiles || gx > kBandBins || gy > kBandBins) return false;
+    return block == 16 && band_lds_fits();
 }
-void set_bin_slots(int v) { g_bin_slots = std::max(0, std::min(kBinSlots, v)); }
-// Measured (profiles/r03b_ab_bin_slots*): the sub-buckets save ~30 us of the
+// sub-bucket slots the LDS binning spreads its chunks over (1..kBinSlots; the
+// scan sums all kBinSlots, unused ones stay zero).  Measured
+// (profiles/r03b_ab_bin_slots*): the sub-buckets save ~30 us of the direct
 // duplicate at config 4 (6.1M Gaussians) and ~4 us at config 2, where the
 // scan's 8x count loads cost more (+6 us): slots only for large scenes.
 int bin_slots_for(int P, int gx, int gy, int block) {
     if (dup_banded(gx, gy, block)) return 1;  // the banded duplicate reserves per-tile runs itself
-    return g_bin_slots ? g_bin_slots : (P >= 2000000 ? kBinSlots : 1);
+    return P >= 2000000 ? kBinSlots : 1;
 }
-void set_dup_diag(int v) { g_dup_diag = v; }
-void set_bin_chunk(int v) { g_bin_chunk = v <= 0 ? 0 : max(kBinThreads, v); }
 
 __device__ __forceinline__ bool gaussian_rect(int idx, const float* __restrict__ means2D,
                                               const int* __restrict__ radii, int block, uint32_t gx, uint32_t gy,
@@ -476,7 +460,7 @@ __global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int c
                                                                     uint32_t* __restrict__ cursor,
                                                                     uint64_t* __restrict__ pair_keys,
                                                                     const uint32_t* __restrict__ hdr, uint32_t cap,
-                                                                    int diag, uint32_t nslots) {
+                                                                    uint32_t nslots) {
     // speculative launch (hdr given): the keys fit the buffer only if K <= cap;
     // otherwise nothing is touched (no cursor moved) and the host relaunches
     if (hdr && hdr[kHdrNumRendered] > cap) return;
@@ -493,12 +477,10 @@ __global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int c
     }
     __syncthreads();
     // one returning atomic per non-empty tile: the chunk's run in the bucket
-    // (g_dup_diag, timing diagnostics only -- wrong keys: 1 = no key stores,
-    // 2 = runs at offset 0 without the device atomics)
     uint32_t* cur = cursor + (size_t)(blockIdx.x % nslots) * T;  // the slot count_tiles counted this chunk in
     for (int i = threadIdx.x; i < T; i += kBinThreads) {
         const uint32_t c = slot[i];
-        if (c) slot[i] = diag == 2 ? 0u : atomicAdd(&cur[i], c);
+        if (c) slot[i] = atomicAdd(&cur[i], c);
     }
     __syncthreads();
     for (int idx = beg + threadIdx.x; idx < end; idx += kBinThreads) {
@@ -508,7 +490,7 @@ __global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int c
         for (uint32_t y = r.y0; y < r.y1; y++)
             for (uint32_t x = r.x0; x < r.x1; x++) {
                 const uint32_t sl = atomicAdd(&slot[y * gx + x], 1u);
-                if (diag != 1) pair_keys[sl] = key;
+                pair_keys[sl] = key;
             }
     }
 }
@@ -705,8 +687,7 @@ struct BandLds {
 // <1024, 2, 1>): fine on gfx950's 160 KB, not on 64-KiB parts.  Checked per
 // device, once; a device where it does not fit keeps the direct duplicate
 // (dup_banded false, so the bin-slot policy follows too).
-constexpr size_t kBandLdsMax = std::max({sizeof(BandLds<1024, 2, 1>), sizeof(BandLds<512, 2, 2>),
-                                         sizeof(BandLds<512, 4, 2>), sizeof(BandLds<512, 2, 1>)});
+constexpr size_t kBandLdsMax = std::max(sizeof(BandLds<1024, 2, 1>), sizeof(BandLds<512, 2, 2>));
 constexpr int kMaxDevices = 64;
 std::atomic<int> g_band_fits[kMaxDevices];  // 0 unknown, 1 fits, 2 does not
 bool band_lds_fits() {
@@ -855,22 +836,19 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
     const uint32_t gx = (uint32_t)((W + block - 1) / block), gy = (uint32_t)((H + block - 1) / block);
     if (dup_banded((int)gx, (int)gy, block)) {
         // ~4 split workgroups per CU over the rows
-        const int nt = g_band_threads ? g_band_threads : (P >= 2000000 ? 513 : 1024);
-        const int want = 4096;  // split workgroups in all
-        const int split = g_band_split ? g_band_split : std::max(1, std::min(256, (want + (int)gy - 1) / (int)gy));
-        switch (nt) {
-        case 1024: launch_banded<1024, 2, 1>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap); break;
-        case 513: launch_banded<512, 2, 2>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap); break;
-        case 514: launch_banded<512, 4, 2>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap); break;
-        default: launch_banded<512, 2, 1>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap); break;
-        }
+        // ~4096 split workgroups in all over the rows (per tile row at config 4:
+        // 62; 16 / 32 / 128 / 256 measured slower, profiles/r03p_ab_band_*.json)
+        const int want = 4096;
+        const int split = std::max(1, std::min(256, (want + (int)gy - 1) / (int)gy));
+        if (P >= 2000000) launch_banded<512, 2, 2>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap);
+        else launch_banded<1024, 2, 1>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap);
         return;
     }
     if (gx * gy <= (uint32_t)kLdsTiles) {
         const int chunk = bin_chunk_for(P);
         hipLaunchKernelGGL(duplicate_lds_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
                            sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, g.depths, radii, block, gx, gy,
-                           img.tile_cursor, b.pair_keys, spec_hdr, spec_cap, g_dup_diag,
+                           img.tile_cursor, b.pair_keys, spec_hdr, spec_cap,
                            (uint32_t)bin_slots_for(P, (int)gx, (int)gy, block));
         return;
     }
@@ -879,18 +857,16 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
 }
 
 // ------------------------------------------------------- launch order ---
-// One workgroup: counting sort of the tiles by descending work (12-bit
+// One workgroup: counting sort of the tiles by descending work (1024 log
 // buckets, order inside a bucket arbitrary -- it only steers scheduling).
+// The AMR units' heaviest-first order (the base backward takes its order from
+// the forward render's work buckets instead, backward.hip).
 constexpr int kOrderThreads = 1024;
 constexpr int kOrderBuckets = 1024;  // one per thread: bucket b = 64 log2(work + 1), heaviest first
-int g_tile_order = 1;
-void set_tile_order(int v) { g_tile_order = v; }
-bool tile_order_enabled() { return g_tile_order != 0; }
 
 __global__ void __launch_bounds__(kOrderThreads) order_tiles_kernel(int T, const uint32_t* __restrict__ ranges,
                                                                     const uint32_t* __restrict__ max_contrib,
-                                                                    uint32_t* __restrict__ order, uint32_t split_tiles,
-                                                                    uint32_t split_ways) {
+                                                                    uint32_t* __restrict__ order) {
     __shared__ uint32_t hist[kOrderBuckets];
     __shared__ uint32_t s_wave[kOrderThreads / 64 + 1];
     const int tid = threadIdx.x;
@@ -909,72 +885,13 @@ __global__ void __launch_bounds__(kOrderThreads) order_tiles_kernel(int T, const
     __syncthreads();
     hist[tid] = base;
     __syncthreads();
-    for (int t = tid; t < T; t += kOrderThreads) {
-        const uint32_t r = atomicAdd(&hist[bucket(t)], 1u);
-        if (r < split_tiles) {  // one of the heaviest: split_ways units, each a set of row groups
-            for (uint32_t w = 0; w < split_ways; w++) {
-                const uint32_t sel = split_ways == 2 ? (w ? 0xCu : 0x3u) : 1u << w;
-                order[r * split_ways + w] = (uint32_t)t | (sel << 28);
-            }
-        } else {
-            order[r + (split_ways - 1) * split_tiles] = (uint32_t)t;
-        }
-    }
+    for (int t = tid; t < T; t += kOrderThreads) order[atomicAdd(&hist[bucket(t)], 1u)] = (uint32_t)t;
 }
 
-// XCD-aware variant (gs_blend.cuh placement): the tiles of XCD chunk x
-// (a compact region) go to the blocks b = 8 k + x, heaviest first within
-// the chunk.  One workgroup, 8 counting sorts (one per chunk) in LDS.
-__global__ void __launch_bounds__(kOrderThreads) order_tiles_xcd_kernel(int T, int gx, int gy,
-                                                                        const uint32_t* __restrict__ ranges,
-                                                                        const uint32_t* __restrict__ max_contrib,
-                                                                        uint32_t* __restrict__ order) {
-    constexpr int kXB = kOrderBuckets / 4;  // 256 buckets per chunk: 8 x 256 counters
-    __shared__ uint32_t hist[8 * kXB];
-    __shared__ uint32_t s_wave[kOrderThreads / 64 + 1];
-    const int tid = threadIdx.x;
-    for (int i = tid; i < 8 * kXB; i += kOrderThreads) hist[i] = 0;
-    __syncthreads();
-    auto key = [&](int t) -> uint32_t {
-        uint32_t w = ranges[2 * t + 1] - ranges[2 * t];
-        if (max_contrib) w = min(w, max_contrib[t]);
-        const uint32_t b = min((uint32_t)(16.0f * __log2f((float)w + 1.0f)), (uint32_t)(kXB - 1));
-        const int x = xcd_chunk_of_pos(xcd_strip_pos_of_tile(t, gx, gy), T);
-        return (uint32_t)x * kXB + (uint32_t)(kXB - 1) - b;  // chunk-major, heaviest first
-    };
-    for (int t = tid; t < T; t += kOrderThreads) atomicAdd(&hist[key(t)], 1u);
-    __syncthreads();
-    // exclusive scan of the 2048 counters, 2 per thread; the chunk starts
-    // (xcd_chunk_start) fall out of it because chunk x holds exactly its tiles
-    const uint32_t a0 = hist[2 * tid], a1 = hist[2 * tid + 1];
-    uint32_t total;
-    const uint32_t base = block_exclusive_scan<kOrderThreads>(a0 + a1, s_wave, total);
-    __syncthreads();
-    hist[2 * tid] = base;
-    hist[2 * tid + 1] = base + a0;
-    __syncthreads();
-    for (int t = tid; t < T; t += kOrderThreads) {
-        const uint32_t k = key(t);
-        const int x = (int)(k / kXB);
-        const int rank = (int)atomicAdd(&hist[k], 1u) - xcd_chunk_start(x, T);
-        order[8 * rank + x] = (uint32_t)t;
-    }
-}
-
-void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s, int gx, int gy,
-                        int split_tiles, int split_ways) {
+void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s) {
     if (T <= 0) return;
-    if (split_ways != 2 && split_ways != 4) split_tiles = 0;
-    split_tiles = std::max(0, std::min(split_tiles, T));
-    if (split_tiles == 0) split_ways = 1;
-    if (split_tiles == 0 && (g_xcd_map & 2) && gx > 0 && T >= 8) {
-        hipLaunchKernelGGL(order_tiles_xcd_kernel, dim3(1), dim3(kOrderThreads), 0, s, T, gx, gy, img.ranges,
-                           use_max_contrib ? img.max_contrib : nullptr, img.tile_order);
-        return;
-    }
     hipLaunchKernelGGL(order_tiles_kernel, dim3(1), dim3(kOrderThreads), 0, s, T, img.ranges,
-                       use_max_contrib ? img.max_contrib : nullptr, img.tile_order, (uint32_t)split_tiles,
-                       (uint32_t)split_ways);
+                       use_max_contrib ? img.max_contrib : nullptr, img.tile_order);
 }
 
 // --------------------------------------------------------- tile sorting ---
@@ -1162,9 +1079,6 @@ __global__ void __launch_bounds__(kSortThreads) sort_tiles_small_kernel(int lo, 
 // with DPP / ds_swizzle / permlane swaps instead of the ds_bpermute of the
 // E = 8 / 16 networks, at the price of log2(kThreads / 64) more LDS stages
 // per merge.  n in (1024, 2048] -> 512 threads, (2048, 4096] -> 1024.
-int g_sort_wide = 1;
-void set_sort_wide(int v) { g_sort_wide = v; }
-
 template <int kThreads>
 __global__ void __launch_bounds__(kThreads) sort_tiles_wide_kernel(int lo, int hi, const uint32_t* __restrict__ ranges,
                                                                    const uint64_t* __restrict__ pair_keys,
@@ -1192,7 +1106,10 @@ __global__ void __launch_bounds__(kThreads) sort_tiles_wide_kernel(int lo, int h
 // (depths clustered far below the tile's range) takes the bitonic network
 // instead, so no distribution is slower than before.
 constexpr int kBucketMax = 64;
-int g_sort_algo = 1;  // set_tuning("sort_algo"): 0 = bitonic networks only, 1 = bucket sort
+// set_tuning("sort_algo"): 1 (default) the bucket sort below, 0 (fallback) the
+// bitonic register networks alone (which the bucket sort also takes for a
+// tile with clustered depths)
+int g_sort_algo = 1;
 void set_sort_algo(int v) { g_sort_algo = v; }
 
 // kT threads, kE keys each (n <= kT kE); nb ~ n >> kBS buckets.
@@ -1313,9 +1230,6 @@ __global__ void __launch_bounds__(kT) sort_tiles_bucket_kernel(int lo, int hi, c
     }
 }
 
-int g_sort_variant = 0;  // set_tuning("sort_variant"): geometry of the bucket kernels (A/B)
-void set_sort_variant(int v) { g_sort_variant = v; }
-
 // Merge-path split: number of elements taken from A for the first `diag`
 // outputs of merge(A[0..na), B[0..nb)); keys are unique.
 __device__ __forceinline__ int merge_path(const uint64_t* A, int na, const uint64_t* B, int nb, int diag) {
@@ -1385,38 +1299,11 @@ void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int ma
 #define GS_BK(TH, E, BS, LO, HI)                                                                      \
     hipLaunchKernelGGL((sort_tiles_bucket_kernel<TH, E, BS>), dim3(T), dim3(TH), 0, s, LO, HI, img.ranges, \
                        b.pair_keys, b.point_list)
-        switch (g_sort_variant) {
-            case 1:  // 256 threads for every class
-                GS_BK(256, 4, 1, 0, 1024);
-                if (max_count_host > 1024) GS_BK(256, 8, 1, 1024, 2048);
-                if (max_count_host > 2048) GS_BK(256, 16, 1, 2048, kSmallCap);
-                break;
-            case 2:  // 1024 threads for the largest class
-                GS_BK(256, 4, 1, 0, 1024);
-                if (max_count_host > 1024) GS_BK(512, 4, 1, 1024, 2048);
-                if (max_count_host > 2048) GS_BK(1024, 4, 1, 2048, kSmallCap);
-                break;
-            case 3:  // ~n / 4 buckets
-                GS_BK(256, 4, 2, 0, 1024);
-                if (max_count_host > 1024) GS_BK(512, 4, 2, 1024, 2048);
-                if (max_count_host > 2048) GS_BK(512, 8, 2, 2048, kSmallCap);
-                break;
-            case 4:  // 128 threads for the smallest class
-                GS_BK(128, 8, 1, 0, 1024);
-                if (max_count_host > 1024) GS_BK(512, 4, 1, 1024, 2048);
-                if (max_count_host > 2048) GS_BK(512, 8, 1, 2048, kSmallCap);
-                break;
-            case 5:
-                GS_BK(256, 4, 1, 0, 1024);
-                if (max_count_host > 1024) GS_BK(512, 4, 1, 1024, 2048);
-                if (max_count_host > 2048) GS_BK(512, 8, 1, 2048, kSmallCap);
-                break;
-            default:  // measured best at configs 2, 3 and 4 (profiles/r03c_ab_sort_variant_*)
-                GS_BK(256, 4, 1, 0, 1024);
-                if (max_count_host > 1024) GS_BK(512, 4, 1, 1024, 2048);
-                if (max_count_host > 2048) GS_BK(512, 8, 2, 2048, kSmallCap);
-                break;
-        }
+        // size classes (measured best at configs 2, 3 and 4 among 6 geometries,
+        // profiles/r03c_ab_sort_variant_*)
+        GS_BK(256, 4, 1, 0, 1024);
+        if (max_count_host > 1024) GS_BK(512, 4, 1, 1024, 2048);
+        if (max_count_host > 2048) GS_BK(512, 8, 2, 2048, kSmallCap);
 #undef GS_BK
         if (num_large_host > 0)
             hipLaunchKernelGGL(sort_tiles_large_kernel, dim3(num_large_host), dim3(kLargeThreads), 0, s,
@@ -1430,15 +1317,12 @@ void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int ma
     // (1024, 2048]: the E = 4 network over 8 waves (AMR tiles: 0.078 -> 0.073 ms
     // at config 3); (2048, 4096] stays on E = 16 over 4 waves (the 16-wave E = 4
     // network measured 0.453 -> 0.467 ms at config 4; profiles/r02f_ab_sort*)
-    if (max_count_host > 1024 && g_sort_wide) {
+    if (max_count_host > 1024) {
         hipLaunchKernelGGL(sort_tiles_wide_kernel<512>, dim3(T), dim3(512), 0, s, 1024, 2048, img.ranges,
                            b.pair_keys, b.point_list);
         if (max_count_host > 2048)
             hipLaunchKernelGGL(sort_tiles_small_kernel<16>, dim3(T), dim3(kSortThreads), 0, s, 2048, kSmallCap,
                                img.ranges, b.pair_keys, b.point_list);
-    } else if (max_count_host > 1024) {
-        hipLaunchKernelGGL(sort_tiles_small_kernel<16>, dim3(T), dim3(kSortThreads), 0, s, 1024, kSmallCap,
-                           img.ranges, b.pair_keys, b.point_list);
     }
     if (num_large_host > 0)
         hipLaunchKernelGGL(sort_tiles_large_kernel, dim3(num_large_host), dim3(kLargeThreads), 0, s,

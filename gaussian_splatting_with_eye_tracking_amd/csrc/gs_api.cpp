@@ -129,12 +129,19 @@ uint32_t* pinned_words() {
 // 0: copy + event; 1: scan-stored words + event; 2 (default): scan-stored
 // words + token, polled by the host (config 3 frame 0.575 -> 0.536 ms, config 2
 // 0.971 -> 0.965 ms per step, profiles/r03m_ab_hdr_mirror.log)
-int g_hdr_mirror = -1;  // set_tuning("hdr_mirror"); -1: GSAMD_HDR_MIRROR (default 2)
+// set_tuning("hdr_mirror"): 2 (default) the polled read-back -- the tile scan
+// stores the header words and a per-call token into mapped host memory and
+// the host spins on the token (no event or copy between the scan and the
+// work behind it: config 3 frame 0.575 -> 0.536 ms, profiles/r03m_ab_hdr_mirror.log);
+// 0 (fallback) a copy + event behind the scan.  (The mirror waited for by an
+// event, and the copy on a side stream, measured no faster: r02q / r02p;
+// removed.)  -1: GSAMD_HDR_MIRROR, else 2.
+int g_hdr_mirror = -1;
 
 bool hdr_mirror_on() {
     if (g_hdr_mirror < 0) {
         const char* e = std::getenv("GSAMD_HDR_MIRROR");
-        g_hdr_mirror = e ? std::atoi(e) : 2;
+        g_hdr_mirror = (e && std::atoi(e) == 0) ? 0 : 2;
     }
     return g_hdr_mirror != 0;
 }
@@ -162,69 +169,33 @@ void read_header(const uint32_t* hdr_dev, uint32_t out[4], hipStream_t s) {
 
 // The same read-back in two halves: the copy (and an event behind it) is
 // enqueued, the caller enqueues work that does not depend on K, then waits for
-// the copy alone -- that work runs while the host reacts to K.
-
-// With side_copy the copy runs on a side stream behind an event on s, so the
-// work enqueued on s after it (the speculative duplicate, the AMR step-0
-// levels) would start right after the tile scan instead of after the copy.
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t ready = nullptr;
-    hipEvent_t done = nullptr;
-};
-
-SideStream& side_stream() {
-    thread_local std::vector<SideStream> per_device;
-    int dev = 0;
-    GS_HIP(hipGetDevice(&dev));
-    if ((int)per_device.size() <= dev) per_device.resize(dev + 1);
-    SideStream& ss = per_device[dev];
-    if (!ss.s) {
-        GS_HIP(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
-        GS_HIP(hipEventCreateWithFlags(&ss.ready, hipEventDisableTiming));
-        GS_HIP(hipEventCreateWithFlags(&ss.done, hipEventDisableTiming));
-    }
-    return ss;
-}
-
-// (measured slower: cfg2 859 -> 834, cfg3 1576 -> 1548 frames/s,
-// profiles/r02p_ab_side_copy.log; the event record + cross-stream wait cost
-// more than the ~6 us dispatch gap they remove)
-int g_side_copy = -1;  // set_tuning("side_copy"); -1: GSAMD_SIDE_COPY (default 0)
-
-// hdr_mirror 2: the scan also stores a per-call token after the words
-// (system-scope release) and the host spins on it -- no event or copy in the
-// stream between the scan and the work enqueued behind it.
+// the copy alone -- that work runs while the host reacts to K.  With the
+// polled mirror (hdr_mirror 2) the scan stores the words into host memory
+// itself, followed by a per-call token the host spins on.
 thread_local uint32_t t_mirror_token = 0;
 uint32_t next_mirror_token() {
     t_mirror_token = t_mirror_token + 1u ? t_mirror_token + 1u : 1u;
     return t_mirror_token;
 }
 
+hipEvent_t& copy_done_event() {
+    thread_local std::vector<hipEvent_t> per_device;
+    int dev = 0;
+    GS_HIP(hipGetDevice(&dev));
+    if ((int)per_device.size() <= dev) per_device.resize(dev + 1, nullptr);
+    if (!per_device[dev]) GS_HIP(hipEventCreateWithFlags(&per_device[dev], hipEventDisableTiming));
+    return per_device[dev];
+}
+
 void begin_header_read(const uint32_t* hdr_dev, hipStream_t s, const uint32_t* mirror = nullptr) {
-    if (mirror) {  // the scan stores the words into host memory itself
-        if (g_hdr_mirror != 2) GS_HIP(hipEventRecord(side_stream().done, s));
-        return;
-    }
-    if (g_side_copy < 0) {
-        const char* e = std::getenv("GSAMD_SIDE_COPY");
-        g_side_copy = e ? std::atoi(e) : 0;
-    }
-    SideStream& ss = side_stream();
-    if (!g_side_copy) {
-        GS_HIP(hipMemcpyAsync(pinned_words(), hdr_dev, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        GS_HIP(hipEventRecord(ss.done, s));
-        return;
-    }
-    GS_HIP(hipEventRecord(ss.ready, s));
-    GS_HIP(hipStreamWaitEvent(ss.s, ss.ready, 0));
-    GS_HIP(hipMemcpyAsync(pinned_words(), hdr_dev, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, ss.s));
-    GS_HIP(hipEventRecord(ss.done, ss.s));
+    if (mirror) return;  // the scan stores the words into host memory itself
+    GS_HIP(hipMemcpyAsync(pinned_words(), hdr_dev, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    GS_HIP(hipEventRecord(copy_done_event(), s));
 }
 
 void finish_header_read(uint32_t out[4], const uint32_t* mirror = nullptr, hipStream_t s = nullptr,
                         const uint32_t* hdr_dev = nullptr) {
-    if (mirror && g_hdr_mirror == 2) {
+    if (mirror) {
         const volatile uint32_t* m = mirror;
         auto token = [&]() { return __atomic_load_n(const_cast<const uint32_t*>(mirror) + 4, __ATOMIC_ACQUIRE); };
         const auto t0 = std::chrono::steady_clock::now();
@@ -252,12 +223,7 @@ void finish_header_read(uint32_t out[4], const uint32_t* mirror = nullptr, hipSt
         }
         return;
     }
-    GS_HIP(hipEventSynchronize(side_stream().done));
-    if (mirror) {
-        const volatile uint32_t* m = mirror;
-        for (int i = 0; i < 4; i++) out[i] = m[i];
-        return;
-    }
+    GS_HIP(hipEventSynchronize(copy_done_event()));
     std::memcpy(out, pinned_words(), 4 * sizeof(uint32_t));
 }
 
@@ -307,12 +273,22 @@ void zero_accum_unless_clean(const GeomView& g, int P, hipStream_t s) {
     GS_HIP(hipMemsetAsync(g.grad_accum, 0, sizeof(float) * kGradRow * (size_t)P, s));
 }
 
+// Per-call options of this thread's forwards (gs_set_thread_option; thread-
+// local, so concurrent callers on other threads are unaffected):
+//   fwd_zero (1): the forward render zeroes the backward's accumulator rows
+//     behind the blend when a backward can follow; 0: the backward memsets them;
+//   sh_drgb (1): the preprocess stores d(rgb)/d(dir) of the SH colours
+//     (GeomView::drgb, 36 B per visible Gaussian) and the backward reads them
+//     instead of the 192-B SH rows; 0: the backward reads the coefficients;
+//   store_cov3d (0): the preprocess writes the geometry buffer's cov3D (the
+//     parity tests read it; nothing in the path does);
+//   fwd_no_grad: one-shot -- the NEXT forward on this thread needs no
+//     backward (below).
+thread_local int t_fwd_zero = 1;
+thread_local int t_sh_drgb = 1;
+thread_local int t_store_cov3d = 0;
 // Capacity for the speculative duplicate: the last base forward's K plus
 // 1/8 (0 before the first call, or when speculation is switched off).
-// set_tuning("fwd_zero"): 1 (default) the forward render zeroes the
-// backward's accumulator rows behind the blend when a backward can follow;
-// 0: never (the backward memsets them)
-int g_fwd_zero = 1;
 int g_spec_dup = 1;  // set_tuning("spec_dup")
 // The speculative duplicate's capacity, remembered per (device, W, H, P):
 // workloads that alternate render sizes or scenes (train 1080p / eval
@@ -399,15 +375,15 @@ uint32_t next_error_token() {
     return t ? t : 1u;
 }
 
-// set_tuning("fwd_no_grad", 1): the NEXT forward on this thread is known to
-// need no backward (the autograd wrappers under no_grad / with no input
-// requiring a gradient): its preprocess skips the SH-derivative rows only the
-// backward reads (the header flag kHdrDrgb then says so, and a backward would
-// fall back to the SH coefficients).  One-shot: every forward entry consumes it.
+// gs_set_thread_option("fwd_no_grad", 1): the NEXT forward on this thread is
+// known to need no backward (the autograd wrappers under no_grad / with no
+// input requiring a gradient): its preprocess skips the SH-derivative rows
+// only the backward reads (the header flag kHdrDrgb then says so, and a
+// backward would fall back to the SH coefficients).  One-shot: every forward
+// entry consumes it.
 thread_local int t_fwd_no_grad = 0;
-int g_fwd_hint = 1;  // set_tuning("fwd_hint", 0): ignore the hint (A/B)
 bool take_fwd_no_grad() {
-    const bool v = t_fwd_no_grad != 0 && g_fwd_hint;
+    const bool v = t_fwd_no_grad != 0;
     t_fwd_no_grad = 0;
     return v;
 }
@@ -438,8 +414,8 @@ PreprocessArgs make_pp(const ForwardIn& in, int tile) {
     a.focal_x = (float)in.width / (2.0f * in.tan_fovx);
     a.block = tile;
     a.prefiltered = in.prefiltered;
-    a.store_cov3d = g_store_cov3d;
-    a.store_drgb = g_sh_drgb && t_store_drgb;
+    a.store_cov3d = t_store_cov3d;
+    a.store_drgb = t_sh_drgb && t_store_drgb;
     a.zero_words = nullptr;
     a.zero_n = 0;
     a.err_token = 0;
@@ -468,7 +444,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     r.T = gx * gy;
     const size_t N = (size_t)W * H;
     // the optional tail (gs_layout.h) only when this forward writes into it
-    const bool tail = g_store_cov3d || (in.colors_precomp == nullptr && g_sh_drgb && t_store_drgb);
+    const bool tail = t_store_cov3d || (in.colors_precomp == nullptr && t_sh_drgb && t_store_drgb);
     char* gbase = call_resize(geometry, carve_geom(nullptr, in.P, nullptr, tail), "geometry");
     carve_geom(gbase, in.P, &r.g);
     set_accum_clean(r.g.grad_accum, false);  // this forward decides afresh
@@ -495,7 +471,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     stage_check(debug, s, "count_tiles");
     const std::pair<uint32_t*, uint32_t*> mirror =
         (r.T > 0 && hdr_mirror_on()) ? mirror_words() : std::pair<uint32_t*, uint32_t*>{nullptr, nullptr};
-    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second, bin_slots_for(in.P, gx, gy, tile), gx, dup_banded(gx, gy, tile), (mirror.second && g_hdr_mirror == 2) ? next_mirror_token() : 0u); }
+    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second, bin_slots_for(in.P, gx, gy, tile), gx, dup_banded(gx, gy, tile), mirror.second ? next_mirror_token() : 0u); }
     stage_check(debug, s, "tile_scan");
     uint32_t hdr[4];
     const bool amr = tile == 32;  // the AMR layout appends records and region lists
@@ -577,7 +553,7 @@ int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image
             // the accumulator rows are zeroed behind the blend only when a
             // backward can follow (not under the forward-only hint: a later
             // backward of this forward then zeroes them itself)
-            const bool zero = g_fwd_zero && t_store_drgb;
+            const bool zero = t_fwd_zero && t_store_drgb;
             zeroed = launch_render_forward(width, height, r.img, r.b, r.g, feats, background, out_color, s,
                                            zero ? r.g.grad_accum : nullptr, zero ? (size_t)kGradRow * (size_t)P : 0,
                                            hit_codes_at(r.b.point_list, (size_t)r.K));
@@ -640,7 +616,7 @@ int rasterizer_backward_impl(int amr_mode, int P, int D, int M, int R, const flo
         a.tan_fovx = tan_fovx;
         a.tan_fovy = tan_fovy;
         a.has_cov_precomp = cov3D_precomp != nullptr;
-        a.drgb = g_sh_drgb ? g.drgb : nullptr;
+        a.drgb = g.drgb;  // read only where the header says this forward wrote the rows
         a.drgb_known = a.drgb != nullptr && drgb_written(g.drgb);
         a.hdr = g.hdr;
         a.dL_dmean2D = dL_dmean2D;
@@ -1056,7 +1032,7 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
             { StageTimer _t(kAmrLevels, s);
               launch_amr_levels(r.T, r.img, s, zero_img ? out_color : nullptr, zero_img ? 3 * (size_t)W * H : 0); }
             stage_check(dbg, s, "amr_levels");
-            if (g_amr_variant >= 3) launch_order_tiles(r.T, r.img, false, s);
+            if (g_amr_variant == 4) launch_order_tiles(r.T, r.img, false, s);
             if (foveaStep != 0) launch_fovea_levels(foveaStep, r.T, r.img, s);
         };
         Binned r = preprocess_and_bin(in, geometry, binning, image, radii, tile, dbg, s, before_k);
@@ -1064,14 +1040,11 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
         // return zero radii as the reference does, and the AMR backward of a
         // step reads the step-0 radii from there -- is written by the preprocess)
         const float* feats = colors_precomp ? colors_precomp : r.g.rgb;
-        if (g_amr_variant >= 3) {
+        if (g_amr_variant == 4) {
             // the AMR blend's work units: tiles heaviest first (ordered above)
-            // and their sub-lists: 16x16 quadrants in the dead sort-key space
-            // (variant 3) or the 8x8 regions + blend records of the AMR binning
-            // layout (4)
-            { StageTimer _t(kAmrLists, s);
-              if (g_amr_variant == 3) launch_amr_quad_lists(W, H, r.img, r.b, r.g, r.K, s);
-              else launch_amr_region_lists(W, H, r.img, r.b, r.ab, r.g, feats, r.K, s); }
+            // and their sub-lists: the 8x8 regions + blend records of the AMR
+            // binning layout
+            { StageTimer _t(kAmrLists, s); launch_amr_region_lists(W, H, r.img, r.b, r.ab, r.g, feats, r.K, s); }
             stage_check(dbg, s, "amr_lists");
         }
         if (foveaStep == 0) return r.K;  // step 0: buffers only, a zero image (amr/cr/rasterizer_impl.cu:651)
@@ -1191,185 +1164,66 @@ int gs_activation_backward(int P, int M, int accumulate, const float* dL_dshs, c
     });
 }
 
+// Process-wide performance choices, each the default or one fallback; every
+// pair produces the same results (bit-identical buffers, sums equal to
+// atomic-order noise), so they are safe to flip between calls.
 int gs_set_tuning(const char* key, int value) {
     if (!key) return -1;
-    if (std::strcmp(key, "fwd_variant") == 0) {
+    if (std::strcmp(key, "fwd_variant") == 0) {  // 0: one wave x 4 px predicate form; else the default
         set_forward_variant(value);
         return 0;
     }
-    if (std::strcmp(key, "bwd_variant") == 0) {
+    if (std::strcmp(key, "bwd_variant") == 0) {  // 0: predicate form, LDS-row sums; else the default
         set_backward_variant(value);
         return 0;
     }
-    if (std::strcmp(key, "bwd_gauss_split") == 0) {
-        set_bwd_gauss_split(value);
-        return 0;
-    }
-    if (std::strcmp(key, "ritnet_small_wgs") == 0) {
-        set_ritnet_small_wgs(value);
-        return 0;
-    }
-    if (std::strcmp(key, "ritnet_mfma") == 0) {
-        set_ritnet_mfma(value);
-        return 0;
-    }
-    if (std::strcmp(key, "amr_variant") == 0) {
+    if (std::strcmp(key, "amr_variant") == 0) {  // 0: full-list AMR blocks; else region sub-lists (default)
         set_amr_variant(value);
         return 0;
     }
-    if (std::strcmp(key, "amr_scramble") == 0) {
-        set_amr_scramble(value);
-        return 0;
-    }
-    if (std::strcmp(key, "sort_wide") == 0) {
-        set_sort_wide(value);
-        return 0;
-    }
-    if (std::strcmp(key, "amr_batch") == 0) {
-        set_amr_batch(value);
-        return 0;
-    }
-    if (std::strcmp(key, "sh_drgb") == 0) {  // the preprocess stores d(rgb)/d(dir) for the SH backward
-        g_sh_drgb = value;
-        return 0;
-    }
-    if (std::strcmp(key, "fwd_no_grad") == 0) {  // one-shot hint for the next forward (make_pp)
-        t_fwd_no_grad = value;
-        return 0;
-    }
-    if (std::strcmp(key, "fwd_hint") == 0) {
-        g_fwd_hint = value;
-        return 0;
-    }
-    if (std::strcmp(key, "store_cov3d") == 0) {
-        set_store_cov3d(value);
-        return 0;
-    }
-    if (std::strcmp(key, "fwd_zero") == 0) {
-        g_fwd_zero = value;
-        return 0;
-    }
-    if (std::strcmp(key, "amr_levels_hist") == 0) {  // AMR percentiles by the two-pass histogram select
-        set_amr_levels_hist(value);
-        return 0;
-    }
-    if (std::strcmp(key, "amr_lists_per") == 0) {
-        set_amr_lists_per(value);
-        return 0;
-    }
-    if (std::strcmp(key, "amr_deep") == 0) {
-        set_amr_deep(value);
-        return 0;
-    }
-    if (std::strcmp(key, "amr_lists_order") == 0) {
-        set_amr_lists_order(value);
-        return 0;
-    }
-    if (std::strcmp(key, "pp_nt") == 0) {
-        set_pp_nt(value);
-        return 0;
-    }
-    if (std::strcmp(key, "zero_nt") == 0) {
-        set_zero_nt(value);
-        return 0;
-    }
-    if (std::strcmp(key, "bg_nt") == 0) {
-        set_bg_nt(value);
-        return 0;
-    }
-    if (std::strcmp(key, "amr_sel") == 0) {
-        set_amr_sel(value);
-        return 0;
-    }
-    if (std::strcmp(key, "amr_fold") == 0) {
-        set_amr_fold(value);
-        return 0;
-    }
-    if (std::strcmp(key, "xcd_map") == 0) {
-        set_xcd_map(value);
-        return 0;
-    }
-    if (std::strcmp(key, "tile_order") == 0) {
-        set_tile_order(value);
-        return 0;
-    }
-    if (std::strcmp(key, "bg_stage_mlp") == 0) {
-        set_bg_stage_mlp(value);
-        return 0;
-    }
-    if (std::strcmp(key, "dup_band") == 0) {
-        set_dup_band(value);
-        return 0;
-    }
-    if (std::strcmp(key, "band_threads") == 0) {
-        set_band_threads(value);
-        return 0;
-    }
-    if (std::strcmp(key, "band_split") == 0) {
-        set_band_split(value);
-        return 0;
-    }
-    if (std::strcmp(key, "pp_dma") == 0) {
-        set_pp_dma(value);
-        return 0;
-    }
-    if (std::strcmp(key, "hit_codes") == 0) {
-        set_hit_codes(value);
-        return 0;
-    }
-    if (std::strcmp(key, "sort_variant") == 0) {
-        set_sort_variant(value);
-        return 0;
-    }
-    if (std::strcmp(key, "sort_algo") == 0) {
+    if (std::strcmp(key, "sort_algo") == 0) {  // 0: bitonic networks only; 1: per-tile bucket sort (default)
         set_sort_algo(value);
         return 0;
     }
-    if (std::strcmp(key, "bin_slots") == 0) {
-        set_bin_slots(value);
+    if (std::strcmp(key, "cull") == 0) {  // 0: no row-group cull in the blends (the exactness A/B)
+        set_cull(value);
         return 0;
     }
-    if (std::strcmp(key, "dup_diag") == 0) {
-        set_dup_diag(value);
-        return 0;
-    }
-    if (std::strcmp(key, "bin_chunk") == 0) {
-        set_bin_chunk(value);
-        return 0;
-    }
-    if (std::strcmp(key, "bwd_split") == 0) {  // ways * 10000 + permille of the tiles split (0: off)
-        set_backward_split(value / 10000, value % 10000);
-        return 0;
-    }
-    if (std::strcmp(key, "bucket_order") == 0) {  // backward order from the forward's work buckets
-        set_bucket_order(value);
-        return 0;
-    }
-    if (std::strcmp(key, "scan_slices") == 0) {  // wave-contiguous tile scan (0: thread-contiguous)
-        set_scan_slices(value);
-        return 0;
-    }
-    if (std::strcmp(key, "hdr_mirror") == 0) {  // header read-back stored by the scan into mapped host memory
-        g_hdr_mirror = value;
-        return 0;
-    }
-    if (std::strcmp(key, "side_copy") == 0) {  // K read-back on a side stream
-        g_side_copy = value;
+    if (std::strcmp(key, "hdr_mirror") == 0) {  // 2: polled K read-back (default); 0: copy + event
+        g_hdr_mirror = value == 0 ? 0 : 2;
         return 0;
     }
     if (std::strcmp(key, "spec_dup") == 0) {  // speculative duplicate before the K read-back (base forward)
         g_spec_dup = value;
         return 0;
     }
-    if (std::strcmp(key, "bwd_flush") == 0) {
-        set_backward_flush(value);
-        return 0;
-    }
-    if (std::strcmp(key, "cull") == 0) {
-        set_cull(value);
+    if (std::strcmp(key, "ritnet_mfma") == 0) {  // 0: the SGPR-weight FMA convolution; 1: matrix cores (default)
+        set_ritnet_mfma(value);
         return 0;
     }
     g_err = std::string("unknown tuning key ") + key;
+    return -1;
+}
+
+int gs_set_thread_option(const char* key, int value) {
+    if (!key) return -1;
+    if (std::strcmp(key, "fwd_no_grad") == 0) {
+        t_fwd_no_grad = value;
+        return 0;
+    }
+    if (std::strcmp(key, "sh_drgb") == 0) {
+        t_sh_drgb = value;
+        return 0;
+    }
+    if (std::strcmp(key, "store_cov3d") == 0) {
+        t_store_cov3d = value;
+        return 0;
+    }
+    if (std::strcmp(key, "fwd_zero") == 0) {
+        t_fwd_zero = value;
+        return 0;
+    }
+    g_err = std::string("unknown thread option ") + key;
     return -1;
 }
 

@@ -14,9 +14,6 @@
 
 namespace gsamd {
 
-constexpr int kPix = 4;      // pixels per lane of the single-wave (backward) geometry
-constexpr int kBatch = 64;   // Gaussians staged per LDS batch in the single-wave geometry
-
 // A 16x16 block is covered by kWaves wave64s with kPPL pixels per lane
 // (kWaves * 64 * kPPL = 256).  The block is 4 row groups of 16x4 pixels;
 // wave w owns the contiguous groups r = w*kPPL + k (k < kPPL), lane l pixel
@@ -29,7 +26,6 @@ struct PixelSetT {
     uint32_t pid[kPPL];
     bool inside[kPPL];
 };
-using PixelSet = PixelSetT<kPix>;
 
 // power = -0.5 (c.x dx^2 + c.z dy^2) - c.y dx dy (forward.cu:331-333,
 // backward.cu:466-468), evaluated pre-scaled by log2(e) so exp(power) is one
@@ -66,33 +62,13 @@ __device__ __forceinline__ float splat_exp(float p2) { return __builtin_amdgcn_e
 // form with the lane mask in an SGPR pair at ~4.3 (tools/valu_rate.hip,
 // profiles/r04a_valu_rate.log).  These helpers select on a 64-bit lane mask
 // from __builtin_amdgcn_fcmpf / _uicmp (v_cmp_*_e64 into an SGPR pair).  The
-// "_v" forms start with s_nop 1: a mask written by a VALU compare and read as
-// a lane mask by a VALU needs 2 wait states on gfx950 (the compiler inserts
-// them for its own selects, but cannot see into the asm).  Masks made by SALU
-// (s_and / s_andn2 of compare masks) need none.
-constexpr int kFcmpOLT = 4, kFcmpUGE = 11, kFcmpULE = 13, kIcmpULT = 36;
+// select starts with s_nop 1: a mask written by a VALU compare and read as a
+// lane mask by a VALU needs 2 wait states on gfx950 (the compiler inserts them
+// for its own selects, but cannot see into the asm).  (Used by the backward
+// blend; in the forward and the AMR fold the mask form measured slower than
+// the compiler's selects)
+constexpr int kFcmpUGE = 11, kFcmpULE = 13, kIcmpULT = 36;
 
-__device__ __forceinline__ float gs_sel_v(uint64_t m, float t, float f) {  // m ? t : f
-    float r;
-    asm("s_nop 1\n\tv_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(t), "v"(f), "s"(m));
-    return r;
-}
-__device__ __forceinline__ float gs_sel_s(uint64_t m, float t, float f) {  // (mask from SALU)
-    float r;
-    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(t), "v"(f), "s"(m));
-    return r;
-}
-__device__ __forceinline__ uint32_t gs_sel_s_u32(uint64_t m, uint32_t t, uint32_t f) {
-    uint32_t r;
-    asm("v_cndmask_b32_e64 %0, %2, %1, %3" : "=v"(r) : "v"(t), "v"(f), "s"(m));
-    return r;
-}
-// m ? -|x| : t (the select form's "finished" transmittance)
-__device__ __forceinline__ float gs_sel_v_negabs(uint64_t m, float x, float t) {
-    float r;
-    asm("s_nop 1\n\tv_cndmask_b32_e64 %0, %2, -|%1|, %3" : "=v"(r) : "v"(x), "v"(t), "s"(m));
-    return r;
-}
 // (m ? x : 0, m ? y : 0)
 __device__ __forceinline__ void gs_sel2_zero_v(uint64_t m, float x, float y, float& rx, float& ry) {
     asm("s_nop 1\n\t"
@@ -130,10 +106,6 @@ __device__ __forceinline__ PixelSetT<kPPL> make_pixels_t(int W, int H, uint32_t 
         p.pid[k] = p.inside[k] ? (uint32_t)W * py + px : 0u;
     }
     return p;
-}
-
-__device__ __forceinline__ PixelSet make_pixels(int W, int H, uint32_t ox, uint32_t oy, uint32_t st) {
-    return make_pixels_t<kPix, 1>(W, H, ox, oy, st);
 }
 
 
@@ -309,49 +281,16 @@ struct BlendStateT {
     uint32_t last[kPPL];
 };
 
-// Front-to-back blend of `range` for the thread's kPPL pixels.  Called by the
-// whole workgroup (kWaves waves); LDS batches hold 64*kWaves Gaussians.
-// (ox, oy, st): the block origin and pixel stride, for the row-group cull.
-// One Gaussian against the lane's pixel, as selects instead of exec-masked
-// branches (kSel): the reference's per-pixel continues / early stop
-// (forward.cu:333-352) become values -- a rejected pair gets alpha 0, which
-// leaves C (C + f * 0 * T), T (T * (1 - 0)) and the stop test (T >= 1e-4 for
-// every pixel still blending) unchanged bit for bit; `last` moves only for
-// alpha != 0.  A finished pixel carries cap = 0 instead of 0.99 in the
-// alpha clamp min(cap, o G), so it rejects every later Gaussian (NaN G
-// included: fminf returns the number) with no extra instruction.  Per pair
-// ~26 VALU and no SALU instead of ~25 VALU + ~20 SALU of exec-mask
-// bookkeeping.
-__device__ __forceinline__ bool blend_one_sel(float2 xy, float4 co, float4 f, float pxx, float pxy, uint32_t contributor,
-                                              float& T, float (&C)[3], uint32_t& last, float& cap) {
-    const float dx = xy.x - pxx, dy = xy.y - pxy;
-    const float p = splat_p2(dx, dy, co);
-    float a = fminf(cap, co.w * splat_exp(p));
-    a = (p > 0.0f) ? 0.0f : a;           // power > 0: skipped
-    a = (a < 1.0f / 255.0f) ? 0.0f : a;  // alpha < 1/255: skipped
-    const float test_T = T * (1.0f - a);
-    const bool stop = test_T < 0.0001f;  // false whenever a == 0 (T >= 1e-4)
-    cap = stop ? 0.0f : cap;
-    a = stop ? 0.0f : a;
-    const float w = a * T;
-    C[0] = __builtin_fmaf(f.x, w, C[0]);
-    C[1] = __builtin_fmaf(f.y, w, C[1]);
-    C[2] = __builtin_fmaf(f.z, w, C[2]);
-    T = stop ? T : test_T;
-    const bool blended = a != 0.0f;
-    last = blended ? contributor : last;
-    return blended;
-}
-
-// The select form with the finished state in T's sign instead of an alpha cap:
-// a pixel that stops keeps T = -|T| (its final transmittance, negated), so
-// T (1 - a) < 1e-4 holds for every later Gaussian and a = 0 follows from the
-// stop test itself -- alpha is the plain min(0.99, o G) (a constant clamp:
-// no NaN-canonicalising max of a loop-carried cap) and the cap's select is
-// gone; the stop select writes -|T| through the VOP3 source modifiers.  The
-// last contributor is tracked as the entry's LDS byte offset (lo, the VGPR the
-// record reads already use) and converted once per 64 entries.  Bits for
-// every pixel still blending are those of blend_one_sel.
+// The select form of one (pixel, Gaussian) pair (forward.cu:333-352): the
+// reference's per-pixel continues / early stop become values -- a rejected
+// pair gets alpha 0, which leaves C (C + f * 0 * T) and T (T * (1 - 0))
+// unchanged bit for bit.  A pixel that stops keeps T = -|T| (its final
+// transmittance, negated), so T (1 - a) < 1e-4 holds for every later Gaussian
+// and a = 0 follows from the stop test itself -- alpha is the plain
+// min(0.99, o G), and the stop select writes -|T| through the VOP3 source
+// modifiers.  The last contributor is tracked as the entry's LDS byte offset
+// (lo, the VGPR the record reads already use) and converted once per 64
+// entries.  No exec masks, no SALU bookkeeping.
 template <bool kSafe = false>
 __device__ __forceinline__ bool blend_one_sel2(float2 xy, float4 co, float4 f, float pxx, float pxy, uint32_t lo,
                                                float& T, float (&C)[3], uint32_t& last_lo) {
@@ -375,35 +314,17 @@ __device__ __forceinline__ bool blend_one_sel2(float2 xy, float4 co, float4 f, f
     return blended;
 }
 
-// blend_one_sel2 with every select on an SGPR-pair lane mask and only the
-// tests the entry needs (`safe`: splat_form_safe, no `power > 0` test).  The
-// stop test and "blended" come out as masks: blended = accepted & !stop (the
-// same lanes as blend_one_sel2's a != 0 -- an accepted alpha is >= 1/255 and
-// never NaN: fminf returns the number).  Returns the blended mask.
-__device__ __forceinline__ uint64_t blend_one_msk(float2 xy, float4 co, float4 f, float pxx, float pxy, uint32_t lo,
-                                                  float& T, float (&C)[3], uint32_t& last_lo, bool safe) {
-    const float dx = xy.x - pxx, dy = xy.y - pxy;
-    const float p = splat_p2(dx, dy, co);
-    const float ar = fminf(0.99f, co.w * splat_exp(p));
-    uint64_t acc = __builtin_amdgcn_fcmpf(ar, 1.0f / 255.0f, kFcmpUGE);  // !(alpha < 1/255)
-    if (!safe) acc &= __builtin_amdgcn_fcmpf(p, 0.0f, kFcmpULE);         // !(power > 0)
-    const float a1 = gs_sel_v(acc, ar, 0.0f);
-    const float test_T = T * (1.0f - a1);
-    const uint64_t stop = __builtin_amdgcn_fcmpf(test_T, 0.0001f, kFcmpOLT);  // true for every finished pixel
-    const uint64_t blended = acc & ~stop;
-    const float w = gs_sel_s(blended, a1, 0.0f) * T;
-    C[0] = __builtin_fmaf(f.x, w, C[0]);
-    C[1] = __builtin_fmaf(f.y, w, C[1]);
-    C[2] = __builtin_fmaf(f.z, w, C[2]);
-    T = gs_sel_v_negabs(stop, T, test_T);
-    last_lo = gs_sel_s_u32(blended, lo, last_lo);
-    return blended;
-}
-
-// kSel: 0 branchy, 1 select form (blend_one_sel2), 2 SGPR-mask select form
-// (blend_one_msk; s_bal then holds kWaves more words: the batch's per-64-slot
-// masks of splat_form_safe Gaussians at s_bal[4 kWaves + c])
-template <int kPPL, int kWaves, int kSel = 0>
+// Front-to-back blend of `range` for the thread's kPPL pixels.  Called by the
+// whole workgroup (kWaves waves); LDS batches hold 64*kWaves Gaussians.
+// (ox, oy, st): the block origin and pixel stride, for the row-group cull.
+// kSel (the base forward's default, 4 waves x 1 pixel per lane): the select
+// form (blend_one_sel2), two Gaussians per iteration, the `power > 0` test
+// dropped in 64-slot chunks whose visited entries are all provably negative
+// definite over the tile (splat_form_safe; one loop copy per case), the
+// wave's exit tested after every pair of entries, and the exact row-group
+// hit codes recorded for the backward.  !kSel: the predicate form for any
+// kPPL (the fallback geometry and the AMR full-list blocks).
+template <int kPPL, int kWaves, bool kSel = false>
 __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const PixelSetT<kPPL>& px, float ox, float oy,
                                                           float st, const uint32_t* __restrict__ point_list,
                                                           const float2* __restrict__ means2D,
@@ -413,18 +334,18 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                                                           bool cull, uint8_t* __restrict__ hit_codes = nullptr,
                                                           uint64_t* s_hit = nullptr) {
 #pragma clang fp contract(fast)
+    static_assert(!kSel || kPPL == 1, "the select form is the 1-pixel-per-lane geometry");
     constexpr uint32_t kB = 64 * kWaves;
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = tid >> 6;
-    // Exact row-group hit codes (kSel, kPPL == 1, hit_codes given): bit w of
-    // entry j's code = some pixel of wave w's row group blended entry j --
-    // precisely the (row group, entry) pairs with a contributing pixel in the
-    // backward (a pixel blends entry j iff j < n_contrib and the alpha tests
-    // pass, backward.cu:466-482).  Wave w collects its 64-bit hit set per 64
-    // batch slots in s_hit[c kWaves + w]; the batch's codes are stored after
-    // the next barrier.
-    constexpr bool kRec = kSel && kPPL == 1;
-    const bool rec = kRec && hit_codes != nullptr;
+    // Exact row-group hit codes (kSel, hit_codes given): bit w of entry j's
+    // code = some pixel of wave w's row group blended entry j -- precisely
+    // the (row group, entry) pairs with a contributing pixel in the backward
+    // (a pixel blends entry j iff j < n_contrib and the alpha tests pass,
+    // backward.cu:466-482).  Wave w collects its 64-bit hit set per 64 batch
+    // slots in s_hit[c kWaves + w]; the batch's codes are stored after the
+    // next barrier.
+    const bool rec = kSel && hit_codes != nullptr;
     auto flush_codes = [&](uint32_t fb0) {
         if (fb0 + tid < range.y - range.x) {
             const uint32_t c = tid >> 6, bit = tid & 63;
@@ -438,7 +359,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
     bool done[kPPL];
 #pragma unroll
     for (int k = 0; k < kPPL; k++) {
-        st_.T[k] = (kSel && kPPL == 1 && !px.inside[k]) ? -1.0f : 1.0f;  // (kSel: finished = negative T)
+        st_.T[k] = (kSel && !px.inside[k]) ? -1.0f : 1.0f;  // (kSel: finished = negative T)
         st_.C[k][0] = st_.C[k][1] = st_.C[k][2] = 0.f;
         st_.last[k] = 0;
         done[k] = !px.inside[k];
@@ -468,10 +389,10 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
             s_co[tid] = splat_coef(co);
             s_b[tid * (kSel ? 4 : 1)] = features[3 * id + 2];  // (kSel: at a 16-B stride, one address for all reads)
             gm = cull ? splat_group_mask(xy, co, ox, oy, st) : 0xfu;
-            if (kSel >= 2) safe = splat_form_safe(splat_coef(co), fabsf(xy.x - ox), fabsf(xy.y - oy));
+            if (kSel) safe = splat_form_safe(splat_coef(co), fabsf(xy.x - ox), fabsf(xy.y - oy));
         }
         publish_group_masks<kWaves>(gm, s_bal);
-        if (kSel >= 2) {
+        if (kSel) {
             const uint64_t sb = __ballot(safe);
             if ((tid & 63) == 0) s_bal[4 * kWaves + (tid >> 6)] = sb;
         }
@@ -490,54 +411,7 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 mk[k] = uniform_u64(s_bal[c * 4 + wave * kPPL + k]);
                 todo |= mk[k];
             }
-            if constexpr (kPPL == 1 && kSel == 2) {
-                // SGPR-mask select form (blend_one_msk), two Gaussians per
-                // iteration, as the kSel 1 loop below
-                const uint64_t safe_m = uniform_u64(s_bal[4 * kWaves + c]);
-                uint64_t hits = 0;
-                uint32_t last_lo = ~0u;
-                const char* sa = reinterpret_cast<const char*>(s_a);
-                const char* sco = reinterpret_cast<const char*>(s_co);
-                const char* sb = reinterpret_cast<const char*>(s_b);
-                while (todo) {
-                    const uint32_t bA = (uint32_t)__builtin_ctzll(todo);
-                    todo &= todo - 1;
-                    const bool two = todo != 0;  // wave-uniform
-                    const uint32_t bB = two ? (uint32_t)__builtin_ctzll(todo) : bA;
-                    if (two) todo &= todo - 1;
-                    const uint32_t loA = (c * 64 + bA) * 16, loB = (c * 64 + bB) * 16;
-                    const float4 sA = *reinterpret_cast<const float4*>(sa + loA);
-                    const float4 sB = *reinterpret_cast<const float4*>(sa + loB);
-                    const float4 coA = *reinterpret_cast<const float4*>(sco + loA);
-                    const float4 coB = *reinterpret_cast<const float4*>(sco + loB);
-                    const float bAc = *reinterpret_cast<const float*>(sb + loA);
-                    const float bBc = *reinterpret_cast<const float*>(sb + loB);
-                    const uint64_t hA = blend_one_msk(make_float2(sA.x, sA.y), coA, make_float4(sA.z, sA.w, bAc, 0.f),
-                                                      px.x, px.y[0], loA, st_.T[0], st_.C[0], last_lo,
-                                                      (safe_m >> bA) & 1ull);
-                    if (kRec) hits |= hA != 0ull ? 1ull << bA : 0ull;
-                    if (two) {
-                        const uint64_t hB = blend_one_msk(make_float2(sB.x, sB.y), coB,
-                                                          make_float4(sB.z, sB.w, bBc, 0.f), px.x, px.y[0], loB,
-                                                          st_.T[0], st_.C[0], last_lo, (safe_m >> bB) & 1ull);
-                        if (kRec) hits |= hB != 0ull ? 1ull << bB : 0ull;
-                    }
-                }
-                if (last_lo != ~0u) st_.last[0] = b0 + (last_lo >> 4) + 1;
-                if (rec && (tid & 63) == 0) s_hit[c * kWaves + wave] = hits;
-                done[0] = st_.T[0] < 0.0f;
-                if (__ballot(!done[0]) == 0ull) wave_alive = false;
-                continue;
-            }
-            if constexpr (kPPL == 1 && kSel >= 3) {
-                // kSel 1 with the `power > 0` test dropped for 64-slot chunks
-                // whose visited entries are all provably negative definite
-                // over the tile (splat_form_safe, published as with kSel 2):
-                // one loop copy per case, chosen per chunk (the same bits).
-                // kSel 4: the wave also leaves the chunk as soon as all its
-                // pixels have finished (one ballot per pair of entries instead
-                // of one per chunk: a saturating wave no longer runs out the
-                // rest of its chunk -- entries no pixel can blend any more)
+            if constexpr (kSel) {
                 const uint64_t safe_m = uniform_u64(s_bal[4 * kWaves + c]);
                 uint64_t hits = 0;
                 uint32_t last_lo = ~0u;
@@ -562,120 +436,25 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                         const bool hA = blend_one_sel2<kSafe>(make_float2(sA.x, sA.y), coA,
                                                               make_float4(sA.z, sA.w, bAc, 0.f), px.x, px.y[0], loA,
                                                               st_.T[0], st_.C[0], last_lo);
-                        if (kRec) hits |= __ballot(hA) != 0ull ? 1ull << bA : 0ull;
+                        hits |= __ballot(hA) != 0ull ? 1ull << bA : 0ull;
                         if (two) {
                             const bool hB = blend_one_sel2<kSafe>(make_float2(sB.x, sB.y), coB,
                                                                   make_float4(sB.z, sB.w, bBc, 0.f), px.x, px.y[0],
                                                                   loB, st_.T[0], st_.C[0], last_lo);
-                            if (kRec) hits |= __ballot(hB) != 0ull ? 1ull << bB : 0ull;
+                            hits |= __ballot(hB) != 0ull ? 1ull << bB : 0ull;
                         }
-                        if (kSel >= 4 && __ballot(st_.T[0] > 0.0f) == 0ull) break;  // wave-uniform
+                        // every pixel of the wave finished: the rest of the chunk
+                        // holds entries no pixel can blend any more
+                        if (__ballot(st_.T[0] > 0.0f) == 0ull) break;  // wave-uniform
                     }
                 };
                 if ((todo & ~safe_m) == 0ull) loop(std::integral_constant<bool, true>{});
                 else loop(std::integral_constant<bool, false>{});
-                if (last_lo != ~0u) st_.last[0] = b0 + (last_lo >> 4) + 1;
-                if (rec && (tid & 63) == 0) s_hit[c * kWaves + wave] = hits;
-                done[0] = st_.T[0] < 0.0f;
-                if (__ballot(!done[0]) == 0ull) wave_alive = false;
-                continue;
-            }
-            if constexpr (kPPL == 1 && kSel) {
-                // select form (blend_one_sel2), two Gaussians per iteration; the
-                // wave's early exit is tested once per 64 batch slots.  A
-                // finished pixel carries a negative T (outside pixels start at
-                // -1), which every later stop test rejects.
-                uint64_t hits = 0;
-                uint32_t last_lo = ~0u;
-                const char* sa = reinterpret_cast<const char*>(s_a);
-                const char* sco = reinterpret_cast<const char*>(s_co);
-                const char* sb = reinterpret_cast<const char*>(s_b);
-                while (todo) {
-                    const uint32_t bA = (uint32_t)__builtin_ctzll(todo);
-                    todo &= todo - 1;
-                    const bool two = todo != 0;  // wave-uniform
-                    const uint32_t bB = two ? (uint32_t)__builtin_ctzll(todo) : bA;
-                    if (two) todo &= todo - 1;
-                    const uint32_t loA = (c * 64 + bA) * 16, loB = (c * 64 + bB) * 16;
-                    const float4 sA = *reinterpret_cast<const float4*>(sa + loA);
-                    const float4 sB = *reinterpret_cast<const float4*>(sa + loB);
-                    const float4 coA = *reinterpret_cast<const float4*>(sco + loA);
-                    const float4 coB = *reinterpret_cast<const float4*>(sco + loB);
-                    const float bAc = *reinterpret_cast<const float*>(sb + loA);
-                    const float bBc = *reinterpret_cast<const float*>(sb + loB);
-                    const bool hA = blend_one_sel2(make_float2(sA.x, sA.y), coA, make_float4(sA.z, sA.w, bAc, 0.f),
-                                                   px.x, px.y[0], loA, st_.T[0], st_.C[0], last_lo);
-                    if (kRec) hits |= __ballot(hA) != 0ull ? 1ull << bA : 0ull;
-                    if (two) {
-                        const bool hB = blend_one_sel2(make_float2(sB.x, sB.y), coB,
-                                                       make_float4(sB.z, sB.w, bBc, 0.f), px.x, px.y[0], loB,
-                                                       st_.T[0], st_.C[0], last_lo);
-                        if (kRec) hits |= __ballot(hB) != 0ull ? 1ull << bB : 0ull;
-                    }
-                }
                 // lo = 16 j, contributor = b0 + j + 1
                 if (last_lo != ~0u) st_.last[0] = b0 + (last_lo >> 4) + 1;
                 if (rec && (tid & 63) == 0) s_hit[c * kWaves + wave] = hits;
                 done[0] = st_.T[0] < 0.0f;
                 if (__ballot(!done[0]) == 0ull) wave_alive = false;
-                continue;
-            }
-            if constexpr (kPPL == 1) {
-                // One row group per wave: every set bit of todo is a visit.  Two
-                // Gaussians per iteration: their LDS reads share one wait and
-                // their alpha chains (independent of T) interleave; the blend
-                // itself stays front to back.
-                while (todo) {
-                    const uint32_t bA = (uint32_t)__builtin_ctzll(todo);
-                    todo &= todo - 1;
-                    const bool two = todo != 0;  // wave-uniform
-                    const uint32_t bB = two ? (uint32_t)__builtin_ctzll(todo) : bA;
-                    if (two) todo &= todo - 1;
-                    const uint32_t jA = c * 64 + bA, jB = c * 64 + bB;
-                    const float4 sA = s_a[jA], sB = s_a[jB];
-                    const float4 coA = s_co[jA], coB = s_co[jB];
-                    const float2 xyA = make_float2(sA.x, sA.y), xyB = make_float2(sB.x, sB.y);
-                    const float4 fA = make_float4(sA.z, sA.w, s_b[jA], 0.f), fB = make_float4(sB.z, sB.w, s_b[jB], 0.f);
-                    const float dxA = xyA.x - px.x, dxB = xyB.x - px.x;
-                    const float dyA = xyA.y - px.y[0], dyB = xyB.y - px.y[0];
-                    const float pA = splat_p2(dxA, dyA, coA);
-                    const float pB = splat_p2(dxB, dyB, coB);
-                    const float aA = fminf(0.99f, coA.w * splat_exp(pA));
-                    const float aB = fminf(0.99f, coB.w * splat_exp(pB));
-                    const bool alive = !done[0];
-                    {
-                        const float test_T = st_.T[0] * (1 - aA);
-                        const bool hit = !done[0] && !(pA > 0.0f) && !(aA < 1.0f / 255.0f);
-                        const bool stop = hit && test_T < 0.0001f;
-                        done[0] = done[0] || stop;
-                        if (hit && !stop) {
-                            const float w = aA * st_.T[0];
-                            st_.C[0][0] = __builtin_fmaf(fA.x, w, st_.C[0][0]);
-                            st_.C[0][1] = __builtin_fmaf(fA.y, w, st_.C[0][1]);
-                            st_.C[0][2] = __builtin_fmaf(fA.z, w, st_.C[0][2]);
-                            st_.T[0] = test_T;
-                            st_.last[0] = b0 + jA + 1;
-                        }
-                    }
-                    if (two) {
-                        const float test_T = st_.T[0] * (1 - aB);
-                        const bool hit = !done[0] && !(pB > 0.0f) && !(aB < 1.0f / 255.0f);
-                        const bool stop = hit && test_T < 0.0001f;
-                        done[0] = done[0] || stop;
-                        if (hit && !stop) {
-                            const float w = aB * st_.T[0];
-                            st_.C[0][0] = __builtin_fmaf(fB.x, w, st_.C[0][0]);
-                            st_.C[0][1] = __builtin_fmaf(fB.y, w, st_.C[0][1]);
-                            st_.C[0][2] = __builtin_fmaf(fB.z, w, st_.C[0][2]);
-                            st_.T[0] = test_T;
-                            st_.last[0] = b0 + jB + 1;
-                        }
-                    }
-                    if (__ballot(alive) == 0ull) {
-                        wave_alive = false;
-                        break;
-                    }
-                }
                 continue;
             }
             while (todo) {
@@ -722,153 +501,11 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
         __syncthreads();
         if (b0 > 0) flush_codes(b0 - kB);
     }
-    if constexpr (kPPL == 1 && kSel) st_.T[0] = fabsf(st_.T[0]);  // (finished pixels: -T_final)
+    if constexpr (kSel) st_.T[0] = fabsf(st_.T[0]);  // (finished pixels: -T_final)
     return st_;
 }
 
-// ------------------------------------------------------------ DPP reduce
-// Sum over the 64 lanes; the total lands in lane 63 (row_shr 1,2,4,8 within
-// 16-lane rows, then row_bcast:15 and row_bcast:31 -- gfx9 DPP).
-__device__ __forceinline__ float dpp_sum_lane63(float v) {
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x111, 0xf, 0xf, true));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x112, 0xf, 0xf, true));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x114, 0xf, 0xf, true));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x118, 0xf, 0xf, true));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x142, 0xa, 0xf, false));
-    v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x143, 0xc, 0xf, false));
-    return v;
-}
-
-// The same reduction for 9 values at once, as fused v_add_f32_dpp (hipcc
-// fuses only a few of the mov_dpp + add pairs above).  Each stage walks the
-// 9 registers, so a DPP source was written >= 9 VALU ops earlier (the gfx9
-// VALU-write -> DPP-read hazard needs 2); the leading s_nop covers the
-// compiler's last writes.  Must run with all 64 lanes active.
-__device__ __forceinline__ void dpp_sum9_lane63(float (&g)[9]) {
-    asm volatile(
-        "s_nop 1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %3, %3, %3 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %4, %4, %4 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %5, %5, %5 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %6, %6, %6 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %7, %7, %7 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %8, %8, %8 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %3, %3, %3 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %4, %4, %4 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %5, %5, %5 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %6, %6, %6 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %7, %7, %7 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %8, %8, %8 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %3, %3, %3 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %4, %4, %4 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %5, %5, %5 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %6, %6, %6 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %7, %7, %7 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %8, %8, %8 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %3, %3, %3 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %4, %4, %4 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %5, %5, %5 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %6, %6, %6 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %7, %7, %7 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %8, %8, %8 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %3, %3, %3 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %4, %4, %4 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %5, %5, %5 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %6, %6, %6 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %7, %7, %7 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %8, %8, %8 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        "v_add_f32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        "v_add_f32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        "v_add_f32_dpp %3, %3, %3 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        "v_add_f32_dpp %4, %4, %4 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        "v_add_f32_dpp %5, %5, %5 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        "v_add_f32_dpp %6, %6, %6 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        "v_add_f32_dpp %7, %7, %7 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        "v_add_f32_dpp %8, %8, %8 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), "+v"(g[6]), "+v"(g[7]),
-          "+v"(g[8]));
-}
-
-// Row-only variant: after it lanes 15, 31, 47 and 63 hold the sums of their
-// 16-lane rows (4 DPP stages instead of 6; the caller adds the 4 partials).
-__device__ __forceinline__ void dpp_sum9_rows(float (&g)[9]) {
-    asm volatile(
-        "s_nop 1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %3, %3, %3 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %4, %4, %4 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %5, %5, %5 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %6, %6, %6 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %7, %7, %7 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %8, %8, %8 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %3, %3, %3 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %4, %4, %4 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %5, %5, %5 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %6, %6, %6 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %7, %7, %7 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %8, %8, %8 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %3, %3, %3 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %4, %4, %4 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %5, %5, %5 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %6, %6, %6 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %7, %7, %7 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %8, %8, %8 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %3, %3, %3 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %4, %4, %4 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %5, %5, %5 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %6, %6, %6 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %7, %7, %7 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %8, %8, %8 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), "+v"(g[6]), "+v"(g[7]),
-          "+v"(g[8]));
-}
-
-// Half-wave variant (5 stages): lanes 31 and 63 hold the sums of lanes
-// 0-31 and 32-63 (row_shr 1,2,4,8, then row_bcast:15 into rows 1 and 3).
-__device__ __forceinline__ void dpp_sum9_halves(float (&g)[9]) {
-    dpp_sum9_rows(g);
-    asm volatile(
-        "s_nop 1\n"
-        "v_add_f32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %3, %3, %3 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %4, %4, %4 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %5, %5, %5 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %6, %6, %6 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %7, %7, %7 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "v_add_f32_dpp %8, %8, %8 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), "+v"(g[6]), "+v"(g[7]),
-          "+v"(g[8]));
-}
-
+// ------------------------------------------------------- wave reductions
 // Full 64-lane sums of 9 values by transposition (gfx950 v_permlane32_swap /
 // v_permlane16_swap) instead of 9 independent DPP trees.  For a group of 4
 // registers (a, b, c, d), rows = 16-lane quarters:
@@ -900,10 +537,7 @@ __device__ __forceinline__ float pl_add16(float a, float b) {
     return __builtin_bit_cast(float, r0) + __builtin_bit_cast(float, r1);
 }
 
-// The same sums with the two add levels as packed f32 adds (v_pk_add_f32, one
-// issue for two lanes' worth of values): the swaps pair (g0, g4) and (g2, g6)
-// so that each level's operands already sit in adjacent registers -- 4 + 2
-// swaps, 3 packed adds and the 14 DPP adds: 23 VALU issues instead of 26.
+// Swaps returning both halves (for packed adds of the pairs).
 typedef float gs_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ gs_f2 pl_swap32(float a, float b) {
     const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
@@ -918,39 +552,7 @@ __device__ __forceinline__ gs_f2 pl_swap16(float a, float b) {
     return gs_f2{__builtin_bit_cast(float, r0), __builtin_bit_cast(float, r1)};
 }
 
-__device__ __forceinline__ void swap_sum9_pk(float (&g)[9], float& za, float& zb) {
-    const gs_f2 p0 = pl_swap32(g[0], g[1]), p4 = pl_swap32(g[4], g[5]);
-    const gs_f2 p2 = pl_swap32(g[2], g[3]), p6 = pl_swap32(g[6], g[7]);
-    const gs_f2 abef = gs_f2{p0.x, p4.x} + gs_f2{p0.y, p4.y};
-    const gs_f2 cdgh = gs_f2{p2.x, p6.x} + gs_f2{p2.y, p6.y};
-    const gs_f2 q0 = pl_swap16(abef.x, cdgh.x), q1 = pl_swap16(abef.y, cdgh.y);
-    const gs_f2 z = gs_f2{q0.x, q1.x} + gs_f2{q0.y, q1.y};
-    za = z.x;
-    zb = z.y;
-    float e = g[8];
-    asm volatile(
-        "s_nop 1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "v_add_f32_dpp %2, %2, %2 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-        "s_nop 1\n"
-        "v_add_f32_dpp %2, %2, %2 row_bcast:15 row_mask:0xa bank_mask:0xf\n"
-        "s_nop 1\n"
-        "v_add_f32_dpp %2, %2, %2 row_bcast:31 row_mask:0xc bank_mask:0xf\n"
-        : "+v"(za), "+v"(zb), "+v"(e));
-    g[8] = e;
-}
-
-// Transposition half of swap_sum9_pk, for sums finished elsewhere: after it
+// Transposition half of swap_sum9 with packed adds, for sums finished elsewhere: after it
 // row r (lanes 16r..16r+15) of za holds the 16 column partials of value
 // swap_sum_slot(r), zb those of 4 + swap_sum_slot(r); g[8] holds row r's sum
 // in lane 16 r + 15.  9 swap / packed-add issues + 4 DPP adds.
@@ -981,7 +583,6 @@ __device__ __forceinline__ void swap_rows8_pk_t(float (&g)[9], float& za, float&
         g[8] = e;
     }
 }
-__device__ __forceinline__ void swap_rows8_pk(float (&g)[9], float& za, float& zb) { swap_rows8_pk_t<true>(g, za, zb); }
 
 __device__ __forceinline__ void swap_sum9(float (&g)[9], float& za, float& zb) {
     const float ab = pl_add32(g[0], g[1]), cd = pl_add32(g[2], g[3]);

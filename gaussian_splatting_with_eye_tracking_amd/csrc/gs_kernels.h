@@ -36,7 +36,6 @@ struct PreprocessArgs {
     uint32_t* zero_words;
     int zero_n;
     uint32_t err_token;
-    int nt = 0;  // bit 0: the SH rows' LDS-DMA loads non-temporal; bit 1: the drgb rows' stores (launcher)
 };
 
 // base/cr/forward.cu:155-256 (+ the tile histogram the binning needs).
@@ -64,32 +63,15 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
 constexpr int kLdsTiles = 16384;
 void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
                         hipStream_t s);
-void set_bin_chunk(int gaussians_per_workgroup);
-void set_dup_diag(int v);  // timing diagnostics only (wrong keys)
-void set_sort_algo(int v);
-void set_pp_dma(int v);
-void set_hit_codes(int v);
-void set_sort_variant(int v);  // 0 = bitonic networks, 1 = bucket sort (default)
-void set_bin_slots(int v);  // 0 = auto
+void set_sort_algo(int v);  // 0 = bitonic networks, 1 = bucket sort (default)
 int bin_slots_for(int P, int gx, int gy, int block);  // sub-bucket slots of the LDS binning (P-Gaussian forward)
 bool dup_banded(int gx, int gy, int block);           // the row-banded duplicate runs for this tile grid
-void set_dup_band(int v);
-void set_band_split(int v);
-void set_band_threads(int v);
-void set_bg_stage_mlp(int v);
 // img.tile_order = tiles sorted by descending work (heaviest first) so the
 // long tiles of a blend launch start early instead of forming its tail.
 // Work = range length, or min(range length, max_contrib) if use_max_contrib.
-// Used by the backward blend (render_bwd 1.15 -> 1.06 ms at config 2).
-// split_tiles > 0 (plain order only): the split_tiles heaviest tiles become
-// split_ways units each, entry = tile | (row-group set << 28) -- 2 ways: row
-// groups {0, 1} / {2, 3}, 4 ways: one row group each; the rest follow as
-// plain tile ids.  tile_order then holds T + (split_ways - 1) * split_tiles
-// entries (<= 4T).
-void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s, int gx = 0, int gy = 0,
-                        int split_tiles = 0, int split_ways = 1);
-bool tile_order_enabled();
-void set_tile_order(int v);
+// (The AMR units' order; the base backward takes its order from the forward
+// render's work buckets.)
+void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s);
 void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int max_count_host, int num_large_host,
                        hipStream_t s);
 // (tile << 32 | depth) reconstruction of the reference's point_list_keys.
@@ -101,35 +83,12 @@ void launch_reconstruct_keys(int T, const ImageView& img, const BinningView& b, 
 bool launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                            const float* features, const float* bg, float* out_color, hipStream_t s,
                            float* zero_rows = nullptr, size_t zero_floats = 0, uint8_t* hit_codes = nullptr);
-// Tuning knob for A/B runs (gs_set_tuning("fwd_variant", v)).
+// Tuning knobs (gs_set_tuning): the default or one fallback each.
 void set_forward_variant(int v);
-void set_xcd_map(int v);
-extern int g_xcd_map;
-void set_cull(int v);
-void set_amr_variant(int v);
-void set_amr_batch(int v);
-void set_amr_fold(int v);
-void set_amr_sel(int v);
-void set_bg_nt(int v);
-void set_zero_nt(int v);
-void set_pp_nt(int v);
-void set_amr_lists_order(int v);
-void set_amr_deep(int v);
-void set_amr_lists_per(int v);
-void set_amr_levels_hist(int v);
-void set_store_cov3d(int v);
-extern int g_store_cov3d;
-extern int g_sh_drgb;
-void set_sort_wide(int v);
-void set_amr_scramble(int v);
-void set_ritnet_mfma(int v);
-void set_ritnet_small_wgs(int v);
-void set_bwd_gauss_split(int v);  // 1: SH backward as its own kernel  // AMR blend geometry (as fwd_variant)  // row-group cull in the blend kernels (default on)
 void set_backward_variant(int v);
-void set_backward_flush(int v);
-void set_backward_split(int ways, int permille);
-void set_scan_slices(int v);
-void set_bucket_order(int v);  // heavy-tile split of the backward blend
+void set_amr_variant(int v);
+void set_cull(int v);  // row-group cull in the blend kernels (default on)
+void set_ritnet_mfma(int v);
 // Blend backward (base/cr/backward.cu:399-557) into g.grad_accum.
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s, int K);
@@ -151,7 +110,7 @@ struct BackwardGaussArgs {
     const float* drgb;      // the forward's d(rgb)/d(dir) [9][P] (nullptr: from the SH coefficients)
     const uint32_t* hdr;    // the geometry header (kHdrDrgb says whether drgb was written)
     int drgb_known;         // the host knows this geometry buffer's forward wrote drgb (gs_api registry)
-    int nt_out = 0;         // the outputs other than dL_dsh stored with the non-temporal hint (launcher)
+    int nt_out = 0;         // the outputs other than dL_dsh stored with the non-temporal hint (off: +3 %)
     // outputs (every element written; no memsets needed)
     float* dL_dmean2D;
     float* dL_dconic;
@@ -192,7 +151,7 @@ struct MultiViewArgs {
     float* grad_norm_accum;  // nullable: densification statistics, accumulated
     float* denom;
     float* max_radii;
-    int nt = 0;  // the dL_dsh rows stored with the non-temporal hint (launcher: bwd_gauss's bg_nt bit 0)
+    int nt = 0;  // the dL_dsh rows stored with the non-temporal hint (launcher: on, as bwd_gauss's)
 };
 void launch_pack_view_grads(int P, const GeomView& g, const int* radii, bool has_sh, const float* viewmatrix,
                             const float* projmatrix, const float* campos, int width, int height, float tan_fovx,
@@ -223,9 +182,6 @@ void launch_eye_preprocess(const uint8_t* gray, int H, int W, const uint8_t* gam
 // AMR (amr/cr/rasterizer_impl.cu:181-243, amr/cr/forward.cu:261-648).
 // zero_image (optional): foveaStep 0's zero image, written by the same launch
 void launch_amr_levels(int T, const ImageView& img, hipStream_t s, float* zero_image = nullptr, size_t zero_floats = 0);
-// The 16x16 quadrant sub-lists of the sorted 32-px tile lists (render.hip).
-void launch_amr_quad_lists(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g, int K,
-                           hipStream_t s);
 // The 8x8-region sub-lists and per-instance blend records (variant 4).
 void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningView& b, const AmrBinningView& ab,
                              const GeomView& g, const float* features, int K, hipStream_t s);

@@ -287,16 +287,27 @@ __device__ __forceinline__ void pp_thread(const PreprocessArgs& a, const GeomVie
     }, stage);
 }
 
-// kStageOut (kDma): a visible Gaussian's d(rgb)/d(dir) row and rgb go into its
+// kDma (SH16, the default): the SH rows through LDS-DMA, and the strided
+// records staged -- a visible Gaussian's d(rgb)/d(dir) row and rgb go into its
 // thread's LDS row (free once its SH coefficients are in registers), and each
 // wave then stores its 64 records as wave-contiguous 16-B pieces instead of
 // per-thread stores at a 48-B / 12-B stride (one store instruction covers
-// whole lines, not a third of each).  Rows of culled Gaussians carry stale
-// words, as their never-read records may.
-template <bool kHasSH, bool kSH16, bool kCovPrecomp, bool kDma = false, bool kStageOut = false, bool kNtIn = false>
+// whole lines, not a third of each): config 4 0.503 -> 0.441 ms, config 3
+// 0.084 -> 0.077, config 2 equal (profiles/r04f_ab_pp*.log).  Rows of culled
+// Gaussians carry stale words, as their never-read records may.  Cache hints
+// (non-temporal: read or written once per pass, and re-read only after more
+// traffic than the caches hold): the SH rows' LDS-DMA loads (0.0645 -> 0.0578
+// ms at config 2, 0.378 -> 0.356 at config 4, profiles/r04z6_ab_pp*.log), the
+// drgb rows' stores (config-4 fwd + bwd step 2.544 -> 2.508 ms,
+// r04z6_ab_ppstep4.log), the geometry loads (0.394 -> 0.380 ms at config 4,
+// r04z7_ab_pp*.log).  Measured and removed: per-thread SH loads with LDS-DMA
+// but unstaged records, a persistent pipelined form (0.537 vs 0.502 ms at
+// config 4, profiles/r04e_ab_pp*.log).
+template <bool kHasSH, bool kSH16, bool kCovPrecomp, bool kDma = false>
 __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a, GeomView g, int* __restrict__ radii,
                                                                 uint32_t* __restrict__ tile_count) {
-    static_assert(!kStageOut || (kDma && kHasSH), "staged records use the SH rows' LDS");
+    static_assert(!kDma || (kHasSH && kSH16), "LDS-DMA stages 16-coefficient SH rows");
+    constexpr bool kStageOut = kDma, kNtIn = kDma;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     __shared__ __attribute__((aligned(16))) float s_sh[kDma ? kPpThreads * 48 : 1];
     if constexpr (kDma) {
@@ -309,10 +320,7 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
 #pragma unroll
         for (int i = 0; i < 12; i++) {
             const size_t f = (size_t)(64 * i + lane) * 4;
-            if (row0 * 48 + f < nfl) {
-                if (a.nt & 1) __builtin_amdgcn_global_load_lds(src + f, dst + 256 * i, 16, 0, 2);  // (nt)
-                else __builtin_amdgcn_global_load_lds(src + f, dst + 256 * i, 16, 0, 0);
-            }
+            if (row0 * 48 + f < nfl) __builtin_amdgcn_global_load_lds(src + f, dst + 256 * i, 16, 0, 2);  // (nt)
         }
     }
     for (int i = idx; i < a.zero_n; i += (int)(gridDim.x * blockDim.x)) a.zero_words[i] = 0u;
@@ -339,8 +347,7 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
                 if (c < 3 * nrow) {
                     const float4 v = *reinterpret_cast<const float4*>(wl + 48 * (c / 3) + 4 * (c % 3));
                     typedef float f4v __attribute__((ext_vector_type(4)));
-                    if (a.nt & 2) __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(out + c));
-                    else out[c] = v;
+                    __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(out + c));
                 }
             }
         }
@@ -377,57 +384,12 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
     pp_thread<kHasSH, kSH16, kCovPrecomp, kDma>(a, g, radii, tile_count, idx, row, nullptr);
 }
 
-// set_tuning("pp_dma"): 0 per-thread SH loads; 1 SH rows through LDS-DMA
-// (kDma) for SH16; 3 = 1 with the strided records staged (kStageOut; the
-// default since round 4: config 4 0.503 -> 0.441 ms, config 3 0.084 -> 0.077,
-// config 2 equal, profiles/r04f_ab_pp*.log); < 0 the default.  (2, a persistent pipelined form -- one-wave workgroups walking
-// batches with the next batch's SH rows and geometry in flight -- measured
-// slower: 0.537 vs 0.502 ms at config 4, 0.095 vs 0.092 at config 2,
-// profiles/r04e_ab_pp*.log; removed)
-constexpr int kDefaultPpDma = 3;
-int g_pp_dma = kDefaultPpDma;
-// set_tuning("pp_nt"): bit 0 the SH rows' LDS-DMA loads non-temporal (0.0645
-// -> 0.0578 ms at config 2, 0.378 -> 0.356 at config 4, forward only;
-// profiles/r04z6_ab_pp*.log), bit 1 the drgb rows' stores (read once, by the
-// Gaussian backward, after more traffic than the caches hold; bits 0 + 1:
-// config-4 fwd + bwd step 2.544 -> 2.508 ms, r04z6_ab_ppstep4.log), bit 2
-// the geometry loads (pp_thread kNtIn: 0.394 -> 0.380 ms at config 4, config
-// 2 -1 %, r04z7_ab_pp*.log); default all three
-int g_pp_nt = 7;
-void set_pp_nt(int v) { g_pp_nt = v; }
-void set_pp_dma(int v) { g_pp_dma = v < 0 ? kDefaultPpDma : v; }
-
 template <bool A, bool B, bool C>
-static void launch_pp(const PreprocessArgs& args, const GeomView& g, int* radii, uint32_t* tile_count, hipStream_t s) {
-    PreprocessArgs a = args;
-    a.nt = g_pp_nt;
+static void launch_pp(const PreprocessArgs& a, const GeomView& g, int* radii, uint32_t* tile_count, hipStream_t s) {
     const int blocks = (a.P + kPpThreads - 1) / kPpThreads;
-    if constexpr (A && B) {
-        if (g_pp_dma == 3 && (g_pp_nt & 4)) {
-            hipLaunchKernelGGL((preprocess_kernel<A, B, C, true, true, true>), dim3(blocks), dim3(kPpThreads), 0, s,
-                               a, g, radii, tile_count);
-            return;
-        }
-        if (g_pp_dma == 3) {
-            hipLaunchKernelGGL((preprocess_kernel<A, B, C, true, true>), dim3(blocks), dim3(kPpThreads), 0, s, a, g,
-                               radii, tile_count);
-            return;
-        }
-    }
-    if (A && B && g_pp_dma)
-        hipLaunchKernelGGL((preprocess_kernel<A, B, C, true>), dim3(blocks), dim3(kPpThreads), 0, s, a, g, radii,
-                           tile_count);
-    else
-        hipLaunchKernelGGL((preprocess_kernel<A, B, C>), dim3(blocks), dim3(kPpThreads), 0, s, a, g, radii,
-                           tile_count);
+    hipLaunchKernelGGL((preprocess_kernel<A, B, C, A && B>), dim3(blocks), dim3(kPpThreads), 0, s, a, g, radii,
+                       tile_count);
 }
-
-int g_store_cov3d = 0;  // set_tuning("store_cov3d"): the parity tests read the geometry buffer's cov3D
-// set_tuning("sh_drgb"): the preprocess stores d(rgb)/d(dir) of the SH colours
-// (GeomView::drgb, 36 B per visible Gaussian) and the backward reads them
-// instead of the 192-B SH rows
-int g_sh_drgb = 1;
-void set_store_cov3d(int v) { g_store_cov3d = v; }
 
 void launch_preprocess(const PreprocessArgs& a, const GeomView& g, int* radii, uint32_t* tile_count,
                        hipStream_t s) {

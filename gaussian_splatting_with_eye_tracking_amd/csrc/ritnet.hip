@@ -310,8 +310,7 @@ __global__ void __launch_bounds__(256) label_moments_kernel(const uint8_t* __res
 
 int g_ritnet_mfma = 1;  // 1: conv_mfma_kernel (default), 0: the SGPR-weight FMA kernel
 void set_ritnet_mfma(int v) { g_ritnet_mfma = v; }
-int g_ritnet_small_wgs = 512;  // below this many 32 x 8 blocks: 32 x 4 blocks (one row per wave)
-void set_ritnet_small_wgs(int v) { g_ritnet_small_wgs = v; }
+constexpr int kRitnetSmallWgs = 512;  // below this many 32 x 8 blocks: 32 x 4 blocks (one row per wave)
 
 void launch_ritnet_conv(int k, const float* const* in_ptr, const int* in_c, const int* in_up, int nseg, int H, int W,
                         const float* w, const float* bias, int lrelu, const float* bn_scale, const float* bn_shift,
@@ -327,7 +326,7 @@ void launch_ritnet_conv(int k, const float* const* in_ptr, const int* in_c, cons
     if (g_ritnet_mfma) {
         // small planes (the deep levels) are latency-bound: one row per wave
         // doubles the workgroups and halves each wave's MFMA chain
-        const bool small = ((W + 31) / 32) * ((H + 7) / 8) < g_ritnet_small_wgs;
+        const bool small = ((W + 31) / 32) * ((H + 7) / 8) < kRitnetSmallWgs;
         const dim3 grid((W + 31) / 32, small ? (H + 3) / 4 : (H + 7) / 8);
 #define GS_CONV_MFMA(K, R) \
     hipLaunchKernelGGL((conv_mfma_kernel<K, R>), grid, dim3(256), 0, s, in, Cin, H, W, w, bias, lrelu, bn_scale, bn_shift, out)

@@ -849,4 +849,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     });
     m.def("profile_read", &ProfileRead, py::arg("reset") = true);
     m.def("set_tuning", [](const std::string& k, int v) { check(gs_set_tuning(k.c_str(), v), "set_tuning"); });
+    m.def("set_thread_option",
+          [](const std::string& k, int v) { check(gs_set_thread_option(k.c_str(), v), "set_thread_option"); });
 }

@@ -56,14 +56,14 @@ def _hint_forward_only(tensors) -> bool:
     (_clear_hint), so a forward that raised before consuming it cannot hand
     it to a later training forward."""
     if not (torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in tensors)):
-        _C.set_tuning("fwd_no_grad", 1)
+        _C.set_thread_option("fwd_no_grad", 1)
         return True
     return False
 
 
 def _clear_hint(hinted: bool) -> None:
     if hinted:
-        _C.set_tuning("fwd_no_grad", 0)
+        _C.set_thread_option("fwd_no_grad", 0)
 
 
 class _RasterizeGaussians(torch.autograd.Function):

@@ -374,18 +374,28 @@ void gs_profile_enable(int on);
  * (default: all).  Each timed stage adds two event records per launch, so
  * the headline timing records only the kernel its roofline is quoted on. */
 void gs_profile_set_mask(unsigned mask);
-/* Kernel-geometry knobs for A/B measurements ("fwd_variant": 0 = one wave
- * per tile x 4 px/lane, 1 = 2 waves x 2 px/lane, 2 = 4 waves x
- * 1 px/lane, the default), "bwd_variant" (0 = 1 wave x 4 px/lane, the default; 1 = 2 x 2; 2 = 4 x 1; 3 = 1 x 4 uncapped registers), "cull" (1 =
- * skip Gaussians whose alpha >= 1/255 box misses a 16x4 row group, the
- * default; 0 only to verify that the cull is exact), "store_cov3d" (1 = the
- * forward also writes the geometry buffer's cov3D, which nothing in the path
- * reads back -- for buffer-level parity checks; default 0), "amr_fold" (bit k
- * = AMR foveaStep k blends in alpha-phase + fold-phase batches, default 0x1e;
- * bit 5 = 16-entry batches), "amr_variant", "amr_batch", "amr_scramble",
- * "sort_wide", "xcd_map", "bin_chunk", "bwd_gauss_split".  Returns 0, or -1
- * for an unknown key. */
+/* Process-wide performance choices for A/B measurements, each the default
+ * or one fallback (every pair gives the same results): "fwd_variant" (0 = one
+ * wave x 4 px/lane predicate form; else the default 4 waves x 1 px/lane select
+ * form), "bwd_variant" (0 = predicate form with LDS-row sums; else the
+ * default select form with staged sums), "amr_variant" (0 = full-list AMR
+ * blocks; else the default 8x8 region sub-lists), "sort_algo" (0 = bitonic
+ * networks only; 1 = per-tile bucket sort, the default), "cull" (1 = skip
+ * Gaussians whose alpha >= 1/255 ellipse misses a 16x4 row group, the
+ * default; 0 only to verify that the cull is exact), "hdr_mirror" (2 = the
+ * polled K read-back, the default; 0 = copy + event), "spec_dup" (1 = the
+ * speculative duplicate before the K read-back, the default), "ritnet_mfma"
+ * (1 = matrix-core convolutions, the default; 0 = SGPR-weight FMA kernel).
+ * Returns 0, or -1 for an unknown key. */
 int gs_set_tuning(const char* key, int value);
+/* Per-call options of the calling thread's forwards (thread-local): "fwd_zero"
+ * (1 = the forward render zeroes the backward's accumulator rows, default),
+ * "sh_drgb" (1 = the preprocess stores d(rgb)/d(view dir) for the SH
+ * backward, default), "store_cov3d" (1 = the forward also writes the geometry
+ * buffer's cov3D, which nothing in the path reads back -- for buffer-level
+ * parity checks; default 0), "fwd_no_grad" (one-shot: the next forward on this
+ * thread needs no backward).  Returns 0, or -1 for an unknown key. */
+int gs_set_thread_option(const char* key, int value);
 int gs_profile_stage_count(void);
 const char* gs_profile_stage_name(int i);
 void gs_profile_read(double* total_ms, long* counts, int reset);

@@ -112,7 +112,8 @@ def test_binning_size_inverse_is_exact(prefix):
 def test_torch_extension_surface():
     from gaussian_splatting_with_eye_tracking_amd import _C, native_library_paths
     for n in ("rasterize_gaussians", "rasterize_gaussians_backward", "mark_visible", "amr_rasterize_gaussians",
-              "distCUDA2", "parse_buffers", "profile_enable", "profile_read", "set_tuning"):
+              "distCUDA2", "parse_buffers", "profile_enable", "profile_read", "set_tuning",
+              "set_thread_option"):
         assert hasattr(_C, n), n
     assert _C.abi_version() == 5
     assert all(os.path.exists(p) and p.startswith(ROOT) for p in native_library_paths())

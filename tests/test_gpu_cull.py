@@ -68,7 +68,7 @@ def _backward(s, t, out, dpix, bwd_variant):
 
 
 @pytest.mark.parametrize("P,W,H,seed", [(6000, 256, 192, 1), (30000, 320, 200, 2)])
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1])  # the fallback and the default blends
 def test_cull_is_exact(P, W, H, seed, variant):
     """Forward: bit-identical.  Backward: every per-Gaussian sum the blend
     kernel accumulates (grad_accum) and the screen-space gradients agree to
@@ -94,8 +94,7 @@ def test_cull_is_exact(P, W, H, seed, variant):
     np.testing.assert_array_equal(res[0][0], res[1][0])  # image, bit-exact
     for k in res[0][1]:
         np.testing.assert_array_equal(res[0][1][k], res[1][1][k], err_msg=k)
-    # float-atomic ordering noise only (variant 2 adds LDS atomics from 4 waves
-    # in arbitrary order on top of the global ones): observed up to ~1.5e-6
+    # float-atomic ordering noise only: observed up to ~1.5e-6
     for i in range(3):  # dL_dmeans2D, dL_dcolors, dL_dopacity
         assert G.rel_err(res[1][2][i], res[0][2][i]) < 5e-6, i
     for c in range(9):  # each accumulated term, column by column
@@ -142,40 +141,42 @@ def test_cull_is_exact_amr_render_once():
     np.testing.assert_array_equal(imgs[0], imgs[1])
 
 
+@pytest.mark.parametrize("fwd", [1, 0])
 @pytest.mark.parametrize("P,W,H,seed", [(6000, 256, 192, 1), (30000, 320, 200, 2)])
-def test_sgpr_mask_backward_matches_select_form(P, W, H, seed):
-    """Backward variant 8 (SGPR-mask selects; the power > 0 test dropped for
+def test_default_backward_matches_fallback(P, W, H, seed, fwd):
+    """The default backward (SGPR-mask selects; the power > 0 test dropped for
     Gaussians whose form is provably negative definite; the contributor test
-    dropped in batches every pixel has started) and 9 (8 + the dx^2 s0 sum
-    formed after the transposition) against variant 7 on the
-    adversarial scene (huge thin splats, near-degenerate conics): the blend
-    sums agree to float-atomic ordering noise."""
+    dropped in batches every pixel has started; staged sums flushed by the
+    staging reduce) against the fallback (predicate form, LDS-row sums) on
+    the adversarial scene (huge thin splats, near-degenerate conics), after
+    the default forward (hit codes) and the fallback forward (geometric
+    cull): the blend sums agree to float-atomic ordering noise."""
     import gaussian_splatting_with_eye_tracking_amd._C as C
     from gaussian_splatting_with_eye_tracking_amd import synthetic as S
     sc, cam = _adversarial_scene(P, W, H, seed)
     dpix = torch.from_numpy(S.make_cotangent(H, W, seed + 1)).cuda()
     res = {}
     try:
-        for v in (7, 8, 9, 10, 11):
-            s, t, out, _bufs = _forward(sc, cam, 5)
+        for v in (0, 1):
+            s, t, out, _bufs = _forward(sc, cam, fwd)
             res[v] = _backward(s, t, out, dpix, v)
     finally:
         C.set_tuning("fwd_variant", -1)
         C.set_tuning("bwd_variant", -1)
-    for v in (8, 9, 10, 11):
-        for i in range(3):  # dL_dmeans2D, dL_dcolors, dL_dopacity
-            assert G.rel_err(res[v][0][i], res[7][0][i]) < 5e-6, (v, i)
-        assert G.rel_err(res[v][1], res[7][1]) < 5e-6, v
+    for i in range(3):  # dL_dmeans2D, dL_dcolors, dL_dopacity
+        assert G.rel_err(res[1][0][i], res[0][0][i]) < 5e-6, i
+    assert G.rel_err(res[1][1], res[0][1]) < 5e-6
 
 
 @pytest.mark.parametrize("P,W,H,seed,adv", [(6000, 256, 192, 1, True), (30000, 320, 200, 2, True),
                                             (10000, 256, 256, 0, False)])
-def test_sgpr_mask_forward_bit_identical(P, W, H, seed, adv):
-    """Forward variant 7 (SGPR-mask selects, no power > 0 test for provably
-    negative-definite forms) against variant 5 (the select form): image,
-    final T, n_contrib, max_contrib and the backward's hit codes bit for bit,
-    on the adversarial scene (huge thin splats, opacities at 1/255) and the
-    default one."""
+def test_default_forward_bit_identical_to_fallback(P, W, H, seed, adv):
+    """The default forward (4 waves x 1 px, select form, no power > 0 test in
+    provably negative-definite chunks, per-pair wave exit) against the
+    fallback (1 wave x 4 px, predicate form): image, final T, n_contrib and
+    max_contrib bit for bit, on the adversarial scene (huge thin splats,
+    opacities at 1/255) and the default one; only the default leaves hit
+    codes."""
     import gaussian_splatting_with_eye_tracking_amd._C as C
     from gaussian_splatting_with_eye_tracking_amd import synthetic as S
     if adv:
@@ -185,17 +186,13 @@ def test_sgpr_mask_forward_bit_identical(P, W, H, seed, adv):
         sc = S.make_scene(P, cam, seed=seed)
     res = {}
     try:
-        for v in (5, 7, 8, 9):
+        for v in (0, 1):
             s, t, out, bufs = _forward(sc, cam, v)
-            K = int(out[0])
-            codes = C.parse_buffers(out[3], out[4], out[5], P, K, W, H, 16)["hit_codes"]
-            res[v] = (out[1].cpu().numpy(), {k: b.cpu().numpy() for k, b in bufs.items()}, codes.cpu().numpy())
+            hdr = C.parse_buffers(out[3], out[4], out[5], P, int(out[0]), W, H, 16)["hdr"]
+            res[v] = (out[1].cpu().numpy(), {k: b.cpu().numpy() for k, b in bufs.items()}, int(hdr[6].item()))
     finally:
         C.set_tuning("fwd_variant", -1)
-    # 8: variant 5 without the power > 0 test in all-safe chunks; 9: 8 leaving
-    # a chunk as soon as every pixel of the wave has finished
-    for v in (7, 8, 9):
-        np.testing.assert_array_equal(res[5][0], res[v][0])
-        for k in res[5][1]:
-            np.testing.assert_array_equal(res[5][1][k], res[v][1][k], err_msg=(v, k))
-        np.testing.assert_array_equal(res[5][2], res[v][2])
+    np.testing.assert_array_equal(res[1][0], res[0][0])
+    for k in res[1][1]:
+        np.testing.assert_array_equal(res[1][1][k], res[0][1][k], err_msg=k)
+    assert (res[1][2], res[0][2]) == (1, 0)  # header word kHdrHitCodes

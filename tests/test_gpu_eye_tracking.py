@@ -63,18 +63,19 @@ def test_ritnet_small_odd_batchnorm_values():
     assert G.rel_err(logits.cpu().numpy(), R.forward(sd, x)) < 1e-5
 
 
-@pytest.mark.parametrize("mfma,small_wgs", [(1, 512), (1, 0), (0, 512)])
-@pytest.mark.parametrize("HW", [(24, 40), (10, 70)])
-def test_conv_virtual_concat_and_upsample(mfma, small_wgs, HW):
+@pytest.mark.parametrize("mfma", [1, 0])
+@pytest.mark.parametrize("HW", [(24, 40), (10, 70), (256, 512)])
+def test_conv_virtual_concat_and_upsample(mfma, HW):
     """One _C.ritnet_conv over three segments, the first read through the
     nearest 2x upsampling, against torch.cat + F.interpolate + F.conv2d, on
-    the matrix-core kernel (default) and the SGPR-weight FMA kernel."""
+    the matrix-core kernel (default) and the SGPR-weight FMA kernel; the
+    small planes take the matrix-core kernel's 32 x 4 blocks, 256 x 512 (512
+    blocks of 32 x 8, ritnet.hip kRitnetSmallWgs) its 32 x 8 blocks."""
     import torch.nn.functional as F
     from gaussian_splatting_with_eye_tracking_amd import _C
     gen = torch.Generator().manual_seed(5)
     H, W = HW
     _C.set_tuning("ritnet_mfma", mfma)
-    _C.set_tuning("ritnet_small_wgs", small_wgs)  # 0: 32 x 8 blocks (two rows per wave) everywhere
     a = torch.randn(32, H // 2, W // 2, generator=gen)
     b = torch.randn(32, H, W, generator=gen)
     c = torch.randn(7, H, W, generator=gen)
@@ -92,7 +93,6 @@ def test_conv_virtual_concat_and_upsample(mfma, small_wgs, HW):
             torch.cuda.synchronize()
         finally:
             _C.set_tuning("ritnet_mfma", 1)
-            _C.set_tuning("ritnet_small_wgs", 512)
         assert G.rel_err(out.cpu().numpy(), ref.numpy()) < 1e-5, k
 
 

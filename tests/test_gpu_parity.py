@@ -49,22 +49,19 @@ def _oracle_forward(sc, cam, colors_precomp=None, cov3D_precomp=None, bg=(0.0, 0
     return s, O.forward(s, sc.means3D, sc.opacities, **kw), kw
 
 
-@pytest.mark.parametrize("pp_dma", [1, 3])  # 3: records staged through LDS, stored coalesced
 @pytest.mark.parametrize("name,P,W,H,seed", CASES)
-def test_forward_buffers_bit_exact(name, P, W, H, seed, pp_dma):
-    _forward_buffers_bit_exact(name, P, W, H, seed, pp_dma)
+def test_forward_buffers_bit_exact(name, P, W, H, seed):
+    _forward_buffers_bit_exact(name, P, W, H, seed)
 
 
-def _forward_buffers_bit_exact(name, P, W, H, seed, pp_dma=-1):
+def _forward_buffers_bit_exact(name, P, W, H, seed):
     import gaussian_splatting_with_eye_tracking_amd._C as C
     sc, cam = G.scene_and_camera(P, W, H, seed)
-    C.set_tuning("store_cov3d", 1)  # the geometry buffer's cov3D is written on request only
-    C.set_tuning("pp_dma", pp_dma)
+    C.set_thread_option("store_cov3d", 1)  # the geometry buffer's cov3D is written on request only
     try:
         _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
     finally:
-        C.set_tuning("store_cov3d", 0)
-        C.set_tuning("pp_dma", -1)
+        C.set_thread_option("store_cov3d", 0)
     _, ref, _ = _oracle_forward(sc, cam)
     assert K == ref.num_rendered
     d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
@@ -158,95 +155,49 @@ def test_backward_parity(name, P, W, H, seed, variant):
             assert G.rel_err(gl.cpu().numpy(), g.cpu().numpy()) < 1e-5, n  # (float atomics: run-order noise)
 
 
-@pytest.mark.parametrize("pp_dma", [1, 3])
-def test_backward_parity_preprocess_forms(pp_dma):
-    """The SH backward reads the d(rgb)/d(dir) rows the preprocess stored:
-    per-thread stores (1) and the LDS-staged coalesced stores (3) both feed it."""
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    C.set_tuning("pp_dma", pp_dma)
-    try:
-        test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
-        test_backward_parity("ragged_3k_250x130", 3000, 250, 130, 7, "sh")
-    finally:
-        C.set_tuning("pp_dma", -1)
-
-
 def test_backward_parity_without_forward_zeroing():
     """fwd_zero 0: the forward leaves the accumulator rows alone and the
     backward zeroes them itself (the path a forward under the forward-only
     hint takes): gradients against the oracle."""
     import gaussian_splatting_with_eye_tracking_amd._C as C
-    C.set_tuning("fwd_zero", 0)
+    C.set_thread_option("fwd_zero", 0)
     try:
         test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
         test_backward_parity("ragged_3k_250x130", 3000, 250, 130, 7, "colors_precomp")
     finally:
-        C.set_tuning("fwd_zero", 1)
+        C.set_thread_option("fwd_zero", 1)
 
 
-@pytest.mark.parametrize("stage", [1, 2, 3])
-def test_backward_parity_gauss_store_forms(stage):
-    """bwd_gauss with the 3-float outputs stored per thread (1), staged
-    through LDS and stored coalesced (2), and the drgb-known kernel (3: the
-    forward stored d(rgb)/d(dir), dL_dsh in two half-size LDS rounds): all
-    against the oracle."""
+def test_backward_parity_gauss_forms():
+    """bwd_gauss's two SH16 kernels against the oracle: the drgb-known kernel
+    (the forward stored d(rgb)/d(dir), dL_dsh in two half-size LDS rounds: the
+    default) and the coefficient kernel (sh_drgb 0: the SH rows staged
+    through LDS); the forward-only hint's path is
+    test_backward_without_stored_sh_derivatives."""
     import gaussian_splatting_with_eye_tracking_amd._C as C
-    C.set_tuning("bg_stage_mlp", stage)
-    try:
-        test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
-        test_backward_parity("ragged_3k_250x130", 3000, 250, 130, 7, "sh")
-        test_backward_parity("g1_64_32x32", 64, 32, 32, 3, "sh")
-    finally:
-        C.set_tuning("bg_stage_mlp", -1)
+    for drgb in (1, 0):
+        C.set_thread_option("sh_drgb", drgb)
+        try:
+            test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
+            test_backward_parity("ragged_3k_250x130", 3000, 250, 130, 7, "sh")
+            test_backward_parity("g1_64_32x32", 64, 32, 32, 3, "sh")
+        finally:
+            C.set_thread_option("sh_drgb", 1)
 
 
-@pytest.mark.parametrize("slots", [1, 3, 8, 0])
-def test_bin_slots_bit_exact(slots):
-    """The binning's per-slot sub-buckets (gs_layout.h kBinSlots) change only
-    where inside a tile's range the duplicate lands each key; after the
-    per-tile sort point_list, keys and ranges are the oracle's bit for bit."""
+@pytest.mark.parametrize("P,W,H", [(20000, 128, 128), (2_100_000, 160, 96), (20000, 1000, 40), (20000, 16400, 16)])
+def test_binning_forms_bit_exact(P, W, H):
+    """The binning's size-dependent forms against the oracle, bit for bit:
+    the row-banded duplicate (binning.hip band_stage_kernel /
+    band_split_kernel: 1024 x 1 below 2M Gaussians, 512 x 2 sources and 8
+    sub-bucket count slots from 2M), a wide grid (few rows, many split
+    workgroups per row) and a grid wider than one append round's 1024 bins
+    (16400 px: the direct LDS duplicate); each forward twice (the second runs
+    the duplicate speculatively)."""
     import gaussian_splatting_with_eye_tracking_amd._C as C
-    P, W, H, seed = 20000, 128, 128, 11
-    sc, cam = G.scene_and_camera(P, W, H, seed)
-    C.set_tuning("bin_slots", slots)
-    try:
-        _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
-    finally:
-        C.set_tuning("bin_slots", 0)  # auto
-    _, ref, _ = _oracle_forward(sc, cam)
-    assert K == ref.num_rendered
-    d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
-    np.testing.assert_array_equal(d["ranges"].cpu().numpy().astype(np.uint32), ref.ranges)
-    np.testing.assert_array_equal(d["point_list"].cpu().numpy().astype(np.uint32), ref.point_list)
-    np.testing.assert_array_equal(d["tile_count"].cpu().numpy().astype(np.uint32), ref.ranges[:, 1] - ref.ranges[:, 0])
-    assert G.image_l1(color.cpu().numpy(), ref.color) < G.IMAGE_L1_TOL
-
-
-@pytest.mark.parametrize("band,split,W,H,threads", [(0, 0, 200, 120, 512), (1, 0, 200, 120, 512),
-                                                      (1, 1, 200, 120, 512), (1, 3, 128, 128, 512),
-                                                      (1, 64, 1000, 40, 512), (1, 0, 16400, 16, 512),
-                                                      (1, 0, 200, 120, 513), (1, 3, 1000, 40, 513),
-                                                      (1, 0, 200, 120, 514), (1, 2, 200, 120, 1024)])
-def test_dup_band_bit_exact(band, split, W, H, threads):
-    """The row-banded duplicate (binning.hip band_stage_kernel /
-    band_split_kernel) stages (Gaussian, tile row) entries and splits them
-    into tile runs through LDS-reordered appends; any split count, a grid
-    wider than one append round's 1024 bins (16400 px: the direct
-    duplicate) and the speculative path (second forward) all give the
-    oracle's point_list and ranges bit for bit."""
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    P, seed = 20000, 12
-    sc, cam = G.scene_and_camera(P, W, H, seed)
-    C.set_tuning("dup_band", band)
-    C.set_tuning("band_split", split)
-    C.set_tuning("band_threads", threads)
-    try:
-        _gpu_forward(sc, cam)  # the second forward runs the duplicate speculatively
-        _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
-    finally:
-        C.set_tuning("dup_band", 1)
-        C.set_tuning("band_split", 0)
-        C.set_tuning("band_threads", 0)
+    sc, cam = G.scene_and_camera(P, W, H, 12)
+    _gpu_forward(sc, cam)
+    _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
     _, ref, _ = _oracle_forward(sc, cam)
     assert K == ref.num_rendered
     d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
@@ -285,8 +236,8 @@ def _clustered_scene(P, cam, seed, kind):
 
 
 @pytest.mark.parametrize("kind", ["ties", "cluster", "two"])
-@pytest.mark.parametrize("sort_algo,variant", [(0, 0), (1, 0), (1, 1), (1, 2), (1, 3), (1, 4)])
-def test_tile_sort_adversarial_depths(kind, sort_algo, variant):
+@pytest.mark.parametrize("sort_algo", [0, 1])
+def test_tile_sort_adversarial_depths(kind, sort_algo):
     """point_list / ranges bit-exact against the oracle's stable (depth, idx)
     order for both tile sorts (bucket sort, bitonic networks) on tiles of
     every size class (<= 1024, <= 2048, <= 4096 and the merge path)."""
@@ -296,12 +247,10 @@ def test_tile_sort_adversarial_depths(kind, sort_algo, variant):
     cam = S.make_camera(W, H)
     sc = _clustered_scene(P, cam, 5, kind)
     C.set_tuning("sort_algo", sort_algo)
-    C.set_tuning("sort_variant", variant)
     try:
         _, _, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
     finally:
         C.set_tuning("sort_algo", 1)
-        C.set_tuning("sort_variant", 0)
     _, ref, _ = _oracle_forward(sc, cam)
     assert K == ref.num_rendered
     n = ref.ranges[:, 1] - ref.ranges[:, 0]
@@ -344,37 +293,6 @@ def test_backward_with_unfilled_work_buckets():
     for a, b in zip(*out):
         assert np.all(np.isfinite(b))
         assert G.rel_err(b, a) < 1e-5
-
-
-@pytest.mark.parametrize("xcd_map", [0, 1, 2, 3])
-def test_xcd_placement_is_result_invariant(xcd_map):
-    """XCD-aware tile placement (gs_blend.cuh; bit 0 forward, bit 1
-    backward) only changes which workgroup renders which tile: forward
-    buffers bit-identical, image and gradients within the bars, on a grid
-    whose tile count is not a multiple of 8 (ragged XCD chunks)."""
-    import oracle as O
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
-    P, W, H, seed = 6000, 250, 130, 7  # 16 x 9 = 144 tiles
-    sc, cam = G.scene_and_camera(P, W, H, seed)
-    C.set_tuning("xcd_map", xcd_map)
-    try:
-        s, t, (K, color, radii, geom, binning, img) = _gpu_forward(sc, cam)
-        dpix = S.make_cotangent(H, W, seed + 1)
-        e = torch.Tensor([])
-        grads = C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, e, t["scales"], t["rotations"],
-                                               s.scale_modifier, e, s.viewmatrix, s.projmatrix, s.tanfovx,
-                                               s.tanfovy, torch.from_numpy(dpix).cuda(), t["shs"], s.sh_degree,
-                                               s.campos, geom, K, binning, img, False)
-        torch.cuda.synchronize()
-    finally:
-        C.set_tuning("xcd_map", 1)
-    os_, ref, kw = _oracle_forward(sc, cam)
-    assert G.image_l1(color.cpu().numpy(), ref.color) < G.IMAGE_L1_TOL
-    rg = O.backward(os_, ref, sc.means3D, dpix, **kw)
-    for n, g in zip(["dL_dmeans2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh",
-                     "dL_dscales", "dL_drotations"], grads):
-        assert G.rel_err(g.cpu().numpy(), rg[n]) < G.GRAD_REL_TOL, n
 
 
 def _psnr(img, gt):
@@ -422,10 +340,12 @@ def test_config2_full_size_parity_and_psnr():
         assert G.rel_err(g.cpu().numpy(), rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(g.cpu().numpy(), rg[n]))
 
 
-@pytest.mark.parametrize("bwd_variant", [0, 1, 2, 3, 5, 6, 7, 8, 9, 10, 11])
-@pytest.mark.parametrize("fwd_variant", [0, 1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("bwd_variant", [0, 1])
+@pytest.mark.parametrize("fwd_variant", [0, 1])
 def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
-    """Every forward / backward blend geometry (gs_set_tuning) against the oracle."""
+    """The default and the fallback forward / backward blends (gs_set_tuning),
+    every pairing, against the oracle (the fallback forward leaves no hit
+    codes: the backward then culls by geometry)."""
     import oracle as O
     import gaussian_splatting_with_eye_tracking_amd._C as C
     from gaussian_splatting_with_eye_tracking_amd import synthetic as S
@@ -452,57 +372,6 @@ def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
              "dL_drotations"]
     for n, g in zip(names, grads):
         assert G.rel_err(g.cpu().numpy(), rg[n]) < G.GRAD_REL_TOL, (n, fwd_variant, bwd_variant)
-
-
-@pytest.mark.parametrize("variant", ["sh", "colors_precomp"])
-def test_bwd_gauss_split_matches_oracle(variant):
-    """SH backward as its own kernel (tuning "bwd_gauss_split") against the oracle."""
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    try:
-        C.set_tuning("bwd_gauss_split", 1)
-        test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, variant)
-    finally:
-        C.set_tuning("bwd_gauss_split", 0)
-
-
-@pytest.mark.parametrize("split", [20300, 41000])
-def test_bwd_heavy_tile_split_matches_oracle(split):
-    """The backward blend with its heaviest tiles split into row-group units
-    (tuning "bwd_split": ways * 10000 + permille of the tiles; off by default,
-    measured slower, profiles/r02p_ab_bwd_split_*) against the oracle."""
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    try:
-        C.set_tuning("bwd_split", split)
-        test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
-    finally:
-        C.set_tuning("bwd_split", 0)
-
-
-@pytest.mark.parametrize("name,P,W,H,seed", CASES[1:3])
-def test_thread_contiguous_tile_scan_matches_oracle(name, P, W, H, seed):
-    """The thread-contiguous tile scan (tuning "scan_slices" 0; the default is
-    the wave-contiguous sliced scan every other test runs) against the oracle."""
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    try:
-        C.set_tuning("scan_slices", 0)
-        _forward_buffers_bit_exact(name, P, W, H, seed)
-    finally:
-        C.set_tuning("scan_slices", 1)
-
-
-@pytest.mark.parametrize("bucket_order", [0, 1])
-def test_bwd_launch_order_sources_match_oracle(bucket_order):
-    """The backward's heaviest-first tile order from the one-workgroup
-    counting sort (0) or from the 64 work buckets the forward render appends
-    its tiles to (1, the default: no order kernel) against the oracle; the
-    second-backward test reuses the buckets of one forward."""
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    try:
-        C.set_tuning("bucket_order", bucket_order)
-        test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
-        test_backward_parity("ragged_3k_250x130", 3000, 250, 130, 7, "colors_precomp")
-    finally:
-        C.set_tuning("bucket_order", 1)
 
 
 def test_autograd_dropin_matches_direct_call():
@@ -654,31 +523,26 @@ def _amr_gpu_steps(sc, cam, interpolate_last=False, bg=(0.0, 0.0, 0.0), after_st
     return acc, radii, steps, (gb, bb, ib)
 
 
-@pytest.mark.parametrize("amr_variant,amr_batch,amr_fold", [(4, 1, 0x1e), (4, 1, 0), (4, 2, 0), (3, 1, 0x1e),
-                                                            (2, 1, 0x1e)])
+@pytest.mark.parametrize("amr_variant", [4, 0])
 @pytest.mark.parametrize("name,P,W,H,seed", [("amr_10k_256", 10000, 256, 256, 0), ("amr_ragged", 4000, 200, 120, 3),
                                              # 66 x 33 = 2178 tiles > 2048: the radix-select percentile path
                                              ("amr_big_grid", 3000, 2112, 1056, 8),
                                              # dense: long sub-lists (several 32-entry batches per region)
                                              ("amr_dense", 60000, 160, 96, 4)])
-def test_amr_foveated_steps(name, P, W, H, seed, amr_variant, amr_batch, amr_fold):
-    """Every AMR blend variant (4: 8x8-region sub-lists + records, the
-    default; 3: 16x16 quadrant sub-lists; 2: full 32-px lists) against the
-    oracle: per-step images, and per pixel n_contrib / final T of the last
-    step that rendered it (the contributor indices of the sub-lists are the
-    positions in the tile list)."""
+def test_amr_foveated_steps(name, P, W, H, seed, amr_variant):
+    """Both AMR blends (4: 8x8-region sub-lists + records, the default; 0:
+    full 32-px lists, the fallback) against the oracle: per-step images, and
+    per pixel n_contrib / final T of the last step that rendered it (the
+    contributor indices of the sub-lists are the positions in the tile
+    list)."""
     import oracle as O
     import gaussian_splatting_with_eye_tracking_amd._C as C
     sc, cam = G.scene_and_camera(P, W, H, seed)
     C.set_tuning("amr_variant", amr_variant)
-    C.set_tuning("amr_batch", amr_batch)
-    C.set_tuning("amr_fold", amr_fold)
     try:
         acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.1, 0.1))
     finally:
         C.set_tuning("amr_variant", 4)
-        C.set_tuning("amr_batch", 1)
-        C.set_tuning("amr_fold", 0x1e)
     s = O.settings_from_camera(cam, bg=(0.1, 0.1, 0.1))
     kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
     racc, rradii, st, rsteps = O.amr_render_foveated(s, kw)
@@ -705,119 +569,60 @@ def test_amr_foveated_steps(name, P, W, H, seed, amr_variant, amr_batch, amr_fol
                                rtol=1e-5, atol=1e-7)
 
 
-@pytest.mark.parametrize("hist", [0, 1])
 @pytest.mark.parametrize("name,P,W,H,seed", [("amr_10k_256", 10000, 256, 256, 0), ("amr_big_grid", 3000, 2112, 1056, 8),
-                                             ("amr_dense", 60000, 160, 96, 4)])
-def test_amr_level_percentiles(name, P, W, H, seed, hist):
-    """The AMR percentiles and levels by the two-pass histogram select (1,
-    counts < 2^16) and by the sort / radix select (0) against the oracle."""
+                                             ("amr_dense", 60000, 160, 96, 4),
+                                             # tile counts >= 2^16: the LDS sort of the counts
+                                             ("amr_huge_counts", 150000, 64, 64, 6),
+                                             # ... on a grid > 2048 tiles: the radix select
+                                             ("amr_huge_counts_big_grid", 150000, 2112, 1056, 6)])
+def test_amr_level_percentiles(name, P, W, H, seed):
+    """The AMR percentiles and levels against the oracle: by the two-pass
+    histogram select (every tile count < 2^16), the LDS sort of the counts
+    and the radix select (a count >= 2^16 on grids of <= / > 2048 tiles)."""
     import oracle as O
     import gaussian_splatting_with_eye_tracking_amd._C as C
     sc, cam = G.scene_and_camera(P, W, H, seed)
-    C.set_tuning("amr_levels_hist", hist)
-    try:
-        acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.1, 0.1))
-    finally:
-        C.set_tuning("amr_levels_hist", 1)
+    if name.startswith("amr_huge_counts"):  # most Gaussians piled onto one spot
+        sc.means3D[: P - P // 8, :2] *= np.float32(1e-3)
+        sc.scales[: P - P // 8] = np.float32(0.003)
+    acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.1, 0.1))
     s = O.settings_from_camera(cam, bg=(0.1, 0.1, 0.1))
     kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
     _, _, st, _ = O.amr_render_foveated(s, kw)
     d = C.parse_buffers(gb, bb, ib, P, st.fwd.num_rendered, W, H, 32)
+    if name.startswith("amr_huge_counts"):
+        n = st.fwd.ranges[:, 1] - st.fwd.ranges[:, 0]
+        assert n.max() >= 1 << 16
     np.testing.assert_array_equal(d["pv"].cpu().numpy()[:3].astype(np.uint32), st.percentile_values)
     np.testing.assert_array_equal(d["levels"].cpu().numpy().astype(np.uint32), st.levels)
 
 
-@pytest.mark.parametrize("name,P,W,H,seed", [("amr_10k_256", 10000, 256, 256, 0), ("amr_ragged", 4000, 200, 130, 3),
-                                             ("amr_dense", 60000, 160, 96, 4)])
-def test_amr_staged_preprocess_records_bit_identical(name, P, W, H, seed):
-    """The preprocess's LDS-staged coalesced record stores (pp_dma 3: rgb,
-    the AMR blend rows) give the per-thread stores' frame bit for bit."""
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    sc, cam = G.scene_and_camera(P, W, H, seed)
-    out = {}
-    try:
-        for v in (1, 3):
-            C.set_tuning("pp_dma", v)
-            acc, radii, steps, _ = _amr_gpu_steps(sc, cam, bg=(0.1, 0.1, 0.1))
-            out[v] = (acc.cpu(), radii.cpu(), [x.cpu() for x in steps])
-    finally:
-        C.set_tuning("pp_dma", -1)
-    assert torch.equal(out[1][0], out[3][0])
-    assert torch.equal(out[1][1], out[3][1])
-    for a, b in zip(out[1][2], out[3][2]):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.parametrize("name,P,W,H,seed", [("amr_10k_256", 10000, 256, 256, 0), ("amr_ragged", 4000, 200, 120, 3)])
-def test_amr_forced_banded_duplicate(name, P, W, H, seed):
-    """The row-banded duplicate forced onto the AMR 32-px grid (dup_band 2;
-    by default AMR grids use the direct duplicate): point_list and ranges are
-    the oracle's bit for bit and the frame matches."""
-    import oracle as O
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    sc, cam = G.scene_and_camera(P, W, H, seed)
-    C.set_tuning("dup_band", 2)
-    try:
-        acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam)
-    finally:
-        C.set_tuning("dup_band", 1)
-    s = O.settings_from_camera(cam)
-    kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
-    racc, rradii, st, rsteps = O.amr_render_foveated(s, kw)
-    K = st.fwd.num_rendered
-    d = C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
-    np.testing.assert_array_equal(d["ranges"].cpu().numpy().astype(np.uint32), st.fwd.ranges)
-    np.testing.assert_array_equal(d["point_list"].cpu().numpy().astype(np.uint32), st.fwd.point_list)
-    assert G.image_l1(acc.cpu().numpy(), racc) < G.IMAGE_L1_TOL
-
-
-DEFAULT_AMR_LISTS_PER = 2  # render.hip g_amr_lists_per
-DEFAULT_AMR_SEL = 1  # render.hip g_amr_sel
-DEFAULT_AMR_LISTS_ORDER = 2  # render.hip g_amr_lists_order
-
-
 @pytest.mark.parametrize("P,W,H,seed", [(10000, 256, 256, 0), (60000, 160, 96, 4), (3000, 2112, 1056, 8)])
-def test_amr_fold_phases_bit_identical(P, W, H, seed):
-    """The steps' alpha-phase + fold-phase batches (amr_fold, the default) and
-    the 32-entry batches (amr_deep) evaluate the same operations on the same
-    operands as the one-entry loop: every step image, n_contrib and final T
-    are bit-identical."""
+def test_amr_variants_bit_identical(P, W, H, seed):
+    """The region sub-lists (default) and the full-list blocks (fallback)
+    evaluate the same operations on the same operands for every (pixel,
+    entry) pair the reference blends -- the sub-lists drop only entries whose
+    alpha < 1/255 at every pixel of the region: every step image, n_contrib
+    and final T are bit-identical."""
     import oracle as O
     import gaussian_splatting_with_eye_tracking_amd._C as C
     sc, cam = G.scene_and_camera(P, W, H, seed)
     out = {}
-    # (amr_fold, amr_deep, amr_lists_per: entries per thread and pass of the
-    # region-lists build -- the lists must not depend on it)
-    # (+ amr_sel: 1 the select-form fold, 2 its SGPR-mask form)
-    variants = {"loop": (0, 0, 4, 1), "fold": (0x1e, 0, 4, 1), "deep": (0x1e, 0x1e, 4, 1), "lists2": (0x1e, 0, 2, 1),
-                "lists5": (0x1e, 0, 5, 1), "lists8": (0x1e, 0, 8, 1), "mask": (0x1e, 0, 2, 2),
-                "order": (0x1e, 0, 2, 1, 0), "heavy": (0x1e, 0, 2, 1, 1)}
-    # (+ amr_lists_order: 0 the lists built in tile-index order instead of the
-    # XCD-compact strips, 1 in the steps' heaviest-first order)
-    for name, (fold, deep, lper, sel, *lord) in variants.items():
-        C.set_tuning("amr_fold", fold)
-        C.set_tuning("amr_deep", deep)
-        C.set_tuning("amr_lists_per", lper)
-        C.set_tuning("amr_sel", sel)
-        C.set_tuning("amr_lists_order", lord[0] if lord else DEFAULT_AMR_LISTS_ORDER)
+    for v in (4, 0):
+        C.set_tuning("amr_variant", v)
         try:
             acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.2, 0.3))
         finally:
-            C.set_tuning("amr_fold", 0x1e)
-            C.set_tuning("amr_deep", 0)
-            C.set_tuning("amr_lists_per", DEFAULT_AMR_LISTS_PER)
-            C.set_tuning("amr_sel", DEFAULT_AMR_SEL)
-            C.set_tuning("amr_lists_order", DEFAULT_AMR_LISTS_ORDER)
+            C.set_tuning("amr_variant", 4)
         d = C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)
         K = int(d["hdr"][0].item())
         d = C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
         # pixels some step rendered (the others are never written)
         lv = d["levels"].cpu().numpy().astype(np.uint32)
         rendered = torch.from_numpy((O.amr_pixel_rounds(W, H) <= O.amr_tile_levels_per_pixel(lv, W, H)).reshape(-1))
-        out[name] = [s_.cpu() for s_ in steps] + [d["n_contrib"].cpu()[rendered], d["accum_alpha"].cpu()[rendered]]
-    for name in ("fold", "deep", "lists2", "lists5", "lists8", "mask", "order", "heavy"):
-        for a, b in zip(out["loop"], out[name]):
-            assert torch.equal(a, b), name
+        out[v] = [s_.cpu() for s_ in steps] + [d["n_contrib"].cpu()[rendered], d["accum_alpha"].cpu()[rendered]]
+    for a_, b_ in zip(out[4], out[0]):
+        assert torch.equal(a_, b_)
 
 
 def test_amr_steps_with_nothing_in_front():
@@ -837,7 +642,7 @@ def test_amr_steps_with_nothing_in_front():
     np.testing.assert_allclose(acc.cpu().numpy(), racc, atol=1e-6)
 
 
-@pytest.mark.parametrize("amr_variant", [4, 3])
+@pytest.mark.parametrize("amr_variant", [4, 0])
 def test_amr_render_once_interpolated(amr_variant):
     import oracle as O
     import gaussian_splatting_with_eye_tracking_amd._C as C
@@ -856,36 +661,6 @@ def test_amr_render_once_interpolated(amr_variant):
     rcol, rrad, st = O.amr_render_once(os_, dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs,
                                                   scales=sc.scales, rotations=sc.rotations))
     assert G.image_l1(color.cpu().numpy(), rcol) < G.IMAGE_L1_TOL
-
-
-@pytest.mark.parametrize("P,W,H,seed", [(8000, 224, 160, 5), (60000, 160, 96, 4)])
-def test_amr_render_once_mask_select_bit_identical(P, W, H, seed):
-    """render_once (all rounds of a tile in one pass, kRounds 4) with the
-    SGPR-mask fold (amr_sel 2) against the select-form fold (amr_sel 1):
-    image, final T and n_contrib bit for bit."""
-    import oracle as O
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    from diff_gaussian_rasterization_amr import GaussianRasterizer
-    sc, cam = G.scene_and_camera(P, W, H, seed)
-    s = G.torch_settings(cam, amr=True)
-    t = G.scene_tensors(sc)
-    out = {}
-    for sel in (1, 2):
-        C.set_tuning("amr_sel", sel)
-        try:
-            color, radii, gb, bb, ib = GaussianRasterizer(s)(
-                means3D=t["means3D"], means2D=torch.zeros_like(t["means3D"]), opacities=t["opacities"],
-                shs=t["shs"], scales=t["scales"], rotations=t["rotations"], foveaStep=-2, interpolate_image=False)
-            torch.cuda.synchronize()
-        finally:
-            C.set_tuning("amr_sel", DEFAULT_AMR_SEL)
-        d = C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)
-        # pixels the call rendered (round <= level; the others are never written)
-        lv = d["levels"].cpu().numpy().astype(np.uint32)
-        rendered = torch.from_numpy((O.amr_pixel_rounds(W, H) <= O.amr_tile_levels_per_pixel(lv, W, H)).reshape(-1))
-        out[sel] = (color.cpu(), d["accum_alpha"].cpu()[rendered], d["n_contrib"].cpu()[rendered])
-    for a, b in zip(out[1], out[2]):
-        assert torch.equal(a, b)
 
 
 def test_amr_step4_interpolate():
@@ -1093,19 +868,20 @@ def test_dist_cuda2_bit_exact(P, seed):
 @pytest.mark.parametrize("how", ["sh_drgb_off", "fwd_no_grad_hint"])
 def test_backward_without_stored_sh_derivatives(how):
     """The SH backward from the coefficients (no stored d(rgb)/d(dir) rows):
-    tuning "sh_drgb" 0, or a forward told it needs no backward (the one-shot
-    "fwd_no_grad" hint the autograd wrappers give under no_grad) followed by a
-    backward anyway -- the header flag makes bwd_gauss re-read the SH rows."""
+    thread option "sh_drgb" 0, or a forward told it needs no backward (the
+    one-shot "fwd_no_grad" hint the autograd wrappers give under no_grad)
+    followed by a backward anyway -- the header flag makes bwd_gauss re-read
+    the SH rows."""
     import gaussian_splatting_with_eye_tracking_amd._C as C
     try:
         if how == "sh_drgb_off":
-            C.set_tuning("sh_drgb", 0)
+            C.set_thread_option("sh_drgb", 0)
         else:
-            C.set_tuning("fwd_no_grad", 1)
+            C.set_thread_option("fwd_no_grad", 1)
         test_backward_parity("cfg1_10k_256", 10000, 256, 256, 0, "sh")
     finally:
-        C.set_tuning("sh_drgb", 1)
-        C.set_tuning("fwd_no_grad", 0)
+        C.set_thread_option("sh_drgb", 1)
+        C.set_thread_option("fwd_no_grad", 0)
 
 
 def test_forward_only_hint_from_autograd_wrapper():

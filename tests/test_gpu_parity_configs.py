@@ -114,11 +114,11 @@ def test_edge_case_parity(name, D, M, mod, bg):
     P, W, H, seed = 8000, 200, 136, 21
     sc, cam = G.scene_and_camera(P, W, H, seed)
     shs = np.ascontiguousarray(sc.shs[:, :M, :])
-    C.set_tuning("store_cov3d", 1)  # the geometry buffer's cov3D is written on request only
+    C.set_thread_option("store_cov3d", 1)  # the geometry buffer's cov3D is written on request only
     try:
         s, t, out = _c_forward(sc, cam, bg=bg, sh_degree=D, scale_modifier=mod, shs=shs)
     finally:
-        C.set_tuning("store_cov3d", 0)
+        C.set_thread_option("store_cov3d", 0)
     os_ = O.settings_from_camera(cam, bg=bg, sh_degree=D, scale_modifier=mod)
     kw = dict(shs=shs, scales=sc.scales, rotations=sc.rotations)
     ref = O.forward(os_, sc.means3D, sc.opacities, **kw)

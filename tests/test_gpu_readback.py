@@ -31,7 +31,7 @@ def _forward(sc, cam):
     return int(K), color.cpu().numpy(), radii.cpu().numpy()
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [2])
 def test_readback_modes_match_copy(mode):
     import gaussian_splatting_with_eye_tracking_amd._C as C
     scenes = [G.scene_and_camera(P, W, H, seed) for P, W, H, seed in

@@ -69,20 +69,6 @@ def main():
             flops += 2 * w.numel() * px
     from gaussian_splatting_with_eye_tracking_amd import _C
 
-    def timed(key, value, n=10):
-        _C.set_tuning(key, value)
-        for _ in range(2):
-            net(x)
-        torch.cuda.synchronize()
-        a.record()
-        for _ in range(n):
-            net(x)
-        b.record()
-        torch.cuda.synchronize()
-        return a.elapsed_time(b) / n
-
-    rows2_ms = timed("ritnet_small_wgs", 0)
-    _C.set_tuning("ritnet_small_wgs", 512)
     _C.set_tuning("ritnet_mfma", 0)
     for _ in range(2):
         net(x)
@@ -96,7 +82,6 @@ def main():
     _C.set_tuning("ritnet_mfma", 1)
     print(json.dumps({"metric": "RITnet eye frames/s (640x400, fp32)", "ritnet_ms": round(net_ms, 4),
                       "ritnet_ms_vector_fma_kernel": round(fma_ms, 4),
-                      "ritnet_ms_two_rows_per_wave_everywhere": round(rows2_ms, 4),
                       "frames_per_s": round(1e3 / net_ms, 1), "gflop_per_frame": round(flops / 1e9, 2),
                       "achieved_tflops": round(flops / (net_ms * 1e-3) / 1e12, 2),
                       "track_ms": round(track_ms, 3), "device_preprocess_ms": round(pre_dev_ms, 4),
