@@ -29,6 +29,8 @@
 #include <algorithm>
 #include <type_traits>
 
+#include <hip/hip_ext.h>
+
 #include "gs_blend.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
@@ -45,7 +47,7 @@ constexpr int kPPL = 4;      // pixels per lane: one wave64 covers the 16x16 til
 // and the flush fused into the staging reduce (below).  !kSel (the fallback,
 // and the AMR backward): the predicate form, full sums by transposition into
 // LDS rows, one 64-B atomic row per (tile, Gaussian) at the end of each batch.
-template <bool kSel, bool kAMR = false>
+template <bool kSel, bool kAMR = false, bool kOpT = false>
 __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
     int W, int H, const uint32_t* __restrict__ ranges, const uint32_t* __restrict__ max_contrib,
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
@@ -264,7 +266,8 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
             s_co[tid] = pc;
             s_b[tid].x = nrgb[2];
             if constexpr (kSel)  // the reference's `power > 0` skip cannot fire (gs_blend.cuh)
-                fastg = splat_form_safe(pc, fabsf(xy.x - (float)ox), fabsf(xy.y - (float)oy));
+                fastg = splat_form_safe(pc, fabsf(xy.x - (float)ox), fabsf(xy.y - (float)oy)) &&
+                        (!kOpT || (pc.w <= 0.99f && pc.w > 0.0f));
             gm = use_codes ? (uint32_t)hit_codes[range.x + top - 1 - tid]
                  : cull ? splat_group_mask(xy, co, (float)ox, (float)oy, (float)pstride) : 0xfu;
         }
@@ -284,7 +287,11 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
         // 4 and 5 -- sum t dx, sum t dy -- fetched by two lane shuffles) and
         // adds them into grad_accum: no accumulator rows in LDS, no per-batch
         // flush pass, one atomic instruction per 7 Gaussians
-        auto stage_reduce = [&](const int nslot) {
+        // kOpT runs of fast entries sum t' = alpha T dL_dalpha / G = o t (below):
+        // the flush takes o out of the mean / conic factors and divides the
+        // opacity sum by it
+        auto stage_reduce = [&](const int nslot, auto kOT) {
+            constexpr bool kOT_ = decltype(kOT)::value;
             if (nslot == kStageSlots || lane < 9 * nslot) {
                 const float* src = &s_stage[4 * lane];
                 const float4 a = *reinterpret_cast<const float4*>(src);
@@ -304,12 +311,13 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
                     const int fq = st_q < 3 ? st_q : st_q == 3 ? 8 : st_q - 1;
                     const float qa = (fq == 3 || fq == 4) ? g4 : tot;
                     const float4 pc = s_co[jj];
-                    const float o = pc.w;
+                    const float o = kOT_ ? 1.0f : pc.w;
                     const float cx = pc.x * (-1.0f / kHalfLog2e), cy = pc.y * (-1.0f / kLog2e),
                                 cz = pc.z * (-1.0f / kHalfLog2e);
                     const float ka = fq == 3 ? -o * cx * ddelx_dx
                                    : fq == 4 ? -o * cy * ddely_dy
-                                   : (fq >= 5 && fq <= 7) ? -0.5f * o : 1.0f;
+                                   : (fq >= 5 && fq <= 7) ? -0.5f * o
+                                   : (kOT_ && fq == 8) ? 1.0f / pc.w : 1.0f;
                     const float kb = fq == 3 ? -o * cy * ddelx_dx : fq == 4 ? -o * cz * ddely_dy : 0.0f;
                     const float v = ka * qa + kb * sy;
                     if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[par][jj] * kGradRow + fq], v);
@@ -377,8 +385,14 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
                     uint64_t msk = __builtin_amdgcn_fcmpf(ar, 1.0f / 255.0f, kFcmpUGE);
                     if (!kFast || !kStarted) msk &= __builtin_amdgcn_uicmp(contributor, last[k], kIcmpULT);
                     if (!kFast) msk &= __builtin_amdgcn_fcmpf(p2, 0.0f, kFcmpULE);
+                    // kOpT and a fast entry (o <= 0.99, p2 <= 0: alpha = o G
+                    // unclamped, bit for bit the rounded product): t' = o t =
+                    // alpha T (c - acc) = dchannel_dcolor diff -- no G select,
+                    // one product fewer; the flush divides o back out
+                    constexpr bool kOT = kOpT && kFast;
                     float G, alpha;
-                    gs_sel2_zero_v(msk, Gr, ar, G, alpha);
+                    if constexpr (kOT) alpha = gs_sel_zero_v(msk, ar);
+                    else gs_sel2_zero_v(msk, Gr, ar, G, alpha);
                     const float rinv = __builtin_amdgcn_rcpf(1.f - alpha);
                     T[k] = T[k] * rinv;
                     const float dchannel_dcolor = alpha * T[k];
@@ -386,12 +400,11 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
                     const float diff = __builtin_fmaf(cf.z, dpx[k][2],
                                                       __builtin_fmaf(cf.y, dpx[k][1],
                                                                      __builtin_fmaf(cf.x, dpx[k][0], -acc_dot[k])));
-                    const float dL_dalpha = diff * T[k];
                     acc_dot[k] = __builtin_fmaf(alpha, diff, acc_dot[k]);
                     c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
                     c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
                     c2 = __builtin_fmaf(dchannel_dcolor, dpx[k][2], c2);
-                    const float t = G * dL_dalpha;
+                    const float t = kOT ? dchannel_dcolor * diff : G * (diff * T[k]);
                     const float tdy = t * dy;
                     s0 += t;
                     s1 += tdy;
@@ -500,18 +513,19 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
                     one(std::integral_constant<int, 5>{});
                     one(std::integral_constant<int, 6>{});
                     if (nst == kStageSlots) {
-                        stage_reduce(kStageSlots);
+                        stage_reduce(kStageSlots, std::integral_constant<bool, kOpT && decltype(kFastT)::value>{});
                         nst = 0;
                         js = 0ull;
                     }
                 }
+                if (nst) stage_reduce(nst, std::integral_constant<bool, kOpT && decltype(kFastT)::value>{});
+                nst = 0;
             };
             // every entry this wave visits has a provably negative-definite form
             const bool bsafe = (todo & ~fast_mask) == 0ull;
             if (bsafe && bstarted) run(T1{}, T1{});
             else if (bsafe) run(T1{}, T0{});
             else run(T0{}, T0{});
-            if (nst) stage_reduce(nst);
         } else {
             while (todo) {
                 const int j = __builtin_ctzll(todo);
@@ -574,7 +588,7 @@ extern int g_cull;  // render.hip
 // plain-store / no-flush timing diagnostics.
 constexpr int kDefaultBwdVariant = 1;
 int g_bwd_variant = kDefaultBwdVariant;
-void set_backward_variant(int v) { g_bwd_variant = v == 0 ? 0 : kDefaultBwdVariant; }
+void set_backward_variant(int v) { g_bwd_variant = (v == 0 || v == 2) ? v : kDefaultBwdVariant; }
 
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s, int K) {
@@ -583,13 +597,17 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
     if (gx == 0 || gy == 0) return;
     // tiles heaviest first: the forward render filled this image buffer's 256
     // work buckets (the kernel falls back to the identity order otherwise)
-#define GS_BWD_LAUNCH(SEL)                                                                                         \
-    hipLaunchKernelGGL((render_bwd_kernel<SEL>), dim3(gx * gy), dim3(64), 0, s, W, H, img.ranges, img.max_contrib, \
+    // (the profiler's stage events, if any, ride on the dispatch itself)
+    const DispatchEvents ev = take_dispatch_events();
+#define GS_BWD_LAUNCH(...)                                                                                         \
+    hipExtLaunchKernelGGL((render_bwd_kernel<__VA_ARGS__>), dim3(gx * gy), dim3(64), 0, s, ev.start, ev.stop, 0, W, H,     \
+                       img.ranges, img.max_contrib,                                                                \
                        b.point_list, reinterpret_cast<const float2*>(g.means2D),                                   \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,    \
                        dL_dpix, bg, g.grad_accum, g_cull, gx, 0, nullptr, img.bucket_count, img.bucket_list,       \
                        hit_codes_at(b.point_list, hit_codes_k), g.hdr)
     if (g_bwd_variant == 0) GS_BWD_LAUNCH(false);
+    else if (g_bwd_variant == 2) GS_BWD_LAUNCH(true, false, true);
     else GS_BWD_LAUNCH(true);
 #undef GS_BWD_LAUNCH
 }

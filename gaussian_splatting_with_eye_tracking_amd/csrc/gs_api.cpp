@@ -89,16 +89,36 @@ struct Profiler {
 Profiler g_prof;
 std::mutex g_prof_mu;
 
+// on_dispatch (single-kernel stages whose launcher takes the pair with
+// take_dispatch_events): the events are recorded by the kernel's own dispatch
+// (hipExtLaunchKernelGGL start / stop events) instead of two marker packets
+// around it -- the markers cost ~6 us of idle queue each around a timed
+// kernel (profiles/r05a_gaptrace: 5.9 + 6.1 us per step around render_bwd).
+thread_local DispatchEvents t_dispatch;
+
 struct StageTimer {
-    int stage; hipStream_t s; hipEvent_t a = nullptr, b = nullptr;
-    StageTimer(int st, hipStream_t str) : stage(st), s(str) {
+    int stage; hipStream_t s; hipEvent_t a = nullptr, b = nullptr; bool on_dispatch;
+    StageTimer(int st, hipStream_t str, bool dispatch = false) : stage(st), s(str), on_dispatch(dispatch) {
         if (!g_prof.on || !((g_prof.mask >> st) & 1u)) return;
         std::lock_guard<std::mutex> l(g_prof_mu);
         a = g_prof.get(); b = g_prof.get();
-        hipEventRecord(a, s);
+        if (on_dispatch) t_dispatch = DispatchEvents{a, b};
+        else hipEventRecord(a, s);
     }
     ~StageTimer() {
         if (!a) return;
+        if (on_dispatch) {
+            const bool taken = t_dispatch.start == nullptr;  // (the launcher cleared it)
+            t_dispatch = DispatchEvents{};
+            std::lock_guard<std::mutex> l(g_prof_mu);
+            if (taken) {
+                g_prof.pending.push_back({stage, a, b});
+            } else {  // no kernel was launched: nothing to time
+                g_prof.pool.push_back(a);
+                g_prof.pool.push_back(b);
+            }
+            return;
+        }
         hipEventRecord(b, s);
         std::lock_guard<std::mutex> l(g_prof_mu);
         g_prof.pending.push_back({stage, a, b});
@@ -521,6 +541,12 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
 
 }  // namespace
 
+DispatchEvents gsamd::take_dispatch_events() {
+    const DispatchEvents e = t_dispatch;
+    t_dispatch = DispatchEvents{};
+    return e;
+}
+
 extern "C" {
 
 int gs_abi_version(void) { return GSPLAT_AMD_ABI_VERSION; }
@@ -549,7 +575,7 @@ int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image
         const float* feats = colors_precomp ? colors_precomp : r.g.rgb;
         bool zeroed;
         {
-            StageTimer _t(kRender, s);
+            StageTimer _t(kRender, s, true);
             // the accumulator rows are zeroed behind the blend only when a
             // backward can follow (not under the forward-only hint: a later
             // backward of this forward then zeroes them itself)
@@ -592,7 +618,7 @@ int rasterizer_backward_impl(int amr_mode, int P, int D, int M, int R, const flo
         zero_accum_unless_clean(g, P, s);
         const float* colors = colors_precomp ? colors_precomp : g.rgb;
         if (R > 0) {
-            StageTimer _t(kRenderBwd, s);
+            StageTimer _t(kRenderBwd, s, amr_mode == 0);
             if (amr_mode != 0) launch_amr_render_backward(width, height, amr_mode, img, b, g, colors, background, dL_dpix, s);
             else launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s, R);
         }
@@ -705,7 +731,7 @@ int gs_rasterizer_backward_view_grads(int P, int R, const float* background, int
         if (!radii) radii = g.radii;
         zero_accum_unless_clean(g, P, s);
         const float* colors = colors_precomp ? colors_precomp : g.rgb;
-        if (R > 0 && P > 0) { StageTimer _t(kRenderBwd, s); launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s, R); }
+        if (R > 0 && P > 0) { StageTimer _t(kRenderBwd, s, true); launch_render_backward(width, height, img, b, g, colors, background, dL_dpix, s, R); }
         stage_check(debug != 0, s, "render_backward");
         launch_pack_view_grads(P, g, radii, colors_precomp == nullptr, viewmatrix, projmatrix, campos, width, height,
                                tan_fovx, tan_fovy, out_record, s);

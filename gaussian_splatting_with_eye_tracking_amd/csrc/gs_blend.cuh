@@ -69,6 +69,12 @@ __device__ __forceinline__ float splat_exp(float p2) { return __builtin_amdgcn_e
 // the compiler's selects)
 constexpr int kFcmpUGE = 11, kFcmpULE = 13, kIcmpULT = 36;
 
+// m ? x : 0
+__device__ __forceinline__ float gs_sel_zero_v(uint64_t m, float x) {
+    float r;
+    asm("s_nop 1\n\tv_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(x), "s"(m));
+    return r;
+}
 // (m ? x : 0, m ? y : 0)
 __device__ __forceinline__ void gs_sel2_zero_v(uint64_t m, float x, float y, float& rx, float& ry) {
     asm("s_nop 1\n\t"

@@ -10,6 +10,15 @@
 
 namespace gsamd {
 
+// Stage-timing events a single-kernel launcher attaches to its dispatch
+// (hipExtLaunchKernelGGL) when the profiler times that stage (gs_api.cpp
+// StageTimer on_dispatch); {nullptr, nullptr} otherwise.  Taking them clears
+// the thread's pending pair.
+struct DispatchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+DispatchEvents take_dispatch_events();
+
 struct PreprocessArgs {
     int P, D, M;
     const float* means3D;

@@ -12,6 +12,8 @@
 // and T<1e-4 tests) are the reference's; the forward additionally records the
 // per-tile maximum n_contrib so the backward can skip the tail of a range no
 // pixel of the tile consumed.
+#include <hip/hip_ext.h>
+
 #include "gs_blend.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
@@ -139,9 +141,11 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
     // (Heaviest-first by range length measured slower here -- early
     // termination makes the range a poor work estimate; the backward orders
     // by max_contrib instead, backward.hip.)
+    // (the profiler's stage events, if any, ride on the dispatch itself)
+    const DispatchEvents ev = take_dispatch_events();
 #define GS_FWD_LAUNCH(PPL, WAVES, ...)                                                                           \
-    hipLaunchKernelGGL((render_fwd_kernel<PPL, WAVES, ##__VA_ARGS__>), dim3(gx * gy), dim3(64 * WAVES), 0, s, W, H, \
-                       img.ranges, \
+    hipExtLaunchKernelGGL((render_fwd_kernel<PPL, WAVES, ##__VA_ARGS__>), dim3(gx * gy), dim3(64 * WAVES), 0, s,  \
+                       ev.start, ev.stop, 0, W, H, img.ranges,                                                   \
                        b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
                        img.max_contrib, bg, out_color, g_cull, gx, zero4, zero_n4,                               \

@@ -157,15 +157,16 @@ def test_default_backward_matches_fallback(P, W, H, seed, fwd):
     dpix = torch.from_numpy(S.make_cotangent(H, W, seed + 1)).cuda()
     res = {}
     try:
-        for v in (0, 1):
+        for v in (0, 1, 2):
             s, t, out, _bufs = _forward(sc, cam, fwd)
             res[v] = _backward(s, t, out, dpix, v)
     finally:
         C.set_tuning("fwd_variant", -1)
         C.set_tuning("bwd_variant", -1)
-    for i in range(3):  # dL_dmeans2D, dL_dcolors, dL_dopacity
-        assert G.rel_err(res[1][0][i], res[0][0][i]) < 5e-6, i
-    assert G.rel_err(res[1][1], res[0][1]) < 5e-6
+    for v in (1, 2):
+        for i in range(3):  # dL_dmeans2D, dL_dcolors, dL_dopacity
+            assert G.rel_err(res[v][0][i], res[0][0][i]) < 5e-6, (v, i)
+        assert G.rel_err(res[v][1], res[0][1]) < 5e-6, v
 
 
 @pytest.mark.parametrize("P,W,H,seed,adv", [(6000, 256, 192, 1, True), (30000, 320, 200, 2, True),

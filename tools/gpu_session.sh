@@ -28,6 +28,9 @@ for step in "$@"; do
     probe) run probe 60 bash -c 'echo "cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>&1)"; echo "cfs: $(cat /sys/fs/cgroup/cpu/cpu.cfs_quota_us 2>&1) / $(cat /sys/fs/cgroup/cpu/cpu.cfs_period_us 2>&1)"; echo "nproc $(nproc) OMP_NUM_THREADS=${OMP_NUM_THREADS:-unset}"; python3 -c "import bench; print(bench.cpu_share())"' ;;
     gaptrace) run gaptrace 600 rocprofv3 --kernel-trace -d "$O/gaptrace" -o run --output-format csv -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sub ;;
     benchns) run bench_ns 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-sub ;;
+    ab) run "ab_${AB_NAME:-x}" 600 python tools/ab_tuning.py $AB_ARGS ;;
+    ab2) run "ab_${AB_NAME:-x}_2" 600 python tools/ab_tuning.py $AB_ARGS2 ;;
+    pytestk) run "pytest_${PT_NAME:-k}" 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf -k "$PT_K" ;;
     tests) run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     configs) run pytest_configs 1100 python -u -m pytest tests/test_gpu_parity_configs.py tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf ;;
     amrtests) run pytest_amr 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_parity_configs.py tests/test_gpu_cull.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf -k "amr or config3 or cull" ;;
