@@ -1538,12 +1538,203 @@ __global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a
     }
 }
 
+// The same sums in one pass over the views with each view's rows staged
+// through LDS: the workgroup's 256 rows of view v (10 KB, contiguous in the
+// record) are read with 8-B loads by consecutive lanes -- five load
+// instructions per thread per view instead of ten per-thread loads at a 40-B
+// stride in each of three passes (the any-check and the two passes above,
+// each touching ~20 cache lines per wave instruction) -- the next view's
+// rows in flight in registers while this view's terms are formed.  Per view
+// the cov2D / projection terms and the SH terms are formed as in the
+// two-pass kernel and accumulated in the same order into the same separate
+// sums (dmean_t, ddir, dsh_t, dcov_t, ...): bit-identical results.
+constexpr int kMvRowF2 = 256 * kViewRow / 2;     // float2 per view per workgroup (1280)
+constexpr int kMvRowPer = (kMvRowF2 + 255) / 256;  // per thread (5)
+template <bool kHasSH, bool kSH16>
+__global__ void __launch_bounds__(256) multiview_backward1_kernel(MultiViewArgs a) {
+    constexpr bool kStage = kHasSH && kSH16;
+    __shared__ float s_sh[kStage ? 256 * kShRow : 1];
+    __shared__ __attribute__((aligned(16))) float s_rows[256 * kViewRow];
+    const int local0 = blockIdx.x * 256;
+    const int nblk = min(256, a.count - local0);
+    if constexpr (kStage) {
+        const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)(a.g0 + local0) * 12;
+        if (nblk == 256) {
+            float4 v[12];
+#pragma unroll
+            for (int k = 0; k < 12; k++) v[k] = in[threadIdx.x + 256 * k];
+#pragma unroll
+            for (int k = 0; k < 12; k++) {
+                const int f = threadIdx.x + 256 * k;
+                float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
+                r[0] = v[k].x; r[1] = v[k].y; r[2] = v[k].z; r[3] = v[k].w;
+            }
+        } else {
+            for (int f = threadIdx.x; f < nblk * 12; f += 256) {
+                const float4 v = in[f];
+                float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
+                r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
+            }
+        }
+    }
+    const int local = local0 + threadIdx.x;
+    const bool live = local < a.count;
+    const int idx = a.g0 + local;
+    float* lrow = kStage ? s_sh + threadIdx.x * kShRow : nullptr;
+    const int nf2 = nblk * (kViewRow / 2);  // this block's float2 per view
+    // view v's rows of this block: a.rows[v] points at Gaussian g0's row
+    auto load_rows = [&](int v, float2 (&r)[kMvRowPer]) {
+        const float2* src = reinterpret_cast<const float2*>(mv_row(a, v) + (size_t)local0 * kViewRow);
+#pragma unroll
+        for (int i = 0; i < kMvRowPer; i++) {
+            const int f = threadIdx.x + 256 * i;
+            r[i] = f < nf2 ? src[f] : make_float2(0.f, 0.f);
+        }
+    };
+    float mx = 0.f, my = 0.f, mz = 0.f;
+    float4 qrot = make_float4(0.f, 0.f, 0.f, 0.f);
+    float scl[3] = {0.f, 0.f, 0.f}, cov3D[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float st_acc = 0.f, st_den = 0.f, st_max = 0.f;
+    const bool stats = a.grad_norm_accum != nullptr;
+    if (live) {
+        mx = a.means3D[3 * idx];
+        my = a.means3D[3 * idx + 1];
+        mz = a.means3D[3 * idx + 2];
+        qrot = reinterpret_cast<const float4*>(a.rotations)[idx];
+        scl[0] = a.scales[3 * idx + 0];
+        scl[1] = a.scales[3 * idx + 1];
+        scl[2] = a.scales[3 * idx + 2];
+        if (stats) {
+            st_acc = a.grad_norm_accum[idx];
+            st_den = a.denom[idx];
+            st_max = a.max_radii[idx];
+        }
+    }
+    compute_cov3d(scl, qrot, a.scale_modifier, cov3D);
+    const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
+    float dmean_t[3] = {0.f, 0.f, 0.f}, ddir[3] = {0.f, 0.f, 0.f};
+    float dcov_t[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dop = 0.f;
+    float dsh_t[kHasSH ? 48 : 1];
+#pragma unroll
+    for (int i = 0; i < (kHasSH ? 48 : 1); i++) dsh_t[i] = 0.f;
+    float s_reg[kHasSH && !kStage ? 16 : 1][3];
+    if constexpr (kHasSH && !kStage) {
+        const float* sh = a.shs + (size_t)(live ? idx : a.g0) * a.M * 3;
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) s_reg[k][c] = (live && k < ncoef) ? sh[3 * k + c] : 0.f;
+    }
+    bool any = false;
+    float2 nxt[kMvRowPer];
+    load_rows(0, nxt);
+    for (int v = 0; v < a.V; v++) {
+        __syncthreads();  // the previous view's rows are read (and, at v = 0, the SH rows staged)
+        float2* srow = reinterpret_cast<float2*>(s_rows);
+#pragma unroll
+        for (int i = 0; i < kMvRowPer; i++) {
+            const int f = threadIdx.x + 256 * i;
+            if (f < kMvRowF2) srow[f] = nxt[i];
+        }
+        __syncthreads();
+        if (v + 1 < a.V) load_rows(v + 1, nxt);  // in flight while view v's terms are formed
+        const float* row = s_rows + threadIdx.x * kViewRow;
+        const uint32_t w9 = __float_as_uint(row[9]);
+        if (!live || w9 == 0u) continue;  // not visible in view v: no terms (the reference's radii > 0 filter)
+        any = true;
+        const float acc[3] = {row[0], row[1], row[2]};
+        const float gx = row[3], gy = row[4], dcx = row[5], dcy = row[6], dcw = row[7], dop_v = row[8];
+        const float* cam = mv_cam(a, v);
+        const Mat4 V = load_mat4(cam);
+        const Mat4 Pm = load_mat4(cam + 16);
+        const float tan_fovx = cam[37], tan_fovy = cam[38];
+        // rasterizer_impl.cu:222-223 / gs_api.cpp: focal from the image size
+        const float focal_x = cam[35] / (2.0f * tan_fovx);
+        const float focal_y = cam[36] / (2.0f * tan_fovy);
+        float dmean[3], dcov[6];
+        cov2d_backward(mx, my, mz, cov3D, dcx, dcy, dcw, V, focal_x, focal_y, tan_fovx, tan_fovy, dmean, dcov);
+        proj_backward(mx, my, mz, Pm, gx, gy, dmean);
+#pragma unroll
+        for (int i = 0; i < 3; i++) dmean_t[i] += dmean[i];
+#pragma unroll
+        for (int i = 0; i < 6; i++) dcov_t[i] += dcov[i];
+        dop += dop_v;
+        if (stats) {
+            st_acc = st_acc + sqrtf(gx * gx + gy * gy);
+            st_den = st_den + 1.f;
+            st_max = fmaxf(st_max, (float)(w9 & 0xFFFFFFu));
+        }
+        if constexpr (kHasSH) {
+            const uint8_t cb = (uint8_t)(w9 >> 24);
+            float dsh_c[16], dRGB[3];
+            if constexpr (kStage) {
+                sh_backward_terms(a.D, cam + 32, mx, my, mz, ShRowPtr{lrow}, cb, acc, dsh_c, dRGB, ddir);
+            } else {
+                sh_backward_terms(a.D, cam + 32, mx, my, mz, s_reg, cb, acc, dsh_c, dRGB, ddir);
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+#pragma unroll
+                for (int c = 0; c < 3; c++)
+                    if (k < ncoef) dsh_t[3 * k + c] += dsh_c[k] * dRGB[c];
+        }
+    }
+    if (live) {
+        // (a Gaussian no view sees: every output is zero, as the two-pass kernel writes)
+        a.dL_dopacity[idx] = any ? dop : 0.f;
+        float dscale[3] = {0.f, 0.f, 0.f};
+        float4 dq = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (any) cov3d_backward(qrot, scl, a.scale_modifier, dcov_t, dscale, dq);
+#pragma unroll
+        for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = dscale[i];
+        reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
+        if (stats && any) {
+            a.grad_norm_accum[idx] = st_acc;
+            a.denom[idx] = st_den;
+            a.max_radii[idx] = st_max;
+        }
+#pragma unroll
+        for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = any ? dmean_t[i] + ddir[i] : 0.f;
+    }
+    if constexpr (kStage) {
+        __syncthreads();  // every thread has read its SH row: the area takes the gradient rows
+        if (live) {
+#pragma unroll
+            for (int i = 0; i < 48; i++) lrow[i] = any ? dsh_t[i] : 0.f;
+        }
+        __syncthreads();
+        float4* out = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)(a.g0 + local0) * 12;
+        for (int f = threadIdx.x; f < nblk * 12; f += 256) {
+            const float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
+            store_out4(&out[f], make_float4(r[0], r[1], r[2], r[3]), a.nt != 0);
+        }
+    } else if constexpr (kHasSH) {
+        if (live)
+            for (int k = 0; k < a.M; k++)
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    float val = 0.f;
+#pragma unroll
+                    for (int kk = 0; kk < 16; kk++) val = (kk == k && any) ? dsh_t[3 * kk + c] : val;
+                    a.dL_dsh[(size_t)idx * a.M * 3 + 3 * k + c] = val;
+                }
+    }
+}
+
+int g_mv_variant = 1;  // set_tuning("mv_variant") (A/B): 1 the one-pass staged kernel, 0 the two-pass kernel
+
 void launch_multiview_backward(const MultiViewArgs& args, hipStream_t s) {
     if (args.count <= 0) return;
     MultiViewArgs a = args;
     a.nt = 1;  // the dL_dsh rows non-temporal (as backward_gaussians_kernel's)
     const dim3 grid((a.count + 255) / 256);
     const bool sh = a.shs != nullptr;
+    if (g_mv_variant) {
+        if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward1_kernel<true, true>), grid, dim3(256), 0, s, a);
+        else if (sh) hipLaunchKernelGGL((multiview_backward1_kernel<true, false>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((multiview_backward1_kernel<false, false>), grid, dim3(256), 0, s, a);
+        return;
+    }
     if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward_kernel<true, true>), grid, dim3(256), 0, s, a);
     else if (sh) hipLaunchKernelGGL((multiview_backward_kernel<true, false>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((multiview_backward_kernel<false, false>), grid, dim3(256), 0, s, a);

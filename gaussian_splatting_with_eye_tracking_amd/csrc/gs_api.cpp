@@ -33,6 +33,7 @@
 #include "gs_layout.h"
 
 using namespace gsamd;
+namespace gsamd { extern int g_mv_variant; }
 
 namespace {
 
@@ -251,7 +252,7 @@ void finish_header_read(uint32_t out[4], const uint32_t* mirror = nullptr, hipSt
 // backward has consumed yet (keyed by the rows' address): the first backward
 // after such a forward skips its memset, any other zeroes the rows itself --
 // a second backward of one forward (retain_graph), an AMR geometry buffer
-// (its rows hold blend records), a forward that could not fuse the zeroing.
+// (the AMR forward does not zero them), a forward that could not fuse the zeroing.
 std::mutex g_clean_mu;
 std::unordered_set<const float*> g_accum_clean;
 
@@ -465,7 +466,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     const size_t N = (size_t)W * H;
     // the optional tail (gs_layout.h) only when this forward writes into it
     const bool tail = t_store_cov3d || (in.colors_precomp == nullptr && t_sh_drgb && t_store_drgb);
-    char* gbase = call_resize(geometry, carve_geom(nullptr, in.P, nullptr, tail), "geometry");
+    char* gbase = call_resize(geometry, carve_geom(nullptr, in.P, nullptr, tail, tile == 32), "geometry");
     carve_geom(gbase, in.P, &r.g);
     set_accum_clean(r.g.grad_accum, false);  // this forward decides afresh
     char* ibase = call_resize(image, carve_image(nullptr, N, r.T, nullptr, tile), "image");
@@ -1223,6 +1224,10 @@ int gs_set_tuning(const char* key, int value) {
         g_spec_dup = value;
         return 0;
     }
+    if (std::strcmp(key, "mv_variant") == 0) {  // (A/B, temporary)
+        g_mv_variant = value;
+        return 0;
+    }
     if (std::strcmp(key, "ritnet_mfma") == 0) {  // 0: the SGPR-weight FMA convolution; 1: matrix cores (default)
         set_ritnet_mfma(value);
         return 0;
@@ -1281,6 +1286,8 @@ void gs_profile_read(double* total_ms, long* counts, int reset) {
 }
 
 size_t gs_geom_bytes(int P) { return carve_geom(nullptr, (size_t)P, nullptr); }
+
+size_t gs_amr_geom_bytes(int P) { return carve_geom(nullptr, (size_t)P, nullptr, true, true); }
 
 size_t gs_image_bytes(int width, int height, int tile) {
     const size_t T = (size_t)((width + tile - 1) / tile) * ((height + tile - 1) / tile);

@@ -68,6 +68,7 @@ struct GeomView {
     float* drgb;           // [P][12] d(rgb)/d(dir): (x, y, z) x (r, g, b) + 3 pad, SH colours, visible Gaussians
     uint32_t* tiles_touched;
     float* grad_accum;  // [P][kGradRow]
+    float* amr_rows;    // [P][16] AMR buffers only: the AMR forward's per-Gaussian blend row (below)
 };
 
 // base is 256-B aligned by the caller (torch allocations are).
@@ -77,7 +78,13 @@ struct GeomView {
 // neither sizes its buffer without it (tail = false: 72 B per Gaussian less,
 // ~440 MB at 6.1M Gaussians); the pointers are carved either way and read
 // only when the header / the request says they were written.
-inline size_t carve_geom(char* base, size_t P, GeomView* v, bool tail = true) {
+// AMR buffers (amr: 32-px tiles) always carry the tail and then amr_rows: one
+// 64-B row per Gaussian -- (x, y, r, g), the log2(e)-scaled conic + opacity,
+// (b, raw conic) and a zero pad -- which the AMR preprocess writes and
+// foveaStep 0's region-list pass gathers, one aligned 64-B sector per
+// instance (48-B rows straddled two sectors in most rows: 286 MB of traffic
+// per launch for ~106 MB of rows at config 3, profiles/r04zf_cfg3_pmc_summary.json).
+inline size_t carve_geom(char* base, size_t P, GeomView* v, bool tail = true, bool amr = false) {
     size_t off = 0;
     GeomView g;
     g.hdr = carve<uint32_t>(base, off, kHdrWords);
@@ -92,8 +99,10 @@ inline size_t carve_geom(char* base, size_t P, GeomView* v, bool tail = true) {
     const size_t head = align_up(off);
     g.drgb = carve<float>(base, off, 12 * P);
     g.cov3D = carve<float>(base, off, 6 * P);
+    const size_t full = align_up(off);
+    g.amr_rows = carve<float>(base, off, 16 * P);
     if (v) *v = g;
-    return tail ? align_up(off) : head;
+    return amr ? align_up(off) : tail ? full : head;
 }
 
 struct ImageView {

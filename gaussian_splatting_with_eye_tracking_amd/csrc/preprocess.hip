@@ -212,10 +212,10 @@ __device__ __forceinline__ void pp_gaussian(const PreprocessArgs& a, const GeomV
     reinterpret_cast<float4*>(g.conic_opacity)[idx] = make_float4(conic_x, conic_y, conic_z, opacity);
     g.tiles_touched[idx] = area;
     if (a.block == 32) {
-        // AMR: the blend record of this Gaussian as ONE 48-B row of the
-        // (forward-idle) grad_accum buffer, so foveaStep 0's region-list pass
-        // (render.hip) gathers one line per instance instead of three:
-        // (x, y, r, g), the log2(e)-scaled conic + opacity, (b, raw conic).
+        // AMR: the blend record of this Gaussian as ONE 64-B row (GeomView::
+        // amr_rows), so foveaStep 0's region-list pass (render.hip) gathers one
+        // aligned sector per instance instead of three records: (x, y, r, g),
+        // the log2(e)-scaled conic + opacity, (b, raw conic), zero pad.
         float r_, g_, b_;
         if (kHasSH) {
             r_ = rgbv.x; g_ = rgbv.y; b_ = rgbv.z;
@@ -223,11 +223,12 @@ __device__ __forceinline__ void pp_gaussian(const PreprocessArgs& a, const GeomV
             r_ = a.colors_precomp[3 * idx]; g_ = a.colors_precomp[3 * idx + 1]; b_ = a.colors_precomp[3 * idx + 2];
         }
         float4* row = stage ? reinterpret_cast<float4*>(stage + 16)
-                            : reinterpret_cast<float4*>(g.grad_accum + (size_t)kGradRow * idx);
+                            : reinterpret_cast<float4*>(g.amr_rows + (size_t)16 * idx);
         const float4 co = make_float4(conic_x, conic_y, conic_z, opacity);
         row[0] = make_float4(pix_x, pix_y, r_, g_);
         row[1] = splat_coef(co);
         row[2] = make_float4(b_, conic_x, conic_y, conic_z);
+        if (!stage) row[3] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
     // Tile histogram with device atomics only when the tile grid is too large
@@ -351,13 +352,14 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
                 }
             }
         }
-        if (a.block == 32) {  // AMR blend rows: 64 x 48 B
-            static_assert(kGradRow == 12, "an AMR blend row is three float4s");
-            float4* out = reinterpret_cast<float4*>(g.grad_accum + (size_t)kGradRow * wrow0);
+        if (a.block == 32) {  // AMR blend rows: 64 x 64 B (three staged float4s + a zero pad each)
+            float4* out = reinterpret_cast<float4*>(g.amr_rows + (size_t)16 * wrow0);
 #pragma unroll
-            for (int i = 0; i < 3; i++) {
+            for (int i = 0; i < 4; i++) {
                 const int c = lane + 64 * i;
-                if (c < 3 * nrow) out[c] = *reinterpret_cast<const float4*>(wl + 48 * (c / 3) + 16 + 4 * (c % 3));
+                if (c < 4 * nrow)
+                    out[c] = (c & 3) == 3 ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                          : *reinterpret_cast<const float4*>(wl + 48 * (c >> 2) + 16 + 4 * (c & 3));
             }
         }
         // 64 x 3 rgb floats = 48 pieces of 4

@@ -257,8 +257,8 @@ __device__ __forceinline__ uint32_t region_mask(float2 xy, float4 co, float ox, 
     return m;
 }
 
-// rows: the per-Gaussian 48-B blend rows the AMR preprocess wrote into
-// grad_accum (preprocess.hip): (x, y, r, g), splat_coef, (b, raw conic).
+// rows: the per-Gaussian 64-B blend rows the AMR preprocess wrote
+// (GeomView::amr_rows): (x, y, r, g), splat_coef, (b, raw conic), pad.
 __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, const uint32_t* __restrict__ ranges,
                                                                       const uint32_t* __restrict__ point_list,
                                                                       const float4* __restrict__ rows,
@@ -291,7 +291,7 @@ __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, c
             m[e] = 0;
             if (i < n) {
                 const uint32_t id = point_list[beg + i];
-                const float4* rr = rows + (size_t)(kGradRow / 4) * id;
+                const float4* rr = rows + (size_t)4 * id;
                 const float4 ra = rr[0], rb = rr[1], rc = rr[2];
                 rec_a[beg + i] = ra;
                 rec_b[beg + i] = rb;
@@ -344,7 +344,7 @@ void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningVi
     }
     (void)features;  // in the rows (the preprocess saw colors_precomp / the SH colours)
     hipLaunchKernelGGL(amr_region_lists_kernel, dim3(tgx * tgy), dim3(kRlThreads), 0, s, tgx, img.ranges,
-                       b.point_list, reinterpret_cast<const float4*>(g.grad_accum), ab.rec_a, ab.rec_b, ab.rec_c,
+                       b.point_list, reinterpret_cast<const float4*>(g.amr_rows), ab.rec_a, ab.rec_b, ab.rec_c,
                        ab.region_lists, img.region_count, img.tile_done, tgy);
 }
 

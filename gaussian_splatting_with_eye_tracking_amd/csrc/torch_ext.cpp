@@ -832,6 +832,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("activate", &Activate);
     m.def("activation_backward", &ActivationBackward);
     m.def("abi_version", []() { return gs_abi_version(); });
+    m.def("amr_geom_bytes", [](int P) { return gs_amr_geom_bytes(P); },
+          "bytes of an AMR forward's geometry buffer (the tail, then the 64-B AMR blend rows)");
     m.def("geom_bytes", [](int P) { return gs_geom_bytes(P); },
           "geometry-buffer bytes with the optional tail (the upper bound a forward asks for)");
     m.def("profile_enable", [](bool on) { gs_profile_enable(on ? 1 : 0); });

@@ -28,8 +28,9 @@
 extern "C" {
 #endif
 
-#define GSPLAT_AMD_ABI_VERSION 5  /* 4: drgb / cov3D moved to an optional tail of the geometry buffer;
-                                     5: grad_accum rows of GSPLAT_AMD_GRAD_ROW = 12 floats (were 16) */
+#define GSPLAT_AMD_ABI_VERSION 6  /* 4: drgb / cov3D moved to an optional tail of the geometry buffer;
+                                     5: grad_accum rows of GSPLAT_AMD_GRAD_ROW = 12 floats (were 16);
+                                     6: AMR geometry buffers end with 64-B blend rows (amr_rows) */
 /* floats per grad_accum row of the geometry buffer (gs_geom_view.grad_accum) */
 #define GSPLAT_AMD_GRAD_ROW 12
 
@@ -309,6 +310,7 @@ typedef struct {
     float* drgb;          /* [P][12] d(rgb)/d(view dir) of the SH colours, (x, y, z) x (r, g, b) + 3 pad (hdr[7] = 1: written), in the optional tail -- ABI 3 / 4 */
     uint32_t* tiles_touched;
     float* grad_accum; /* [P][GSPLAT_AMD_GRAD_ROW] */
+    float* amr_rows;   /* [P][16] AMR blend rows after the tail (AMR geometry buffers only) -- ABI 6 */
 } gs_geom_view;
 
 typedef struct {
@@ -345,6 +347,9 @@ typedef struct {
  * cov3D pointers are then past the end of that buffer (read them only when
  * header word kHdrDrgb / the store_cov3d request says they were written). */
 size_t gs_geom_bytes(int P);
+/* An AMR (32-px) forward's geometry buffer: the tail always, then the 64-B
+ * AMR blend rows (gs_geom_view.amr_rows) -- ABI 6. */
+size_t gs_amr_geom_bytes(int P);
 size_t gs_image_bytes(int width, int height, int tile);
 size_t gs_binning_bytes(int K);
 /* Inverse of gs_binning_bytes (exact; -1 if nbytes is not a binning size). */

@@ -909,9 +909,9 @@ def test_forward_only_hint_from_autograd_wrapper():
         c_, _r, gb, bb, ib = _RasterizeGaussians.apply(*a, 0, e, u8, u8, u8, False, st)
         torch.cuda.synchronize()
         flag = int(C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)["hdr"][7].item())
-        # the geometry buffer's optional tail (d(rgb)/d(dir) + cov3D, 72 B per
-        # Gaussian) is allocated exactly when the rows are written
-        assert (gb.numel() == C.geom_bytes(P)) == (flag == 1), (gb.numel(), C.geom_bytes(P), flag)
+        # an AMR geometry buffer always carries the optional tail (d(rgb)/d(dir)
+        # + cov3D) and then the 64-B AMR blend rows (ABI 6)
+        assert gb.numel() == C.amr_geom_bytes(P), (gb.numel(), C.amr_geom_bytes(P), flag)
         return flag
 
     with torch.no_grad():
