@@ -317,10 +317,8 @@ int g_spec_dup = 1;  // set_tuning("spec_dup")
 // renders and missing on the large ones.  A few entries per thread, least
 // recently used replaced; an unknown key runs the synchronous path.
 struct SpecKey {
-    int dev, W, H, P, tile;
-    bool operator==(const SpecKey& o) const {
-        return dev == o.dev && W == o.W && H == o.H && P == o.P && tile == o.tile;
-    }
+    int dev, W, H, P;
+    bool operator==(const SpecKey& o) const { return dev == o.dev && W == o.W && H == o.H && P == o.P; }
 };
 struct SpecEntry {
     SpecKey key;
@@ -330,10 +328,10 @@ struct SpecEntry {
 constexpr int kSpecEntries = 8;
 thread_local SpecEntry t_spec[kSpecEntries] = {};
 thread_local uint64_t t_spec_clock = 0;
-SpecKey spec_key(int W, int H, int P, int tile) {
+SpecKey spec_key(int W, int H, int P) {
     int dev = -1;
     if (hipGetDevice(&dev) != hipSuccess) dev = -1;
-    return SpecKey{dev, W, H, P, tile};
+    return SpecKey{dev, W, H, P};
 }
 size_t spec_capacity(const SpecKey& k) {
     if (!g_spec_dup) return 0;
@@ -505,25 +503,13 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     // kernel does nothing if K > capacity; then the buffer is re-sized for K
     // and the duplicate relaunched.  Only point_list (offset 0) outlives the
     // forward, so a buffer carved for capacity >= K serves the backward as is.
-    // AMR (foveaStep 0 / render_once): the same, behind the work that needs
-    // the tile counts but not K (before_k: levels, tile order); the binning
-    // buffer is then carved for the capacity, and so is every later carve of
-    // it -- the progressive steps recover the instance count they carve with
-    // from the buffer's size (gs_amr_binning_count_of_bytes), the backward
-    // reads only point_list (offset 0).
     bool dup_done = false;
-    const SpecKey skey = spec_key(W, H, in.P, tile);
-    const size_t cap = (r.T > 0 && !debug) ? spec_capacity(skey) : 0;
+    const SpecKey skey = spec_key(W, H, in.P);
+    const size_t cap = (!amr && !before_k && r.T > 0 && !debug) ? spec_capacity(skey) : 0;
     if (before_k) {
         begin_header_read(r.g.hdr, s, mirror.first);
         before_k(r);
-        if (cap > 0) {
-            char* sbase = call_resize(binning, carve_binning(nullptr, cap, nullptr, nullptr, amr), "binning");
-            carve_binning(sbase, cap, &r.b, amr ? &r.ab : nullptr);
-            { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, (uint32_t)cap, r.g.hdr, (uint32_t)cap); }
-        }
         finish_header_read(hdr, mirror.first, s, r.g.hdr);
-        dup_done = cap > 0 && hdr[kHdrNumRendered] <= cap;
     } else if (cap > 0) {
         begin_header_read(r.g.hdr, s, mirror.first);
         char* sbase = call_resize(binning, carve_binning(nullptr, cap, nullptr), "binning");
@@ -540,7 +526,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     if (in.prefiltered && hdr[kHdrError] == pa.err_token)
         throw GsError("Point is filtered although prefiltered is set. This shouldn't happen!");
     r.K = (int)hdr[kHdrNumRendered];
-    note_k(skey, r.K);
+    if (!amr) note_k(skey, r.K);
     if (!dup_done) {
         char* bbase = call_resize(binning, carve_binning(nullptr, r.K, nullptr, nullptr, amr), "binning");
         carve_binning(bbase, r.K, &r.b, amr ? &r.ab : nullptr);

@@ -456,41 +456,6 @@ def test_speculative_duplicate_matches_synchronous():
             assert float((x - y).abs().max()) <= 1e-5 * max(float(x.abs().max()), 1e-30), i
 
 
-def test_amr_speculative_duplicate_matches_synchronous():
-    """The AMR forward (foveaStep 0) launches its duplicate behind the levels
-    and before K is on the host, into a binning buffer carved for the last
-    call's K (+1/8) -- every later step carves it for that capacity (they
-    recover it from the buffer's size).  Same (P, W, H) scenes whose K grows
-    past the capacity (larger splats: relaunch) and shrinks again (kept):
-    every step image, the radii and the frame are bit-identical to the
-    synchronous path (tuning "spec_dup" 0)."""
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    base, cam = G.scene_and_camera(20000, 256, 192, 0)
-    scenes = []
-    for f in (1.0, 1.0, 2.5, 1.0, 0.7):
-        sc, _ = G.scene_and_camera(20000, 256, 192, 0)
-        sc.scales = (base.scales * np.float32(f)).astype(np.float32)
-        scenes.append(sc)
-
-    def run():
-        out = []
-        for sc in scenes:
-            acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.2, 0.3))
-            out.append([acc.cpu(), radii.cpu()] + [x.cpu() for x in steps])
-        return out
-
-    try:
-        C.set_tuning("spec_dup", 0)
-        ref = run()
-        C.set_tuning("spec_dup", 1)
-        spec = run()
-    finally:
-        C.set_tuning("spec_dup", 1)
-    for i, (a, b) in enumerate(zip(ref, spec)):
-        for x, y in zip(a, b):
-            assert torch.equal(x, y), i
-
-
 def test_empty_scene():
     from diff_gaussian_rasterization import GaussianRasterizer
     sc, cam = G.scene_and_camera(0, 64, 48)
