@@ -994,6 +994,14 @@ def main(argv=None):
     import torch
     import torch.distributed as dist
     build_digest()  # refuse a native library built from other sources than this tree's (after torch: its HIP runtime)
+    # A/B hook: GSAMD_TUNING="key=value,..." (gs_set_tuning: performance-only
+    # choices with identical results); recorded in the line when set
+    tuning = os.environ.get("GSAMD_TUNING", "")
+    if tuning:
+        from gaussian_splatting_with_eye_tracking_amd import _C
+        for kv in tuning.split(","):
+            k, v = kv.split("=")
+            _C.set_tuning(k.strip(), int(v))
     distributed = world > 1
     # GS_BENCH_SHARE_DEVICE=1 / GS_BENCH_BACKEND=gloo only rehearse the N>1 path
     # on a one-GPU box (every rank on device 0); real runs use one GPU per rank
@@ -1043,6 +1051,8 @@ def main(argv=None):
         if kind in ("fwd_bwd", "multiview"):
             out["cpu_baseline"] = cpu_baselines(sc, cam)
         out["cpu_amr_test_path"] = cpu_amr_test_path(args.seed)
+    if tuning:
+        out["tuning"] = tuning
     if rank == 0:
         print(json.dumps(out), flush=True)
     if distributed:
