@@ -481,6 +481,31 @@ class Ctx:
         return tuple(float(v) for v in t.tolist())
 
 
+def settle(fn, warmup: int, ctx: "Ctx") -> int:
+    """The W warmup steps, then untimed steps until about --ramp-ms of work
+    has run.  The GPU's clocks ramp over the first ~40 ms of sustained load
+    (profiles/r05a_launch_ramp_cfg2.txt: render_bwd 360 -> 309 us per launch
+    across 45 launches); without this the timed region averages part of the
+    ramp.  Every rank runs the same number of extra steps (max over ranks),
+    so steps that hold collectives stay matched.  Returns that number."""
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if ctx.args.ramp_ms <= 0:
+        return 0
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    (dt,) = ctx.max_over_ranks(time.perf_counter() - t0)
+    n = int(min(2000, max(0, np.ceil(ctx.args.ramp_ms * 1e-3 / max(dt, 1e-5)))))
+    (n,) = ctx.max_over_ranks(float(n))
+    for _ in range(int(n)):
+        fn()
+    torch.cuda.synchronize()
+    return int(n) + 1
+
+
 def raster_settings(cam, dev, module="diff_gaussian_rasterization"):
     import importlib
 
@@ -564,9 +589,7 @@ def run_fwd_bwd(cfg_name: str, ctx: Ctx, steps: int, warmup: int) -> dict:
                                    shs=params["shs"], scales=params["scales"], rotations=params["rotations"])
         torch.autograd.backward(color, dpix)
 
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
+    ramp = settle(step, warmup, ctx)
     # Inside the timed region only the roofline kernel (render_bwd, the
     # dominant stage at configs 2 and 4) records its event pair: each timed
     # stage costs two event records per launch (~4 us of queue time).
@@ -593,7 +616,8 @@ def run_fwd_bwd(cfg_name: str, ctx: Ctx, steps: int, warmup: int) -> dict:
         prof = _C.profile_read(True)
         _C.profile_enable(False)
     (elapsed,) = ctx.max_over_ranks(elapsed)
-    res = {"value": ctx.world * steps / elapsed, "unit": "views/s", "ms_per_step": 1000.0 * elapsed / steps}
+    res = {"value": ctx.world * steps / elapsed, "unit": "views/s", "ms_per_step": 1000.0 * elapsed / steps,
+           "ramp_steps": ramp}
     if ctx.rank != 0:
         return res
     ws = workload_stats(settings, params, P, W, H)
@@ -688,9 +712,7 @@ def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange
         (el,) = ctx.max_over_ranks(time.perf_counter() - t0)
         return el
 
-    for _ in range(warmup):
-        step_views()
-    torch.cuda.synchronize()
+    ramp = settle(step_views, warmup, ctx)
     el_views = timed(step_views, steps)
     prof = {}
     if not ctx.args.no_profile:
@@ -700,7 +722,8 @@ def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange
         timed(step_views, steps)
         prof = _C.profile_read(True)
         _C.profile_enable(False)
-    res = {"value": G * steps / el_views, "unit": "views/s", "ms_per_step": 1000.0 * el_views / steps}
+    res = {"value": G * steps / el_views, "unit": "views/s", "ms_per_step": 1000.0 * el_views / steps,
+           "ramp_steps": ramp}
     extra = {}
     if exchange_alt:
         for _ in range(max(1, warmup // 2)):
@@ -820,11 +843,12 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
         return rast(means3D=t["means3D"], means2D=means2D, opacities=t["opacities"], shs=t["shs"],
                     scales=t["scales"], rotations=t["rotations"], foveaStep=-2, interpolate_image=True)[0]
 
+    def warm_pair():
+        frame_5step()
+        frame_once()
+
     with torch.no_grad():
-        for _ in range(warmup):
-            frame_5step()
-            frame_once()
-        torch.cuda.synchronize()
+        ramp = settle(warm_pair, warmup, ctx)
         ctx.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -884,7 +908,7 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
         elb = time.perf_counter() - t0
     el5, el1 = ctx.max_over_ranks(el5, el1)
     res = {"value": ctx.world * steps / el5, "unit": "frames/s", "ms_per_step": 1000.0 * el5 / steps,
-           "render_once_fps": ctx.world * steps / el1}
+           "render_once_fps": ctx.world * steps / el1, "ramp_steps": ramp}
     if ctx.rank != 0:
         return res
     with torch.no_grad():
@@ -932,7 +956,7 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
 
 
 def summary(r: dict, keys=("value", "unit", "ms_per_step", "config", "roofline", "step_roofline", "per_step_ms",
-                           "render_once_fps", "exchange_params")) -> dict:
+                           "render_once_fps", "exchange_params", "ramp_steps")) -> dict:
     out = {k: r[k] for k in keys if k in r}
     if r.get("stages"):  # compact per-stage ms per step (or per frame)
         out["stages_ms"] = {n: round(v.get("ms_per_step", v.get("ms_per_frame", 0.0)), 4)
@@ -949,6 +973,9 @@ def parse_args(argv=None):
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
                     help="default: cfg2_1080p_1M at N = 1, cfg5_8view_1080p_1M at N > 1")
     ap.add_argument("--views", type=int, default=8, help="config 5: global views per step")
+    ap.add_argument("--ramp-ms", type=float, default=100.0,
+                    help="after the W warmup steps, untimed steps for about this long so the GPU clocks "
+                         "have settled before the timed region (0: off); the count is in the line as ramp_steps")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sub", action="store_true", help="N = 1: skip the config 3 / 4 / 5 sub-results")
