@@ -41,51 +41,13 @@ for step in "$@"; do
     bench4) run bench_cfg4 600 python bench.py --config cfg4_bicycle_6M --steps 10 --warmup 3 --no-cpu-baseline ;;
     dist2) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 ;;
     dist2l) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2_launcher 600 python bench.py --gpus 2 --steps 5 --warmup 2 ;;
-    dist2p) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2p 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --steps 5 --warmup 2 --exchange params ;;
     dist2amr) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2amr 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --steps 5 --warmup 2 --config cfg3_amr_1080p_1M ;;
     benchnp) run bench_np 400 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-profile &&
              run bench_p 400 python bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
     benchq) run bench 400 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-profile ;;
-    pmc_fetch) run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
-    pmc_valu) run pmc_valu 600 rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace -d gpurun_out/pmc_valu -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
-    pmc_write) run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile ;;
-    ab_fwd) run ab_fwd 400 python tools/ab_tuning.py --key fwd_variant --values 0 1 2 --stage render ;;
-    ab_bwd) run ab_bwd 400 python tools/ab_tuning.py --key bwd_variant --values 0 1 2 0 1 2 --stage render_bwd --backward ;;
-    ab_cull) run ab_cull_fwd 400 python tools/ab_tuning.py --key cull --values 0 1 --stage render &&
-             run ab_cull_bwd 400 python tools/ab_tuning.py --key cull --values 0 1 --stage render_bwd --backward ;;
-    ab_chunk) run ab_chunk_dup 400 python tools/ab_tuning.py --key bin_chunk --values 2048 4096 8192 16384 --stage duplicate &&
-              run ab_chunk_cnt 400 python tools/ab_tuning.py --key bin_chunk --values 2048 4096 8192 16384 --stage count_tiles ;;
-    ab_order) run ab_order_fwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render &&
-              run ab_order_bwd 400 python tools/ab_tuning.py --key tile_order --values 0 1 --stage render_bwd --backward ;;
-    ab_pair) run ab_pair 400 python tools/ab_tuning.py --key bwd_variant --values 0 4 --stage render_bwd --backward ;;
-    pmc_ql) run pmc_ql 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_LDS --kernel-trace -d gpurun_out/pmc_ql -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 3 --warmup 1 --no-profile --no-ext --no-cpu-baseline ;;
-    ab_flush) run ab_flush 400 python tools/ab_tuning.py --key bwd_flush --values 0 1 2 --stage render_bwd --backward ;;
-    ab_amrb) run ab_amrb 400 python tools/ab_tuning.py --key amr_batch --values 1 2 1 2 --stage amr_render --amr ;;
-    ab_sort) run ab_sort4 400 python tools/ab_tuning.py --key sort_wide --values 0 1 0 1 --stage sort_tiles --P 6100000 --W 1600 --H 1063 --rounds 4 &&
-             run ab_sort3 400 python tools/ab_tuning.py --key sort_wide --values 0 1 0 1 --stage sort_tiles --amr ;;
-    ab_scr) run ab_scr 400 python tools/ab_tuning.py --key amr_scramble --values 0 1 0 1 --stage amr_render --amr ;;
-    ab_chunk4) run ab_chunk4_dup 400 python tools/ab_tuning.py --key bin_chunk --values 4096 8192 16384 32768 --stage duplicate --P 6100000 --W 1600 --H 1063 --rounds 3 &&
-               run ab_chunk4_cnt 400 python tools/ab_tuning.py --key bin_chunk --values 4096 8192 16384 32768 --stage count_tiles --P 6100000 --W 1600 --H 1063 --rounds 3 ;;
-    ab_dup) run ab_dup2 400 python tools/ab_tuning.py --key bin_two_phase --values 0 1 0 1 --stage duplicate &&
-            run ab_dup4 400 python tools/ab_tuning.py --key bin_two_phase --values 0 1 0 1 --stage duplicate --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
-    ab_band) run ab_band_split4 400 python tools/ab_tuning.py --key band_split --values 0 16 32 128 256 --stage duplicate --P 6100000 --W 1600 --H 1063 --rounds 4 &&
-             run ab_band_thr4 400 python tools/ab_tuning.py --key band_threads --values 513 514 512 1024 --stage duplicate --P 6100000 --W 1600 --H 1063 --rounds 4 &&
-             run ab_band_split2 400 python tools/ab_tuning.py --key band_split --values 0 16 32 128 256 --stage duplicate --rounds 4 ;;
-    ab_fold) run ab_fold 400 python tools/ab_tuning.py --key amr_fold --values 0 30 62 --stage amr_render --amr &&
-             run ab_fold_once 400 python tools/ab_tuning.py --key amr_fold --values 0 1 --stage amr_render --amr-once ;;
-    ab_amr) run ab_amr 400 python tools/ab_tuning.py --key amr_variant --values 3 4 3 4 --stage amr_render --amr ;;
-    ab_split) run ab_split2 400 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward &&
-              run ab_split4 600 python tools/ab_tuning.py --key bwd_gauss_split --values 0 1 --stage bwd_gauss --backward --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
-    pmc_sq) run pmc_sq 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_sq -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
-    pmc_sq2) run pmc_sq2 600 rocprofv3 --pmc SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_sq2 -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 1 --rounds 1 --iters 2 --backward --stage render_bwd ;;
-    pmc_bwd_a) run pmc_bwd_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_bwd_a -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
-    pmc_bwd_b) run pmc_bwd_b 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVES SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_bwd_b -o run --output-format csv -- python3 tools/ab_tuning.py --key bwd_variant --values 0 --rounds 1 --iters 2 --backward --stage render_bwd ;;
-    pmc_ql2) run pmc_ql2 300 rocprofv3 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_ql2 -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 3 --warmup 1 --no-profile --no-ext --no-cpu-baseline ;;
     pmc_issue2) run pmc_issue2 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace -d gpurun_out/pmc_issue2 -o run --output-format csv -- python3 bench.py --config cfg2_1080p_1M --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
     pmc_issue4) run pmc_issue4 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace -d gpurun_out/pmc_issue4 -o run --output-format csv -- python3 bench.py --config cfg4_bicycle_6M --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
-    pmc_fwd_a) run pmc_fwd_a 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace -d gpurun_out/pmc_fwd_a -o run --output-format csv -- python3 tools/ab_tuning.py --key fwd_variant --values 2 --rounds 1 --iters 2 --stage render ;;
-    pmc_fwd_b) run pmc_fwd_b 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_WAVES SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --kernel-trace -d gpurun_out/pmc_fwd_b -o run --output-format csv -- python3 tools/ab_tuning.py --key fwd_variant --values 2 --rounds 1 --iters 2 --stage render ;;
     mv) run pytest_mv 400 python -m pytest tests/test_gpu_multiview.py tests/test_gpu_dist_views.py -q -m gpu -p no:cacheprovider --timeout 300 -rf &&
         run bench_exchange 400 python tools/bench_exchange.py ;;
     eye) run pytest_eye 400 python -m pytest tests/test_gpu_eye_tracking.py -q -m gpu -p no:cacheprovider --timeout 300 -rf &&
@@ -100,6 +62,8 @@ for step in "$@"; do
       run "pmc_${c}_fetch" 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "gpurun_out/pmc_${c}_fetch" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext &&
       run "pmc_${c}_write" 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "gpurun_out/pmc_${c}_write" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext &&
       run "pmc_${c}_valu" 300 rocprofv3 --pmc SQ_INSTS_VALU --kernel-trace -d "gpurun_out/pmc_${c}_valu" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
+    gaptrace3) run gaptrace3 600 rocprofv3 --kernel-trace -d "$O/gaptrace3" -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 20 --warmup 3 --no-cpu-baseline --no-ext ;;
+    bench5) run bench_cfg5 600 python bench.py --config cfg5_8view_1080p_1M --steps 10 --warmup 3 --no-cpu-baseline ;;
     trace3) run trace_cfg3 300 rocprofv3 --kernel-trace -d gpurun_out/trace_cfg3 -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-ext ;;
     sqa2|sqa4|sqb2|sqb4)  # SQ issue / wait counters per kernel (two 8-counter sets)
       c=$(cfg_of "$step")
@@ -108,8 +72,6 @@ for step in "$@"; do
         *) cnt="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_ANY SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" ;;
       esac
       run "${step}_$c" 300 rocprofv3 --pmc $cnt --kernel-trace -d "gpurun_out/${step}_$c" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
-    ab_pp4) run ab_pp4 400 python tools/ab_tuning.py --key pp_dma --values 1 0 1 0 --stage preprocess --P 6100000 --W 1600 --H 1063 --rounds 4 &&
-            run ab_drgb4 400 python tools/ab_tuning.py --key sh_drgb --values 1 0 1 0 --stage preprocess --P 6100000 --W 1600 --H 1063 --rounds 4 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
