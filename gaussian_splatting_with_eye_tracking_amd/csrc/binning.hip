@@ -122,24 +122,20 @@ __device__ __forceinline__ void mirror_header(uint32_t* m, uint32_t K, uint32_t 
 }
 
 
-// Banded duplicate (below): the bw consecutive tiles of a band of a tile row
-// are consecutive in the sorted layout, so the band's instances are one
-// contiguous range starting at the exclusive prefix of its first tile.  The
-// scan stores that start (and the staging cursor) per band: bin = row * nb +
-// column / bw (bw = gx: one band per row).
+// Row-banded duplicate (below): a tile row's tiles are consecutive, so its
+// instances are one contiguous range of the sorted layout, starting at the
+// exclusive prefix of its first tile.  The scan stores that start (and the
+// staging cursor) per row.
 struct BandScan {
     uint32_t* start;  // nullptr: direct duplicate
     uint32_t* cursor;
     uint32_t gx;
     uint32_t mirror_token;  // the polled header read-back's token (0: none; see mirror_header)
-    uint32_t bw, nb;        // band width (tiles), bands per row
     __device__ __forceinline__ void emit(int i, uint32_t ex) const {
-        if (!start) return;
-        const uint32_t col = (uint32_t)i % gx;
-        if (col % bw) return;
-        const uint32_t bin = ((uint32_t)i / gx) * nb + col / bw;
-        start[bin] = ex;
-        cursor[bin] = ex;
+        if (!start || (uint32_t)i % gx) return;
+        const uint32_t row = (uint32_t)i / gx;
+        start[row] = ex;
+        cursor[row] = ex;
     }
 };
 
@@ -313,9 +309,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, u
 
 void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s, uint32_t* hdr_mirror, int nslots,
                       int gx, bool banded, uint32_t mirror_token) {
-    const int gxx = std::max(gx, 1), gy = (T + gxx - 1) / gxx;
-    const int bw = banded ? band_width_for(gxx, gy) : gxx;
-    BandScan band{nullptr, nullptr, (uint32_t)gxx, mirror_token, (uint32_t)bw, (uint32_t)((gxx + bw - 1) / bw)};
+    BandScan band{nullptr, nullptr, (uint32_t)std::max(gx, 1), mirror_token};
     if (banded) {
         band.start = img.band_start;
         band.cursor = img.band_cursor;
@@ -411,20 +405,6 @@ constexpr int kBandBins = 1024;  // bins of one coalesced append round (rows, or
 // at 1080p, ~2.2 instances per Gaussian) the direct duplicate is cheaper
 // (46 vs 56 us at config 3, profiles/r03h_ab_amr_band.json).
 bool band_lds_fits();  // (below: the banded kernels' dynamic LDS fits the current device)
-// Band width in tiles: the split pass's workgroups each own the tiles of one
-// band (bw tiles of a row) and append only into those, so every append round
-// writes runs of ~kNT kRound / bw keys per tile (whole lines) instead of
-// spreading a round over a whole row's gx tiles (runs of a few keys: partial
-// lines); entries crossing a band edge are staged once per band.  The
-// narrowest of 8, 16, 32, ... tiles whose gy x (bands per row) bins fit one
-// append round; gx: one band per row (round 4's row-banded scheme).
-int g_band_width = 8;  // set_tuning("band_width") (A/B, temporary): 0 = whole rows
-int band_width_for(int gx, int gy) {
-    if (g_band_width <= 0) return gx;
-    for (int bw = g_band_width; bw < gx; bw *= 2)
-        if ((int64_t)gy * ((gx + bw - 1) / bw) <= kBandBins) return bw;
-    return gx;
-}
 bool dup_banded(int gx, int gy, int block) {
     if (gx * gy > kLdsTiles || gx > kBandBins || gy > kBandBins) return false;
     return block == 16 && band_lds_fits();
@@ -641,7 +621,6 @@ struct SourceLds {
     uint64_t key[kNS];
     uint32_t aux[kNS];
     uint32_t first[kNS];
-    uint32_t wid[kNS];   // source j's r-th pair -> bin first + (r / wid) stride + r % wid
     uint32_t pref[kNS];  // exclusive prefix of the counts
     uint32_t wave[kNS / 64 + 1];
 };
@@ -649,9 +628,8 @@ struct SourceLds {
 template <bool kAux, int kNT, int kRound, int kSPT>
 __device__ __forceinline__ void expand_sources(SourceLds<kNT * kSPT>& S, AppendLds<kNT, kRound>& L,
                                                const uint32_t* cnt, const uint64_t* key, const uint32_t* aux,
-                                               const uint32_t* first, const uint32_t* wid, uint32_t stride,
-                                               uint64_t* __restrict__ out_key, uint32_t* __restrict__ out_aux,
-                                               uint32_t limit) {
+                                               const uint32_t* first, uint64_t* __restrict__ out_key,
+                                               uint32_t* __restrict__ out_aux, uint32_t limit) {
     constexpr int kNS = kNT * kSPT;
     const int tid = threadIdx.x;
     uint32_t sum = 0;
@@ -665,7 +643,6 @@ __device__ __forceinline__ void expand_sources(SourceLds<kNT * kSPT>& S, AppendL
         S.key[i] = key[q];
         if constexpr (kAux) S.aux[i] = aux[q];
         S.first[i] = first[q];
-        S.wid[i] = wid[q] ? wid[q] : 1u;
         S.pref[i] = pre;
         pre += cnt[q];
     }
@@ -689,8 +666,7 @@ __device__ __forceinline__ void expand_sources(SourceLds<kNT * kSPT>& S, AppendL
         for (int r = 0; r < kRound; r++, j++) {
             if (j < np) {
                 while (lo + 1 < kNS && S.pref[lo + 1] <= j) lo++;
-                const uint32_t r_ = j - S.pref[lo], w_ = S.wid[lo];
-                bin[n] = S.first[lo] + (r_ / w_) * stride + r_ % w_;
+                bin[n] = S.first[lo] + (j - S.pref[lo]);
                 ky[n] = S.key[lo];
                 if constexpr (kAux) ax[n] = S.aux[lo];
                 n++;
@@ -735,8 +711,7 @@ template <int kNT, int kRound, int kSPT>
 __global__ void __launch_bounds__(kNT) band_stage_kernel(int P, const float* __restrict__ means2D,
                                                          const float* __restrict__ depths,
                                                          const int* __restrict__ radii, int block, uint32_t gx,
-                                                         uint32_t gy, uint32_t bw, uint32_t nb,
-                                                         uint32_t* __restrict__ row_cursor,
+                                                         uint32_t gy, uint32_t* __restrict__ row_cursor,
                                                          uint64_t* __restrict__ stage_keys,
                                                          uint32_t* __restrict__ stage_cols,
                                                          const uint32_t* __restrict__ hdr, uint32_t cap,
@@ -746,22 +721,18 @@ __global__ void __launch_bounds__(kNT) band_stage_kernel(int P, const float* __r
     static_assert(kStageG % kSPT == 0, "whole source groups");
     extern __shared__ __align__(16) unsigned char lds_raw[];
     BandLds<kNT, kRound, kSPT>& B = *reinterpret_cast<BandLds<kNT, kRound, kSPT>*>(lds_raw);
-    // the thread's Gaussians: kSPT consecutive indices per group; one entry
-    // per (tile row, band) the rect touches: bins first + row * nb + band
-    uint32_t cnt[kStageG], cols[kStageG], first[kStageG], wid[kStageG];
+    // the thread's Gaussians: kSPT consecutive indices per group
+    uint32_t cnt[kStageG], cols[kStageG], y0[kStageG];
     uint64_t key[kStageG];
 #pragma unroll
     for (int g = 0; g < kStageG; g++) {
         const int idx = blockIdx.x * kStageChunk + ((g / kSPT) * kNT + threadIdx.x) * kSPT + g % kSPT;
-        cnt[g] = cols[g] = first[g] = 0;
-        wid[g] = 1;
+        cnt[g] = cols[g] = y0[g] = 0;
         key[g] = 0;
         Rect rc;
         if (idx < P && gaussian_rect(idx, means2D, radii, block, gx, gy, rc) && rc.x1 > rc.x0) {
-            const uint32_t b0 = rc.x0 / bw, b1 = (rc.x1 - 1) / bw;
-            wid[g] = b1 - b0 + 1;
-            cnt[g] = (rc.y1 - rc.y0) * wid[g];
-            first[g] = rc.y0 * nb + b0;
+            cnt[g] = rc.y1 - rc.y0;  // one entry per tile row
+            y0[g] = rc.y0;
             cols[g] = rc.x0 | (rc.x1 << 16);
             key[g] = ((uint64_t)float_bits(depths[idx]) << 32) | (uint32_t)idx;
         }
@@ -770,17 +741,16 @@ __global__ void __launch_bounds__(kNT) band_stage_kernel(int P, const float* __r
     __syncthreads();
 #pragma unroll
     for (int g = 0; g < kStageG; g++)
-        for (uint32_t r = 0; r < cnt[g]; r++) atomicAdd(&B.a.run[first[g] + (r / wid[g]) * nb + r % wid[g]], 1u);
-    reserve_runs(B.a, row_cursor, gy * nb);
+        for (uint32_t y = y0[g]; y < y0[g] + cnt[g]; y++) atomicAdd(&B.a.run[y], 1u);
+    reserve_runs(B.a, row_cursor, gy);
 #pragma unroll
     for (int g = 0; g < kStageG; g += kSPT)
-        expand_sources<true, kNT, kRound, kSPT>(B.src, B.a, cnt + g, key + g, cols + g, first + g, wid + g, nb,
-                                                stage_keys, stage_cols, limit);
+        expand_sources<true, kNT, kRound, kSPT>(B.src, B.a, cnt + g, key + g, cols + g, y0 + g, stage_keys,
+                                                stage_cols, limit);
 }
 
 template <int kNT, int kRound, int kSPT>
-__global__ void __launch_bounds__(kNT) band_split_kernel(uint32_t gx, uint32_t bw, uint32_t nb, int split,
-                                                         const uint32_t* __restrict__ row_start,
+__global__ void __launch_bounds__(kNT) band_split_kernel(uint32_t gx, int split, const uint32_t* __restrict__ row_start,
                                                          const uint32_t* __restrict__ row_cursor,
                                                          const uint64_t* __restrict__ stage_keys,
                                                          const uint32_t* __restrict__ stage_cols,
@@ -792,11 +762,8 @@ __global__ void __launch_bounds__(kNT) band_split_kernel(uint32_t gx, uint32_t b
     constexpr uint32_t kCh = kNT * kSPT;  // entries per chunk
     extern __shared__ __align__(16) unsigned char lds_raw[];
     BandLds<kNT, kRound, kSPT>& B = *reinterpret_cast<BandLds<kNT, kRound, kSPT>*>(lds_raw);
-    // this workgroup: part `part` of band bin's entries, appended into the
-    // band's tiles [lo, hi) of its row
-    const uint32_t bin = blockIdx.x / (uint32_t)split, part = blockIdx.x % (uint32_t)split;
-    const uint32_t row = bin / nb, lo = (bin % nb) * bw, hi = min(gx, lo + bw);
-    const uint32_t beg = row_start[bin], n_ent = row_cursor[bin] - beg;
+    const uint32_t row = blockIdx.x / (uint32_t)split, part = blockIdx.x % (uint32_t)split;
+    const uint32_t beg = row_start[row], n_ent = row_cursor[row] - beg;
     const uint32_t stride = (uint32_t)split * kCh;
     // the workgroup's entries: chunks of kCh at part, part + split, ...;
     // thread tid holds entries c0 + tid kSPT + q
@@ -814,9 +781,9 @@ __global__ void __launch_bounds__(kNT) band_split_kernel(uint32_t gx, uint32_t b
             }
 #pragma unroll
         for (int u = 0; u < kU * kSPT; u++)
-            for (uint32_t x = max(c[u] & 0xffffu, lo); x < min(c[u] >> 16, hi); x++) atomicAdd(&B.a.run[x - lo], 1u);
+            for (uint32_t x = c[u] & 0xffffu; x < (c[u] >> 16); x++) atomicAdd(&B.a.run[x], 1u);
     }
-    reserve_runs(B.a, tile_cursor + row * gx + lo, hi - lo);
+    reserve_runs(B.a, tile_cursor + row * gx, gx);
     for (uint32_t c0 = part * kCh; c0 < n_ent; c0 += stride) {
         uint32_t cnt[kSPT], x0[kSPT];
         uint64_t key[kSPT];
@@ -828,20 +795,18 @@ __global__ void __launch_bounds__(kNT) band_split_kernel(uint32_t gx, uint32_t b
             if (e < n_ent) {
                 const uint32_t c = stage_cols[beg + e];
                 key[q] = stage_keys[beg + e];
-                const uint32_t a0 = max(c & 0xffffu, lo), a1 = min(c >> 16, hi);
-                x0[q] = a0 - lo;
-                cnt[q] = a1 > a0 ? a1 - a0 : 0u;
+                x0[q] = c & 0xffffu;
+                cnt[q] = (c >> 16) - x0[q];
             }
         }
-        expand_sources<false, kNT, kRound, kSPT>(B.src, B.a, cnt, key, x0, x0, cnt, 0u, pair_keys, nullptr, limit);
+        expand_sources<false, kNT, kRound, kSPT>(B.src, B.a, cnt, key, x0, x0, pair_keys, nullptr, limit);
     }
 }
 
 template <int kNT, int kR, int kSPT>
-void launch_banded(int P, const GeomView& g, const int* radii, int block, uint32_t gx, uint32_t gy, uint32_t bw,
-                   int split, const ImageView& img, const BinningView& b, hipStream_t s, uint32_t n_keys,
+void launch_banded(int P, const GeomView& g, const int* radii, int block, uint32_t gx, uint32_t gy, int split,
+                   const ImageView& img, const BinningView& b, hipStream_t s, uint32_t n_keys,
                    const uint32_t* spec_hdr, uint32_t spec_cap) {
-    const uint32_t nb = (gx + bw - 1) / bw;
     using Lds = BandLds<kNT, kR, kSPT>;
     // > 64 KiB of dynamic LDS: the attribute once per device (and variant)
     static std::atomic<int> attr[kMaxDevices];
@@ -857,11 +822,11 @@ void launch_banded(int P, const GeomView& g, const int* radii, int block, uint32
         attr[dev].store(1, std::memory_order_release);
     }
     hipLaunchKernelGGL((band_stage_kernel<kNT, kR, kSPT>), dim3((P + kStageChunk - 1) / kStageChunk), dim3(kNT),
-                       sizeof(Lds), s, P, g.means2D, g.depths, radii, block, gx, gy, bw, nb, img.band_cursor,
-                       b.scratch, b.point_list, spec_hdr, spec_cap, n_keys);
-    hipLaunchKernelGGL((band_split_kernel<kNT, kR, kSPT>), dim3(gy * nb * split), dim3(kNT), sizeof(Lds), s, gx, bw,
-                       nb, split, img.band_start, img.band_cursor, b.scratch, b.point_list, img.tile_cursor,
-                       b.pair_keys, spec_hdr, spec_cap, n_keys);
+                       sizeof(Lds), s, P, g.means2D, g.depths, radii, block, gx, gy, img.band_cursor, b.scratch,
+                       b.point_list, spec_hdr, spec_cap, n_keys);
+    hipLaunchKernelGGL((band_split_kernel<kNT, kR, kSPT>), dim3(gy * split), dim3(kNT), sizeof(Lds), s, gx, split,
+                       img.band_start, img.band_cursor, b.scratch, b.point_list, img.tile_cursor, b.pair_keys,
+                       spec_hdr, spec_cap, n_keys);
 }
 
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
@@ -871,15 +836,12 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
     const uint32_t gx = (uint32_t)((W + block - 1) / block), gy = (uint32_t)((H + block - 1) / block);
     if (dup_banded((int)gx, (int)gy, block)) {
         // ~4 split workgroups per CU over the rows
-        // ~4096 split workgroups in all over the bands (whole rows at config 4:
-        // 62 per row; 16 / 32 / 128 / 256 measured slower, profiles/r03p_ab_band_*.json)
-        const uint32_t bw = (uint32_t)band_width_for((int)gx, (int)gy), nbins = gy * ((gx + bw - 1) / bw);
+        // ~4096 split workgroups in all over the rows (per tile row at config 4:
+        // 62; 16 / 32 / 128 / 256 measured slower, profiles/r03p_ab_band_*.json)
         const int want = 4096;
-        const int split = std::max(1, std::min(256, (want + (int)nbins - 1) / (int)nbins));
-        if (P >= 2000000)
-            launch_banded<512, 2, 2>(P, g, radii, block, gx, gy, bw, split, img, b, s, n_keys, spec_hdr, spec_cap);
-        else
-            launch_banded<1024, 2, 1>(P, g, radii, block, gx, gy, bw, split, img, b, s, n_keys, spec_hdr, spec_cap);
+        const int split = std::max(1, std::min(256, (want + (int)gy - 1) / (int)gy));
+        if (P >= 2000000) launch_banded<512, 2, 2>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap);
+        else launch_banded<1024, 2, 1>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap);
         return;
     }
     if (gx * gy <= (uint32_t)kLdsTiles) {

@@ -33,7 +33,7 @@
 #include "gs_layout.h"
 
 using namespace gsamd;
-namespace gsamd { extern int g_mv_variant; extern int g_band_width; }
+namespace gsamd { extern int g_mv_variant; }
 
 namespace {
 
@@ -1222,10 +1222,6 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "spec_dup") == 0) {  // speculative duplicate before the K read-back (base forward)
         g_spec_dup = value;
-        return 0;
-    }
-    if (std::strcmp(key, "band_width") == 0) {  // (A/B, temporary)
-        g_band_width = value;
         return 0;
     }
     if (std::strcmp(key, "mv_variant") == 0) {  // (A/B, temporary)

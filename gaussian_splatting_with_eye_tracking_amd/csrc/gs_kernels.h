@@ -74,8 +74,7 @@ void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H
                         hipStream_t s);
 void set_sort_algo(int v);  // 0 = bitonic networks, 1 = bucket sort (default)
 int bin_slots_for(int P, int gx, int gy, int block);  // sub-bucket slots of the LDS binning (P-Gaussian forward)
-bool dup_banded(int gx, int gy, int block);           // the banded duplicate runs for this tile grid
-int band_width_for(int gx, int gy);                   // its band width in tiles (scan and duplicate agree)
+bool dup_banded(int gx, int gy, int block);           // the row-banded duplicate runs for this tile grid
 // img.tile_order = tiles sorted by descending work (heaviest first) so the
 // long tiles of a blend launch start early instead of forming its tail.
 // Work = range length, or min(range length, max_contrib) if use_max_contrib.
