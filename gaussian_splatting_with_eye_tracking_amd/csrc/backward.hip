@@ -1351,203 +1351,15 @@ __device__ __forceinline__ const float* mv_cam(const MultiViewArgs& a, int v) {
     return a.table ? a.table[a.V + v] : a.cams[v];
 }
 
-template <bool kHasSH, bool kSH16>
-__global__ void __launch_bounds__(256) multiview_backward_kernel(MultiViewArgs a) {
-    // SH16: the workgroup's 256 SH rows staged in LDS (coalesced in, and the
-    // gradient rows coalesced out, as backward_gaussians_kernel), and read
-    // from there by the per-view SH terms: the 48 coefficients do not occupy
-    // registers across the view loop.
-    constexpr bool kStage = kHasSH && kSH16;
-    __shared__ float s_sh[kStage ? 256 * kShRow : 1];
-    const int local0 = blockIdx.x * 256;
-    const int nblk = min(256, a.count - local0);
-    if constexpr (kStage) {
-        const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)(a.g0 + local0) * 12;
-        if (nblk == 256) {
-            // a full workgroup: the 12 loads of each thread issued back to back
-            // (one memory round trip, as backward_gaussians_kernel's staging:
-            // multiview_bwd 0.3614 -> 0.3393 ms per 8-view step at config 5,
-            // profiles/r04ze_bench_cfg5.log against r04zz_bench.log)
-            float4 v[12];
-#pragma unroll
-            for (int k = 0; k < 12; k++) v[k] = in[threadIdx.x + 256 * k];
-#pragma unroll
-            for (int k = 0; k < 12; k++) {
-                const int f = threadIdx.x + 256 * k;
-                float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
-                r[0] = v[k].x; r[1] = v[k].y; r[2] = v[k].z; r[3] = v[k].w;
-            }
-        } else {
-            for (int f = threadIdx.x; f < nblk * 12; f += 256) {
-                const float4 v = in[f];
-                float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
-                r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
-            }
-        }
-        __syncthreads();
-    }
-    const int local = local0 + threadIdx.x;
-    const bool live = local < a.count;
-    const int idx = a.g0 + local;
-    float* lrow = kStage ? s_sh + threadIdx.x * kShRow : nullptr;
-    // view v's row of this Gaussian (a.rows[v] points at Gaussian g0's)
-    const size_t roff = (size_t)local * kViewRow;
-    bool any = false;
-    if (live)
-        for (int v = 0; v < a.V; v++) any |= __float_as_uint(mv_row(a, v)[roff + 9]) != 0u;
-    if (live && !any) {
-#pragma unroll
-        for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = 0.f;
-        if (kStage) {
-#pragma unroll
-            for (int i = 0; i < 48; i++) lrow[i] = 0.f;
-        } else if (kHasSH) {
-            for (int i = 0; i < a.M * 3; i++) a.dL_dsh[(size_t)idx * a.M * 3 + i] = 0.f;
-        }
-        a.dL_dopacity[idx] = 0.f;
-        for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = 0.f;
-        reinterpret_cast<float4*>(a.dL_drot)[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (live && any) {
-        const float mx = a.means3D[3 * idx], my = a.means3D[3 * idx + 1], mz = a.means3D[3 * idx + 2];
-        float dmean_t[3] = {0.f, 0.f, 0.f};
-        // ---- pass 1: cov2D + projection terms, opacity, statistics; then the
-        // cov3D backward once on the summed dL/dcov3D
-        {
-            const float4 qrot = reinterpret_cast<const float4*>(a.rotations)[idx];
-            const float scl[3] = {a.scales[3 * idx + 0], a.scales[3 * idx + 1], a.scales[3 * idx + 2]};
-            float cov3D[6];
-            compute_cov3d(scl, qrot, a.scale_modifier, cov3D);
-            float dcov_t[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dop = 0.f;
-            float st_acc = 0.f, st_den = 0.f, st_max = 0.f;
-            const bool stats = a.grad_norm_accum != nullptr;
-            if (stats) {
-                st_acc = a.grad_norm_accum[idx];
-                st_den = a.denom[idx];
-                st_max = a.max_radii[idx];
-            }
-            for (int v = 0; v < a.V; v++) {
-                const float* row = mv_row(a, v) + roff;
-                const uint32_t w9 = __float_as_uint(row[9]);
-                if (w9 == 0u) continue;  // not visible in view v: no terms (the reference's radii > 0 filter)
-                // mean2D.y, conic x, y, w (rows are 40 B: 8-B aligned only)
-                const float2 r1a = *reinterpret_cast<const float2*>(row + 4);
-                const float2 r1b = *reinterpret_cast<const float2*>(row + 6);
-                const float4 r1 = make_float4(r1a.x, r1a.y, r1b.x, r1b.y);
-                const float gx = row[3], dop_v = row[8];
-                const float* cam = mv_cam(a, v);
-                const Mat4 V = load_mat4(cam);
-                const Mat4 Pm = load_mat4(cam + 16);
-                const float tan_fovx = cam[37], tan_fovy = cam[38];
-                // rasterizer_impl.cu:222-223 / gs_api.cpp: focal from the image size
-                const float focal_x = cam[35] / (2.0f * tan_fovx);
-                const float focal_y = cam[36] / (2.0f * tan_fovy);
-                float dmean[3], dcov[6];
-                cov2d_backward(mx, my, mz, cov3D, r1.y, r1.z, r1.w, V, focal_x, focal_y, tan_fovx, tan_fovy, dmean,
-                               dcov);
-                proj_backward(mx, my, mz, Pm, gx, r1.x, dmean);
-#pragma unroll
-                for (int i = 0; i < 3; i++) dmean_t[i] += dmean[i];
-#pragma unroll
-                for (int i = 0; i < 6; i++) dcov_t[i] += dcov[i];
-                dop += dop_v;
-                if (stats) {
-                    st_acc = st_acc + sqrtf(gx * gx + r1.x * r1.x);
-                    st_den = st_den + 1.f;
-                    st_max = fmaxf(st_max, (float)(w9 & 0xFFFFFFu));
-                }
-            }
-            a.dL_dopacity[idx] = dop;
-            float dscale[3];
-            float4 dq;
-            cov3d_backward(qrot, scl, a.scale_modifier, dcov_t, dscale, dq);
-#pragma unroll
-            for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = dscale[i];
-            reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
-            if (stats) {
-                a.grad_norm_accum[idx] = st_acc;
-                a.denom[idx] = st_den;
-                a.max_radii[idx] = st_max;
-            }
-        }
-        // ---- pass 2: SH coefficient gradients and the view-direction term
-        if (kHasSH) {
-            const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
-            float dsh_t[48];
-#pragma unroll
-            for (int i = 0; i < 48; i++) dsh_t[i] = 0.f;
-            float s_reg[kStage ? 1 : 16][3];
-            if (!kStage) {
-                const float* sh = a.shs + (size_t)idx * a.M * 3;
-#pragma unroll
-                for (int k = 0; k < (kStage ? 1 : 16); k++)
-#pragma unroll
-                    for (int c = 0; c < 3; c++) s_reg[k][c] = (k < ncoef) ? sh[3 * k + c] : 0.f;
-            }
-            float ddir[3] = {0.f, 0.f, 0.f};
-            for (int v = 0; v < a.V; v++) {
-                const float* row = mv_row(a, v) + roff;
-                const uint32_t w9 = __float_as_uint(row[9]);
-                if (w9 == 0u) continue;
-                const float acc[3] = {row[0], row[1], row[2]};
-                const uint8_t cb = (uint8_t)(w9 >> 24);
-                const float* cam = mv_cam(a, v);
-                float dsh_c[16], dRGB[3];
-                if constexpr (kStage) {
-                    sh_backward_terms(a.D, cam + 32, mx, my, mz, ShRowPtr{lrow}, cb, acc, dsh_c, dRGB, ddir);
-                } else {
-                    float s16[16][3];
-#pragma unroll
-                    for (int k = 0; k < 16; k++)
-#pragma unroll
-                        for (int c = 0; c < 3; c++) s16[k][c] = s_reg[kStage ? 0 : k][c];
-                    sh_backward_terms(a.D, cam + 32, mx, my, mz, s16, cb, acc, dsh_c, dRGB, ddir);
-                }
-#pragma unroll
-                for (int k = 0; k < 16; k++)
-#pragma unroll
-                    for (int c = 0; c < 3; c++)
-                        if (k < ncoef) dsh_t[3 * k + c] += dsh_c[k] * dRGB[c];
-            }
-#pragma unroll
-            for (int i = 0; i < 3; i++) dmean_t[i] += ddir[i];
-            if (kStage) {
-#pragma unroll
-                for (int i = 0; i < 48; i++) lrow[i] = dsh_t[i];
-            } else {
-                for (int k = 0; k < a.M; k++)
-#pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        float val = 0.f;
-#pragma unroll
-                        for (int kk = 0; kk < 16; kk++) val = (kk == k) ? dsh_t[3 * kk + c] : val;
-                        a.dL_dsh[(size_t)idx * a.M * 3 + 3 * k + c] = val;
-                    }
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = dmean_t[i];
-    }
-    if constexpr (kStage) {  // the workgroup's gradient rows out, wave-contiguous
-        __syncthreads();
-        float4* out = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)(a.g0 + local0) * 12;
-        for (int f = threadIdx.x; f < nblk * 12; f += 256) {
-            const float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
-            store_out4(&out[f], make_float4(r[0], r[1], r[2], r[3]), a.nt != 0);
-        }
-    }
-}
-
-// The same sums in one pass over the views with each view's rows staged
-// through LDS: the workgroup's 256 rows of view v (10 KB, contiguous in the
-// record) are read with 8-B loads by consecutive lanes -- five load
-// instructions per thread per view instead of ten per-thread loads at a 40-B
-// stride in each of three passes (the any-check and the two passes above,
-// each touching ~20 cache lines per wave instruction) -- the next view's
-// rows in flight in registers while this view's terms are formed.  Per view
-// the cov2D / projection terms and the SH terms are formed as in the
-// two-pass kernel and accumulated in the same order into the same separate
-// sums (dmean_t, ddir, dsh_t, dcov_t, ...): bit-identical results.
+// One pass over the views with each view's rows staged through LDS: the
+// workgroup's 256 rows of view v (10 KB, contiguous in the record) are read
+// with 8-B loads by consecutive lanes -- five load instructions per thread per
+// view instead of ten per-thread loads at a 40-B stride (each touching ~20
+// cache lines per wave instruction) -- the next view's rows in flight in
+// registers while this view's terms are formed.  (Round 4's two-pass form --
+// an any-check pass, the geometry pass, the SH pass, each re-reading the rows
+// per thread -- measured 0.3386 against 0.3360 ms per 8-view step at config
+// 5, profiles/r05c_bench_cfg5_mv*.log, and is removed.)
 constexpr int kMvRowF2 = 256 * kViewRow / 2;     // float2 per view per workgroup (1280)
 constexpr int kMvRowPer = (kMvRowF2 + 255) / 256;  // per thread (5)
 template <bool kHasSH, bool kSH16>
@@ -1721,23 +1533,15 @@ __global__ void __launch_bounds__(256) multiview_backward1_kernel(MultiViewArgs 
     }
 }
 
-int g_mv_variant = 1;  // set_tuning("mv_variant") (A/B): 1 the one-pass staged kernel, 0 the two-pass kernel
-
 void launch_multiview_backward(const MultiViewArgs& args, hipStream_t s) {
     if (args.count <= 0) return;
     MultiViewArgs a = args;
     a.nt = 1;  // the dL_dsh rows non-temporal (as backward_gaussians_kernel's)
     const dim3 grid((a.count + 255) / 256);
     const bool sh = a.shs != nullptr;
-    if (g_mv_variant) {
-        if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward1_kernel<true, true>), grid, dim3(256), 0, s, a);
-        else if (sh) hipLaunchKernelGGL((multiview_backward1_kernel<true, false>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((multiview_backward1_kernel<false, false>), grid, dim3(256), 0, s, a);
-        return;
-    }
-    if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward_kernel<true, true>), grid, dim3(256), 0, s, a);
-    else if (sh) hipLaunchKernelGGL((multiview_backward_kernel<true, false>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((multiview_backward_kernel<false, false>), grid, dim3(256), 0, s, a);
+    if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward1_kernel<true, true>), grid, dim3(256), 0, s, a);
+    else if (sh) hipLaunchKernelGGL((multiview_backward1_kernel<true, false>), grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((multiview_backward1_kernel<false, false>), grid, dim3(256), 0, s, a);
 }
 
 }  // namespace gsamd

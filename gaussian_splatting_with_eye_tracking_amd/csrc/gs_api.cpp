@@ -33,7 +33,6 @@
 #include "gs_layout.h"
 
 using namespace gsamd;
-namespace gsamd { extern int g_mv_variant; }
 
 namespace {
 
@@ -1222,10 +1221,6 @@ int gs_set_tuning(const char* key, int value) {
     }
     if (std::strcmp(key, "spec_dup") == 0) {  // speculative duplicate before the K read-back (base forward)
         g_spec_dup = value;
-        return 0;
-    }
-    if (std::strcmp(key, "mv_variant") == 0) {  // (A/B, temporary)
-        g_mv_variant = value;
         return 0;
     }
     if (std::strcmp(key, "ritnet_mfma") == 0) {  // 0: the SGPR-weight FMA convolution; 1: matrix cores (default)
