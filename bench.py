@@ -675,18 +675,26 @@ def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange
     e0 = torch.empty(0, device=ctx.dev)
     pg = params
 
+    vs = {"n": max(1, int(getattr(ctx.args, "view_streams", 2)))}
+
     def step_views():
         # each view's record is all-gathered as soon as it exists (overlapping
         # the next view's forward + blend backward), the last in chunks that
         # overlap the multi-view backward (data_parallel.ViewExchange)
+        # (the views' forward + blend backward alternate over view_streams
+        # HIP streams, data_parallel.run_views_on_streams)
         with torch.no_grad():
             ex = DP.ViewExchange(P, vl, ctx.dev)
-            for j, vw in enumerate(views):
+
+            def one(j):
+                vw = views[j]
                 st = vw["st"]
                 K, _color, radii, geom, binning, img = _C.rasterize_gaussians(
                     st.bg, pg["means3D"], e0, pg["opacities"], pg["scales"], pg["rotations"], 1.0, e0,
                     st.viewmatrix, st.projmatrix, st.tanfovx, st.tanfovy, H, W, pg["shs"], 3, st.campos, False, False)
                 ex.add(j, DP.view_record(st, radii, geom, K, binning, img, vw["dpix"]))
+
+            DP.run_views_on_streams(len(views), one, vs["n"])
             return ex.finish(st0, pg["means3D"], pg["shs"], pg["scales"], pg["rotations"])
 
     flat = DP.FlatGrads(params)
@@ -716,14 +724,18 @@ def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange
     el_views = timed(step_views, steps)
     prof = {}
     if not ctx.args.no_profile:
+        # (per-stage events on one stream: concurrent views would time each
+        # other's kernels)
+        n_streams, vs["n"] = vs["n"], 1
         _C.profile_enable(True)
         _C.profile_stages([])
         _C.profile_read(True)
         timed(step_views, steps)
         prof = _C.profile_read(True)
         _C.profile_enable(False)
+        vs["n"] = n_streams
     res = {"value": G * steps / el_views, "unit": "views/s", "ms_per_step": 1000.0 * el_views / steps,
-           "ramp_steps": ramp}
+           "ramp_steps": ramp, "view_streams": vs["n"]}
     extra = {}
     if exchange_alt:
         for _ in range(max(1, warmup // 2)):
@@ -956,7 +968,7 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
 
 
 def summary(r: dict, keys=("value", "unit", "ms_per_step", "config", "roofline", "step_roofline", "per_step_ms",
-                           "render_once_fps", "exchange_params", "ramp_steps")) -> dict:
+                           "render_once_fps", "exchange_params", "ramp_steps", "view_streams")) -> dict:
     out = {k: r[k] for k in keys if k in r}
     if r.get("stages"):  # compact per-stage ms per step (or per frame)
         out["stages_ms"] = {n: round(v.get("ms_per_step", v.get("ms_per_frame", 0.0)), 4)
@@ -973,6 +985,8 @@ def parse_args(argv=None):
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
                     help="default: cfg2_1080p_1M at N = 1, cfg5_8view_1080p_1M at N > 1")
     ap.add_argument("--views", type=int, default=8, help="config 5: global views per step")
+    ap.add_argument("--view-streams", type=int, default=2,
+                    help="config 5: HIP streams the rank's views alternate over (1: one stream)")
     ap.add_argument("--ramp-ms", type=float, default=100.0,
                     help="after the W warmup steps, untimed steps for about this long so the GPU clocks "
                          "have settled before the timed region (0: off); the count is in the line as ramp_steps")

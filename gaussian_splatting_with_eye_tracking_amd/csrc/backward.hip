@@ -574,21 +574,28 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
 }
 
 extern int g_cull;  // render.hip
-// Backward variants (set_tuning("bwd_variant")).  Default (round 4's variant
-// 11): the select form with SGPR-pair masks, per-batch compare sets, staged
-// sums and the flush fused into the staging reduce -- render_bwd 0.3707
+// Backward variants (set_tuning("bwd_variant")).  Default: round 4's variant
+// 11 -- the select form with SGPR-pair masks, per-batch compare sets, staged
+// sums and the flush fused into the staging reduce: render_bwd 0.3707
 // (variant 7) -> 0.3634 (masks) -> 0.3512 (s2 in the transposition) ->
 // 0.3403 (unrolled slots) -> 0.3139 ms (fused flush) at config 2, 0.2887 ->
 // 0.2433 at config 4 (profiles/r04b_ab_bwd*.log, r04e_ab_bwd*.log,
-// r04l_ab_bwd*_m.log).  Fallback (0): the predicate form with full sums in
-// LDS rows (also the AMR backward's form).  Measured and removed (logs in
-// profiles/): 2 waves x 2 px and 4 x 1 geometries, half-wave DPP-tree sums,
-// a 5-wave occupancy cap (spills), the un-fused staged forms, the heavy-tile
-// split (r01h / DESIGN.md §8e), an XCD-compact tile order (r04u_ab_xcd*),
-// plain-store / no-flush timing diagnostics.
-constexpr int kDefaultBwdVariant = 1;
+// r04l_ab_bwd*_m.log) -- plus, since round 5, the opacity-scaled sums
+// (kOpT): in batches of provably negative-definite entries with o <= 0.99
+// (alpha = o G unclamped, bit for bit the rounded product) the visit sums t'
+// = alpha T (c - acc) . dL_dpix = o t, which needs no G select and one
+// product less, and the flush takes o out of the mean / conic factors and
+// divides the opacity sum by it (0.3116 -> 0.3063 ms at config 2, 0.2385 ->
+// 0.2348 at config 4, profiles/r05d_ab_bwd_opt*.log).  Fallback (0): the
+// predicate form with full sums in LDS rows (also the AMR backward's form).
+// Measured and removed (logs in profiles/): 2 waves x 2 px and 4 x 1
+// geometries, half-wave DPP-tree sums, a 5-wave occupancy cap (spills), the
+// un-fused staged forms, the heavy-tile split (r01h / DESIGN.md §8e), an
+// XCD-compact tile order (r04u_ab_xcd*), plain-store / no-flush timing
+// diagnostics.
+constexpr int kDefaultBwdVariant = 2;
 int g_bwd_variant = kDefaultBwdVariant;
-void set_backward_variant(int v) { g_bwd_variant = (v == 0 || v == 2) ? v : kDefaultBwdVariant; }
+void set_backward_variant(int v) { g_bwd_variant = v == 0 ? 0 : kDefaultBwdVariant; }
 
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s, int K) {
@@ -607,8 +614,7 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
                        dL_dpix, bg, g.grad_accum, g_cull, gx, 0, nullptr, img.bucket_count, img.bucket_list,       \
                        hit_codes_at(b.point_list, hit_codes_k), g.hdr)
     if (g_bwd_variant == 0) GS_BWD_LAUNCH(false);
-    else if (g_bwd_variant == 2) GS_BWD_LAUNCH(true, false, true);
-    else GS_BWD_LAUNCH(true);
+    else GS_BWD_LAUNCH(true, false, true);
 #undef GS_BWD_LAUNCH
 }
 
@@ -1539,6 +1545,12 @@ void launch_multiview_backward(const MultiViewArgs& args, hipStream_t s) {
     a.nt = 1;  // the dL_dsh rows non-temporal (as backward_gaussians_kernel's)
     const dim3 grid((a.count + 255) / 256);
     const bool sh = a.shs != nullptr;
+    // (A role-split form -- 64 Gaussians per workgroup, wave 3 the geometry
+    // terms, waves 0-2 one colour channel each, 128 VGPRs and 22 KB of LDS:
+    // 4 waves per SIMD instead of 2 -- measured 0.4358 against 0.3360 ms per
+    // 8-view step at config 5, profiles/r05d_bench_cfg5_roles.log: the
+    // per-view barrier waits on the geometry wave and the channel waves redo
+    // the direction and basis; removed.)
     if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward1_kernel<true, true>), grid, dim3(256), 0, s, a);
     else if (sh) hipLaunchKernelGGL((multiview_backward1_kernel<true, false>), grid, dim3(256), 0, s, a);
     else hipLaunchKernelGGL((multiview_backward1_kernel<false, false>), grid, dim3(256), 0, s, a);

@@ -1199,7 +1199,7 @@ int gs_set_tuning(const char* key, int value) {
         set_forward_variant(value);
         return 0;
     }
-    if (std::strcmp(key, "bwd_variant") == 0) {  // 0: predicate form, LDS-row sums; else the default
+    if (std::strcmp(key, "bwd_variant") == 0) {  // 0: predicate form, LDS-row sums; else the default (opacity-scaled sums)
         set_backward_variant(value);
         return 0;
     }

@@ -287,6 +287,47 @@ class ViewExchange:
         return outs
 
 
+_SIDE_STREAMS: Dict[Tuple[int, int], List[torch.cuda.Stream]] = {}
+
+
+def run_views_on_streams(n_views: int, render_one, n_streams: int = 2, device=None) -> None:
+    """render_one(j) for j in [0, n_views), view j enqueued on stream
+    j % n_streams (stream 0 = the current stream, the others cached side
+    streams), so the independent per-view forward + blend backward of one
+    step overlap on the GPU: view j + 1's preprocess and binning (HBM- and
+    latency-bound) run beside view j's blends (VALU-bound).  The host still
+    enqueues in view order -- each forward waits on the host for its own
+    instance count -- so every view's collectives (ViewExchange.add inside
+    render_one) are issued in the same order on every rank.  The side streams
+    start after the work already on the current stream, and the current
+    stream continues after all of them."""
+    if n_views <= 0:
+        return
+    if n_streams <= 1 or not torch.cuda.is_available():
+        for j in range(n_views):
+            render_one(j)
+        return
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    key = (dev.index if dev.index is not None else torch.cuda.current_device(), n_streams)
+    side = _SIDE_STREAMS.get(key)
+    if side is None:
+        side = [torch.cuda.Stream(device=dev) for _ in range(n_streams - 1)]
+        _SIDE_STREAMS[key] = side
+    cur = torch.cuda.current_stream(dev)
+    streams = [cur] + side
+    for s in side:
+        s.wait_stream(cur)
+    for j in range(n_views):
+        s = streams[j % n_streams]
+        if s is cur:
+            render_one(j)
+        else:
+            with torch.cuda.stream(s):
+                render_one(j)
+    for s in side:
+        cur.wait_stream(s)
+
+
 def _empty_param_grads(means3D: torch.Tensor, shs: Optional[torch.Tensor]):
     dev = means3D.device
     P = means3D.shape[0]

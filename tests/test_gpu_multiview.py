@@ -27,23 +27,24 @@ def _views(P, W, H, yaws, seed=0):
     return sc, cams
 
 
-def _forward(C, s, t):
+def _forward(C, s, t, deg=3):
     e = torch.Tensor([])
     return C.rasterize_gaussians(s.bg, t["means3D"], e, t["opacities"], t["scales"], t["rotations"], 1.0, e,
                                  s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width,
-                                 t["shs"], 3, s.campos, False, False)
+                                 t["shs"], deg, s.campos, False, False)
 
 
-def _full_backward(C, s, t, fwd, dpix):
+def _full_backward(C, s, t, fwd, dpix, deg=3):
     K, color, radii, geom, binning, img = fwd
     e = torch.Tensor([])
     return C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, e, t["scales"], t["rotations"], 1.0, e,
-                                          s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, dpix, t["shs"], 3,
+                                          s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, dpix, t["shs"], deg,
                                           s.campos, geom, K, binning, img, False)
 
 
-@pytest.mark.parametrize("yaws", [(0.0,), (-5.0, 0.0, 5.0), (-12.0, -3.0, 4.0, 9.0, 15.0)])
-def test_multiview_equals_sum_of_view_backwards(yaws):
+@pytest.mark.parametrize("yaws,deg", [((0.0,), 3), ((-5.0, 0.0, 5.0), 3), ((-12.0, -3.0, 4.0, 9.0, 15.0), 3),
+                                      ((-5.0, 0.0, 5.0), 1)])
+def test_multiview_equals_sum_of_view_backwards(yaws, deg):
     import gaussian_splatting_with_eye_tracking_amd._C as C
     from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
     from gaussian_splatting_with_eye_tracking_amd import synthetic as S
@@ -56,8 +57,8 @@ def test_multiview_equals_sum_of_view_backwards(yaws):
     for v, cam in enumerate(cams):
         s = G.torch_settings(cam)
         dpix = torch.from_numpy(S.make_cotangent(H, W, 10 + v)).cuda()
-        fwd = _forward(C, s, t)
-        g = _full_backward(C, s, t, fwd, dpix)
+        fwd = _forward(C, s, t, deg)
+        g = _full_backward(C, s, t, fwd, dpix, deg)
         # (dL_dmeans3D, dL_dsh, dL_dopacity, dL_dscales, dL_drotations) of this view
         per = [g[3], g[5], g[2], g[6], g[7]]
         want = [x.double().clone() for x in per] if want is None else [a + x.double() for a, x in zip(want, per)]
@@ -65,7 +66,7 @@ def test_multiview_equals_sum_of_view_backwards(yaws):
         records.append(DP.view_record(s, fwd[2], fwd[3], fwd[0], fwd[4], fwd[5], dpix))
     views = torch.stack(records)
     stats = [torch.zeros(P, device="cuda") for _ in range(3)]
-    got = DP.multiview_param_grads(views, t["means3D"], t["shs"], 3, t["scales"], t["rotations"], 1.0,
+    got = DP.multiview_param_grads(views, t["means3D"], t["shs"], deg, t["scales"], t["rotations"], 1.0,
                                    stats=tuple(stats))
     torch.cuda.synchronize()
     names = ("dL_dmeans3D", "dL_dsh", "dL_dopacity", "dL_dscales", "dL_drotations")
@@ -152,3 +153,38 @@ def test_multiview_more_than_64_views():
     torch.cuda.synchronize()
     for a, b in zip(got, outs):
         assert torch.equal(a.reshape(-1), b.reshape(-1))
+
+
+@pytest.mark.parametrize("n_streams", [2, 3])
+def test_views_on_streams_match_one_stream(n_streams):
+    """data_parallel.run_views_on_streams (config 5's step): the views'
+    forward + blend backward alternating over HIP streams give the records
+    and parameter gradients of the one-stream loop (float-atomic order noise:
+    1e-5 relative)."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    P, W, H = 30000, 320, 240
+    yaws = (-9.0, -3.0, 2.0, 6.0, 11.0)
+    sc, cams = _views(P, W, H, yaws)
+    t = G.scene_tensors(sc)
+    sets = [G.torch_settings(c) for c in cams]
+    dpix = [torch.from_numpy(S.make_cotangent(H, W, 50 + v)).cuda() for v in range(len(cams))]
+
+    def step(ns):
+        ex = DP.ViewExchange(P, len(cams), "cuda")
+
+        def one(j):
+            fwd = _forward(C, sets[j], t)
+            ex.add(j, DP.view_record(sets[j], fwd[2], fwd[3], fwd[0], fwd[4], fwd[5], dpix[j]))
+
+        DP.run_views_on_streams(len(cams), one, ns)
+        out = ex.finish(sets[0], t["means3D"], t["shs"], t["scales"], t["rotations"])
+        return ex.records(), out
+
+    rec1, g1 = step(1)
+    rec2, g2 = step(n_streams)
+    torch.cuda.synchronize()
+    assert G.rel_err(rec2.cpu().numpy(), rec1.cpu().numpy()) < REL
+    for a, b in zip(g2, g1):
+        assert G.rel_err(a.cpu().numpy(), b.cpu().numpy()) < REL

@@ -340,7 +340,7 @@ def test_config2_full_size_parity_and_psnr():
         assert G.rel_err(g.cpu().numpy(), rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(g.cpu().numpy(), rg[n]))
 
 
-@pytest.mark.parametrize("bwd_variant", [0, 1, 2])
+@pytest.mark.parametrize("bwd_variant", [0, 1])  # the fallback and the default (opacity-scaled sums)
 @pytest.mark.parametrize("fwd_variant", [0, 1])
 def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
     """The default and the fallback forward / backward blends (gs_set_tuning),
