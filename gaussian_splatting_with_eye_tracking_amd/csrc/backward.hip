@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ bg,
     float* __restrict__ grad_accum, int cull, int gx, int amr_mode, const uint32_t* __restrict__ levels,
     const uint32_t* __restrict__ bucket_count, const uint32_t* __restrict__ bucket_list,
-    const uint8_t* __restrict__ hit_codes, const uint32_t* __restrict__ hdr) {
+    const uint32_t* __restrict__ hdr) {
 #pragma clang fp contract(fast)
     static_assert(!(kSel && kAMR), "the AMR backward is the fallback form");
     constexpr int kB = 64;  // Gaussians per LDS batch
@@ -205,7 +205,9 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
     // Row masks: the forward's exact hit codes when it left them (gs_blend.cuh
     // blend_tile_t: bit r = row group r has a pixel that blended the entry,
     // i.e. a pixel this backward takes it at), else the geometric cull.
-    const bool use_codes = !kAMR && hit_codes != nullptr && hdr != nullptr && hdr[kHdrHitCodes] == 1u;
+    // (where the forward stored them: the header word, gs_layout.h hit_codes_of)
+    const uint8_t* const codes = (!kAMR && hdr != nullptr) ? hit_codes_of(point_list, hdr[kHdrHitCodes]) : nullptr;
+    const bool use_codes = codes != nullptr;
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
     const int comp = lane & 15;
@@ -268,7 +270,7 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
             if constexpr (kSel)  // the reference's `power > 0` skip cannot fire (gs_blend.cuh)
                 fastg = splat_form_safe(pc, fabsf(xy.x - (float)ox), fabsf(xy.y - (float)oy)) &&
                         (!kOpT || (pc.w <= 0.99f && pc.w > 0.0f));
-            gm = use_codes ? (uint32_t)hit_codes[range.x + top - 1 - tid]
+            gm = use_codes ? (uint32_t)codes[range.x + top - 1 - tid]
                  : cull ? splat_group_mask(xy, co, (float)ox, (float)oy, (float)pstride) : 0xfu;
         }
         const int ntop = top - kB;  // the next batch: entries [ntop - ncnt, ntop)
@@ -599,7 +601,7 @@ void set_backward_variant(int v) { g_bwd_variant = v == 0 ? 0 : kDefaultBwdVaria
 
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s, int K) {
-    const size_t hit_codes_k = (size_t)(K > 0 ? K : 0);  // (the forward's instance count: where its codes are)
+    (void)K;  // (the forward's hit codes are found through the header, gs_layout.h hit_codes_of)
     const int gx = (W + 15) / 16, gy = (H + 15) / 16;
     if (gx == 0 || gy == 0) return;
     // tiles heaviest first: the forward render filled this image buffer's 256
@@ -612,7 +614,7 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
                        b.point_list, reinterpret_cast<const float2*>(g.means2D),                                   \
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,    \
                        dL_dpix, bg, g.grad_accum, g_cull, gx, 0, nullptr, img.bucket_count, img.bucket_list,       \
-                       hit_codes_at(b.point_list, hit_codes_k), g.hdr)
+                       g.hdr)
     if (g_bwd_variant == 0) GS_BWD_LAUNCH(false);
     else GS_BWD_LAUNCH(true, false, true);
 #undef GS_BWD_LAUNCH
@@ -630,7 +632,7 @@ void launch_amr_render_backward(int W, int H, int mode, const ImageView& img, co
     hipLaunchKernelGGL((render_bwd_kernel<false, true>), dim3(4 * tgx * tgy), dim3(64), 0, s, W, H, img.ranges,
                        img.max_contrib, b.point_list, reinterpret_cast<const float2*>(g.means2D),
                        reinterpret_cast<const float4*>(g.conic_opacity), colors, img.accum_alpha, img.n_contrib,
-                       dL_dpix, bg, g.grad_accum, g_cull, tgx, mode, img.levels, nullptr, nullptr, nullptr, nullptr);
+                       dL_dpix, bg, g.grad_accum, g_cull, tgx, mode, img.levels, nullptr, nullptr, nullptr);
 }
 
 // ------------------------------------------------------ per-Gaussian bwd ---

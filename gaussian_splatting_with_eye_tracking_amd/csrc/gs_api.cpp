@@ -457,7 +457,7 @@ struct Binned {
 // and run while the host waits for it.
 Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const gs_buffer& binning,
                           const gs_buffer& image, int* radii, int tile, bool debug, hipStream_t s,
-                          const std::function<void(Binned&)>& before_k = nullptr) {
+                          const std::function<void(Binned&)>& before_k = nullptr, int fused_sort_max = 0) {
     Binned r;
     const int W = in.width, H = in.height;
     const int gx = (W + tile - 1) / tile, gy = (H + tile - 1) / tile;
@@ -533,7 +533,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     if (r.K > 0) {
         if (!dup_done) { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, (uint32_t)r.K); }
         stage_check(debug, s, "duplicate");
-        { StageTimer _t(kSort, s); launch_sort_tiles(r.T, r.img, r.b, (int)hdr[kHdrMaxTileCount], (int)hdr[kHdrNumLargeTiles], s); }
+        { StageTimer _t(kSort, s); launch_sort_tiles(r.T, r.img, r.b, (int)hdr[kHdrMaxTileCount], (int)hdr[kHdrNumLargeTiles], s, fused_sort_max); }
         stage_check(debug, s, "sort_tiles");
     }
     return r;
@@ -582,7 +582,7 @@ int gs_rasterizer_forward(gs_buffer geometry, gs_buffer binning, gs_buffer image
             const bool zero = t_fwd_zero && t_store_drgb;
             zeroed = launch_render_forward(width, height, r.img, r.b, r.g, feats, background, out_color, s,
                                            zero ? r.g.grad_accum : nullptr, zero ? (size_t)kGradRow * (size_t)P : 0,
-                                           hit_codes_at(r.b.point_list, (size_t)r.K));
+                                           reinterpret_cast<uint8_t*>(r.b.scratch));
         }
         if (zeroed) set_accum_clean(r.g.grad_accum, true);
         stage_check(debug != 0, s, "render");
@@ -1061,7 +1061,10 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
             if (g_amr_variant == 4) launch_order_tiles(r.T, r.img, false, s);
             if (foveaStep != 0) launch_fovea_levels(foveaStep, r.T, r.img, s);
         };
-        Binned r = preprocess_and_bin(in, geometry, binning, image, radii, tile, dbg, s, before_k);
+        // the region-list pass sorts the tiles of <= kAmrFusedSortMax instances itself
+        const bool fuse = g_amr_variant == 4 && fused_sort_on();
+        Binned r = preprocess_and_bin(in, geometry, binning, image, radii, tile, dbg, s, before_k,
+                                      fuse ? kAmrFusedSortMax : 0);
         // (the geometry buffer's own copy of the radii -- the progressive steps
         // return zero radii as the reference does, and the AMR backward of a
         // step reads the step-0 radii from there -- is written by the preprocess)
@@ -1070,7 +1073,7 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
             // the AMR blend's work units: tiles heaviest first (ordered above)
             // and their sub-lists: the 8x8 regions + blend records of the AMR
             // binning layout
-            { StageTimer _t(kAmrLists, s); launch_amr_region_lists(W, H, r.img, r.b, r.ab, r.g, feats, r.K, s); }
+            { StageTimer _t(kAmrLists, s); launch_amr_region_lists(W, H, r.img, r.b, r.ab, r.g, feats, r.K, s, fuse); }
             stage_check(dbg, s, "amr_lists");
         }
         if (foveaStep == 0) return r.K;  // step 0: buffers only, a zero image (amr/cr/rasterizer_impl.cu:651)

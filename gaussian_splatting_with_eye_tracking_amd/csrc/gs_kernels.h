@@ -81,14 +81,21 @@ bool dup_banded(int gx, int gy, int block);           // the row-banded duplicat
 // (The AMR units' order; the base backward takes its order from the forward
 // render's work buckets.)
 void launch_order_tiles(int T, const ImageView& img, bool use_max_contrib, hipStream_t s);
+// fused_max: tiles of <= fused_max instances (0 or kAmrFusedSortMax) are
+// left to the kernel that consumes them first -- the AMR region-list pass
+// (amr_region_lists_kernel kFuse) -- which sorts its own tile.
 void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int max_count_host, int num_large_host,
-                       hipStream_t s);
+                       hipStream_t s, int fused_max = 0);
+constexpr int kAmrFusedSortMax = 2048;
+bool fused_sort_on();  // the AMR region-list pass sorts its tiles of <= kAmrFusedSortMax instances itself
 // (tile << 32 | depth) reconstruction of the reference's point_list_keys.
 void launch_reconstruct_keys(int T, const ImageView& img, const BinningView& b, const GeomView& g, uint64_t* keys,
                              hipStream_t s);
 
 // Blend (base/cr/forward.cu:261-374).  zero_rows: zeroed (zero_floats,
 // a multiple of 4, 16-B aligned) by the same launch; returns whether it was.
+// hit_codes: where the render stores its row-group hit codes (the binning
+// scratch, gs_layout.h hit_codes_of; null: none).
 bool launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                            const float* features, const float* bg, float* out_color, hipStream_t s,
                            float* zero_rows = nullptr, size_t zero_floats = 0, uint8_t* hit_codes = nullptr);
@@ -192,8 +199,10 @@ void launch_eye_preprocess(const uint8_t* gray, int H, int W, const uint8_t* gam
 // zero_image (optional): foveaStep 0's zero image, written by the same launch
 void launch_amr_levels(int T, const ImageView& img, hipStream_t s, float* zero_image = nullptr, size_t zero_floats = 0);
 // The 8x8-region sub-lists and per-instance blend records (variant 4).
+// fused_sort: tiles of <= kAmrFusedSortMax instances arrive unsorted
+// (launch_sort_tiles fused_max) and are sorted by the launch itself.
 void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningView& b, const AmrBinningView& ab,
-                             const GeomView& g, const float* features, int K, hipStream_t s);
+                             const GeomView& g, const float* features, int K, hipStream_t s, bool fused_sort = false);
 extern int g_amr_variant;
 void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s, int P = 0, int* zero_radii = nullptr);
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,

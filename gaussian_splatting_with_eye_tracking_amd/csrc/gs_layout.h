@@ -41,7 +41,7 @@ enum HdrWord : int {
     kHdrNumLargeTiles = 3,
     kHdrP = 4,
     kHdrT = 5,
-    kHdrHitCodes = 6,     // 1: the base forward render stored exact row-group hit codes (hit_codes_of)
+    kHdrHitCodes = 6,     // != 0: where the base forward render stored exact row-group hit codes (hit_codes_of)
     kHdrDrgb = 7,         // 1: the preprocess stored d(rgb)/d(view dir) of every visible Gaussian (GeomView::drgb)
     kHdrWords = 64,
 };
@@ -80,7 +80,8 @@ struct GeomView {
 // only when the header / the request says they were written.
 // AMR buffers (amr: 32-px tiles) always carry the tail and then amr_rows: one
 // 64-B row per Gaussian -- (x, y, r, g), the log2(e)-scaled conic + opacity,
-// (b, raw conic) and a zero pad -- which the AMR preprocess writes and
+// (b, the alpha >= 1/255 box's half-widths and threshold), (the edge-minimum
+// slopes, 0, 0) (gs_blend.cuh amr_row_box) -- which the AMR preprocess writes and
 // foveaStep 0's region-list pass gathers, one aligned 64-B sector per
 // instance (48-B rows straddled two sectors in most rows: 286 MB of traffic
 // per launch for ~106 MB of rows at config 3, profiles/r04zf_cfg3_pmc_summary.json).
@@ -176,15 +177,21 @@ struct BinningView {
     uint64_t* scratch;     // [K]  merge-sort ping-pong
 };
 
-// Base forward: once the tile lists are sorted, pair_keys is dead; K bytes at
-// the offset a K-entry carve gives pair_keys hold the render's exact row-group
-// hit code of every sorted instance (bit r: row group r of the tile has a
-// pixel that blended it), which the backward uses as its row masks.  The
-// offset comes from K, not from the buffer's carve: the speculative
-// duplicate carves the forward's buffer for a capacity >= K, while the
-// backward carves it for K (both leave point_list at 0).
-inline uint8_t* hit_codes_at(uint32_t* point_list, size_t K) {
-    return reinterpret_cast<uint8_t*>(point_list) + align_up(sizeof(uint32_t) * K);
+// Base forward: the render's exact row-group hit code of every sorted
+// instance (1 B; bit r: row group r of the tile has a pixel that blended it),
+// which the backward uses as its row masks, lives in the forward's binning
+// scratch -- dead once the duplicate and the large-tile merges are done; not
+// pair_keys, which the render still reads while it writes codes (it sorts its
+// own small tiles, render.hip kFuse).  The header word kHdrHitCodes says
+// where: 0 = no codes, else 1 + (byte offset from point_list) / kAlign.  The
+// offset cannot come from K: a speculative forward carves the buffer for a
+// capacity >= K (its scratch further out), the backward carves it for K; both
+// leave point_list at 0.
+inline uint32_t hit_codes_word(const uint32_t* point_list, const uint8_t* codes) {
+    return codes ? 1u + (uint32_t)((size_t)(codes - reinterpret_cast<const uint8_t*>(point_list)) / kAlign) : 0u;
+}
+__host__ __device__ inline const uint8_t* hit_codes_of(const uint32_t* point_list, uint32_t word) {
+    return word ? reinterpret_cast<const uint8_t*>(point_list) + (size_t)(word - 1u) * kAlign : nullptr;
 }
 
 // AMR (32-px tiles): once the tile lists are sorted, pair_keys and scratch

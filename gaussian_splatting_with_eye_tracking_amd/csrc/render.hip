@@ -17,6 +17,7 @@
 #include "gs_blend.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
+#include "gs_tilesort.cuh"
 
 namespace gsamd {
 
@@ -45,6 +46,12 @@ __device__ __forceinline__ void write_pixels(const PixelSetT<kPPL>& px, const Bl
 }
 
 // One 16x16 tile per workgroup of kWaves waves (kPPL pixels per lane).
+// (A form that sorted its own tile of <= 1024 instances before blending it,
+// in LDS the batches reuse, measured 0.9978 -> 0.9948 ms per config-2 step
+// and 2.4819 -> 2.4954 at config 4 -- the sort's latency hides behind the
+// other workgroups' blending, but its LDS and registers cost the blend
+// occupancy; profiles/r05g_ab_fuse*.log.  The AMR region-list pass keeps it,
+// amr_region_lists_kernel.)
 template <int kPPL, int kWaves, int kMinWaves = 1, bool kSel = false>
 __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
                                                                  const uint32_t* __restrict__ point_list,
@@ -60,7 +67,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
                                                                  uint32_t* __restrict__ bucket_count,
                                                                  uint32_t* __restrict__ bucket_list,
                                                                  uint8_t* __restrict__ hit_codes,
-                                                                 uint32_t* __restrict__ hdr) {
+                                                                 uint32_t* __restrict__ hdr, uint32_t hit_word) {
     // The backward's per-Gaussian accumulator rows (grad_accum, idle in the
     // base forward) are zeroed here, behind the blend, instead of by a memset
     // on the backward's critical path: fire-and-forget stores in a kernel
@@ -79,7 +86,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
     if (kWaves > 1 && threadIdx.x == 0) s_max = 0;
     // whether this forward leaves exact row-group hit codes for the backward
     // (the select form records them; the fallback leaves 0)
-    if (hdr && blockIdx.x == 0 && threadIdx.x == 0) hdr[kHdrHitCodes] = (kSel && hit_codes) ? 1u : 0u;
+    if (hdr && blockIdx.x == 0 && threadIdx.x == 0) hdr[kHdrHitCodes] = (kSel && hit_codes) ? hit_word : 0u;
     const int tile = xcd_block_tile((int)blockIdx.x, gx, (int)(gridDim.x / gx));
     const uint32_t ox = (uint32_t)(tile % gx) * 16, oy = (uint32_t)(tile / gx) * 16;
     const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, 1);
@@ -149,7 +156,7 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
                        b.point_list, reinterpret_cast<const float2*>(g.means2D), features,                       \
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib,         \
                        img.max_contrib, bg, out_color, g_cull, gx, zero4, zero_n4,                               \
-                       img.bucket_count, img.bucket_list, hit_codes, g.hdr)
+                       img.bucket_count, img.bucket_list, hit_codes, g.hdr, hit_codes_word(b.point_list, hit_codes))
     if (g_fwd_variant == 0) GS_FWD_LAUNCH(4, 1);
     else GS_FWD_LAUNCH(1, 4, 8, true);  // <= 64 VGPRs: 8 waves per SIMD
 #undef GS_FWD_LAUNCH
@@ -231,8 +238,8 @@ constexpr int kRlPer = 2;
 // Region mask of one entry: the exact ellipse test (splat_rect_hit) on the
 // four 16x16 quadrants, refined to the 8x8 regions by the alpha >= 1/255
 // ellipse's bounding box (both conservative).  Bit g = 4 row + col.
-__device__ __forceinline__ uint32_t region_mask(float2 xy, float4 co, float ox, float oy) {
-    const SplatBox b = splat_box(xy, co);
+__device__ __forceinline__ uint32_t region_mask(const SplatBox& b, float ox, float oy) {
+    const float2 xy = b.xy;
     uint32_t qm = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -258,17 +265,28 @@ __device__ __forceinline__ uint32_t region_mask(float2 xy, float4 co, float ox, 
 }
 
 // rows: the per-Gaussian 64-B blend rows the AMR preprocess wrote
-// (GeomView::amr_rows): (x, y, r, g), splat_coef, (b, raw conic), pad.
+// (GeomView::amr_rows): (x, y, r, g), splat_coef, (b, box half-widths,
+// threshold), (edge slopes, 0, 0) -- gs_blend.cuh amr_row_box.
+// kFuse (the default): a tile of 2..kAmrFusedSortMax instances arrives
+// unsorted in pair_keys; the workgroup sorts it first (gs_tilesort.cuh bucket
+// sort, 8 keys per thread), writes point_list and walks the sorted ids from
+// LDS (no separate sort launches below 2048 instances, no point_list re-read).
+template <bool kFuse>
 __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, const uint32_t* __restrict__ ranges,
-                                                                      const uint32_t* __restrict__ point_list,
+                                                                      uint32_t* __restrict__ point_list,
                                                                       const float4* __restrict__ rows,
                                                                       float4* __restrict__ rec_a,
                                                                       float4* __restrict__ rec_b,
                                                                       float* __restrict__ rec_c,
                                                                       uint32_t* __restrict__ lists,
                                                                       uint32_t* __restrict__ region_count,
-                                                                      uint32_t* __restrict__ tile_done, int tgy) {
+                                                                      uint32_t* __restrict__ tile_done, int tgy,
+                                                                      const uint64_t* __restrict__ pair_keys) {
     constexpr int kW = kRlThreads / 64;
+    static_assert(kRlThreads == 256, "the fused sort's workgroup");
+    using SortL = TileSortLds<256, kAmrFusedSortMax / 256, 1>;
+    __shared__ SortL s_sort[1];
+    __shared__ uint32_t s_ids[kFuse ? kAmrFusedSortMax : 1];
     // per pass: hits of (slot e, region g, wave w), then their exclusive
     // offsets in the pass's (e, w) order, per region
     __shared__ uint32_t s_cnt[16][kRlPer * kW];
@@ -279,6 +297,21 @@ __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, c
     const int n = (int)(ranges[2 * tile + 1] - beg);
     const float ox = (float)((tile % tgx) * 32), oy = (float)((tile / tgx) * 32);
     uint32_t* out = lists + 16 * (size_t)beg;
+    const uint32_t* ids = point_list + beg;  // (kFuse and n <= kAmrFusedSortMax: the LDS copy below)
+    if constexpr (kFuse) {
+        if (n >= 2 && n <= kAmrFusedSortMax) {  // block-uniform
+            tile_bucket_sort<256, kAmrFusedSortMax / 256, 1>(pair_keys + beg, n, point_list + beg, s_sort[0], s_ids);
+            ids = s_ids;
+        } else if (n == 1) {
+            if (tid == 0) {
+                const uint32_t v = (uint32_t)pair_keys[beg];
+                point_list[beg] = v;
+                s_ids[0] = v;
+            }
+            ids = s_ids;
+        }
+        __syncthreads();  // the LDS ids
+    }
     if (tid < 16) s_base[tid] = 0;
     const uint64_t below = (1ull << lane) - 1ull;
     for (int c0 = 0; c0 < n; c0 += kRlThreads * kRlPer) {
@@ -290,13 +323,13 @@ __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, c
             const int i = c0 + e * kRlThreads + tid;
             m[e] = 0;
             if (i < n) {
-                const uint32_t id = point_list[beg + i];
+                const uint32_t id = ids[i];
                 const float4* rr = rows + (size_t)4 * id;
-                const float4 ra = rr[0], rb = rr[1], rc = rr[2];
+                const float4 ra = rr[0], rb = rr[1], rc = rr[2], rd = rr[3];
                 rec_a[beg + i] = ra;
                 rec_b[beg + i] = rb;
                 rec_c[beg + i] = rc.x;
-                m[e] = region_mask(make_float2(ra.x, ra.y), make_float4(rc.y, rc.z, rc.w, rb.w), ox, oy);
+                m[e] = region_mask(amr_row_box(ra, rb, rc, rd), ox, oy);
             }
 #pragma unroll
             for (int g = 0; g < 16; g++) {
@@ -333,7 +366,7 @@ __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, c
 }
 
 void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningView& b, const AmrBinningView& ab,
-                             const GeomView& g, const float* features, int K, hipStream_t s) {
+                             const GeomView& g, const float* features, int K, hipStream_t s, bool fused_sort) {
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0) return;
     if (K == 0) {  // no lists to build; the counts must still read 0
@@ -343,9 +376,13 @@ void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningVi
         return;
     }
     (void)features;  // in the rows (the preprocess saw colors_precomp / the SH colours)
-    hipLaunchKernelGGL(amr_region_lists_kernel, dim3(tgx * tgy), dim3(kRlThreads), 0, s, tgx, img.ranges,
-                       b.point_list, reinterpret_cast<const float4*>(g.amr_rows), ab.rec_a, ab.rec_b, ab.rec_c,
-                       ab.region_lists, img.region_count, img.tile_done, tgy);
+#define GS_RL_LAUNCH(F)                                                                                           \
+    hipLaunchKernelGGL(amr_region_lists_kernel<F>, dim3(tgx * tgy), dim3(kRlThreads), 0, s, tgx, img.ranges,      \
+                       b.point_list, reinterpret_cast<const float4*>(g.amr_rows), ab.rec_a, ab.rec_b, ab.rec_c,   \
+                       ab.region_lists, img.region_count, img.tile_done, tgy, b.pair_keys)
+    if (fused_sort) GS_RL_LAUNCH(true);
+    else GS_RL_LAUNCH(false);
+#undef GS_RL_LAUNCH
 }
 
 // One wave per (tile, quadrant): its four 16-lane groups are the quadrant's

@@ -668,11 +668,17 @@ py::dict ParseBuffers(const Tensor& geomBuffer, const Tensor& binningBuffer, con
     }
     if (K > 0) {
         d["point_list"] = view(b.point_list, {K}, i32);
-        // the forward's per-instance row-group hit codes (base grid; valid when hdr[kHdrHitCodes] == 1)
-        // (gs_layout.h hit_codes_at: right after point_list, 256-B aligned)
-        if (tile == 16)
-            d["hit_codes"] = view(reinterpret_cast<uint8_t*>(b.point_list) + ((sizeof(uint32_t) * (size_t)K + 255) & ~(size_t)255),
-                                  {K}, o.dtype(torch::kUInt8));
+        // the forward's per-instance row-group hit codes (base grid), where
+        // the header word says they are (gs_layout.h hit_codes_of: 0 = none,
+        // else 1 + byte offset from point_list / 256)
+        if (tile == 16) {
+            uint32_t w = 0;
+            TORCH_CHECK(hipMemcpy(&w, g.hdr + 6, sizeof(uint32_t), hipMemcpyDeviceToHost) == hipSuccess,
+                        "parse_buffers: header read-back failed");
+            const size_t off = w ? (size_t)(w - 1u) * 256u : 0u;
+            if (w && off + (size_t)K <= (size_t)binningBuffer.numel())
+                d["hit_codes"] = view(reinterpret_cast<uint8_t*>(b.point_list) + off, {K}, o.dtype(torch::kUInt8));
+        }
         Tensor keys = torch::empty({K}, o.dtype(torch::kInt64));
         check(gs_reconstruct_keys(reinterpret_cast<char*>(geomBuffer.data_ptr()),
                                   reinterpret_cast<char*>(binningBuffer.data_ptr()),

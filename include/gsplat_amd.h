@@ -28,9 +28,11 @@
 extern "C" {
 #endif
 
-#define GSPLAT_AMD_ABI_VERSION 6  /* 4: drgb / cov3D moved to an optional tail of the geometry buffer;
+#define GSPLAT_AMD_ABI_VERSION 7  /* 4: drgb / cov3D moved to an optional tail of the geometry buffer;
                                      5: grad_accum rows of GSPLAT_AMD_GRAD_ROW = 12 floats (were 16);
-                                     6: AMR geometry buffers end with 64-B blend rows (amr_rows) */
+                                     6: AMR geometry buffers end with 64-B blend rows (amr_rows);
+                                     7: the base forward's hit codes in the binning scratch, located by
+                                        header word 6 (1 + byte offset from point_list / 256) */
 /* floats per grad_accum row of the geometry buffer (gs_geom_view.grad_accum) */
 #define GSPLAT_AMD_GRAD_ROW 12
 

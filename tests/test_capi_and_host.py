@@ -63,7 +63,7 @@ def test_host_layout_helpers():
     # 2: gs_image_view gained the band arrays; 3: gs_geom_view gained drgb;
     # 4: drgb and cov3D moved to an optional tail of the geometry buffer;
     # 5: 48-B grad_accum rows
-    assert lib.gs_abi_version() == 6
+    assert lib.gs_abi_version() == 7
     g1, g2 = lib.gs_geom_bytes(1000), lib.gs_geom_bytes(2000)
     assert g2 > g1 > 1000 * (4 + 4 + 8 + 16 + 12 + 24 + 1 + 48 + 4 + 48)
     assert lib.gs_image_bytes(1920, 1080, 16) >= 1920 * 1080 * 8 + 120 * 68 * 8
@@ -115,7 +115,7 @@ def test_torch_extension_surface():
               "distCUDA2", "parse_buffers", "profile_enable", "profile_read", "set_tuning",
               "set_thread_option"):
         assert hasattr(_C, n), n
-    assert _C.abi_version() == 6
+    assert _C.abi_version() == 7
     assert all(os.path.exists(p) and p.startswith(ROOT) for p in native_library_paths())
 
 

@@ -196,4 +196,4 @@ def test_default_forward_bit_identical_to_fallback(P, W, H, seed, adv):
     np.testing.assert_array_equal(res[1][0], res[0][0])
     for k in res[1][1]:
         np.testing.assert_array_equal(res[1][1][k], res[0][1][k], err_msg=k)
-    assert (res[1][2], res[0][2]) == (1, 0)  # header word kHdrHitCodes
+    assert res[1][2] != 0 and res[0][2] == 0  # header word kHdrHitCodes (where the codes are; 0: none)

@@ -959,3 +959,79 @@ def test_forward_only_hint_cleared_when_the_forward_raises():
                                 s.debug)
     torch.cuda.synchronize()
     assert int(C.parse_buffers(out[3], out[4], out[5], P, 0, W, H, 16)["hdr"][7].item()) == 1
+
+
+def test_hit_codes_and_point_list_repeatable():
+    """The forward render stores its row-group hit codes in the binning
+    scratch and says where in header word 6 (gs_layout.h hit_codes_of).
+    Twenty forwards of a scene with few, full tiles (96 tiles, some above
+    1024 instances) give the bitonic sort's point_list (sort_algo 0) every
+    time, and the default backward (reading the codes) matches the fallback
+    backward kernel to float-atomic noise."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
+    P, W, H = 12000, 192, 128
+    sc = S.make_scene(P, S.make_camera(W, H), seed=3)
+    cam = S.make_orbit_camera(W, H, 4.0)
+    s = G.torch_settings(cam)
+    t = G.scene_tensors(sc)
+    e = torch.Tensor([])
+
+    def fwd():
+        return C.rasterize_gaussians(s.bg, t["means3D"], e, t["opacities"], t["scales"], t["rotations"], 1.0, e,
+                                     s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, H, W, t["shs"], 3, s.campos,
+                                     False, False)
+
+    C.set_tuning("sort_algo", 0)
+    try:
+        K0, c0, r0, g0, b0, i0 = fwd()
+        want = C.parse_buffers(g0, b0, i0, P, K0, W, H, 16)["point_list"].cpu()
+    finally:
+        C.set_tuning("sort_algo", 1)
+    dpix = torch.from_numpy(S.make_cotangent(H, W, 7)).cuda()
+    for _ in range(20):
+        K, color, radii, geom, binning, img = fwd()
+        assert K == K0
+        d = C.parse_buffers(geom, binning, img, P, K, W, H, 16)
+        assert torch.equal(d["point_list"].cpu(), want)
+        assert torch.equal(color.cpu(), c0.cpu())
+        assert int(d["hdr"][6].item()) != 0 and "hit_codes" in d
+    g = C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, e, t["scales"], t["rotations"], 1.0, e,
+                                       s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, dpix, t["shs"], 3,
+                                       s.campos, geom, K, binning, img, False)
+    C.set_tuning("bwd_variant", 0)
+    try:
+        gf = C.rasterize_gaussians_backward(s.bg, t["means3D"], radii, e, t["scales"], t["rotations"], 1.0, e,
+                                            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, dpix, t["shs"], 3,
+                                            s.campos, geom, K, binning, img, False)
+    finally:
+        C.set_tuning("bwd_variant", -1)
+    torch.cuda.synchronize()
+    for a, b in zip(g[:3], gf[:3]):  # dL_dmeans2D, dL_dcolors, dL_dopacity
+        assert G.rel_err(a.cpu().numpy(), b.cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("P,W,H,seed", [(10000, 256, 256, 0), (60000, 160, 96, 4), (3000, 2112, 1056, 8)])
+def test_amr_fused_tile_sort_matches_separate_sort(P, W, H, seed):
+    """The AMR region-list pass sorts the tiles of <= 2048 instances itself
+    (render.hip amr_region_lists_kernel kFuse; larger ones by the size-class
+    launches): point_list, the records, the region lists and every step image
+    equal the separately sorted build's (sort_algo 0: bitonic networks, no
+    fusion) bit for bit, repeatedly."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    sc, cam = G.scene_and_camera(P, W, H, seed)
+    out = {}
+    for algo in (0, 1, 1):
+        C.set_tuning("sort_algo", algo)
+        try:
+            acc, radii, steps, (gb, bb, ib) = _amr_gpu_steps(sc, cam, bg=(0.1, 0.2, 0.3))
+        finally:
+            C.set_tuning("sort_algo", 1)
+        K = int(C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)["hdr"][0].item())
+        d = C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
+        r = [d["point_list"].cpu(), d["region_count"].cpu()] + [s_.cpu() for s_ in steps]
+        if 0 in out:
+            for a_, b_ in zip(r, out[0]):
+                assert torch.equal(a_, b_)
+        else:
+            out[0] = r
