@@ -675,7 +675,9 @@ def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange
     e0 = torch.empty(0, device=ctx.dev)
     pg = params
 
-    vs = {"n": max(1, int(getattr(ctx.args, "view_streams", 2)))}
+    # (3 streams: 1362.7 views/s at config 5 on one GPU; 2: 1340; 1: 1242.6;
+    # 4: 1363.1 -- profiles/r05j_bench5_vs*.log)
+    vs = {"n": max(1, int(getattr(ctx.args, "view_streams", 3)))}
 
     def step_views():
         # each view's record is all-gathered as soon as it exists (overlapping
@@ -985,7 +987,7 @@ def parse_args(argv=None):
     ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
                     help="default: cfg2_1080p_1M at N = 1, cfg5_8view_1080p_1M at N > 1")
     ap.add_argument("--views", type=int, default=8, help="config 5: global views per step")
-    ap.add_argument("--view-streams", type=int, default=2,
+    ap.add_argument("--view-streams", type=int, default=3,
                     help="config 5: HIP streams the rank's views alternate over (1: one stream)")
     ap.add_argument("--ramp-ms", type=float, default=100.0,
                     help="after the W warmup steps, untimed steps for about this long so the GPU clocks "

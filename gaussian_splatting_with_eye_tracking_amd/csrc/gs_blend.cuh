@@ -240,28 +240,6 @@ __device__ __forceinline__ bool splat_rect_hit(const SplatBox& b, float x0, floa
     return !(q > b.thr);  // NaN -> kept
 }
 
-// The AMR blend row's encoding of a SplatBox (preprocess.hip, render.hip
-// amr_region_lists_kernel): `never` as half-widths of -inf (every box test
-// misses), `!ok` as a threshold of +inf (every edge test keeps it); the
-// conic comes back from the row's log2(e)-scaled copy (a few ulp: far inside
-// the threshold's 2 % slack).
-__device__ __forceinline__ float amr_row_hx(const SplatBox& b) { return b.never ? -__builtin_inff() : b.hx; }
-__device__ __forceinline__ float amr_row_hy(const SplatBox& b) { return b.never ? -__builtin_inff() : b.hy; }
-__device__ __forceinline__ float amr_row_thr(const SplatBox& b) { return b.ok ? b.thr : __builtin_inff(); }
-__device__ __forceinline__ SplatBox amr_row_box(float4 ra, float4 rb, float4 rc, float4 rd) {
-    SplatBox b;
-    b.xy = make_float2(ra.x, ra.y);
-    b.co = make_float4(rb.x * (-1.0f / kHalfLog2e), rb.y * (-1.0f / kLog2e), rb.z * (-1.0f / kHalfLog2e), rb.w);
-    b.hx = rc.y;
-    b.hy = rc.z;
-    b.thr = rc.w;
-    b.kyx = rd.x;
-    b.kxy = rd.y;
-    b.ok = true;
-    b.never = false;
-    return b;
-}
-
 // Bit r set when the Gaussian can reach row group r of the 16x16 block at
 // (ox, oy) with pixel stride st (1 = base, 2 = AMR sub-lattice).
 __device__ __forceinline__ uint32_t splat_group_mask(float2 xy, float4 co, float ox, float oy, float st) {

@@ -80,8 +80,7 @@ struct GeomView {
 // only when the header / the request says they were written.
 // AMR buffers (amr: 32-px tiles) always carry the tail and then amr_rows: one
 // 64-B row per Gaussian -- (x, y, r, g), the log2(e)-scaled conic + opacity,
-// (b, the alpha >= 1/255 box's half-widths and threshold), (the edge-minimum
-// slopes, 0, 0) (gs_blend.cuh amr_row_box) -- which the AMR preprocess writes and
+// (b, raw conic) and a zero pad -- which the AMR preprocess writes and
 // foveaStep 0's region-list pass gathers, one aligned 64-B sector per
 // instance (48-B rows straddled two sectors in most rows: 286 MB of traffic
 // per launch for ~106 MB of rows at config 3, profiles/r04zf_cfg3_pmc_summary.json).

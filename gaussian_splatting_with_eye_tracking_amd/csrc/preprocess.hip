@@ -215,11 +215,7 @@ __device__ __forceinline__ void pp_gaussian(const PreprocessArgs& a, const GeomV
         // AMR: the blend record of this Gaussian as ONE 64-B row (GeomView::
         // amr_rows), so foveaStep 0's region-list pass (render.hip) gathers one
         // aligned sector per instance instead of three records: (x, y, r, g),
-        // the log2(e)-scaled conic + opacity, (b, the alpha >= 1/255 box's
-        // half-widths and threshold), (the edge-minimum slopes, 0, 0) -- the
-        // per-Gaussian part of the region test (gs_blend.cuh splat_box),
-        // computed once here instead of once per instance (~2.6 per visible
-        // Gaussian at config 3).
+        // the log2(e)-scaled conic + opacity, (b, raw conic), zero pad.
         float r_, g_, b_;
         if (kHasSH) {
             r_ = rgbv.x; g_ = rgbv.y; b_ = rgbv.z;
@@ -229,11 +225,10 @@ __device__ __forceinline__ void pp_gaussian(const PreprocessArgs& a, const GeomV
         float4* row = stage ? reinterpret_cast<float4*>(stage + 16)
                             : reinterpret_cast<float4*>(g.amr_rows + (size_t)16 * idx);
         const float4 co = make_float4(conic_x, conic_y, conic_z, opacity);
-        const SplatBox bx = splat_box(make_float2(pix_x, pix_y), co);
         row[0] = make_float4(pix_x, pix_y, r_, g_);
         row[1] = splat_coef(co);
-        row[2] = make_float4(b_, amr_row_hx(bx), amr_row_hy(bx), amr_row_thr(bx));
-        row[3] = make_float4(bx.kyx, bx.kxy, 0.f, 0.f);
+        row[2] = make_float4(b_, conic_x, conic_y, conic_z);
+        if (!stage) row[3] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
 
     // Tile histogram with device atomics only when the tile grid is too large
@@ -357,12 +352,14 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
                 }
             }
         }
-        if (a.block == 32) {  // AMR blend rows: 64 x 64 B (four staged float4s each)
+        if (a.block == 32) {  // AMR blend rows: 64 x 64 B (three staged float4s + a zero pad each)
             float4* out = reinterpret_cast<float4*>(g.amr_rows + (size_t)16 * wrow0);
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const int c = lane + 64 * i;
-                if (c < 4 * nrow) out[c] = *reinterpret_cast<const float4*>(wl + 48 * (c >> 2) + 16 + 4 * (c & 3));
+                if (c < 4 * nrow)
+                    out[c] = (c & 3) == 3 ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                          : *reinterpret_cast<const float4*>(wl + 48 * (c >> 2) + 16 + 4 * (c & 3));
             }
         }
         // 64 x 3 rgb floats = 48 pieces of 4

@@ -238,8 +238,12 @@ constexpr int kRlPer = 2;
 // Region mask of one entry: the exact ellipse test (splat_rect_hit) on the
 // four 16x16 quadrants, refined to the 8x8 regions by the alpha >= 1/255
 // ellipse's bounding box (both conservative).  Bit g = 4 row + col.
-__device__ __forceinline__ uint32_t region_mask(const SplatBox& b, float ox, float oy) {
-    const float2 xy = b.xy;
+// (The per-Gaussian part -- splat_box's log, square roots and divisions --
+// precomputed by the preprocess into the row's free words measured no
+// faster, 0.0888 vs 0.0886 ms, with the preprocess 6 us slower,
+// profiles/r05j_bench_cfg3.log; not kept.)
+__device__ __forceinline__ uint32_t region_mask(float2 xy, float4 co, float ox, float oy) {
+    const SplatBox b = splat_box(xy, co);
     uint32_t qm = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -265,8 +269,7 @@ __device__ __forceinline__ uint32_t region_mask(const SplatBox& b, float ox, flo
 }
 
 // rows: the per-Gaussian 64-B blend rows the AMR preprocess wrote
-// (GeomView::amr_rows): (x, y, r, g), splat_coef, (b, box half-widths,
-// threshold), (edge slopes, 0, 0) -- gs_blend.cuh amr_row_box.
+// (GeomView::amr_rows): (x, y, r, g), splat_coef, (b, raw conic), pad.
 // kFuse (the default): a tile of 2..kAmrFusedSortMax instances arrives
 // unsorted in pair_keys; the workgroup sorts it first (gs_tilesort.cuh bucket
 // sort, 8 keys per thread), writes point_list and walks the sorted ids from
@@ -325,11 +328,11 @@ __global__ void __launch_bounds__(kRlThreads) amr_region_lists_kernel(int tgx, c
             if (i < n) {
                 const uint32_t id = ids[i];
                 const float4* rr = rows + (size_t)4 * id;
-                const float4 ra = rr[0], rb = rr[1], rc = rr[2], rd = rr[3];
+                const float4 ra = rr[0], rb = rr[1], rc = rr[2];
                 rec_a[beg + i] = ra;
                 rec_b[beg + i] = rb;
                 rec_c[beg + i] = rc.x;
-                m[e] = region_mask(amr_row_box(ra, rb, rc, rd), ox, oy);
+                m[e] = region_mask(make_float2(ra.x, ra.y), make_float4(rc.y, rc.z, rc.w, rb.w), ox, oy);
             }
 #pragma unroll
             for (int g = 0; g < 16; g++) {

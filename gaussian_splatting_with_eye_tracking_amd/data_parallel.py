@@ -290,7 +290,7 @@ class ViewExchange:
 _SIDE_STREAMS: Dict[Tuple[int, int], List[torch.cuda.Stream]] = {}
 
 
-def run_views_on_streams(n_views: int, render_one, n_streams: int = 2, device=None) -> None:
+def run_views_on_streams(n_views: int, render_one, n_streams: int = 3, device=None) -> None:
     """render_one(j) for j in [0, n_views), view j enqueued on stream
     j % n_streams (stream 0 = the current stream, the others cached side
     streams), so the independent per-view forward + blend backward of one
