@@ -920,7 +920,7 @@ int g_sort_algo = 1;
 void set_sort_algo(int v) { g_sort_algo = v; }
 
 // kT threads, kE keys each (n <= kT kE); nb ~ n >> kBS buckets.
-template <int kT, int kE, int kBS>
+template <int kT, int kE, int kBS, bool kStageOut = false>
 __global__ void __launch_bounds__(kT) sort_tiles_bucket_kernel(int lo, int hi, const uint32_t* __restrict__ ranges,
                                                                 const uint64_t* __restrict__ pair_keys,
                                                                 uint32_t* __restrict__ point_list) {
@@ -935,7 +935,7 @@ __global__ void __launch_bounds__(kT) sort_tiles_bucket_kernel(int lo, int hi, c
         if (threadIdx.x == 0) out[0] = (uint32_t)keys[0];
         return;
     }
-    tile_bucket_sort<kT, kE, kBS>(keys, n, out, L);
+    tile_bucket_sort<kT, kE, kBS, kStageOut>(keys, n, out, L);
 }
 
 // Merge-path split: number of elements taken from A for the first `diag`
@@ -1009,14 +1009,17 @@ void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int ma
                        hipStream_t s, int fused_max) {
     if (T == 0) return;
     if (g_sort_algo == 1) {
-#define GS_BK(TH, E, BS, LO, HI)                                                                      \
-    hipLaunchKernelGGL((sort_tiles_bucket_kernel<TH, E, BS>), dim3(T), dim3(TH), 0, s, LO, HI, img.ranges, \
+#define GS_BK(TH, E, BS, LO, HI, OUT)                                                                 \
+    hipLaunchKernelGGL((sort_tiles_bucket_kernel<TH, E, BS, OUT>), dim3(T), dim3(TH), 0, s, LO, HI, img.ranges, \
                        b.pair_keys, b.point_list)
         // size classes (measured best at configs 2, 3 and 4 among 6 geometries,
-        // profiles/r03c_ab_sort_variant_*)
-        if (fused_max < 1024) GS_BK(256, 4, 1, 0, 1024);
-        if (max_count_host > 1024 && fused_max < 2048) GS_BK(512, 4, 1, 1024, 2048);
-        if (max_count_host > 2048) GS_BK(512, 8, 2, 2048, kSmallCap);
+        // profiles/r03c_ab_sort_variant_*); the (2048, 4096] class stores its
+        // sorted ids through LDS, wave-contiguous (0.1616 -> 0.1225 ms at config 4;
+        // the small class measured 0.0293 -> 0.0303 ms at config 2 that way and
+        // keeps the direct stores, profiles/r05k_ab_sortout*.log)
+        if (fused_max < 1024) GS_BK(256, 4, 1, 0, 1024, false);
+        if (max_count_host > 1024 && fused_max < 2048) GS_BK(512, 4, 1, 1024, 2048, false);
+        if (max_count_host > 2048) GS_BK(512, 8, 2, 2048, kSmallCap, true);
 #undef GS_BK
         if (num_large_host > 0)
             hipLaunchKernelGGL(sort_tiles_large_kernel, dim3(num_large_host), dim3(kLargeThreads), 0, s,

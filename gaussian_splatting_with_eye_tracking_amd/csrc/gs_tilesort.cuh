@@ -225,7 +225,10 @@ struct TileSortLds {
 // One tile's n keys (2 <= n <= kT kE) sorted by the whole workgroup of kT
 // threads into out (point_list + the tile's start) and, when ids is given,
 // into that LDS array too.  Block-uniform n.
-template <int kT, int kE, int kBS>
+// kStageOut: the sorted ids are placed in LDS (over the keys, once every rank
+// is known) and stored by consecutive threads, instead of each thread storing
+// its keys' ids at their scattered final positions.
+template <int kT, int kE, int kBS, bool kStageOut = false>
 __device__ __forceinline__ void tile_bucket_sort(const uint64_t* __restrict__ keys, int n, uint32_t* __restrict__ out,
                                                  TileSortLds<kT, kE, kBS>& L, uint32_t* ids = nullptr) {
     constexpr int kW = kT / 64;
@@ -314,16 +317,34 @@ __device__ __forceinline__ void tile_bucket_sort(const uint64_t* __restrict__ ke
         if (i < n) s_tmp[atomicAdd(&s_fill[bk[e]], 1u)] = k[e];
     }
     __syncthreads();
+    uint32_t pos[kE];
 #pragma unroll
     for (int e = 0; e < kE; e++) {
         const int i = e * kT + tid;
+        pos[e] = ~0u;
         if (i < n) {
             const uint32_t b = bk[e];
             const uint32_t bs = b ? s_fill[b - 1] : 0u, be = s_fill[b];
             uint32_t r = 0;
             for (uint32_t j = bs; j < be; j++) r += s_tmp[j] < k[e] ? 1u : 0u;
-            out[bs + r] = (uint32_t)k[e];
-            if (ids) ids[bs + r] = (uint32_t)k[e];
+            pos[e] = bs + r;
+            if constexpr (!kStageOut) {
+                out[bs + r] = (uint32_t)k[e];
+                if (ids) ids[bs + r] = (uint32_t)k[e];
+            }
+        }
+    }
+    if constexpr (kStageOut) {
+        uint32_t* s_out = reinterpret_cast<uint32_t*>(s_tmp);
+        __syncthreads();  // every rank loop has read the keys
+#pragma unroll
+        for (int e = 0; e < kE; e++)
+            if (pos[e] != ~0u) s_out[pos[e]] = (uint32_t)k[e];
+        __syncthreads();
+        for (int i = tid; i < n; i += kT) {
+            const uint32_t v = s_out[i];
+            out[i] = v;
+            if (ids) ids[i] = v;
         }
     }
 }
