@@ -812,7 +812,8 @@ def amr_algorithmic_bytes(ranges: np.ndarray, levels: np.ndarray) -> float:
 def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
     """Config 3: forward-only foveated rendering (gaussian_renderer_amr's
     render(): foveaStep 0..4 through _RasterizeGaussians, summing the step
-    images; and render_once(): foveaStep -2 with interpolation).  Per-frame and
+    images -- rasterization_amr.render_steps, the sums fused into the steps;
+    and render_once(): foveaStep -2 with interpolation).  Per-frame and
     single-GPU: for N > 1 every rank renders its own frames (replicas only)."""
     import torch
     from diff_gaussian_rasterization_amr import GaussianRasterizer, _RasterizeGaussians
@@ -835,20 +836,16 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
     # reference's unused fovea radii W/2 .. W/16 restricting the AMR levels
     fov_centres, fov_radii = RA.reference_foveae(W, H, (361.74 / 640 * W, 248.19 / 400 * H))
 
-    def frame_5step(record=False, fovea=False):
+    def frame_5step(record=False, fovea=False, fused=True):
+        # gaussian_renderer_amr.render's rasterizer sequence (renderer_amr.render
+        # without its Python camera / model plumbing): fused, the steps add
+        # their pixels into the frame in the kernel; fused=False the literal
+        # apply + torch-add sequence (apply_chain_fps below)
+        lv = (lambda ib: RA.apply_fovea_levels(ib, W, H, fov_centres, fov_radii)) if fovea else None
         if record:
             ev[0].record()
-        c_, _radii, gb, bb, ib = _RasterizeGaussians.apply(*a, 0, e, u8, u8, u8, False, st)
-        if fovea:
-            RA.apply_fovea_levels(ib, W, H, fov_centres, fov_radii)
-        acc = c_
-        if record:
-            ev[1].record()
-        for k in range(1, 5):
-            c_, _, gb, bb, ib = _RasterizeGaussians.apply(*a, k, acc, gb, bb, ib, False, st)
-            acc = acc + c_
-            if record:
-                ev[k + 1].record()
+        acc, _radii, gb, bb, ib = RA.render_steps(*a, st, fused=fused, enders=ev[1:] if record else None,
+                                                  after_step0=lv)
         return acc, gb, bb, ib
 
     rast = GaussianRasterizer(st)
@@ -871,6 +868,15 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
         torch.cuda.synchronize()
         ctx.barrier()
         el5 = time.perf_counter() - t0
+        for _ in range(max(2, warmup)):  # (its step images and sums: allocator blocks the fused frame never asks for)
+            frame_5step(fused=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            frame_5step(fused=False)
+        torch.cuda.synchronize()
+        ctx.barrier()
+        el5u = time.perf_counter() - t0
         # per-stage and per-step times: a second pass with events
         prof = {}
         step_ms = np.zeros(5)
@@ -920,9 +926,13 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
             frame_once_fwd_bwd()
         torch.cuda.synchronize()
         elb = time.perf_counter() - t0
-    el5, el1 = ctx.max_over_ranks(el5, el1)
+    el5, el1, el5u = ctx.max_over_ranks(el5, el1, el5u)
     res = {"value": ctx.world * steps / el5, "unit": "frames/s", "ms_per_step": 1000.0 * el5 / steps,
-           "render_once_fps": ctx.world * steps / el1, "ramp_steps": ramp}
+           "render_once_fps": ctx.world * steps / el1, "ramp_steps": ramp,
+           "apply_chain_fps": ctx.world * steps / el5u,
+           "frame": "renderer_amr.render's sequence with the step-image sums fused into the step kernels "
+                    "(gs_amr_accumulate_step, bit-identical); apply_chain_fps: the literal apply + torch-add "
+                    "sequence"}
     if ctx.rank != 0:
         return res
     with torch.no_grad():
@@ -970,7 +980,8 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
 
 
 def summary(r: dict, keys=("value", "unit", "ms_per_step", "config", "roofline", "step_roofline", "per_step_ms",
-                           "render_once_fps", "exchange_params", "ramp_steps", "view_streams")) -> dict:
+                           "render_once_fps", "apply_chain_fps", "exchange_params", "ramp_steps",
+                           "view_streams")) -> dict:
     out = {k: r[k] for k in keys if k in r}
     if r.get("stages"):  # compact per-stage ms per step (or per frame)
         out["stages_ms"] = {n: round(v.get("ms_per_step", v.get("ms_per_frame", 0.0)), 4)

@@ -1090,6 +1090,43 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
     });
 }
 
+int gs_amr_accumulate_step(int P, const float* background, int width, int height, const float* colors_precomp,
+                           int foveaStep, char* geom_buffer_precomp, char* binning_buffer_precomp,
+                           char* image_buffer_precomp, float* accum, int* radii, int debug, int num_rendered_hint,
+                           void* stream) {
+    return guarded([&]() -> int {
+        if (P <= 0) return 0;
+        if (foveaStep < 1 || foveaStep > 4) throw GsError("gs_amr_accumulate_step: foveaStep in 1..4");
+        if (g_amr_variant != 4) throw GsError("gs_amr_accumulate_step needs the default amr_variant (4)");
+        if (!geom_buffer_precomp || !image_buffer_precomp || !accum)
+            throw GsError("gs_amr_accumulate_step needs the buffers returned by foveaStep 0 and the running image");
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        const int W = width, H = height;
+        const int T = ((W + 31) / 32) * ((H + 31) / 32);
+        GeomView g;
+        ImageView img;
+        BinningView b;
+        carve_geom(geom_buffer_precomp, P, &g);
+        carve_image(image_buffer_precomp, (size_t)W * H, T, &img, 32);
+        int K = num_rendered_hint;
+        if (K < 0) {
+            uint32_t hdr[4];
+            read_header(g.hdr, hdr, s);
+            K = (int)hdr[kHdrNumRendered];
+        }
+        if (K > 0 && !binning_buffer_precomp)
+            throw GsError("gs_amr_accumulate_step needs the binning buffer returned by foveaStep 0");
+        AmrBinningView ab;
+        carve_binning(binning_buffer_precomp, K, &b, &ab);
+        const float* feats = colors_precomp ? colors_precomp : g.rgb;
+        { StageTimer _t(kAmrRender, s);
+          launch_amr_render(W, H, img, img.levels, img.levels_last, b, ab, g, feats, background, accum, foveaStep, s,
+                            true, P, radii, true); }
+        stage_check(debug != 0, s, "amr_render (accumulate)");
+        return K;
+    });
+}
+
 int gs_amr_fovea_levels(char* image_buffer, size_t image_buffer_bytes, int width, int height, int nfovea, const float* centres_xy,
                         const float* radii, int min_level, int replace, void* stream) {
     return guarded([&]() -> int {

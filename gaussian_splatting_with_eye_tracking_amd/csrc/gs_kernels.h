@@ -208,7 +208,7 @@ void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s, i
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,
                        const float* bg, float* out_color, int foveaStep, hipStream_t s, bool fused = false, int P = 0,
-                       int* zero_radii = nullptr);
+                       int* zero_radii = nullptr, bool accumulate = false);
 void launch_amr_interpolate(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                             float* out_color, int foveaStep, const float* out_color_precomp, hipStream_t s);
 

@@ -409,7 +409,7 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     const float* __restrict__ feats_override, float* __restrict__ final_T, uint32_t* __restrict__ n_contrib,
     const float* __restrict__ bg, float* __restrict__ out_color, int foveaStep,
     uint32_t* __restrict__ lv_current, uint32_t* __restrict__ lv_last, uint32_t* __restrict__ tile_done, int P,
-    int* __restrict__ zero_radii) {
+    int* __restrict__ zero_radii, int accumulate) {
 #pragma clang fp contract(fast)
     constexpr int kPer = 1;
     constexpr int kFold = kRounds == 1 ? 8 : 0;
@@ -439,6 +439,11 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     // where this call renders nothing), stored at the end as 64-B row
     // segments (lane = row * 4 + 4-pixel chunk), so the caller needs no fill
     // and the image stores are coalesced.
+    // accumulate (the 5-step driver's fused image sum, gs_amr_accumulate_step):
+    // out_color holds the frame's running sum; the unit adds its quadrant
+    // (zeros where it renders nothing) to it -- the caller's
+    // `out_color_precomp + rendered_image_k` (gaussian_renderer_amr/__init__.py:341)
+    // on the same fp32 operands -- and a unit that renders nothing leaves it.
     __shared__ float s_out[3][16][16];
     const uint32_t qx0 = (uint32_t)(tile % tgx) * 32 + 16 * (q & 1), qy0 = (uint32_t)(tile / tgx) * 32 + 16 * (q >> 1);
     const uint32_t orow = lane >> 2, ocol = 4 * (lane & 3);
@@ -452,12 +457,18 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
                                   : *reinterpret_cast<const float4*>(&s_out[ch][orow][ocol]);
             float* dst = out_color + ch * plane + pp;
             if ((W & 3) == 0 && x + 3 < (uint32_t)W) {
-                *reinterpret_cast<float4*>(dst) = v;
+                if (accumulate) {
+                    const float4 o = *reinterpret_cast<const float4*>(dst);
+                    *reinterpret_cast<float4*>(dst) = make_float4(__fadd_rn(o.x, v.x), __fadd_rn(o.y, v.y),
+                                                                  __fadd_rn(o.z, v.z), __fadd_rn(o.w, v.w));
+                } else {
+                    *reinterpret_cast<float4*>(dst) = v;
+                }
             } else {
-                if (x < (uint32_t)W) dst[0] = v.x;
-                if (x + 1 < (uint32_t)W) dst[1] = v.y;
-                if (x + 2 < (uint32_t)W) dst[2] = v.z;
-                if (x + 3 < (uint32_t)W) dst[3] = v.w;
+                const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (x + j < (uint32_t)W) dst[j] = accumulate ? __fadd_rn(dst[j], vv[j]) : vv[j];
             }
         }
     };
@@ -495,7 +506,7 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     };
     // Block-uniform early exits (amr/cr/forward.cu:287-367).
     if (L <= L_last) {
-        store_quadrant(true);
+        if (!accumulate) store_quadrant(true);
         finish_unit();
         return;
     }
@@ -729,7 +740,7 @@ void set_amr_variant(int v) { g_amr_variant = v == 0 ? 0 : 4; }
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,
                        const float* bg, float* out_color, int foveaStep, hipStream_t s, bool fused, int P,
-                       int* zero_radii) {
+                       int* zero_radii, bool accumulate) {
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0) return;
     if (g_amr_variant == 4) {
@@ -743,12 +754,13 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
                            img.ranges, ab.region_lists, img.region_count, levels, levels_last, ab.rec_a, ab.rec_b, \
                            ab.rec_c, b.point_list, ov, img.accum_alpha, img.n_contrib, bg, out_color, foveaStep,   \
                            fused ? img.levels_current : nullptr, img.levels_last, img.tile_done, P,               \
-                           fused ? zero_radii : nullptr)
+                           fused ? zero_radii : nullptr, accumulate ? 1 : 0)
         if (foveaStep > 0) GS_AMR_REGION(1);
         else GS_AMR_REGION(4);
 #undef GS_AMR_REGION
         return;
     }
+    (void)accumulate;  // (variant 4 only: gs_amr_accumulate_step checks)
     hipLaunchKernelGGL((amr_render_kernel<4, 1>), dim3(2 * tgx, 2 * tgy), dim3(64), 0, s, W, H, tgx, img.ranges,
                        levels, levels_last, b.point_list, reinterpret_cast<const float2*>(g.means2D), features,
                        reinterpret_cast<const float4*>(g.conic_opacity), img.accum_alpha, img.n_contrib, bg,

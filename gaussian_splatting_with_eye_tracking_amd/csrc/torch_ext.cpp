@@ -183,6 +183,32 @@ std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> AMRRasterizeGaussians(
                           binningBuffer_precomp, imageBuffer_precomp, interpolate_image, debug);
 }
 
+// The 5-step driver's step k with its image sum fused (gs_amr_accumulate_step):
+// accum += rendered_image_k in place; returns the step's zero radii.
+Tensor AmrAccumulateStep(const Tensor& background, const Tensor& colors_in, int image_height, int image_width,
+                         int P, int foveaStep, Tensor& accum, const Tensor& geom, const Tensor& bin,
+                         const Tensor& img, bool debug) {
+    TORCH_CHECK(accum.is_cuda() && accum.scalar_type() == torch::kFloat32 && accum.is_contiguous() &&
+                    accum.numel() == 3LL * image_height * image_width,
+                "accum must be a contiguous float32 [3, H, W] device tensor");
+    const at::OptionalDeviceGuard guard(device_of(accum));
+    const Tensor bg = background.contiguous(), colors = colors_in.contiguous();
+    require_like(bg, accum, "bg", 3);
+    require_like(colors, accum, "colors_precomp", 3LL * P);
+    for (const Tensor* bt : {&geom, &bin, &img}) require_like(*bt, accum, "precomp buffer", -1, torch::kByte);
+    TORCH_CHECK(geom.numel() && img.numel(), "amr_accumulate_step needs the buffers returned by foveaStep 0");
+    Tensor radii = torch::empty({P}, accum.options().dtype(torch::kInt32));
+    if (P == 0) return radii;
+    const int hint = gs_amr_binning_count_of_bytes((size_t)bin.numel());
+    check(gs_amr_accumulate_step(P, fptr(bg), image_width, image_height, fptr(colors), foveaStep,
+                                 reinterpret_cast<char*>(geom.data_ptr()),
+                                 bin.numel() ? reinterpret_cast<char*>(bin.data_ptr()) : nullptr,
+                                 reinterpret_cast<char*>(img.data_ptr()), accum.data_ptr<float>(), radii.data_ptr<int>(),
+                                 debug ? 1 : 0, hint, stream_of(accum)),
+          "amr_accumulate_step");
+    return radii;
+}
+
 // base/rasterize_points.cu:117-196
 using Grads8 = std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor>;
 
@@ -830,6 +856,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("eye_preprocess", &EyePreprocess);
     m.def("amr_fovea_levels", &AmrFoveaLevels);
     m.def("amr_rasterize_gaussians", &AMRRasterizeGaussians);
+    m.def("amr_accumulate_step", &AmrAccumulateStep);
     m.def("distCUDA2", &DistCUDA2);
     m.def("parse_buffers", &ParseBuffers);
     m.def("l1_ssim_loss", &L1SsimLoss);

@@ -149,6 +149,61 @@ class GaussianRasterizer(nn.Module):
             self.raster_settings)
 
 
+# --------------------------------------------------------- 5-step driver ---
+def render_steps(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                 raster_settings, interpolate_image: bool = False, fused: Optional[bool] = None,
+                 starters=None, enders=None, after_step0=None):
+    """The rasterizer sequence of ``gaussian_renderer_amr.render``
+    (gaussian_renderer_amr/__init__.py:126-594): foveaStep 0 (buffers and a
+    zero image), then foveaStep 1..4 on step 0's buffers, the caller summing
+    ``out_color_precomp = out_color_precomp + rendered_image_k`` (step 4
+    with ``interpolate_image``, steps 1..3 without).  Operands as
+    ``_RasterizeGaussians.apply`` (empty tensors for absent ones).  Returns
+    (image, radii, geomBuffer, binningBuffer, imageBuffer): the reference's
+    ``render`` image and step 0's radii.
+
+    ``fused`` (default: whenever no autograd graph is recorded and step 4 does
+    not interpolate): steps 1..4 add the pixels they render straight into the
+    running image (``_C.amr_accumulate_step``, gs_amr_accumulate_step) --
+    the same fp32 adds, so the same bits -- instead of writing a full step
+    image each that the caller then adds (four full-image reads and writes
+    per frame).  ``fused=False`` is the literal apply-and-add sequence.
+    ``after_step0(imageBuffer)`` runs between step 0 and step 1 (e.g.
+    apply_fovea_levels).  ``starters`` / ``enders``: CUDA events recorded
+    around each step, as the reference's fps harness passes them."""
+    s = raster_settings
+    args = (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
+    grad = torch.is_grad_enabled() and any(isinstance(a, torch.Tensor) and a.requires_grad for a in args)
+    if fused is None:
+        fused = not grad and not interpolate_image
+    elif fused and (grad or interpolate_image):
+        raise RuntimeError("render_steps(fused=True) is forward-only without interpolation: run it under "
+                           "torch.no_grad() with interpolate_image=False")
+    e = torch.empty(0, device=means3D.device)
+    u8 = torch.empty(0, dtype=torch.uint8, device=means3D.device)
+
+    def mark(evs, k):
+        if evs is not None:
+            evs[k].record()
+
+    mark(starters, 0)
+    acc, radii, gb, bb, ib = _RasterizeGaussians.apply(*args, 0, e, u8, u8, u8, False, s)
+    mark(enders, 0)
+    if after_step0 is not None:
+        after_step0(ib)
+    for k in range(1, 5):
+        mark(starters, k)
+        if fused:
+            _C.amr_accumulate_step(s.bg, colors_precomp, int(s.image_height), int(s.image_width),
+                                   int(means3D.shape[0]), k, acc, gb, bb, ib, bool(s.debug))
+        else:
+            c, _, gb, bb, ib = _RasterizeGaussians.apply(*args, k, acc, gb, bb, ib,
+                                                          bool(interpolate_image) if k == 4 else False, s)
+            acc = acc + c
+        mark(enders, k)
+    return acc, radii, gb, bb, ib
+
+
 # ------------------------------------------------ fovea-driven levels (ext.) ---
 def reference_foveae(width: int, height: int, centre: Optional[Tuple[float, float]] = None):
     """The fovea discs the reference builds and leaves unused

@@ -217,6 +217,22 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
                                  char* binning_buffer_precomp, char* image_buffer_precomp, float* out_color,
                                  int* radii, int interpolate_image, int debug, int num_rendered_hint, void* stream);
 
+/* The 5-step driver's progressive step fused with its image sum: the
+ * caller's `rendered_image_k = rasterize(foveaStep k, ...)` followed by
+ * `out_color_precomp = out_color_precomp + rendered_image_k`
+ * (gaussian_renderer_amr/__init__.py:295-341, 384-427, 470-510, 553-594;
+ * interpolate_image false).  `accum` (3 x height x width floats, the running
+ * sum, step 0's zero image at first) is updated in place: every pixel this
+ * step renders gets accum + (C + T bg), the same fp32 add, and the rest keep
+ * their value (+ 0 in the reference) -- bit-identical to the reference's sum.
+ * Buffers, radii (zeros written), num_rendered_hint and return value as
+ * gs_amr_rasterizer_forward_ex at foveaStep >= 1.  Needs the default AMR
+ * variant (gs_set_tuning("amr_variant") 4). */
+int gs_amr_accumulate_step(int P, const float* background, int width, int height, const float* colors_precomp,
+                           int foveaStep, char* geom_buffer_precomp, char* binning_buffer_precomp,
+                           char* image_buffer_precomp, float* accum, int* radii, int debug, int num_rendered_hint,
+                           void* stream);
+
 /* Replaces SimpleKNN::knn (knn/simple_knn.h:16-19, knn/simple_knn.cu:185-221)
  * behind simple_knn._C.distCUDA2.  `scratch` is resized to the workspace
  * size; no host synchronisation. */

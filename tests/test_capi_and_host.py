@@ -217,6 +217,14 @@ def test_new_entry_points_validate_before_any_device_call():
     assert amr_bwd(0, 0) < 0 and b"renders nothing" in lib.gs_last_error()
     assert amr_bwd(2, 1) < 0 and b"render_once only" in lib.gs_last_error()
     assert amr_bwd(5, 0) < 0 and b"1..4" in lib.gs_last_error()
+    # the fused step-and-sum: foveaStep 1..4 only, and the step-0 buffers
+    def acc_step(step, geom):
+        return lib.gs_amr_accumulate_step(ctypes.c_int(10), null, ctypes.c_int(64), ctypes.c_int(64), null,
+                                          ctypes.c_int(step), geom, null, geom, geom, null, ctypes.c_int(0),
+                                          ctypes.c_int(-1), null)
+    assert acc_step(0, buf) < 0 and b"1..4" in lib.gs_last_error()
+    assert acc_step(5, buf) < 0 and b"1..4" in lib.gs_last_error()
+    assert acc_step(2, null) < 0 and b"foveaStep 0" in lib.gs_last_error()
 
 
 def test_extension_entry_points_in_torch_module():
