@@ -23,8 +23,8 @@ ROOT = os.path.dirname(PKG)
 INCLUDE = os.path.join(ROOT, "include")
 BUILD = os.path.join(PKG, "_build")
 LIB = os.path.join(PKG, "libgsplat_amd.so")
-HIP_SOURCES = ["preprocess.hip", "binning.hip", "render.hip", "backward.hip", "amr.hip", "knn.hip", "loss.hip",
-               "train.hip", "ritnet.hip", "eye_preprocess.hip", "gs_api.cpp"]
+HIP_SOURCES = ["preprocess.hip", "binning.hip", "render.hip", "backward.hip", "multiview.hip", "amr.hip", "knn.hip",
+               "loss.hip", "train.hip", "ritnet.hip", "eye_preprocess.hip", "gs_api.cpp"]
 ARCH = os.environ.get("GSAMD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -ffp-contract=off is part of the parity contract (see gs_device.cuh).
@@ -34,6 +34,11 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off", "-munsafe-fp-atomics",
              "-fno-slp-vectorize",
              "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}"]
+# Per-source flags after HIP_FLAGS: the multi-view backward's gradients are
+# held to a tolerance (tests/test_gpu_multiview.py), so it compiles with FMA
+# contraction and reciprocal math (30 % fewer VALU instructions per view,
+# DESIGN.md §8f); everything on the keys / images keeps the contract above.
+SOURCE_FLAGS = {"multiview.hip": ["-ffp-contract=fast", "-freciprocal-math", "-fapprox-func"]}
 # extra flags for code-generation experiments (e.g. GSAMD_EXTRA_HIPFLAGS=-fno-slp-vectorize)
 HIP_FLAGS += shlex.split(os.environ.get("GSAMD_EXTRA_HIPFLAGS", ""))
 
@@ -76,7 +81,7 @@ def _object_digest(src: str, digest: str) -> str:
     for f in [os.path.join(CSRC, src)] + sorted(_headers()):
         with open(f, "rb") as fh:
             h.update(os.path.basename(f).encode() + fh.read())
-    h.update(" ".join(f for f in HIP_FLAGS if not f.startswith("-I")).encode())
+    h.update(" ".join(f for f in HIP_FLAGS + SOURCE_FLAGS.get(src, []) if not f.startswith("-I")).encode())
     if src == "gs_api.cpp":
         h.update(digest.encode())
     return h.hexdigest()[:16]
@@ -101,7 +106,7 @@ def build_hip_lib(jobs: int = 8, verbose: bool = False) -> str:
         od = _object_digest(src, digest)
         if not os.path.exists(o) or _read(o + ".digest") != od:
             extra = [f"-DGSAMD_DIGEST=\"{digest}\""] if src == "gs_api.cpp" else []
-            todo.append((o, od, [HIPCC] + HIP_FLAGS + extra + ["-x", "hip", "-c", s, "-o", o]))
+            todo.append((o, od, [HIPCC] + HIP_FLAGS + SOURCE_FLAGS.get(src, []) + extra + ["-x", "hip", "-c", s, "-o", o]))
     if todo:
         def one(t):
             o, od, cmd = t
@@ -190,6 +195,7 @@ def source_digest() -> str:
         with open(f, "rb") as fh:
             h.update(fh.read())
     h.update(" ".join(f for f in HIP_FLAGS if not f.startswith("-I")).encode())  # (paths differ per box)
+    h.update(repr(sorted(SOURCE_FLAGS.items())).encode())
     return h.hexdigest()[:16]
 
 

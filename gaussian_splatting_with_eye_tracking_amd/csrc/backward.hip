@@ -32,6 +32,7 @@
 #include <hip/hip_ext.h>
 
 #include "gs_blend.cuh"
+#include "gs_bwd_math.cuh"
 #include "gs_device.cuh"
 #include "gs_kernels.h"
 
@@ -635,271 +636,7 @@ void launch_amr_render_backward(int W, int H, int mode, const ImageView& img, co
                        dL_dpix, bg, g.grad_accum, g_cull, tgx, mode, img.levels, nullptr, nullptr, nullptr);
 }
 
-// ------------------------------------------------------ per-Gaussian bwd ---
-__device__ __forceinline__ void dnormvdv3(float vx, float vy, float vz, float dx, float dy, float dz, float& ox,
-                                          float& oy, float& oz) {
-    // base/cr/auxiliary.h:107-117
-    const float sum2 = vx * vx + vy * vy + vz * vz;
-    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-    ox = ((+sum2 - vx * vx) * dx - vy * vx * dy - vz * vx * dz) * invsum32;
-    oy = (-vx * vy * dx + (sum2 - vy * vy) * dy - vz * vy * dz) * invsum32;
-    oz = (-vx * vz * dx - vy * vz * dy + (sum2 - vz * vz) * dz) * invsum32;
-}
-
-// SH rows of Gaussian idx into s[16][3] (zero past (D+1)^2 and M).
-template <bool kSH16>
-__device__ __forceinline__ void load_sh_rows(const BackwardGaussArgs& a, int idx, float (&s)[16][3],
-                                             const float* lrow = nullptr) {
-    const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
-    const float* sh = a.shs + (size_t)idx * a.M * 3;
-    if (kSH16 && lrow) {  // row staged in LDS by the workgroup's coalesced load
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) s[k][c] = (k < ncoef) ? lrow[3 * k + c] : 0.f;
-    } else if (kSH16) {
-        const float4* s4 = reinterpret_cast<const float4*>(sh);
-        float buf[48];
-#pragma unroll
-        for (int i = 0; i < 12; i++) {
-            const float4 v4 = (i * 4 < ncoef * 3) ? s4[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-            buf[4 * i + 0] = v4.x; buf[4 * i + 1] = v4.y; buf[4 * i + 2] = v4.z; buf[4 * i + 3] = v4.w;
-        }
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) s[k][c] = buf[3 * k + c];
-    } else {
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) s[k][c] = (k < ncoef) ? sh[3 * k + c] : 0.f;
-    }
-}
-
-// computeColorFromSH backward (backward.cu:20-139), shared part: the
-// per-coefficient factors dsh_c[k] (dL_dsh[k][c] = dsh_c[k] * dRGB[c])
-// and the view-direction term added to dmean (+=).
-// (SH: float[16][3] in registers, or ShRowPtr, a row of 48 coefficients in LDS.)
-struct ShRowPtr {
-    const float* p;
-    __device__ __forceinline__ const float* operator[](int k) const { return p + 3 * k; }
-};
-
-template <typename SH>
-__device__ __forceinline__ void sh_backward_terms(int deg, const float* campos, float mx, float my, float mz,
-                                                  const SH& s, uint8_t cb, const float* acc,
-                                                  float (&dsh_c)[16], float (&dRGB)[3], float (&dmean)[3],
-                                                  const float* drgb9 = nullptr) {
-    const float dox = mx - campos[0], doy = my - campos[1], doz = mz - campos[2];
-    const float len = sqrtf(dot3(dox, doy, doz, dox, doy, doz));
-    const float x = dox / len, y = doy / len, z = doz / len;
-#pragma unroll
-    for (int c = 0; c < 3; c++) dRGB[c] = acc[c] * (((cb >> c) & 1) ? 0.0f : 1.0f);
-    float dx3[3], dy3[3], dz3[3];
-    sh_basis(deg, x, y, z, dsh_c);
-    if (drgb9) {  // the forward's derivatives (sh_ddir on the same operands: the same bits)
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            dx3[c] = drgb9[c];
-            dy3[c] = drgb9[3 + c];
-            dz3[c] = drgb9[6 + c];
-        }
-    } else {
-        sh_ddir(deg, s, x, y, z, dx3, dy3, dz3);
-    }
-    const float ddx = dot3(dx3[0], dx3[1], dx3[2], dRGB[0], dRGB[1], dRGB[2]);
-    const float ddy = dot3(dy3[0], dy3[1], dy3[2], dRGB[0], dRGB[1], dRGB[2]);
-    const float ddz = dot3(dz3[0], dz3[1], dz3[2], dRGB[0], dRGB[1], dRGB[2]);
-    float ox, oy, oz;
-    dnormvdv3(dox, doy, doz, ddx, ddy, ddz, ox, oy, oz);
-    dmean[0] += ox;
-    dmean[1] += oy;
-    dmean[2] += oz;
-}
-
-// computeColorFromSH backward (backward.cu:20-139) for one Gaussian: writes
-// its dL_dsh row and adds the view-direction term to dmean (+=, after the
-// cov2D (=) and projection (+=) terms, the reference's order).
-template <bool kSH16>
-__device__ __forceinline__ void sh_backward(const BackwardGaussArgs& a, int idx, float mx, float my, float mz,
-                                            const float (&s)[16][3], uint8_t cb, const float* acc,
-                                            float (&dmean)[3], float* lrow = nullptr, const float* drgb9 = nullptr) {
-    const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
-    float* dsh = a.dL_dsh + (size_t)idx * a.M * 3;
-    float dsh_c[16], dRGB[3];
-    sh_backward_terms(a.D, a.campos, mx, my, mz, s, cb, acc, dsh_c, dRGB, dmean, drgb9);
-    if (kSH16) {
-        float o[48];
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) o[3 * k + c] = (k < ncoef) ? dsh_c[k] * dRGB[c] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 12; i++)
-            if (lrow) {  // staged in LDS; the workgroup stores its rows coalesced
-#pragma unroll
-                for (int e = 0; e < 4; e++) lrow[4 * i + e] = o[4 * i + e];
-            } else {
-                reinterpret_cast<float4*>(dsh)[i] = make_float4(o[4 * i], o[4 * i + 1], o[4 * i + 2], o[4 * i + 3]);
-            }
-    } else {
-        for (int k = 0; k < a.M; k++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                float v = 0.f;
-#pragma unroll
-                for (int kk = 0; kk < 16; kk++) v = (kk == k && k < ncoef) ? dsh_c[kk] * dRGB[c] : v;
-                dsh[3 * k + c] = v;
-            }
-    }
-}
-
-// computeCov2DCUDA backward (backward.cu:144-274) for one Gaussian and one
-// view: dL_dconic (x, y, w) -> dmean (assigned, `=`) and dL_dcov3D.
-__device__ __forceinline__ void cov2d_backward(float mx, float my, float mz, const float (&cov3D)[6],
-                                               float dcx, float dcy, float dcz, const Mat4& V, float h_x, float h_y,
-                                               float tan_fovx, float tan_fovy, float (&dmean)[3], float (&dcov)[6]) {
-    float3 t = transform_point_4x3(mx, my, mz, V);
-    const float limx = 1.3f * tan_fovx;
-    const float limy = 1.3f * tan_fovy;
-    const float txtz = t.x / t.z;
-    const float tytz = t.y / t.z;
-    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
-    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
-    const float x_grad_mul = txtz < -limx || txtz > limx ? 0 : 1;
-    const float y_grad_mul = tytz < -limy || tytz > limy ? 0 : 1;
-    const Mat3 J = mat3_cols(h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z), 0.0f, h_y / t.z,
-                             -(h_y * t.y) / (t.z * t.z), 0, 0, 0);
-    const float* v = V.m;
-    const Mat3 Wm = mat3_cols(v[0], v[4], v[8], v[1], v[5], v[9], v[2], v[6], v[10]);
-    const Mat3 Vrk = mat3_cols(cov3D[0], cov3D[1], cov3D[2], cov3D[1], cov3D[3], cov3D[4], cov3D[2], cov3D[4],
-                               cov3D[5]);
-    const Mat3 T = mat3_mul(Wm, J);
-    Mat3 cov2D = mat3_mul(mat3_mul(mat3_transpose(T), mat3_transpose(Vrk)), T);
-    const float aa = cov2D.m[0][0] += 0.3f;
-    const float bb = cov2D.m[0][1];
-    const float cc = cov2D.m[1][1] += 0.3f;
-    const float denom = aa * cc - bb * bb;
-    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-    const auto& Tm = T.m;
-    const auto& Vm = Vrk.m;
-    // (the reference's `if (denom2inv != 0)` as selects on the same
-    // expressions -- the same values; as a branch, the compiler sank the two
-    // paths' dcov stores into a pointer phi and kept dcov in scratch memory)
-    const bool ok = denom2inv != 0;
-    const float dL_da = ok ? denom2inv * (-cc * cc * dcx + 2 * bb * cc * dcy + (denom - aa * cc) * dcz) : 0.f;
-    const float dL_dc = ok ? denom2inv * (-aa * aa * dcz + 2 * aa * bb * dcy + (denom - aa * cc) * dcx) : 0.f;
-    const float dL_db = ok ? denom2inv * 2 * (bb * cc * dcx - (denom + 2 * bb * bb) * dcy + aa * bb * dcz) : 0.f;
-    dcov[0] = ok ? (Tm[0][0] * Tm[0][0] * dL_da + Tm[0][0] * Tm[1][0] * dL_db + Tm[1][0] * Tm[1][0] * dL_dc) : 0.f;
-    dcov[3] = ok ? (Tm[0][1] * Tm[0][1] * dL_da + Tm[0][1] * Tm[1][1] * dL_db + Tm[1][1] * Tm[1][1] * dL_dc) : 0.f;
-    dcov[5] = ok ? (Tm[0][2] * Tm[0][2] * dL_da + Tm[0][2] * Tm[1][2] * dL_db + Tm[1][2] * Tm[1][2] * dL_dc) : 0.f;
-    dcov[1] = ok ? 2 * Tm[0][0] * Tm[0][1] * dL_da + (Tm[0][0] * Tm[1][1] + Tm[0][1] * Tm[1][0]) * dL_db +
-                       2 * Tm[1][0] * Tm[1][1] * dL_dc
-                 : 0.f;
-    dcov[2] = ok ? 2 * Tm[0][0] * Tm[0][2] * dL_da + (Tm[0][0] * Tm[1][2] + Tm[0][2] * Tm[1][0]) * dL_db +
-                       2 * Tm[1][0] * Tm[1][2] * dL_dc
-                 : 0.f;
-    dcov[4] = ok ? 2 * Tm[0][2] * Tm[0][1] * dL_da + (Tm[0][1] * Tm[1][2] + Tm[0][2] * Tm[1][1]) * dL_db +
-                       2 * Tm[1][1] * Tm[1][2] * dL_dc
-                 : 0.f;
-    const float dL_dT00 = 2 * (Tm[0][0] * Vm[0][0] + Tm[0][1] * Vm[0][1] + Tm[0][2] * Vm[0][2]) * dL_da +
-                          (Tm[1][0] * Vm[0][0] + Tm[1][1] * Vm[0][1] + Tm[1][2] * Vm[0][2]) * dL_db;
-    const float dL_dT01 = 2 * (Tm[0][0] * Vm[1][0] + Tm[0][1] * Vm[1][1] + Tm[0][2] * Vm[1][2]) * dL_da +
-                          (Tm[1][0] * Vm[1][0] + Tm[1][1] * Vm[1][1] + Tm[1][2] * Vm[1][2]) * dL_db;
-    const float dL_dT02 = 2 * (Tm[0][0] * Vm[2][0] + Tm[0][1] * Vm[2][1] + Tm[0][2] * Vm[2][2]) * dL_da +
-                          (Tm[1][0] * Vm[2][0] + Tm[1][1] * Vm[2][1] + Tm[1][2] * Vm[2][2]) * dL_db;
-    const float dL_dT10 = 2 * (Tm[1][0] * Vm[0][0] + Tm[1][1] * Vm[0][1] + Tm[1][2] * Vm[0][2]) * dL_dc +
-                          (Tm[0][0] * Vm[0][0] + Tm[0][1] * Vm[0][1] + Tm[0][2] * Vm[0][2]) * dL_db;
-    const float dL_dT11 = 2 * (Tm[1][0] * Vm[1][0] + Tm[1][1] * Vm[1][1] + Tm[1][2] * Vm[1][2]) * dL_dc +
-                          (Tm[0][0] * Vm[1][0] + Tm[0][1] * Vm[1][1] + Tm[0][2] * Vm[1][2]) * dL_db;
-    const float dL_dT12 = 2 * (Tm[1][0] * Vm[2][0] + Tm[1][1] * Vm[2][1] + Tm[1][2] * Vm[2][2]) * dL_dc +
-                          (Tm[0][0] * Vm[2][0] + Tm[0][1] * Vm[2][1] + Tm[0][2] * Vm[2][2]) * dL_db;
-    const auto& Wq = Wm.m;
-    const float dL_dJ00 = Wq[0][0] * dL_dT00 + Wq[0][1] * dL_dT01 + Wq[0][2] * dL_dT02;
-    const float dL_dJ02 = Wq[2][0] * dL_dT00 + Wq[2][1] * dL_dT01 + Wq[2][2] * dL_dT02;
-    const float dL_dJ11 = Wq[1][0] * dL_dT10 + Wq[1][1] * dL_dT11 + Wq[1][2] * dL_dT12;
-    const float dL_dJ12 = Wq[2][0] * dL_dT10 + Wq[2][1] * dL_dT11 + Wq[2][2] * dL_dT12;
-    const float tz = 1.f / t.z;
-    const float tz2 = tz * tz;
-    const float tz3 = tz2 * tz;
-    const float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
-    const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
-    const float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
-                         (2 * h_y * t.y) * tz3 * dL_dJ12;
-    // transformVec4x3Transpose (auxiliary.h:89-97): assign (=)
-    dmean[0] = v[0] * dL_dtx + v[1] * dL_dty + v[2] * dL_dtz;
-    dmean[1] = v[4] * dL_dtx + v[5] * dL_dty + v[6] * dL_dtz;
-    dmean[2] = v[8] * dL_dtx + v[9] * dL_dty + v[10] * dL_dtz;
-}
-
-// preprocessCUDA backward, projection part (backward.cu:370-387): adds
-// (+=) the mean2D gradient (gx, gy) pulled back through the projection.
-__device__ __forceinline__ void proj_backward(float mx, float my, float mz, const Mat4& Pm, float gx, float gy,
-                                              float (&dmean)[3]) {
-    const float* proj = Pm.m;
-    const float4 m_hom = transform_point_4x4(mx, my, mz, Pm);
-    const float m_w = 1.0f / (m_hom.w + 0.0000001f);
-    const float mul1 = (proj[0] * mx + proj[4] * my + proj[8] * mz + proj[12]) * m_w * m_w;
-    const float mul2 = (proj[1] * mx + proj[5] * my + proj[9] * mz + proj[13]) * m_w * m_w;
-    dmean[0] += (proj[0] * m_w - proj[3] * mul1) * gx + (proj[1] * m_w - proj[3] * mul2) * gy;
-    dmean[1] += (proj[4] * m_w - proj[7] * mul1) * gx + (proj[5] * m_w - proj[7] * mul2) * gy;
-    dmean[2] += (proj[8] * m_w - proj[11] * mul1) * gx + (proj[9] * m_w - proj[11] * mul2) * gy;
-}
-
-// computeCov3D backward (backward.cu:278-341): dL_dcov3D -> dL_dscale and
-// dL_drot (w.r.t. the unnormalised quaternion, as the reference).
-__device__ __forceinline__ void cov3d_backward(float4 qrot, const float (&scl)[3], float scale_modifier,
-                                               const float (&dcov)[6], float (&dscale)[3], float4& dq) {
-    const float r = qrot.x, x = qrot.y, y = qrot.z, z = qrot.w;
-    const Mat3 R = quat_to_R(r, x, y, z);
-    const float sx = scale_modifier * scl[0];
-    const float sy = scale_modifier * scl[1];
-    const float sz = scale_modifier * scl[2];
-    Mat3 S = mat3_cols(1, 0, 0, 0, 1, 0, 0, 0, 1);
-    S.m[0][0] = sx; S.m[1][1] = sy; S.m[2][2] = sz;
-    const Mat3 Mm = mat3_mul(S, R);
-    const float* dc = dcov;
-    const Mat3 dL_dSigma = mat3_cols(dc[0], 0.5f * dc[1], 0.5f * dc[2], 0.5f * dc[1], dc[3], 0.5f * dc[4],
-                                     0.5f * dc[2], 0.5f * dc[4], dc[5]);
-    Mat3 M2;
-#pragma unroll
-    for (int c = 0; c < 3; c++)
-#pragma unroll
-        for (int rr = 0; rr < 3; rr++) M2.m[c][rr] = 2.0f * Mm.m[c][rr];
-    const Mat3 dL_dM = mat3_mul(M2, dL_dSigma);
-    const Mat3 Rt = mat3_transpose(R);
-    Mat3 D = mat3_transpose(dL_dM);
-    dscale[0] = dot3(Rt.m[0][0], Rt.m[0][1], Rt.m[0][2], D.m[0][0], D.m[0][1], D.m[0][2]);
-    dscale[1] = dot3(Rt.m[1][0], Rt.m[1][1], Rt.m[1][2], D.m[1][0], D.m[1][1], D.m[1][2]);
-    dscale[2] = dot3(Rt.m[2][0], Rt.m[2][1], Rt.m[2][2], D.m[2][0], D.m[2][1], D.m[2][2]);
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        D.m[0][k] *= sx;
-        D.m[1][k] *= sy;
-        D.m[2][k] *= sz;
-    }
-    const auto& Dm = D.m;
-    dq.x = 2 * z * (Dm[0][1] - Dm[1][0]) + 2 * y * (Dm[2][0] - Dm[0][2]) + 2 * x * (Dm[1][2] - Dm[2][1]);
-    dq.y = 2 * y * (Dm[1][0] + Dm[0][1]) + 2 * z * (Dm[2][0] + Dm[0][2]) + 2 * r * (Dm[1][2] - Dm[2][1]) -
-           4 * x * (Dm[2][2] + Dm[1][1]);
-    dq.z = 2 * x * (Dm[1][0] + Dm[0][1]) + 2 * r * (Dm[2][0] - Dm[0][2]) + 2 * z * (Dm[1][2] + Dm[2][1]) -
-           4 * y * (Dm[2][2] + Dm[0][0]);
-    dq.w = 2 * r * (Dm[0][1] - Dm[1][0]) + 2 * x * (Dm[2][0] + Dm[0][2]) + 2 * y * (Dm[1][2] + Dm[2][1]) -
-           4 * z * (Dm[1][1] + Dm[0][0]);
-}
-
-// A 16-B store of an output nothing in this pass reads back; nt: with the
-// non-temporal hint (the line is not kept in L2 for reuse).
-__device__ __forceinline__ void store_out4(float4* p, float4 v, bool nt) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    if (nt) __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(p));
-    else *p = v;
-}
-__device__ __forceinline__ void store_out1(float* p, float v, bool nt) {
-    if (nt) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
+// (the per-Gaussian backward math: gs_bwd_math.cuh)
 
 // kSH16: SH with M = 16 coefficients (degree-3 models): compile-time loops,
 // 16-B loads and stores of the 192-B SH rows.
@@ -1099,12 +836,6 @@ __device__ __forceinline__ void backward_gaussian_body(const BackwardGaussArgs& 
     }
 }
 
-// One thread per Gaussian (backward_gaussian_body).  With SH16 the 192-B SH
-// gradient rows are staged in LDS (49-float rows: conflict-free per-thread
-// writes) and the workgroup stores its contiguous 256 x 192 B with
-// wave-contiguous 16-B stores: per-thread 192-B row stores measured ~3.5 TB/s
-// against ~5.4 TB/s coalesced on MI355X (tools/membench.hip).
-constexpr int kShRow = 49;
 constexpr int kBgStageNt = 16;  // backward_gaussians_kernel stage flag: dL_dsh rows non-temporal
 
 
@@ -1279,283 +1010,3 @@ void launch_backward_gaussians(const BackwardGaussArgs& args, const GeomView& g,
 
 }  // namespace gsamd
 
-namespace gsamd {
-
-// ------------------------------------------- data-parallel view exchange ---
-// each rank back-propagates its own view.  The reference's
-// per-Gaussian backward (computeCov2DCUDA / preprocessCUDA / SH / cov3D
-// backward, backward.cu:20-396) is linear in the 9 screen-space sums the
-// blend produces, given the view's camera, radius and SH clamp bits.  So the
-// ranks exchange those (10 words per Gaussian per view, kViewRow) instead of
-// the 59-float parameter gradients, and every rank rebuilds the sum over all
-// views of the parameter gradients in one pass that reads the parameters
-// once: (N-1) x 40 B per Gaussian received per rank instead of a ring
-// all-reduce's 2 (N-1)/N x 236 B.
-//
-// Row layout: dL_dcolor[3], dL_dmean2D.xy[2], dL_dconic (x, y, w)[3],
-// dL_dopacity, and word 9 = radius | clamped_bits << 24 (0 = not visible).
-// A view record is the P rows followed by the view's camera (kCamWords:
-// viewmatrix, projmatrix, campos, width, height, tan_fovx, tan_fovy, 0), so
-// one all-gather moves everything the multi-view backward needs.
-__global__ void __launch_bounds__(256) pack_view_grads_kernel(int P, const float* __restrict__ grad_accum,
-                                                              const int* __restrict__ radii,
-                                                              const uint8_t* __restrict__ clamped,
-                                                              const float* __restrict__ viewmatrix,
-                                                              const float* __restrict__ projmatrix,
-                                                              const float* __restrict__ campos, float width,
-                                                              float height, float tan_fovx, float tan_fovy,
-                                                              float* __restrict__ out) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (blockIdx.x == 0 && threadIdx.x < kCamWords) {
-        const int w = threadIdx.x;
-        float c = 0.f;
-        if (w < 16) c = viewmatrix[w];
-        else if (w < 32) c = projmatrix[w - 16];
-        else if (w < 35) c = campos[w - 32];
-        else if (w == 35) c = width;
-        else if (w == 36) c = height;
-        else if (w == 37) c = tan_fovx;
-        else if (w == 38) c = tan_fovy;
-        out[(size_t)P * kViewRow + w] = c;
-    }
-    if (idx >= P) return;
-    const int r = radii[idx];
-    float v[kViewRow];
-#pragma unroll
-    for (int q = 0; q < kViewRow; q++) v[q] = 0.f;
-    if (r > 0) {
-        const float4* row = reinterpret_cast<const float4*>(grad_accum + (size_t)idx * kGradRow);
-        const float4 r0 = row[0], r1 = row[1];
-        v[0] = r0.x; v[1] = r0.y; v[2] = r0.z; v[3] = r0.w;
-        v[4] = r1.x; v[5] = r1.y; v[6] = r1.z; v[7] = r1.w;
-        v[8] = grad_accum[(size_t)idx * kGradRow + 8];
-        const uint32_t cb = clamped ? clamped[idx] : 0u;
-        v[9] = __uint_as_float((uint32_t)min(r, 0xFFFFFF) | (cb << 24));
-    }
-    float2* o = reinterpret_cast<float2*>(out + (size_t)idx * kViewRow);
-#pragma unroll
-    for (int q = 0; q < kViewRow / 2; q++) o[q] = make_float2(v[2 * q], v[2 * q + 1]);
-}
-
-void launch_pack_view_grads(int P, const GeomView& g, const int* radii, bool has_sh, const float* viewmatrix,
-                            const float* projmatrix, const float* campos, int width, int height, float tan_fovx,
-                            float tan_fovy, float* out, hipStream_t s) {
-    hipLaunchKernelGGL(pack_view_grads_kernel, dim3((P + 255) / 256 > 0 ? (P + 255) / 256 : 1), dim3(256), 0, s,
-                       P, g.grad_accum, radii, has_sh ? g.clamped : nullptr, viewmatrix, projmatrix, campos,
-                       (float)width, (float)height, tan_fovx, tan_fovy, out);
-}
-
-// One thread per Gaussian: sum over the V views (in view order) of the
-// reference's per-view parameter gradients.  Per view the terms are formed
-// exactly as backward_gaussian_body does (cov2D `=`, projection `+=`, SH
-// direction `+=`); dL_dcov3D is summed over views before the (linear) cov3D
-// backward runs once.  Optional densification statistics (train.py:111-113)
-// are accumulated view by view: accum += ||dL/dmean2D.xy||, denom += 1,
-// max_radii = max(max_radii, radius) for every view that sees the Gaussian.
-__device__ __forceinline__ const float* mv_row(const MultiViewArgs& a, int v) {
-    return a.table ? a.table[v] : a.rows[v];
-}
-__device__ __forceinline__ const float* mv_cam(const MultiViewArgs& a, int v) {
-    return a.table ? a.table[a.V + v] : a.cams[v];
-}
-
-// One pass over the views with each view's rows staged through LDS: the
-// workgroup's 256 rows of view v (10 KB, contiguous in the record) are read
-// with 8-B loads by consecutive lanes -- five load instructions per thread per
-// view instead of ten per-thread loads at a 40-B stride (each touching ~20
-// cache lines per wave instruction) -- the next view's rows in flight in
-// registers while this view's terms are formed.  (Round 4's two-pass form --
-// an any-check pass, the geometry pass, the SH pass, each re-reading the rows
-// per thread -- measured 0.3386 against 0.3360 ms per 8-view step at config
-// 5, profiles/r05c_bench_cfg5_mv*.log, and is removed.)
-constexpr int kMvRowF2 = 256 * kViewRow / 2;     // float2 per view per workgroup (1280)
-constexpr int kMvRowPer = (kMvRowF2 + 255) / 256;  // per thread (5)
-template <bool kHasSH, bool kSH16>
-__global__ void __launch_bounds__(256) multiview_backward1_kernel(MultiViewArgs a) {
-    constexpr bool kStage = kHasSH && kSH16;
-    __shared__ float s_sh[kStage ? 256 * kShRow : 1];
-    __shared__ __attribute__((aligned(16))) float s_rows[256 * kViewRow];
-    const int local0 = blockIdx.x * 256;
-    const int nblk = min(256, a.count - local0);
-    if constexpr (kStage) {
-        const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)(a.g0 + local0) * 12;
-        if (nblk == 256) {
-            float4 v[12];
-#pragma unroll
-            for (int k = 0; k < 12; k++) v[k] = in[threadIdx.x + 256 * k];
-#pragma unroll
-            for (int k = 0; k < 12; k++) {
-                const int f = threadIdx.x + 256 * k;
-                float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
-                r[0] = v[k].x; r[1] = v[k].y; r[2] = v[k].z; r[3] = v[k].w;
-            }
-        } else {
-            for (int f = threadIdx.x; f < nblk * 12; f += 256) {
-                const float4 v = in[f];
-                float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
-                r[0] = v.x; r[1] = v.y; r[2] = v.z; r[3] = v.w;
-            }
-        }
-    }
-    const int local = local0 + threadIdx.x;
-    const bool live = local < a.count;
-    const int idx = a.g0 + local;
-    float* lrow = kStage ? s_sh + threadIdx.x * kShRow : nullptr;
-    const int nf2 = nblk * (kViewRow / 2);  // this block's float2 per view
-    // view v's rows of this block: a.rows[v] points at Gaussian g0's row
-    auto load_rows = [&](int v, float2 (&r)[kMvRowPer]) {
-        const float2* src = reinterpret_cast<const float2*>(mv_row(a, v) + (size_t)local0 * kViewRow);
-#pragma unroll
-        for (int i = 0; i < kMvRowPer; i++) {
-            const int f = threadIdx.x + 256 * i;
-            r[i] = f < nf2 ? src[f] : make_float2(0.f, 0.f);
-        }
-    };
-    float mx = 0.f, my = 0.f, mz = 0.f;
-    float4 qrot = make_float4(0.f, 0.f, 0.f, 0.f);
-    float scl[3] = {0.f, 0.f, 0.f}, cov3D[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float st_acc = 0.f, st_den = 0.f, st_max = 0.f;
-    const bool stats = a.grad_norm_accum != nullptr;
-    if (live) {
-        mx = a.means3D[3 * idx];
-        my = a.means3D[3 * idx + 1];
-        mz = a.means3D[3 * idx + 2];
-        qrot = reinterpret_cast<const float4*>(a.rotations)[idx];
-        scl[0] = a.scales[3 * idx + 0];
-        scl[1] = a.scales[3 * idx + 1];
-        scl[2] = a.scales[3 * idx + 2];
-        if (stats) {
-            st_acc = a.grad_norm_accum[idx];
-            st_den = a.denom[idx];
-            st_max = a.max_radii[idx];
-        }
-    }
-    compute_cov3d(scl, qrot, a.scale_modifier, cov3D);
-    const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
-    float dmean_t[3] = {0.f, 0.f, 0.f}, ddir[3] = {0.f, 0.f, 0.f};
-    float dcov_t[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dop = 0.f;
-    float dsh_t[kHasSH ? 48 : 1];
-#pragma unroll
-    for (int i = 0; i < (kHasSH ? 48 : 1); i++) dsh_t[i] = 0.f;
-    float s_reg[kHasSH && !kStage ? 16 : 1][3];
-    if constexpr (kHasSH && !kStage) {
-        const float* sh = a.shs + (size_t)(live ? idx : a.g0) * a.M * 3;
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) s_reg[k][c] = (live && k < ncoef) ? sh[3 * k + c] : 0.f;
-    }
-    bool any = false;
-    float2 nxt[kMvRowPer];
-    load_rows(0, nxt);
-    for (int v = 0; v < a.V; v++) {
-        __syncthreads();  // the previous view's rows are read (and, at v = 0, the SH rows staged)
-        float2* srow = reinterpret_cast<float2*>(s_rows);
-#pragma unroll
-        for (int i = 0; i < kMvRowPer; i++) {
-            const int f = threadIdx.x + 256 * i;
-            if (f < kMvRowF2) srow[f] = nxt[i];
-        }
-        __syncthreads();
-        if (v + 1 < a.V) load_rows(v + 1, nxt);  // in flight while view v's terms are formed
-        const float* row = s_rows + threadIdx.x * kViewRow;
-        const uint32_t w9 = __float_as_uint(row[9]);
-        if (!live || w9 == 0u) continue;  // not visible in view v: no terms (the reference's radii > 0 filter)
-        any = true;
-        const float acc[3] = {row[0], row[1], row[2]};
-        const float gx = row[3], gy = row[4], dcx = row[5], dcy = row[6], dcw = row[7], dop_v = row[8];
-        const float* cam = mv_cam(a, v);
-        const Mat4 V = load_mat4(cam);
-        const Mat4 Pm = load_mat4(cam + 16);
-        const float tan_fovx = cam[37], tan_fovy = cam[38];
-        // rasterizer_impl.cu:222-223 / gs_api.cpp: focal from the image size
-        const float focal_x = cam[35] / (2.0f * tan_fovx);
-        const float focal_y = cam[36] / (2.0f * tan_fovy);
-        float dmean[3], dcov[6];
-        cov2d_backward(mx, my, mz, cov3D, dcx, dcy, dcw, V, focal_x, focal_y, tan_fovx, tan_fovy, dmean, dcov);
-        proj_backward(mx, my, mz, Pm, gx, gy, dmean);
-#pragma unroll
-        for (int i = 0; i < 3; i++) dmean_t[i] += dmean[i];
-#pragma unroll
-        for (int i = 0; i < 6; i++) dcov_t[i] += dcov[i];
-        dop += dop_v;
-        if (stats) {
-            st_acc = st_acc + sqrtf(gx * gx + gy * gy);
-            st_den = st_den + 1.f;
-            st_max = fmaxf(st_max, (float)(w9 & 0xFFFFFFu));
-        }
-        if constexpr (kHasSH) {
-            const uint8_t cb = (uint8_t)(w9 >> 24);
-            float dsh_c[16], dRGB[3];
-            if constexpr (kStage) {
-                sh_backward_terms(a.D, cam + 32, mx, my, mz, ShRowPtr{lrow}, cb, acc, dsh_c, dRGB, ddir);
-            } else {
-                sh_backward_terms(a.D, cam + 32, mx, my, mz, s_reg, cb, acc, dsh_c, dRGB, ddir);
-            }
-#pragma unroll
-            for (int k = 0; k < 16; k++)
-#pragma unroll
-                for (int c = 0; c < 3; c++)
-                    if (k < ncoef) dsh_t[3 * k + c] += dsh_c[k] * dRGB[c];
-        }
-    }
-    if (live) {
-        // (a Gaussian no view sees: every output is zero, as the two-pass kernel writes)
-        a.dL_dopacity[idx] = any ? dop : 0.f;
-        float dscale[3] = {0.f, 0.f, 0.f};
-        float4 dq = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (any) cov3d_backward(qrot, scl, a.scale_modifier, dcov_t, dscale, dq);
-#pragma unroll
-        for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = dscale[i];
-        reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
-        if (stats && any) {
-            a.grad_norm_accum[idx] = st_acc;
-            a.denom[idx] = st_den;
-            a.max_radii[idx] = st_max;
-        }
-#pragma unroll
-        for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = any ? dmean_t[i] + ddir[i] : 0.f;
-    }
-    if constexpr (kStage) {
-        __syncthreads();  // every thread has read its SH row: the area takes the gradient rows
-        if (live) {
-#pragma unroll
-            for (int i = 0; i < 48; i++) lrow[i] = any ? dsh_t[i] : 0.f;
-        }
-        __syncthreads();
-        float4* out = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)(a.g0 + local0) * 12;
-        for (int f = threadIdx.x; f < nblk * 12; f += 256) {
-            const float* r = s_sh + (f / 12) * kShRow + 4 * (f % 12);
-            store_out4(&out[f], make_float4(r[0], r[1], r[2], r[3]), a.nt != 0);
-        }
-    } else if constexpr (kHasSH) {
-        if (live)
-            for (int k = 0; k < a.M; k++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    float val = 0.f;
-#pragma unroll
-                    for (int kk = 0; kk < 16; kk++) val = (kk == k && any) ? dsh_t[3 * kk + c] : val;
-                    a.dL_dsh[(size_t)idx * a.M * 3 + 3 * k + c] = val;
-                }
-    }
-}
-
-void launch_multiview_backward(const MultiViewArgs& args, hipStream_t s) {
-    if (args.count <= 0) return;
-    MultiViewArgs a = args;
-    a.nt = 1;  // the dL_dsh rows non-temporal (as backward_gaussians_kernel's)
-    const dim3 grid((a.count + 255) / 256);
-    const bool sh = a.shs != nullptr;
-    // (A role-split form -- 64 Gaussians per workgroup, wave 3 the geometry
-    // terms, waves 0-2 one colour channel each, 128 VGPRs and 22 KB of LDS:
-    // 4 waves per SIMD instead of 2 -- measured 0.4358 against 0.3360 ms per
-    // 8-view step at config 5, profiles/r05d_bench_cfg5_roles.log: the
-    // per-view barrier waits on the geometry wave and the channel waves redo
-    // the direction and basis; removed.)
-    if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward1_kernel<true, true>), grid, dim3(256), 0, s, a);
-    else if (sh) hipLaunchKernelGGL((multiview_backward1_kernel<true, false>), grid, dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((multiview_backward1_kernel<false, false>), grid, dim3(256), 0, s, a);
-}
-
-}  // namespace gsamd
