@@ -74,20 +74,11 @@ def main():
             with torch.no_grad():
                 if args.amr_once:
                     return AR.apply(*a, -2, e, u8, u8, u8, True, ast)[0]
-                if args.per_step:
-                    evs[0].record()
-                c, _, gb, bb, ib = AR.apply(*a, 0, e, u8, u8, u8, False, ast)
-                if args.per_step:
-                    evs[1].record()
-                acc = c
-                for k in range(1, 5):
-                    if args.per_step:
-                        evs[2 * k].record()
-                    c, _, gb, bb, ib = AR.apply(*a, k, acc, gb, bb, ib, False, ast)
-                    if args.per_step:
-                        evs[2 * k + 1].record()
-                    acc = acc + c
-            return acc
+                # the bench's frame: rasterization_amr.render_steps (sums fused)
+                from gaussian_splatting_with_eye_tracking_amd import rasterization_amr as RA
+                st_ev = [evs[2 * k] for k in range(5)] if args.per_step else None
+                en_ev = [evs[2 * k + 1] for k in range(5)] if args.per_step else None
+                return RA.render_steps(*a, ast, starters=st_ev, enders=en_ev)[0]
 
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(10)]
     step_ms = {v: [] for v in args.values}
