@@ -34,11 +34,13 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contract=off", "-munsafe-fp-atomics",
              "-fno-slp-vectorize",
              "-Wall", "-Wno-unused-function", f"-I{INCLUDE}", f"-I{CSRC}"]
-# Per-source flags after HIP_FLAGS: the multi-view backward's gradients are
-# held to a tolerance (tests/test_gpu_multiview.py), so it compiles with FMA
-# contraction and reciprocal math (30 % fewer VALU instructions per view,
-# DESIGN.md §8f); everything on the keys / images keeps the contract above.
-SOURCE_FLAGS = {"multiview.hip": ["-ffp-contract=fast", "-freciprocal-math", "-fapprox-func"]}
+# Per-source flags after HIP_FLAGS: the backward passes' gradients are held
+# to a tolerance (1e-4; tests/test_gpu_multiview.py 1e-5 against the per-view
+# sum), so they compile with reciprocal math (and the multi-view kernel with
+# FMA contraction too: 30 % fewer VALU instructions per view);
+# everything on the keys / images keeps the exact contract above.
+SOURCE_FLAGS = {"multiview.hip": ["-ffp-contract=fast", "-freciprocal-math", "-fapprox-func"],
+                "backward.hip": ["-freciprocal-math", "-fapprox-func"]}
 # extra flags for code-generation experiments (e.g. GSAMD_EXTRA_HIPFLAGS=-fno-slp-vectorize)
 HIP_FLAGS += shlex.split(os.environ.get("GSAMD_EXTRA_HIPFLAGS", ""))
 

@@ -211,7 +211,11 @@ def test_config3_full_size_amr(oracle_threads):
             ck, _, gb, bb, ib = _RasterizeGaussians.apply(*args, k, acc, gb, bb, ib, False, s)
             acc = acc + ck
             steps.append(ck.cpu().numpy())
+        # the fused driver (renderer_amr.render's sequence): the same frame, bit for bit
+        from gaussian_splatting_with_eye_tracking_amd.rasterization_amr import render_steps
+        fused, fradii, _, _, _ = render_steps(*args, s)
         torch.cuda.synchronize()
+        assert torch.equal(fused, acc) and torch.equal(fradii, radii)
     os_ = O.settings_from_camera(cam)
     kw = dict(means3D=sc.means3D, opacities=sc.opacities, shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
     racc, rradii, st, rsteps = O.amr_render_foveated(os_, kw)
