@@ -206,3 +206,25 @@ def test_base_renderer_matches_explicit_call():
         pipe_py = types.SimpleNamespace(debug=False, compute_cov3D_python=False, convert_SHs_python=True)
         img_py = R.render(camera, pc, pipe_py, bg)["render"]
         assert G.image_l1(img_py.cpu().numpy(), ref.cpu().numpy()) < G.IMAGE_L1_TOL
+
+
+@pytest.mark.gpu
+def test_fused_steps_with_nothing_visible():
+    """Every Gaussian off-screen (K = 0, empty tile lists, every tile at the
+    lowest level): the fused driver's frame equals the literal sequence's
+    (the background where the rounds render, zero elsewhere)."""
+    from gaussian_splatting_with_eye_tracking_amd.rasterization_amr import render_steps
+    P, W, H = 5_000, 320, 240
+    sc, cam = G.scene_and_camera(P, W, H, 7)
+    t, pc, camera, pipe = _duck(sc, cam)
+    t["means3D"][:, 0] += 1.0e4
+    s = _settings_of(camera, torch.tensor([0.3, 0.2, 0.1], dtype=torch.float32, device="cuda"))
+    e = torch.Tensor([]).cuda()
+    m2 = torch.zeros_like(t["means3D"])
+    args = (t["means3D"], m2, t["shs"], e, t["opacities"], t["scales"], t["rotations"], e)
+    with torch.no_grad():
+        ref, rradii, _, _, _ = _chain(args, s)
+        got, radii, _, _, _ = render_steps(*args, s)
+        torch.cuda.synchronize()
+    assert int((rradii > 0).sum()) == 0
+    assert torch.equal(got, ref) and torch.equal(radii, rradii)
