@@ -509,6 +509,7 @@ struct AppendLds {
     uint64_t key[kNT * kRound];
     uint32_t aux[kNT * kRound];
     uint32_t to[kNT * kRound];
+    uint16_t src[kNT * kRound];  // expand_sources: the source of each pair of the round
 };
 
 // The workgroup's whole histogram (accumulated in L.run by the caller) ->
@@ -583,9 +584,10 @@ __device__ __forceinline__ void coalesced_append(AppendLds<kNT, kRound>& L, int 
 
 // Sources (kSPT per thread: Gaussians, or staged entries) expand to count
 // consecutive bins from first; the workgroup's expansion is handed out in
-// blocks of kRound consecutive pairs per thread (the block's first pair ->
-// its source by a binary search over the scanned counts, then a forward
-// walk), kRound x kNT pairs per append round.
+// blocks of kRound consecutive pairs per thread, kRound x kNT pairs per append
+// round.  Each round the sources overlapping its window write their index
+// into the window's pair slots (L.src) and every pair reads its source from
+// there (one LDS read instead of a binary search over the scanned counts).
 template <int kNS>
 struct SourceLds {
     uint64_t key[kNS];
@@ -605,8 +607,11 @@ __device__ __forceinline__ void expand_sources(SourceLds<kNT * kSPT>& S, AppendL
     uint32_t sum = 0;
 #pragma unroll
     for (int q = 0; q < kSPT; q++) sum += cnt[q];
+    static_assert(kNS <= 65536, "16-bit source indices");
+    constexpr uint32_t kW = kNT * kRound;  // pairs per round
     uint32_t np;
     uint32_t pre = block_exclusive_scan<kNT>(sum, S.wave, np);
+    uint32_t pr[kSPT];
 #pragma unroll
     for (int q = 0; q < kSPT; q++) {
         const int i = tid * kSPT + q;
@@ -614,31 +619,28 @@ __device__ __forceinline__ void expand_sources(SourceLds<kNT * kSPT>& S, AppendL
         if constexpr (kAux) S.aux[i] = aux[q];
         S.first[i] = first[q];
         S.pref[i] = pre;
+        pr[q] = pre;
         pre += cnt[q];
     }
-    __syncthreads();
-    for (uint32_t j0 = 0; j0 < np; j0 += kNT * kRound) {
+    for (uint32_t j0 = 0; j0 < np; j0 += kW) {
+        // the window's pairs -> their sources
+#pragma unroll
+        for (int q = 0; q < kSPT; q++) {
+            const uint32_t lo = max(pr[q], j0), hi = min(pr[q] + cnt[q], j0 + kW);
+            for (uint32_t k = lo; k < hi; k++) L.src[k - j0] = (uint16_t)(tid * kSPT + q);
+        }
+        __syncthreads();  // (also: the sources' LDS rows, at the first round)
         uint32_t bin[kRound], ax[kRound];
         uint64_t ky[kRound];
         int n = 0;
-        // the last source with pref <= j (a source with count 0 shares its
-        // pref with the next; the last of equal prefs is the one with pairs)
         uint32_t j = j0 + (uint32_t)(tid * kRound);
-        int lo = 0;
-        if (j < np) {
-            int hi = kNS - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (S.pref[mid] <= j) lo = mid; else hi = mid - 1;
-            }
-        }
 #pragma unroll
         for (int r = 0; r < kRound; r++, j++) {
             if (j < np) {
-                while (lo + 1 < kNS && S.pref[lo + 1] <= j) lo++;
-                bin[n] = S.first[lo] + (j - S.pref[lo]);
-                ky[n] = S.key[lo];
-                if constexpr (kAux) ax[n] = S.aux[lo];
+                const int s = L.src[j - j0];
+                bin[n] = S.first[s] + (j - S.pref[s]);
+                ky[n] = S.key[s];
+                if constexpr (kAux) ax[n] = S.aux[s];
                 n++;
             }
         }
