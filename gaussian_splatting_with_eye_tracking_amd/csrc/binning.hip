@@ -755,23 +755,31 @@ __global__ void __launch_bounds__(kNT) band_split_kernel(uint32_t gx, int split,
         for (int u = 0; u < kU * kSPT; u++)
             for (uint32_t x = c[u] & 0xffffu; x < (c[u] >> 16); x++) atomicAdd(&B.a.run[x], 1u);
     }
-    reserve_runs(B.a, tile_cursor + row * gx, gx);
-    for (uint32_t c0 = part * kCh; c0 < n_ent; c0 += stride) {
-        uint32_t cnt[kSPT], x0[kSPT];
-        uint64_t key[kSPT];
+    // the entries of the chunk after the one being expanded are in flight
+    // (the first chunk's behind the run reservation's device atomics)
+    uint32_t col[kSPT];
+    uint64_t key[kSPT];
+    auto load_chunk = [&](uint32_t c0) {
 #pragma unroll
         for (int q = 0; q < kSPT; q++) {
             const uint32_t e = c0 + threadIdx.x * kSPT + q;
-            cnt[q] = x0[q] = 0;
-            key[q] = 0;
-            if (e < n_ent) {
-                const uint32_t c = stage_cols[beg + e];
-                key[q] = stage_keys[beg + e];
-                x0[q] = c & 0xffffu;
-                cnt[q] = (c >> 16) - x0[q];
-            }
+            col[q] = e < n_ent ? stage_cols[beg + e] : 0u;
+            key[q] = e < n_ent ? stage_keys[beg + e] : 0ull;
         }
-        expand_sources<false, kNT, kRound, kSPT>(B.src, B.a, cnt, key, x0, x0, pair_keys, nullptr, limit);
+    };
+    load_chunk(part * kCh);
+    reserve_runs(B.a, tile_cursor + row * gx, gx);
+    for (uint32_t c0 = part * kCh; c0 < n_ent; c0 += stride) {
+        uint32_t cnt[kSPT], x0[kSPT];
+        uint64_t k[kSPT];
+#pragma unroll
+        for (int q = 0; q < kSPT; q++) {
+            x0[q] = col[q] & 0xffffu;
+            cnt[q] = (col[q] >> 16) - x0[q];
+            k[q] = key[q];
+        }
+        if (c0 + stride < n_ent) load_chunk(c0 + stride);
+        expand_sources<false, kNT, kRound, kSPT>(B.src, B.a, cnt, k, x0, x0, pair_keys, nullptr, limit);
     }
 }
 
