@@ -62,12 +62,12 @@ STAGES = [
     ("sort_tiles_radix_kernel", "sort_tiles"),
     ("sort_tiles_bucket_kernel", "sort_tiles"),
     ("tile_scan", "tile_scan"),
-    ("amr_region_render_kernel<1,", "amr_render"),
-    ("amr_region_render_kernel<4,", "amr_render_once"),
+    ("amr_region_render_kernel<1", "amr_render"),
+    ("amr_region_render_kernel<4", "amr_render_once"),
     ("amr_region_lists_kernel", "amr_lists"),
     ("amr_levels_kernel", "amr_levels"),
     ("amr_interpolate_kernel", "amr_interp"),
-    ("multiview_backward_kernel", "multiview_bwd"),
+    ("multiview_backward", "multiview_bwd"),
     ("pack_view_grads_kernel", "pack_view"),
 ]
 
