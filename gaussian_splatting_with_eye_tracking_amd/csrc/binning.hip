@@ -399,18 +399,39 @@ __device__ __forceinline__ bool gaussian_rect(int idx, const float* __restrict__
     return true;
 }
 
+// The rect of a Gaussian whose radius and mean are already loaded (the
+// binning loops request every Gaussian's loads up front: a loop over
+// gaussian_rect waited for the radius, then -- behind its branch -- for the
+// mean, twice per Gaussian).
+__device__ __forceinline__ bool rect_of(int rad, float2 xy, int block, uint32_t gx, uint32_t gy, Rect& r) {
+    if (rad <= 0) return false;
+    r = get_rect(xy.x, xy.y, rad, block, block, gx, gy);
+    return true;
+}
+constexpr int kBinPerMax = 8;  // Gaussians per thread per binning chunk (bin_chunk_for / kBinThreads)
+
 __global__ void __launch_bounds__(kBinThreads) count_tiles_kernel(int P, int chunk, const float* __restrict__ means2D,
                                                                   const int* __restrict__ radii, int block,
                                                                   uint32_t gx, uint32_t gy,
                                                                   uint32_t* __restrict__ tile_count, uint32_t nslots) {
     extern __shared__ uint32_t hist[];
     const int T = (int)(gx * gy);
+    const int beg = blockIdx.x * chunk, end = min(P, beg + chunk);
+    int rad[kBinPerMax];
+    float2 xy[kBinPerMax];
+#pragma unroll
+    for (int u = 0; u < kBinPerMax; u++) {
+        const int idx = beg + threadIdx.x + u * kBinThreads;
+        const bool in = u * kBinThreads < chunk && idx < end;
+        rad[u] = in ? radii[idx] : 0;
+        xy[u] = in ? reinterpret_cast<const float2*>(means2D)[idx] : make_float2(0.f, 0.f);
+    }
     for (int i = threadIdx.x; i < T; i += kBinThreads) hist[i] = 0;
     __syncthreads();
-    const int beg = blockIdx.x * chunk, end = min(P, beg + chunk);
-    for (int idx = beg + threadIdx.x; idx < end; idx += kBinThreads) {
+#pragma unroll
+    for (int u = 0; u < kBinPerMax; u++) {
         Rect r;
-        if (!gaussian_rect(idx, means2D, radii, block, gx, gy, r)) continue;
+        if (!rect_of(rad[u], xy[u], block, gx, gy, r)) continue;
         for (uint32_t y = r.y0; y < r.y1; y++)
             for (uint32_t x = r.x0; x < r.x1; x++) atomicAdd(&hist[y * gx + x], 1u);
     }
@@ -436,12 +457,26 @@ __global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int c
     if (hdr && hdr[kHdrNumRendered] > cap) return;
     extern __shared__ uint32_t slot[];
     const int T = (int)(gx * gy);
+    const int beg = blockIdx.x * chunk, end = min(P, beg + chunk);
+    // the chunk's radii, means and depths, requested up front and kept for
+    // both passes
+    int rad[kBinPerMax];
+    float2 xy[kBinPerMax];
+    float dep[kBinPerMax];
+#pragma unroll
+    for (int u = 0; u < kBinPerMax; u++) {
+        const int idx = beg + threadIdx.x + u * kBinThreads;
+        const bool in = u * kBinThreads < chunk && idx < end;
+        rad[u] = in ? radii[idx] : 0;
+        xy[u] = in ? reinterpret_cast<const float2*>(means2D)[idx] : make_float2(0.f, 0.f);
+        dep[u] = in ? depths[idx] : 0.f;
+    }
     for (int i = threadIdx.x; i < T; i += kBinThreads) slot[i] = 0;
     __syncthreads();
-    const int beg = blockIdx.x * chunk, end = min(P, beg + chunk);
-    for (int idx = beg + threadIdx.x; idx < end; idx += kBinThreads) {
+#pragma unroll
+    for (int u = 0; u < kBinPerMax; u++) {
         Rect r;
-        if (!gaussian_rect(idx, means2D, radii, block, gx, gy, r)) continue;
+        if (!rect_of(rad[u], xy[u], block, gx, gy, r)) continue;
         for (uint32_t y = r.y0; y < r.y1; y++)
             for (uint32_t x = r.x0; x < r.x1; x++) atomicAdd(&slot[y * gx + x], 1u);
     }
@@ -453,10 +488,12 @@ __global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int c
         if (c) slot[i] = atomicAdd(&cur[i], c);
     }
     __syncthreads();
-    for (int idx = beg + threadIdx.x; idx < end; idx += kBinThreads) {
+#pragma unroll
+    for (int u = 0; u < kBinPerMax; u++) {
         Rect r;
-        if (!gaussian_rect(idx, means2D, radii, block, gx, gy, r)) continue;
-        const uint64_t key = ((uint64_t)float_bits(depths[idx]) << 32) | (uint32_t)idx;
+        if (!rect_of(rad[u], xy[u], block, gx, gy, r)) continue;
+        const int idx = beg + threadIdx.x + u * kBinThreads;
+        const uint64_t key = ((uint64_t)float_bits(dep[u]) << 32) | (uint32_t)idx;
         for (uint32_t y = r.y0; y < r.y1; y++)
             for (uint32_t x = r.x0; x < r.x1; x++) {
                 const uint32_t sl = atomicAdd(&slot[y * gx + x], 1u);
@@ -696,17 +733,27 @@ __global__ void __launch_bounds__(kNT) band_stage_kernel(int P, const float* __r
     // the thread's Gaussians: kSPT consecutive indices per group
     uint32_t cnt[kStageG], cols[kStageG], y0[kStageG];
     uint64_t key[kStageG];
+    int rad[kStageG];
+    float2 xy[kStageG];
+    float dep[kStageG];
+#pragma unroll
+    for (int g = 0; g < kStageG; g++) {  // every Gaussian's loads requested up front
+        const int idx = blockIdx.x * kStageChunk + ((g / kSPT) * kNT + threadIdx.x) * kSPT + g % kSPT;
+        rad[g] = idx < P ? radii[idx] : 0;
+        xy[g] = idx < P ? reinterpret_cast<const float2*>(means2D)[idx] : make_float2(0.f, 0.f);
+        dep[g] = idx < P ? depths[idx] : 0.f;
+    }
 #pragma unroll
     for (int g = 0; g < kStageG; g++) {
         const int idx = blockIdx.x * kStageChunk + ((g / kSPT) * kNT + threadIdx.x) * kSPT + g % kSPT;
         cnt[g] = cols[g] = y0[g] = 0;
         key[g] = 0;
         Rect rc;
-        if (idx < P && gaussian_rect(idx, means2D, radii, block, gx, gy, rc) && rc.x1 > rc.x0) {
+        if (rect_of(rad[g], xy[g], block, gx, gy, rc) && rc.x1 > rc.x0) {
             cnt[g] = rc.y1 - rc.y0;  // one entry per tile row
             y0[g] = rc.y0;
             cols[g] = rc.x0 | (rc.x1 << 16);
-            key[g] = ((uint64_t)float_bits(depths[idx]) << 32) | (uint32_t)idx;
+            key[g] = ((uint64_t)float_bits(dep[g]) << 32) | (uint32_t)idx;
         }
     }
     for (int b = threadIdx.x; b < kBandBins; b += kNT) B.a.run[b] = 0;
