@@ -65,7 +65,7 @@ for step in "$@"; do
     gaptrace3) run gaptrace3 600 rocprofv3 --kernel-trace -d "$O/gaptrace3" -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 20 --warmup 3 --no-cpu-baseline --no-ext ;;
     bench5) run bench_cfg5 600 python bench.py --config cfg5_8view_1080p_1M --steps 10 --warmup 3 --no-cpu-baseline ;;
     trace3) run trace_cfg3 300 rocprofv3 --kernel-trace -d gpurun_out/trace_cfg3 -o run --output-format csv -- python3 bench.py --config cfg3_amr_1080p_1M --steps 10 --warmup 3 --no-cpu-baseline --no-profile --no-ext ;;
-    sqa2|sqa4|sqa5|sqb2|sqb4|sqb5)  # SQ issue / wait counters per kernel (two 8-counter sets)
+    sqa2|sqa3|sqa4|sqa5|sqb2|sqb3|sqb4|sqb5)  # SQ issue / wait counters per kernel (two 8-counter sets)
       c=$(cfg_of "$step")
       case "$step" in
         sqa*) cnt="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY" ;;
