@@ -533,7 +533,11 @@ void launch_count_tiles(int P, const GeomView& g, const int* radii, int W, int H
 //          (entry, tile) key into the tile's range, bins = the row's tiles.
 // Per tile the multiset of keys is the direct duplicate's; the sort makes
 // the order exact (bit-identical point_list).
-constexpr int kStageChunk = 4096;  // Gaussians per stage workgroup (runs reserved once per row per chunk)
+// Gaussians per stage workgroup (runs reserved once per row per chunk): 2048
+// -- twice the workgroups of 4096, two or four Gaussians per thread -- against
+// 4096: duplicate 0.0678 -> 0.0663 ms at config 2, 0.2464 -> 0.2409 at config
+// 4 (1024: 0.0702; profiles/r05at_ab_stage_chunk_*.log)
+constexpr int kStageChunk = 2048;
 
 // kNT threads per workgroup; each owns kBandBins / kNT consecutive bins in
 // the per-bin steps.
