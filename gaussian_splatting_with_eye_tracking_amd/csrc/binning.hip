@@ -74,16 +74,20 @@ __device__ __forceinline__ void slot_cursors(uint32_t* __restrict__ count, uint3
 // the call's token in word 4 -- the host spins on the token instead of
 // waiting for an event after the scan, so the stream carries no marker packet
 // between the scan and the work behind it.
-__device__ __forceinline__ void mirror_header(uint32_t* m, uint32_t K, uint32_t err, uint32_t maxc, uint32_t nlarge,
-                                              uint32_t token) {
-    if (token) {
-        // seqlock: the slot's token is invalidated before the words change, so a
-        // reader that saw a token, copied the words and sees the same token
-        // again read words no later scan had started to rewrite
-        // (gs_api.cpp finish_header_read)
+// seqlock: the slot's token is invalidated before the words change, so a
+// reader that saw a token, copied the words and sees the same token again read
+// words no later scan had started to rewrite (gs_api.cpp finish_header_read).
+// The invalidation (and its fence) is issued by the scan's first thread at the
+// top of the kernel, under the count loads, instead of in the tail after the
+// scan: one system-scope round trip fewer on the scan's critical path.
+__device__ __forceinline__ void mirror_invalidate(uint32_t* m, uint32_t token) {
+    if (m && token) {
         __hip_atomic_store(m + 4, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __threadfence_system();
     }
+}
+__device__ __forceinline__ void mirror_header(uint32_t* m, uint32_t K, uint32_t err, uint32_t maxc, uint32_t nlarge,
+                                              uint32_t token) {
     *reinterpret_cast<uint4*>(m) = make_uint4(K, err, maxc, nlarge);  // kHdrNumRendered, kHdrError, kHdrMaxTileCount, kHdrNumLargeTiles
     if (token) {
         __threadfence_system();
@@ -130,6 +134,9 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, uint32_t
     const int beg = min(T, tid * per), end = min(T, beg + per);
     uint32_t sum = 0, mx = 0;
     uint32_t cv[kPer > 0 ? kPer : 1];
+    // (the preprocess's error word, read while the counts load; this kernel
+    // does not write it)
+    const uint32_t err = (tid == 0 && hdr_mirror) ? hdr[kHdrError] : 0u;
     if constexpr (kPer > 0) {
 #pragma unroll
         for (int k = 0; k < kPer; k++) cv[k] = beg + k < end ? slot_total(count, T, beg + k, nslots) : 0u;
@@ -145,7 +152,10 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, uint32_t
             mx = max(mx, c);
         }
     }
-    if (tid == 0) nlarge = 0;
+    if (tid == 0) {
+        nlarge = 0;
+        mirror_invalidate(hdr_mirror, band.mirror_token);
+    }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
     if ((tid & 63) == 0) s_max[tid >> 6] = mx;
@@ -177,7 +187,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_kernel(int T, uint32_t
         hdr[kHdrMaxTileCount] = m;
         hdr[kHdrNumLargeTiles] = nlarge;
         hdr[kHdrT] = (uint32_t)T;
-        if (hdr_mirror) mirror_header(hdr_mirror, total, hdr[kHdrError], m, nlarge, band.mirror_token);
+        if (hdr_mirror) mirror_header(hdr_mirror, total, err, m, nlarge, band.mirror_token);
     }
 }
 
@@ -207,6 +217,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, u
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t c[kS], incl[kS];
     uint32_t mx = 0;
+    const uint32_t err = (tid == 0 && hdr_mirror) ? hdr[kHdrError] : 0u;  // (as tile_scan_kernel)
 #pragma unroll
     for (int k = 0; k < kS; k++) {
         const int i = k * kScanThreads + tid;
@@ -214,7 +225,10 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, u
         incl[k] = c[k];
         mx = max(mx, c[k]);
     }
-    if (tid == 0) nlarge = 0;
+    if (tid == 0) {
+        nlarge = 0;
+        mirror_invalidate(hdr_mirror, band.mirror_token);
+    }
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
 #pragma unroll
@@ -273,7 +287,7 @@ __global__ void __launch_bounds__(kScanThreads) tile_scan_slices_kernel(int T, u
         hdr[kHdrMaxTileCount] = m;
         hdr[kHdrNumLargeTiles] = nlarge;
         hdr[kHdrT] = (uint32_t)T;
-        if (hdr_mirror) mirror_header(hdr_mirror, run, hdr[kHdrError], m, nlarge, band.mirror_token);
+        if (hdr_mirror) mirror_header(hdr_mirror, run, err, m, nlarge, band.mirror_token);
     }
 }
 
