@@ -839,8 +839,10 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
     def frame_5step(record=False, fovea=False, fused=True):
         # gaussian_renderer_amr.render's rasterizer sequence (renderer_amr.render
         # without its Python camera / model plumbing): fused, the steps add
-        # their pixels into the frame in the kernel; fused=False the literal
-        # apply + torch-add sequence (apply_chain_fps below)
+        # their pixels into the frame in the kernel, steps 1..4 as one launch
+        # (render_steps' default without per-step events); record: per-step
+        # events, so steps 1..4 launched one by one (per_step_ms); fused=False
+        # the literal apply + torch-add sequence (apply_chain_fps below)
         lv = (lambda ib: RA.apply_fovea_levels(ib, W, H, fov_centres, fov_radii)) if fovea else None
         if record:
             ev[0].record()
@@ -868,29 +870,39 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
         torch.cuda.synchronize()
         ctx.barrier()
         el5 = time.perf_counter() - t0
-        for _ in range(max(2, warmup)):  # (its step images and sums: allocator blocks the fused frame never asks for)
-            frame_5step(fused=False)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            frame_5step(fused=False)
-        torch.cuda.synchronize()
-        ctx.barrier()
-        el5u = time.perf_counter() - t0
-        # per-stage and per-step times: a second pass with events
+        # (--no-profile, the rocprofv3 runs: only the timed frame's launches, so
+        # the kernel statistics are the frame's -- no apply-chain or per-step
+        # passes launching the step kernel one step at a time)
+        diag = not ctx.args.no_profile
+        el5u = float("nan")
+        if diag:
+            for _ in range(max(2, warmup)):  # (its step images and sums: allocator blocks the fused frame never asks for)
+                frame_5step(fused=False)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                frame_5step(fused=False)
+            torch.cuda.synchronize()
+            ctx.barrier()
+            el5u = time.perf_counter() - t0
+        # per-stage times: a second pass of the timed frame with stage events;
+        # per-step times: a third, with events between steps 1..4 launched
+        # one by one
         prof = {}
         step_ms = np.zeros(5)
         if not ctx.args.no_profile:
             _C.profile_enable(True)
             _C.profile_stages([])
             _C.profile_read(True)
-        for _ in range(steps):
+            for _ in range(steps):
+                frame_5step()
+            torch.cuda.synchronize()
+            prof = _C.profile_read(True)
+            _C.profile_enable(False)
+        for _ in range(steps if diag else 0):
             frame_5step(record=True)
             torch.cuda.synchronize()
             step_ms += np.array([ev[i].elapsed_time(ev[i + 1]) for i in range(5)])
-        if not ctx.args.no_profile:
-            prof = _C.profile_read(True)
-            _C.profile_enable(False)
         t0 = time.perf_counter()
         for _ in range(steps):
             frame_once()
@@ -929,10 +941,11 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
     el5, el1, el5u = ctx.max_over_ranks(el5, el1, el5u)
     res = {"value": ctx.world * steps / el5, "unit": "frames/s", "ms_per_step": 1000.0 * el5 / steps,
            "render_once_fps": ctx.world * steps / el1, "ramp_steps": ramp,
-           "apply_chain_fps": ctx.world * steps / el5u,
-           "frame": "renderer_amr.render's sequence with the step-image sums fused into the step kernels "
-                    "(gs_amr_accumulate_step, bit-identical); apply_chain_fps: the literal apply + torch-add "
-                    "sequence"}
+           "apply_chain_fps": ctx.world * steps / el5u if el5u == el5u else None,
+           "frame": "renderer_amr.render's sequence with the step-image sums fused into the step kernels and "
+                    "steps 1..4 in one launch (gs_amr_accumulate_step, bit-identical); per_step_ms: the steps "
+                    "launched one by one with events between them; apply_chain_fps: the literal apply + "
+                    "torch-add sequence"}
     if ctx.rank != 0:
         return res
     with torch.no_grad():
@@ -957,14 +970,14 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
         # the PMC summary holds means per launch; the roofline is per frame
         roofline = make_roofline("amr_render", by, ms, config_key(P, W, H, 32), "stage-profile pass",
                                  per=stages["amr_render"]["launches"] / steps, stream_read=0.0)
-        roofline["per"] = "frame (the 4 amr_render launches of steps 1..4 summed; traffic per frame)"
+        roofline["per"] = "frame (the one amr_render launch of steps 1..4; traffic per frame)"
     res.update({
         "metric": "foveated AMR frames/sec (forward-only render(), 5 fovea steps) at 1080p, 1M Gaussians",
         "config": {"workload": f"cfg3_amr_1080p_1M: {P} Gaussians, {W}x{H}, 32x32 AMR tiles, 5-step foveated "
                                f"render() per frame" + (", replicas" if ctx.world > 1 else ""),
                    "P": P, "width": W, "height": H, "K_instances": K, "parallelism": f"replicas{ctx.world}",
                    "levels_hist": np.bincount(lv, minlength=5)[1:].tolist()},
-        "per_step_ms": [round(x / steps, 4) for x in step_ms],
+        "per_step_ms": [round(x / steps, 4) for x in step_ms] if diag else None,
         "roofline": roofline, "stages": stages,
         "step_roofline": step_roofline(step_bytes_amr_frame(P, V3, K, len(lv), rng, lv), res["ms_per_step"],
                                        "SURVEY.md §8(d) forward-only AMR frame 32P + 307V + 44K + 24T + "

@@ -1096,7 +1096,8 @@ int gs_amr_accumulate_step(int P, const float* background, int width, int height
                            void* stream) {
     return guarded([&]() -> int {
         if (P <= 0) return 0;
-        if (foveaStep < 1 || foveaStep > 4) throw GsError("gs_amr_accumulate_step: foveaStep in 1..4");
+        if ((foveaStep < 1 || foveaStep > 4) && foveaStep != kAmrStepsAll)
+            throw GsError("gs_amr_accumulate_step: foveaStep in 1..4 or GSPLAT_AMD_AMR_STEPS_1_TO_4");
         if (g_amr_variant != 4) throw GsError("gs_amr_accumulate_step needs the default amr_variant (4)");
         if (!geom_buffer_precomp || !image_buffer_precomp || !accum)
             throw GsError("gs_amr_accumulate_step needs the buffers returned by foveaStep 0 and the running image");

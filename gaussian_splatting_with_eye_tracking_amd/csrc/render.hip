@@ -478,7 +478,11 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     // by each of the tile's four units from the previous current level; the
     // last unit of the tile to finish stores it (tile_done counts units mod 4),
     // so every unit has read the previous value before it is replaced.
-    uint32_t L_last, L;
+    // (GSPLAT_AMD_AMR_STEPS_1_TO_4: steps 1..4 in one launch -- the unit
+    // renders rounds 1..min(level, 4), the rounds steps 1..4 give it one by
+    // one, and stores the level state step 4 leaves: current min(level, 4),
+    // last min(level, 3))
+    uint32_t L_last, L, L_last_store;
     if (lv_current) {
         const uint32_t Lp = levels[tile], prev = lv_current[tile];
         if (foveaStep == 1) {
@@ -487,19 +491,24 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
         } else if (foveaStep <= 4) {
             L_last = prev;
             L = Lp >= (uint32_t)foveaStep ? (uint32_t)foveaStep : prev;
+        } else if (foveaStep == kAmrStepsAll) {
+            L_last = 0;
+            L = min(Lp, 4u);
         } else {
             L_last = 0;
             L = Lp;
         }
+        L_last_store = foveaStep == kAmrStepsAll ? min(Lp, 3u) : L_last;
     } else {
         L_last = levels_last[tile];
         L = levels[tile];
+        L_last_store = L_last;
     }
     const uint32_t L_store = L;
     auto finish_unit = [&]() {
         if (lv_current && threadIdx.x == 0) {
             if ((atomicAdd(&tile_done[tile], 1u) & 3u) == 3u) {
-                lv_last[tile] = L_last;
+                lv_last[tile] = L_last_store;
                 lv_current[tile] = L_store;
             }
         }

@@ -150,9 +150,10 @@ class GaussianRasterizer(nn.Module):
 
 
 # --------------------------------------------------------- 5-step driver ---
+AMR_STEPS_1_TO_4 = 14  # include/gsplat_amd.h GSPLAT_AMD_AMR_STEPS_1_TO_4: foveaStep 1..4 in one launch
 def render_steps(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                  raster_settings, interpolate_image: bool = False, fused: Optional[bool] = None,
-                 starters=None, enders=None, after_step0=None):
+                 starters=None, enders=None, after_step0=None, one_launch: Optional[bool] = None):
     """The rasterizer sequence of ``gaussian_renderer_amr.render``
     (gaussian_renderer_amr/__init__.py:126-594): foveaStep 0 (buffers and a
     zero image), then foveaStep 1..4 on step 0's buffers, the caller summing
@@ -168,6 +169,12 @@ def render_steps(means3D, means2D, sh, colors_precomp, opacities, scales, rotati
     the same fp32 adds, so the same bits -- instead of writing a full step
     image each that the caller then adds (four full-image reads and writes
     per frame).  ``fused=False`` is the literal apply-and-add sequence.
+    ``one_launch`` (fused only; default: whenever no per-step events are
+    asked for): steps 1..4 as ONE launch (GSPLAT_AMD_AMR_STEPS_1_TO_4) --
+    each (tile, quadrant) unit renders its rounds 1..min(level, 4) in turn,
+    so the steps' tails overlap instead of each step waiting for its
+    heaviest tile; same frame, final T, n_contrib, radii and level state as
+    the four launches (each pixel belongs to one round).
     ``after_step0(imageBuffer)`` runs between step 0 and step 1 (e.g.
     apply_fovea_levels).  ``starters`` / ``enders``: CUDA events recorded
     around each step, as the reference's fps harness passes them."""
@@ -179,6 +186,10 @@ def render_steps(means3D, means2D, sh, colors_precomp, opacities, scales, rotati
     elif fused and (grad or interpolate_image):
         raise RuntimeError("render_steps(fused=True) is forward-only without interpolation: run it under "
                            "torch.no_grad() with interpolate_image=False")
+    if one_launch is None:
+        one_launch = fused and starters is None and enders is None
+    elif one_launch and not fused:
+        raise RuntimeError("render_steps(one_launch=True) needs the fused steps")
     e = torch.empty(0, device=means3D.device)
     u8 = torch.empty(0, dtype=torch.uint8, device=means3D.device)
 
@@ -191,6 +202,10 @@ def render_steps(means3D, means2D, sh, colors_precomp, opacities, scales, rotati
     mark(enders, 0)
     if after_step0 is not None:
         after_step0(ib)
+    if one_launch:
+        _C.amr_accumulate_step(s.bg, colors_precomp, int(s.image_height), int(s.image_width),
+                               int(means3D.shape[0]), AMR_STEPS_1_TO_4, acc, gb, bb, ib, bool(s.debug))
+        return acc, radii, gb, bb, ib
     for k in range(1, 5):
         mark(starters, k)
         if fused:

@@ -227,7 +227,14 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
  * their value (+ 0 in the reference) -- bit-identical to the reference's sum.
  * Buffers, radii (zeros written), num_rendered_hint and return value as
  * gs_amr_rasterizer_forward_ex at foveaStep >= 1.  Needs the default AMR
- * variant (gs_set_tuning("amr_variant") 4). */
+ * variant (gs_set_tuning("amr_variant") 4).
+ * foveaStep = GSPLAT_AMD_AMR_STEPS_1_TO_4: steps 1, 2, 3 and 4 in order in ONE
+ * launch -- each (tile, quadrant) unit renders the rounds 1..min(level, 4)
+ * those four calls would give it, one after another, and leaves accum, final
+ * T, n_contrib, radii and the buffers' level state exactly as the four calls
+ * do (each pixel belongs to one round, so every rendered pixel gets one
+ * accum + (C + T bg) either way). */
+#define GSPLAT_AMD_AMR_STEPS_1_TO_4 14
 int gs_amr_accumulate_step(int P, const float* background, int width, int height, const float* colors_precomp,
                            int foveaStep, char* geom_buffer_precomp, char* binning_buffer_precomp,
                            char* image_buffer_precomp, float* accum, int* radii, int debug, int num_rendered_hint,

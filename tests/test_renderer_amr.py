@@ -8,8 +8,10 @@ SURVEY §8 row B8) and its fused 5-step driver.
   the kernel (gs_amr_accumulate_step) gives the same bits as the reference's
   literal sequence -- foveaStep 0..4 through _RasterizeGaussians.apply and
   `out_color_precomp + rendered_image_k` in torch -- with the same image
-  buffer (levels, final T, n_contrib) and radii; renderer_amr.render /
-  render_once equal the explicit calls.
+  buffer (levels, final T, n_contrib) and radii, with steps 1..4 launched
+  one by one or as one launch (GSPLAT_AMD_AMR_STEPS_1_TO_4, also after the
+  fovea-level hook); renderer_amr.render / render_once equal the explicit
+  calls.
 """
 import math
 import os
@@ -88,8 +90,9 @@ CASES = [  # (P, W, H, seed, bg, colours precomputed)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("one_launch", [False, True], ids=["per_step", "one_launch"])
 @pytest.mark.parametrize("case", CASES, ids=lambda c: f"P{c[0]}_{c[1]}x{c[2]}")
-def test_fused_steps_bit_identical_to_reference_sequence(case):
+def test_fused_steps_bit_identical_to_reference_sequence(case, one_launch):
     import gaussian_splatting_with_eye_tracking_amd._C as C
     from gaussian_splatting_with_eye_tracking_amd.rasterization_amr import render_steps
     P, W, H, seed, bg, precomp = case
@@ -103,7 +106,7 @@ def test_fused_steps_bit_identical_to_reference_sequence(case):
     args = (t["means3D"], m2, shs, cols, t["opacities"], t["scales"], t["rotations"], e)
     with torch.no_grad():
         ref, rradii, _, _, rib = _chain(args, s)
-        got, radii, gb, bb, ib = render_steps(*args, s)
+        got, radii, gb, bb, ib = render_steps(*args, s, one_launch=one_launch)
         torch.cuda.synchronize()
     assert torch.equal(radii, rradii)
     assert torch.equal(got, ref), float((got - ref).abs().max())
@@ -228,3 +231,42 @@ def test_fused_steps_with_nothing_visible():
         torch.cuda.synchronize()
     assert int((rradii > 0).sum()) == 0
     assert torch.equal(got, ref) and torch.equal(radii, rradii)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("replace", [False, True])
+def test_one_launch_after_fovea_levels_matches_per_step(replace):
+    """Steps 1..4 as one launch after apply_fovea_levels (levels lowered, or
+    replaced by the fovea discs alone) leave the frame, radii, level state
+    and every rendered pixel's final T / n_contrib of the four launches."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import rasterization_amr as RA
+    P, W, H = 80_000, 960, 544
+    sc, cam = G.scene_and_camera(P, W, H, 11)
+    t, pc, camera, pipe = _duck(sc, cam)
+    s = _settings_of(camera, torch.tensor([0.1, 0.2, 0.3], dtype=torch.float32, device="cuda"))
+    e = torch.Tensor([]).cuda()
+    m2 = torch.zeros_like(t["means3D"])
+    args = (t["means3D"], m2, t["shs"], e, t["opacities"], t["scales"], t["rotations"], e)
+    centres, radii_f = RA.reference_foveae(W, H, (0.3 * W, 0.6 * H))
+    hook = lambda ib: RA.apply_fovea_levels(ib, W, H, centres, radii_f, replace=replace)  # noqa: E731
+    out = {}
+    with torch.no_grad():
+        for one in (False, True):
+            img, radii, gb, bb, ib = RA.render_steps(*args, s, after_step0=hook, one_launch=one)
+            torch.cuda.synchronize()
+            K = int(C.parse_buffers(gb, bb, ib, P, 0, W, H, 32)["hdr"][0].item())
+            d = C.parse_buffers(gb, bb, ib, P, K, W, H, 32)
+            out[one] = (img.clone(), radii.clone(), {k: d[k].clone() for k in
+                        ("levels", "levels_last", "levels_current", "n_contrib", "accum_alpha")})
+    (i0, r0, d0), (i1, r1, d1) = out[False], out[True]
+    assert torch.equal(i0, i1) and torch.equal(r0, r1)
+    for k in ("levels", "levels_last", "levels_current"):
+        assert torch.equal(d0[k], d1[k]), k
+    lv = np.minimum(d0["levels"].cpu().numpy(), 4)
+    assert len(np.unique(lv)) > 1
+    y, x = np.mgrid[0:H, 0:W]
+    rnd = np.array([[1, 3], [4, 2]])[y % 2, x % 2]
+    mask = (rnd <= lv[(y // 32) * ((W + 31) // 32) + x // 32]).ravel()
+    for k in ("n_contrib", "accum_alpha"):
+        np.testing.assert_array_equal(d0[k].cpu().numpy()[mask], d1[k].cpu().numpy()[mask], k)
