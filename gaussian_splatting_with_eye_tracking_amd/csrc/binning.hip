@@ -1013,6 +1013,33 @@ __global__ void __launch_bounds__(kT) sort_tiles_bucket_kernel(int lo, int hi, c
     tile_bucket_sort<kT, kE, kBS, kStageOut>(keys, n, out, L);
 }
 
+// All three bucket-sort classes in one launch of 512-thread workgroups
+// (tiles of <= 2048 keys on the <512, 4, 1> path, (2048, 4096] on <512, 8, 2>
+// through LDS), for grids whose tiles span the classes: one grid of T
+// workgroups instead of three grids of mostly early-exiting ones (the same
+// LDS and 59 vs 58 VGPRs as the largest class alone): config-4 sort_tiles
+// 0.1222 -> 0.1089 ms (profiles/r05bb_ab_sort_mixed_cfg4.log).
+__global__ void __launch_bounds__(512) sort_tiles_mixed_kernel(const uint32_t* __restrict__ ranges,
+                                                               const uint64_t* __restrict__ pair_keys,
+                                                               uint32_t* __restrict__ point_list) {
+    __shared__ union {
+        TileSortLds<512, 4, 1> a;
+        TileSortLds<512, 8, 2> b;
+    } L;
+    const int tile = blockIdx.x;
+    const uint32_t beg = ranges[2 * tile], end = ranges[2 * tile + 1];
+    const int n = (int)(end - beg);
+    if (n == 0 || n > kSmallCap) return;
+    const uint64_t* keys = pair_keys + beg;
+    uint32_t* out = point_list + beg;
+    if (n == 1) {
+        if (threadIdx.x == 0) out[0] = (uint32_t)keys[0];
+        return;
+    }
+    if (n <= 2048) tile_bucket_sort<512, 4, 1, false>(keys, n, out, L.a);
+    else tile_bucket_sort<512, 8, 2, true>(keys, n, out, L.b);
+}
+
 // Merge-path split: number of elements taken from A for the first `diag`
 // outputs of merge(A[0..na), B[0..nb)); keys are unique.
 __device__ __forceinline__ int merge_path(const uint64_t* A, int na, const uint64_t* B, int nb, int diag) {
@@ -1092,9 +1119,14 @@ void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int ma
         // sorted ids through LDS, wave-contiguous (0.1616 -> 0.1225 ms at config 4;
         // the small class measured 0.0293 -> 0.0303 ms at config 2 that way and
         // keeps the direct stores, profiles/r05k_ab_sortout*.log)
-        if (fused_max < 1024) GS_BK(256, 4, 1, 0, 1024, false);
-        if (max_count_host > 1024 && fused_max < 2048) GS_BK(512, 4, 1, 1024, 2048, false);
-        if (max_count_host > 2048) GS_BK(512, 8, 2, 2048, kSmallCap, true);
+        if (fused_max == 0 && max_count_host > 2048) {
+            hipLaunchKernelGGL(sort_tiles_mixed_kernel, dim3(T), dim3(512), 0, s, img.ranges, b.pair_keys,
+                               b.point_list);
+        } else {
+            if (fused_max < 1024) GS_BK(256, 4, 1, 0, 1024, false);
+            if (max_count_host > 1024 && fused_max < 2048) GS_BK(512, 4, 1, 1024, 2048, false);
+            if (max_count_host > 2048) GS_BK(512, 8, 2, 2048, kSmallCap, true);
+        }
 #undef GS_BK
         if (num_large_host > 0)
             hipLaunchKernelGGL(sort_tiles_large_kernel, dim3(num_large_host), dim3(kLargeThreads), 0, s,
