@@ -96,6 +96,19 @@ __device__ __forceinline__ void mirror_header(uint32_t* m, uint32_t K, uint32_t 
 }
 
 
+// The speculative duplicate publishes the read-back instead of the scan: the
+// header words are final once the scan has ended, and its first workgroup's
+// first thread copies them to the mapped host slot while the rest of the
+// duplicate runs -- the system-scope stores and fences leave the scan's tail
+// (the critical path of every forward) for a thread whose wave is one of
+// hundreds.  Before the capacity test, so a refused launch still publishes K.
+__device__ __forceinline__ void publish_header(const uint32_t* __restrict__ hdr, uint32_t* m, uint32_t token) {
+    if (!m || !token || blockIdx.x != 0 || threadIdx.x != 0) return;
+    const uint4 w = make_uint4(hdr[kHdrNumRendered], hdr[kHdrError], hdr[kHdrMaxTileCount], hdr[kHdrNumLargeTiles]);
+    mirror_invalidate(m, token);
+    mirror_header(m, w.x, w.y, w.z, w.w, token);
+}
+
 // Row-banded duplicate (below): a tile row's tiles are consecutive, so its
 // instances are one contiguous range of the sorted layout, starting at the
 // exclusive prefix of its first tile.  The scan stores that start (and the
@@ -327,7 +340,9 @@ __global__ void __launch_bounds__(256) duplicate_kernel(int P, const float* __re
                                                         const int* __restrict__ radii, int block, uint32_t gx,
                                                         uint32_t gy, uint32_t* __restrict__ cursor,
                                                         uint64_t* __restrict__ pair_keys,
-                                                        const uint32_t* __restrict__ hdr, uint32_t cap) {
+                                                        const uint32_t* __restrict__ hdr, uint32_t cap,
+                                                        uint32_t* mirror, uint32_t mirror_token) {
+    publish_header(hdr, mirror, mirror_token);
     if (hdr && hdr[kHdrNumRendered] > cap) return;  // speculative launch, K > cap (duplicate_lds_kernel)
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= P) return;
@@ -465,7 +480,9 @@ __global__ void __launch_bounds__(kBinThreads) duplicate_lds_kernel(int P, int c
                                                                     uint32_t* __restrict__ cursor,
                                                                     uint64_t* __restrict__ pair_keys,
                                                                     const uint32_t* __restrict__ hdr, uint32_t cap,
-                                                                    uint32_t nslots) {
+                                                                    uint32_t nslots, uint32_t* mirror,
+                                                                    uint32_t mirror_token) {
+    publish_header(hdr, mirror, mirror_token);
     // speculative launch (hdr given): the keys fit the buffer only if K <= cap;
     // otherwise nothing is touched (no cursor moved) and the host relaunches
     if (hdr && hdr[kHdrNumRendered] > cap) return;
@@ -742,7 +759,8 @@ __global__ void __launch_bounds__(kNT) band_stage_kernel(int P, const float* __r
                                                          uint64_t* __restrict__ stage_keys,
                                                          uint32_t* __restrict__ stage_cols,
                                                          const uint32_t* __restrict__ hdr, uint32_t cap,
-                                                         uint32_t limit) {
+                                                         uint32_t limit, uint32_t* mirror, uint32_t mirror_token) {
+    publish_header(hdr, mirror, mirror_token);
     if (hdr && hdr[kHdrNumRendered] > cap) return;  // speculative launch, K > cap (duplicate_lds_kernel)
     constexpr int kStageG = kStageChunk / kNT;
     static_assert(kStageG % kSPT == 0, "whole source groups");
@@ -851,7 +869,7 @@ __global__ void __launch_bounds__(kNT) band_split_kernel(uint32_t gx, int split,
 template <int kNT, int kR, int kSPT>
 void launch_banded(int P, const GeomView& g, const int* radii, int block, uint32_t gx, uint32_t gy, int split,
                    const ImageView& img, const BinningView& b, hipStream_t s, uint32_t n_keys,
-                   const uint32_t* spec_hdr, uint32_t spec_cap) {
+                   const uint32_t* spec_hdr, uint32_t spec_cap, uint32_t* mirror, uint32_t mirror_token) {
     using Lds = BandLds<kNT, kR, kSPT>;
     // > 64 KiB of dynamic LDS: the attribute once per device (and variant)
     static std::atomic<int> attr[kMaxDevices];
@@ -868,7 +886,7 @@ void launch_banded(int P, const GeomView& g, const int* radii, int block, uint32
     }
     hipLaunchKernelGGL((band_stage_kernel<kNT, kR, kSPT>), dim3((P + kStageChunk - 1) / kStageChunk), dim3(kNT),
                        sizeof(Lds), s, P, g.means2D, g.depths, radii, block, gx, gy, img.band_cursor, b.scratch,
-                       b.point_list, spec_hdr, spec_cap, n_keys);
+                       b.point_list, spec_hdr, spec_cap, n_keys, mirror, mirror_token);
     hipLaunchKernelGGL((band_split_kernel<kNT, kR, kSPT>), dim3(gy * split), dim3(kNT), sizeof(Lds), s, gx, split,
                        img.band_start, img.band_cursor, b.scratch, b.point_list, img.tile_cursor, b.pair_keys,
                        spec_hdr, spec_cap, n_keys);
@@ -876,7 +894,7 @@ void launch_banded(int P, const GeomView& g, const int* radii, int block, uint32
 
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
                       const BinningView& b, hipStream_t s, uint32_t n_keys, const uint32_t* spec_hdr,
-                      uint32_t spec_cap) {
+                      uint32_t spec_cap, uint32_t* mirror, uint32_t mirror_token) {
     if (P == 0) return;
     const uint32_t gx = (uint32_t)((W + block - 1) / block), gy = (uint32_t)((H + block - 1) / block);
     if (dup_banded((int)gx, (int)gy, block)) {
@@ -885,8 +903,12 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
         // 62; 16 / 32 / 128 / 256 measured slower, profiles/r03p_ab_band_*.json)
         const int want = 4096;
         const int split = std::max(1, std::min(256, (want + (int)gy - 1) / (int)gy));
-        if (P >= 2000000) launch_banded<512, 2, 2>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap);
-        else launch_banded<1024, 2, 1>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap);
+        if (P >= 2000000)
+            launch_banded<512, 2, 2>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap, mirror,
+                                     mirror_token);
+        else
+            launch_banded<1024, 2, 1>(P, g, radii, block, gx, gy, split, img, b, s, n_keys, spec_hdr, spec_cap, mirror,
+                                      mirror_token);
         return;
     }
     if (gx * gy <= (uint32_t)kLdsTiles) {
@@ -894,11 +916,11 @@ void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, 
         hipLaunchKernelGGL(duplicate_lds_kernel, dim3((P + chunk - 1) / chunk), dim3(kBinThreads),
                            sizeof(uint32_t) * gx * gy, s, P, chunk, g.means2D, g.depths, radii, block, gx, gy,
                            img.tile_cursor, b.pair_keys, spec_hdr, spec_cap,
-                           (uint32_t)bin_slots_for(P, (int)gx, (int)gy, block));
+                           (uint32_t)bin_slots_for(P, (int)gx, (int)gy, block), mirror, mirror_token);
         return;
     }
     hipLaunchKernelGGL(duplicate_kernel, dim3((P + 255) / 256), dim3(256), 0, s, P, g.means2D, g.depths, radii,
-                       block, gx, gy, img.tile_cursor, b.pair_keys, spec_hdr, spec_cap);
+                       block, gx, gy, img.tile_cursor, b.pair_keys, spec_hdr, spec_cap, mirror, mirror_token);
 }
 
 // ------------------------------------------------------- launch order ---

@@ -491,9 +491,6 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     stage_check(debug, s, "count_tiles");
     const std::pair<uint32_t*, uint32_t*> mirror =
         (r.T > 0 && hdr_mirror_on()) ? mirror_words() : std::pair<uint32_t*, uint32_t*>{nullptr, nullptr};
-    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, mirror.second, bin_slots_for(in.P, gx, gy, tile), gx, dup_banded(gx, gy, tile), mirror.second ? next_mirror_token() : 0u); }
-    stage_check(debug, s, "tile_scan");
-    uint32_t hdr[4];
     const bool amr = tile == 32;  // the AMR layout appends records and region lists
     // Base forward: the duplicate is launched speculatively into a binning
     // buffer sized for the capacity the last calls suggest, before K is on
@@ -505,6 +502,14 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
     bool dup_done = false;
     const SpecKey skey = spec_key(W, H, in.P);
     const size_t cap = (!amr && !before_k && r.T > 0 && !debug) ? spec_capacity(skey) : 0;
+    // the polled read-back's words: published by the speculative duplicate's
+    // first thread when there is one (binning.hip publish_header), else by the
+    // scan
+    const uint32_t mtoken = mirror.second ? next_mirror_token() : 0u;
+    const bool pub_dup = cap > 0 && mirror.second != nullptr;
+    if (r.T > 0) { StageTimer _t(kScan, s); launch_tile_scan(r.T, r.img, r.g.hdr, s, pub_dup ? nullptr : mirror.second, bin_slots_for(in.P, gx, gy, tile), gx, dup_banded(gx, gy, tile), pub_dup ? 0u : mtoken); }
+    stage_check(debug, s, "tile_scan");
+    uint32_t hdr[4];
     if (before_k) {
         begin_header_read(r.g.hdr, s, mirror.first);
         before_k(r);
@@ -513,7 +518,7 @@ Binned preprocess_and_bin(const ForwardIn& in, const gs_buffer& geometry, const 
         begin_header_read(r.g.hdr, s, mirror.first);
         char* sbase = call_resize(binning, carve_binning(nullptr, cap, nullptr), "binning");
         carve_binning(sbase, cap, &r.b);
-        { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, (uint32_t)cap, r.g.hdr, (uint32_t)cap); }
+        { StageTimer _t(kDup, s); launch_duplicate(in.P, r.g, r.radii, W, H, tile, r.img, r.b, s, (uint32_t)cap, r.g.hdr, (uint32_t)cap, pub_dup ? mirror.second : nullptr, pub_dup ? mtoken : 0u); }
         finish_header_read(hdr, mirror.first, s, r.g.hdr);
         dup_done = hdr[kHdrNumRendered] <= cap;
     } else if (mirror.first) {

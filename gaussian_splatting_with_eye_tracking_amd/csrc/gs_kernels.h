@@ -64,9 +64,11 @@ void launch_tile_scan(int T, const ImageView& img, uint32_t* hdr, hipStream_t s,
 // before the host knows K; it does nothing when the header's K > spec_cap.
 // n_keys: the instance capacity the binning buffer was carved for (K, or the
 // speculative capacity); the banded duplicate never writes past it.
+// mirror / mirror_token (the speculative launch): the header read-back is
+// published by the duplicate's first thread instead of the tile scan.
 void launch_duplicate(int P, const GeomView& g, const int* radii, int W, int H, int block, const ImageView& img,
                       const BinningView& b, hipStream_t s, uint32_t n_keys, const uint32_t* spec_hdr = nullptr,
-                      uint32_t spec_cap = 0);
+                      uint32_t spec_cap = 0, uint32_t* mirror = nullptr, uint32_t mirror_token = 0);
 // Tile grids up to kLdsTiles are binned with workgroup-private LDS histograms
 // (count_tiles + chunked duplicate); larger grids use device atomics.
 constexpr int kLdsTiles = 16384;
