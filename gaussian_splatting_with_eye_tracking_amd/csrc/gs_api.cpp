@@ -408,6 +408,12 @@ bool take_fwd_no_grad() {
     return v;
 }
 thread_local bool t_store_drgb = true;  // this forward's choice (take_fwd_no_grad)
+// gs_set_thread_option("amr_step0_unfilled", 1): one-shot -- the NEXT AMR
+// forward on this thread, if at foveaStep 0, leaves its image unwritten: the
+// caller overwrites every pixel (gs_amr_accumulate_step with
+// GSPLAT_AMD_AMR_STEPS_1_TO_4_FILL), so step 0's 3 x H x W zero fill is skipped.
+// Every AMR forward entry consumes it.
+thread_local int t_amr_step0_unfilled = 0;
 
 PreprocessArgs make_pp(const ForwardIn& in, int tile) {
     PreprocessArgs a;
@@ -1003,6 +1009,8 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
                                  char* binning_buffer_precomp, char* image_buffer_precomp, float* out_color,
                                  int* radii, int interpolate_image, int debug, int num_rendered_hint, void* stream) {
     t_store_drgb = !take_fwd_no_grad();
+    const bool step0_unfilled = t_amr_step0_unfilled != 0;  // (one-shot, consumed by every AMR forward)
+    t_amr_step0_unfilled = 0;
     return guarded([&]() -> int {
         if (P <= 0) return 0;
         hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1059,7 +1067,7 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
         auto before_k = [&](Binned& r) {
             // (variant 4 writes the zeros of the pixels it does not render;
             // otherwise, and at foveaStep 0, the levels launch zeroes the image)
-            const bool zero_img = foveaStep == 0 || g_amr_variant != 4;
+            const bool zero_img = (foveaStep == 0 && !step0_unfilled) || g_amr_variant != 4;
             { StageTimer _t(kAmrLevels, s);
               launch_amr_levels(r.T, r.img, s, zero_img ? out_color : nullptr, zero_img ? 3 * (size_t)W * H : 0); }
             stage_check(dbg, s, "amr_levels");
@@ -1101,8 +1109,12 @@ int gs_amr_accumulate_step(int P, const float* background, int width, int height
                            void* stream) {
     return guarded([&]() -> int {
         if (P <= 0) return 0;
-        if ((foveaStep < 1 || foveaStep > 4) && foveaStep != kAmrStepsAll)
-            throw GsError("gs_amr_accumulate_step: foveaStep in 1..4 or GSPLAT_AMD_AMR_STEPS_1_TO_4");
+        if ((foveaStep < 1 || foveaStep > 4) && foveaStep != kAmrStepsAll && foveaStep != kAmrStepsAllFill)
+            throw GsError("gs_amr_accumulate_step: foveaStep in 1..4 or GSPLAT_AMD_AMR_STEPS_1_TO_4(_FILL)");
+        // _FILL: the same launch storing every pixel (0 + value, zeros where
+        // nothing renders) instead of adding: accum holds an unfilled step-0 image
+        const bool fill = foveaStep == kAmrStepsAllFill;
+        if (fill) foveaStep = kAmrStepsAll;
         if (g_amr_variant != 4) throw GsError("gs_amr_accumulate_step needs the default amr_variant (4)");
         if (!geom_buffer_precomp || !image_buffer_precomp || !accum)
             throw GsError("gs_amr_accumulate_step needs the buffers returned by foveaStep 0 and the running image");
@@ -1127,7 +1139,7 @@ int gs_amr_accumulate_step(int P, const float* background, int width, int height
         const float* feats = colors_precomp ? colors_precomp : g.rgb;
         { StageTimer _t(kAmrRender, s);
           launch_amr_render(W, H, img, img.levels, img.levels_last, b, ab, g, feats, background, accum, foveaStep, s,
-                            true, P, radii, true); }
+                            true, P, radii, !fill); }
         stage_check(debug != 0, s, "amr_render (accumulate)");
         return K;
     });
@@ -1293,6 +1305,10 @@ int gs_set_thread_option(const char* key, int value) {
     }
     if (std::strcmp(key, "fwd_zero") == 0) {
         t_fwd_zero = value;
+        return 0;
+    }
+    if (std::strcmp(key, "amr_step0_unfilled") == 0) {
+        t_amr_step0_unfilled = value;
         return 0;
     }
     g_err = std::string("unknown thread option ") + key;

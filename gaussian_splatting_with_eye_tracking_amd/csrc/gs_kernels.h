@@ -90,6 +90,7 @@ void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int ma
                        hipStream_t s, int fused_max = 0);
 constexpr int kAmrFusedSortMax = 2048;
 constexpr int kAmrStepsAll = GSPLAT_AMD_AMR_STEPS_1_TO_4;  // foveaStep: steps 1..4 in one launch (gs_amr_accumulate_step)
+constexpr int kAmrStepsAllFill = GSPLAT_AMD_AMR_STEPS_1_TO_4_FILL;  // ... storing every pixel instead of adding
 bool fused_sort_on();  // the AMR region-list pass sorts its tiles of <= kAmrFusedSortMax instances itself
 // (tile << 32 | depth) reconstruction of the reference's point_list_keys.
 void launch_reconstruct_keys(int T, const ImageView& img, const BinningView& b, const GeomView& g, uint64_t* keys,

@@ -151,6 +151,7 @@ class GaussianRasterizer(nn.Module):
 
 # --------------------------------------------------------- 5-step driver ---
 AMR_STEPS_1_TO_4 = 14  # include/gsplat_amd.h GSPLAT_AMD_AMR_STEPS_1_TO_4: foveaStep 1..4 in one launch
+AMR_STEPS_1_TO_4_FILL = 15  # ... storing every pixel into an unfilled step-0 image (GSPLAT_AMD_AMR_STEPS_1_TO_4_FILL)
 def render_steps(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                  raster_settings, interpolate_image: bool = False, fused: Optional[bool] = None,
                  starters=None, enders=None, after_step0=None, one_launch: Optional[bool] = None):
@@ -170,11 +171,13 @@ def render_steps(means3D, means2D, sh, colors_precomp, opacities, scales, rotati
     image each that the caller then adds (four full-image reads and writes
     per frame).  ``fused=False`` is the literal apply-and-add sequence.
     ``one_launch`` (fused only; default: whenever no per-step events are
-    asked for): steps 1..4 as ONE launch (GSPLAT_AMD_AMR_STEPS_1_TO_4) --
-    each (tile, quadrant) unit renders its rounds 1..min(level, 4) in turn,
-    so the steps' tails overlap instead of each step waiting for its
-    heaviest tile; same frame, final T, n_contrib, radii and level state as
-    the four launches (each pixel belongs to one round).
+    asked for): steps 1..4 as ONE launch (GSPLAT_AMD_AMR_STEPS_1_TO_4_FILL)
+    -- each (tile, quadrant) unit renders its rounds 1..min(level, 4) in
+    turn, so the steps' tails overlap instead of each step waiting for its
+    heaviest tile, and stores its whole quadrant into step 0's image, which
+    is therefore not zero-filled first; same frame, final T, n_contrib,
+    radii and level state as the four launches (each pixel belongs to one
+    round).
     ``after_step0(imageBuffer)`` runs between step 0 and step 1 (e.g.
     apply_fovea_levels).  ``starters`` / ``enders``: CUDA events recorded
     around each step, as the reference's fps harness passes them."""
@@ -198,13 +201,23 @@ def render_steps(means3D, means2D, sh, colors_precomp, opacities, scales, rotati
             evs[k].record()
 
     mark(starters, 0)
-    acc, radii, gb, bb, ib = _RasterizeGaussians.apply(*args, 0, e, u8, u8, u8, False, s)
+    unfilled = one_launch and means3D.shape[0] > 0
+    if unfilled:
+        # step 0's zero image is never read before the one launch below stores
+        # every pixel of it: skip the fill (one-shot option, consumed by this call)
+        _C.set_thread_option("amr_step0_unfilled", 1)
+    try:
+        acc, radii, gb, bb, ib = _RasterizeGaussians.apply(*args, 0, e, u8, u8, u8, False, s)
+    finally:
+        if unfilled:
+            _C.set_thread_option("amr_step0_unfilled", 0)  # (in case the call never reached the library)
     mark(enders, 0)
     if after_step0 is not None:
         after_step0(ib)
     if one_launch:
         _C.amr_accumulate_step(s.bg, colors_precomp, int(s.image_height), int(s.image_width),
-                               int(means3D.shape[0]), AMR_STEPS_1_TO_4, acc, gb, bb, ib, bool(s.debug))
+                               int(means3D.shape[0]), AMR_STEPS_1_TO_4_FILL if unfilled else AMR_STEPS_1_TO_4,
+                               acc, gb, bb, ib, bool(s.debug))
         return acc, radii, gb, bb, ib
     for k in range(1, 5):
         mark(starters, k)

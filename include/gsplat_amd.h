@@ -233,8 +233,14 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
  * those four calls would give it, one after another, and leaves accum, final
  * T, n_contrib, radii and the buffers' level state exactly as the four calls
  * do (each pixel belongs to one round, so every rendered pixel gets one
- * accum + (C + T bg) either way). */
+ * accum + (C + T bg) either way).
+ * foveaStep = GSPLAT_AMD_AMR_STEPS_1_TO_4_FILL: the same launch for a frame
+ * that is step 0's image left unfilled (gs_set_thread_option
+ * "amr_step0_unfilled" before that step-0 call): every pixel of accum is
+ * stored -- C + T bg where a round renders, 0 elsewhere: the bits of 0 + the
+ * four steps' images -- instead of added to. */
 #define GSPLAT_AMD_AMR_STEPS_1_TO_4 14
+#define GSPLAT_AMD_AMR_STEPS_1_TO_4_FILL 15
 int gs_amr_accumulate_step(int P, const float* background, int width, int height, const float* colors_precomp,
                            int foveaStep, char* geom_buffer_precomp, char* binning_buffer_precomp,
                            char* image_buffer_precomp, float* accum, int* radii, int debug, int num_rendered_hint,
@@ -424,7 +430,10 @@ int gs_set_tuning(const char* key, int value);
  * backward, default), "store_cov3d" (1 = the forward also writes the geometry
  * buffer's cov3D, which nothing in the path reads back -- for buffer-level
  * parity checks; default 0), "fwd_no_grad" (one-shot: the next forward on this
- * thread needs no backward).  Returns 0, or -1 for an unknown key. */
+ * thread needs no backward), "amr_step0_unfilled" (one-shot: the next AMR
+ * forward, if at foveaStep 0, leaves its image unwritten for a
+ * GSPLAT_AMD_AMR_STEPS_1_TO_4_FILL launch to fill).  Returns 0, or -1 for an
+ * unknown key. */
 int gs_set_thread_option(const char* key, int value);
 int gs_profile_stage_count(void);
 const char* gs_profile_stage_name(int i);

@@ -227,6 +227,8 @@ def test_new_entry_points_validate_before_any_device_call():
     assert acc_step(2, null) < 0 and b"foveaStep 0" in lib.gs_last_error()
     # GSPLAT_AMD_AMR_STEPS_1_TO_4 (steps 1..4 in one launch) passes the step check
     assert acc_step(14, null) < 0 and b"foveaStep 0" in lib.gs_last_error()
+    assert acc_step(15, null) < 0 and b"foveaStep 0" in lib.gs_last_error()
+    assert lib.gs_set_thread_option(b"amr_step0_unfilled", 0) == 0
 
 
 def test_extension_entry_points_in_torch_module():

@@ -270,3 +270,27 @@ def test_one_launch_after_fovea_levels_matches_per_step(replace):
     mask = (rnd <= lv[(y // 32) * ((W + 31) // 32) + x // 32]).ravel()
     for k in ("n_contrib", "accum_alpha"):
         np.testing.assert_array_equal(d0[k].cpu().numpy()[mask], d1[k].cpu().numpy()[mask], k)
+
+
+@pytest.mark.gpu
+def test_unfilled_step0_option_does_not_leak():
+    """The one-launch frame skips step 0's zero fill through a one-shot thread
+    option; the next standalone step-0 call still returns a zero image."""
+    from diff_gaussian_rasterization_amr import _RasterizeGaussians
+    from gaussian_splatting_with_eye_tracking_amd.rasterization_amr import render_steps
+    P, W, H = 20_000, 320, 240
+    sc, cam = G.scene_and_camera(P, W, H, 5)
+    t, pc, camera, pipe = _duck(sc, cam)
+    s = _settings_of(camera, torch.tensor([0.3, 0.2, 0.1], dtype=torch.float32, device="cuda"))
+    e = torch.Tensor([]).cuda()
+    u8 = torch.empty(0, dtype=torch.uint8, device="cuda")
+    m2 = torch.zeros_like(t["means3D"])
+    args = (t["means3D"], m2, t["shs"], e, t["opacities"], t["scales"], t["rotations"], e)
+    with torch.no_grad():
+        ref, _, _, _, _ = _chain(args, s)
+        for _ in range(2):
+            got, _, _, _, _ = render_steps(*args, s)
+            img0 = _RasterizeGaussians.apply(*args, 0, e, u8, u8, u8, False, s)[0]
+            torch.cuda.synchronize()
+            assert torch.equal(got, ref)
+            assert int(torch.count_nonzero(img0)) == 0
