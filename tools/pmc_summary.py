@@ -61,6 +61,7 @@ STAGES = [
     ("sort_tiles_large_kernel", "sort_tiles"),
     ("sort_tiles_radix_kernel", "sort_tiles"),
     ("sort_tiles_bucket_kernel", "sort_tiles"),
+    ("sort_tiles_mixed_kernel", "sort_tiles"),
     ("tile_scan", "tile_scan"),
     ("amr_region_render_kernel<1", "amr_render"),
     ("amr_region_render_kernel<4", "amr_render_once"),
