@@ -645,6 +645,17 @@ def run_fwd_bwd(cfg_name: str, ctx: Ctx, steps: int, warmup: int) -> dict:
 
 
 # ------------------------------------------------------------- config 5 ---
+def views_of_rank(global_views: int, world: int, rank: int):
+    """Config 5's schedule: `global_views` yawed views per step (-17.5 ..
+    +17.5 degrees at 8), global_views / world consecutive ones per rank.
+    Returns (this rank's view indices, every view's yaw)."""
+    if global_views % world:
+        raise SystemExit(f"--views {global_views} is not a multiple of the world size {world}")
+    vl = global_views // world
+    yaws = [(v - (global_views - 1) / 2.0) * 5.0 for v in range(global_views)]
+    return list(range(rank * vl, (rank + 1) * vl)), yaws
+
+
 def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange_alt: bool = True) -> dict:
     """a fixed global batch of `global_views` yawed views per
     step, global_views / N per rank; every rank ends the step with the summed
@@ -658,13 +669,10 @@ def run_multiview(ctx: Ctx, steps: int, warmup: int, global_views: int, exchange
     c = CONFIGS["cfg5_8view_1080p_1M"]
     P, W, H = c["P"], c["W"], c["H"]
     G = global_views
-    if G % ctx.world:
-        raise SystemExit(f"--views {G} is not a multiple of the world size {ctx.world}")
-    vl = G // ctx.world
+    mine, yaws = views_of_rank(G, ctx.world, ctx.rank)
+    vl = len(mine)
     sc, _cam0 = ctx.scene(P, W, H)
     params = device_params(sc, ctx.dev, True)
-    yaws = [(v - (G - 1) / 2.0) * 5.0 for v in range(G)]  # config 5: -17.5 .. +17.5 at G = 8
-    mine = list(range(ctx.rank * vl, (ctx.rank + 1) * vl))
     views = []
     for v in mine:
         cam = S.make_orbit_camera(W, H, yaws[v])
@@ -1027,20 +1035,54 @@ def parse_args(argv=None):
     return ap.parse_args(argv)
 
 
-def dry_run(world, rank):
-    """CPU test of the launcher: every rank joins a gloo group, rank 0 prints."""
+def dry_run(world, rank, global_views: int = 8):
+    """CPU test of the launcher: every rank joins a gloo group and rehearses
+    config 5's exchange schedule on small records -- this rank's views
+    (views_of_rank), each record handed to data_parallel.ViewExchange as
+    run_multiview does (the last view gathered in chunks), and the flat
+    parameter-gradient all-reduce; rank 0 prints whether every rank received
+    every view's record in rank-then-view order and the all-reduced sum, bit
+    for bit on every rank."""
     import torch
     import torch.distributed as dist
+    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
     if world > 1:
         dist.init_process_group("gloo")
-        t = torch.tensor([float(rank)])
-        dist.all_reduce(t)
-        ok = float(t.item()) == world * (world - 1) / 2
+    t = torch.tensor([float(rank)])
+    DP.allreduce_(t)
+    ok = float(t.item()) == world * (world - 1) / 2
+    mine, _yaws = views_of_rank(global_views, world, rank)
+    P = 37
+    n = DP.view_record_numel(P)
+    ex = DP.ViewExchange(P, len(mine), "cpu", chunks=4)
+    for j, v in enumerate(mine):  # record of view v: its values say which view it is
+        ex.add(j, torch.arange(n, dtype=torch.float32) + 1000.0 * v)
+    want = torch.stack([torch.arange(n, dtype=torch.float32) + 1000.0 * v for v in range(global_views)])
+    views_ok = bool(torch.equal(ex.records(), want))
+    flat = torch.zeros(DP.flat_numel_per_gaussian() * P)
+    for v in mine:  # each view's gradients accumulated into the one flat buffer, then one all-reduce
+        flat += torch.linspace(-1.0, 1.0, flat.numel()) * (v + 1)
+    DP.allreduce_(flat)
+    want_flat = torch.zeros_like(flat)
+    for r in range(world):  # the same adds in rank order: a reference for the all-reduced sum
+        acc = torch.zeros_like(flat)
+        for v in views_of_rank(global_views, world, r)[0]:
+            acc += torch.linspace(-1.0, 1.0, flat.numel()) * (v + 1)
+        want_flat += acc
+    sum_ok = bool(torch.allclose(flat, want_flat, rtol=1e-6, atol=1e-6))
+    # every rank holds the same bits (what rank 0 holds, broadcast and compared)
+    ref = flat.clone()
+    recs = ex.records()
+    if world > 1:
+        dist.broadcast(ref, 0)
+    same = torch.tensor([float(torch.equal(ref, flat) and torch.equal(recs, want))])
+    DP.allreduce_(same)
+    if world > 1:
         dist.destroy_process_group()
-    else:
-        ok = True
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "n_gpus": world, "dry_run": True, "allreduce_ok": ok}), flush=True)
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "dry_run": True, "allreduce_ok": ok,
+                          "views_per_rank": len(mine), "view_exchange_ok": views_ok, "grad_allreduce_ok": sum_ok,
+                          "ranks_identical": float(same.item()) == world}), flush=True)
 
 
 def main(argv=None):

@@ -41,6 +41,8 @@ HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-ffp-contr
 # everything on the keys / images keeps the exact contract above.
 SOURCE_FLAGS = {"multiview.hip": ["-ffp-contract=fast", "-freciprocal-math", "-fapprox-func"],
                 "backward.hip": ["-freciprocal-math", "-fapprox-func"]}
+if os.environ.get("GSAMD_EXACT_BWD"):  # diagnostic builds: the backward passes under the exact contract too
+    SOURCE_FLAGS = {}
 # extra flags for code-generation experiments (e.g. GSAMD_EXTRA_HIPFLAGS=-fno-slp-vectorize)
 HIP_FLAGS += shlex.split(os.environ.get("GSAMD_EXTRA_HIPFLAGS", ""))
 

@@ -828,6 +828,10 @@ int multiview_impl(int P, int g0, int count, int D, int M, int V, const float* c
                 vt->host[(size_t)V + v] = cams[v];
             }
             GS_HIP(hipMemcpyAsync(vt->dev, vt->host, 2 * (size_t)V * sizeof(const float*), hipMemcpyHostToDevice, s));
+            // recorded at once, so a launch that throws below still leaves the
+            // next call waiting for this copy before it rewrites (or frees) the
+            // pinned staging the copy reads; recorded again after the kernel
+            GS_HIP(hipEventRecord(vt->done, s));
             a.table = vt->dev;
         }
         a.means3D = means3D;
@@ -1285,6 +1289,24 @@ int gs_set_tuning(const char* key, int value) {
         set_ritnet_mfma(value);
         return 0;
     }
+    g_err = std::string("unknown tuning key ") + key;
+    return -1;
+}
+
+// The current value of a gs_set_tuning key (the variants as they are used:
+// 0 = the fallback, else the default's number).
+int gs_get_tuning(const char* key, int* value) {
+    if (!key || !value) return -1;
+    hdr_mirror_on();  // (resolves the GSAMD_HDR_MIRROR default)
+    const struct { const char* k; const int* v; } table[] = {
+        {"fwd_variant", &g_fwd_variant}, {"bwd_variant", &g_bwd_variant}, {"amr_variant", &g_amr_variant},
+        {"sort_algo", &g_sort_algo},     {"cull", &g_cull},               {"hdr_mirror", &g_hdr_mirror},
+        {"spec_dup", &g_spec_dup},       {"ritnet_mfma", &g_ritnet_mfma}};
+    for (const auto& e : table)
+        if (std::strcmp(key, e.k) == 0) {
+            *value = *e.v;
+            return 0;
+        }
     g_err = std::string("unknown tuning key ") + key;
     return -1;
 }

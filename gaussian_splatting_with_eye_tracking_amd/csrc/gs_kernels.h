@@ -208,6 +208,8 @@ void launch_amr_levels(int T, const ImageView& img, hipStream_t s, float* zero_i
 void launch_amr_region_lists(int W, int H, const ImageView& img, const BinningView& b, const AmrBinningView& ab,
                              const GeomView& g, const float* features, int K, hipStream_t s, bool fused_sort = false);
 extern int g_amr_variant;
+// the other gs_set_tuning choices (read by gs_get_tuning)
+extern int g_fwd_variant, g_bwd_variant, g_sort_algo, g_cull, g_ritnet_mfma;
 void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s, int P = 0, int* zero_radii = nullptr);
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,

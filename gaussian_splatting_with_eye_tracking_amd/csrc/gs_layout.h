@@ -179,9 +179,11 @@ struct BinningView {
 // Base forward: the render's exact row-group hit code of every sorted
 // instance (1 B; bit r: row group r of the tile has a pixel that blended it),
 // which the backward uses as its row masks, lives in the forward's binning
-// scratch -- dead once the duplicate and the large-tile merges are done; not
-// pair_keys, which the render still reads while it writes codes (it sorts its
-// own small tiles, render.hip kFuse).  The header word kHdrHitCodes says
+// scratch: the merge-sort ping-pong, dead once the duplicate and the
+// large-tile merges are done, and nothing after the sort reads it.  (Only the
+// AMR region-list pass sorts tiles during a render, from pair_keys,
+// render.hip amr_region_lists_kernel kFuse; the base render writes codes
+// alone.)  The header word kHdrHitCodes says
 // where: 0 = no codes, else 1 + (byte offset from point_list) / kAlign.  The
 // offset cannot come from K: a speculative forward carves the buffer for a
 // capacity >= K (its scratch further out), the backward carves it for K; both

@@ -884,6 +884,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     });
     m.def("profile_read", &ProfileRead, py::arg("reset") = true);
     m.def("set_tuning", [](const std::string& k, int v) { check(gs_set_tuning(k.c_str(), v), "set_tuning"); });
+    m.def("get_tuning", [](const std::string& k) {
+        int v = 0;
+        check(gs_get_tuning(k.c_str(), &v), "get_tuning");
+        return v;
+    });
     m.def("set_thread_option",
           [](const std::string& k, int v) { check(gs_set_thread_option(k.c_str(), v), "set_thread_option"); });
 }

@@ -317,15 +317,20 @@ def run_views_on_streams(n_views: int, render_one, n_streams: int = 3, device=No
     streams = [cur] + side
     for s in side:
         s.wait_stream(cur)
-    for j in range(n_views):
-        s = streams[j % n_streams]
-        if s is cur:
-            render_one(j)
-        else:
-            with torch.cuda.stream(s):
+    try:
+        for j in range(n_views):
+            s = streams[j % n_streams]
+            if s is cur:
                 render_one(j)
-    for s in side:
-        cur.wait_stream(s)
+            else:
+                with torch.cuda.stream(s):
+                    render_one(j)
+    finally:
+        # joined back even when a view raises: the caller's stream (and the
+        # caching allocator's reuse of its blocks) must not run ahead of
+        # side-stream work still reading or writing them
+        for s in side:
+            cur.wait_stream(s)
 
 
 def _empty_param_grads(means3D: torch.Tensor, shs: Optional[torch.Tensor]):

@@ -164,8 +164,9 @@ def render_steps(means3D, means2D, sh, colors_precomp, opacities, scales, rotati
     (image, radii, geomBuffer, binningBuffer, imageBuffer): the reference's
     ``render`` image and step 0's radii.
 
-    ``fused`` (default: whenever no autograd graph is recorded and step 4 does
-    not interpolate): steps 1..4 add the pixels they render straight into the
+    ``fused`` (default: whenever no autograd graph is recorded, step 4 does
+    not interpolate and the library runs the default AMR variant -- the
+    fused step exists for the region-list form only): steps 1..4 add the pixels they render straight into the
     running image (``_C.amr_accumulate_step``, gs_amr_accumulate_step) --
     the same fp32 adds, so the same bits -- instead of writing a full step
     image each that the caller then adds (four full-image reads and writes
@@ -185,7 +186,7 @@ def render_steps(means3D, means2D, sh, colors_precomp, opacities, scales, rotati
     args = (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
     grad = torch.is_grad_enabled() and any(isinstance(a, torch.Tensor) and a.requires_grad for a in args)
     if fused is None:
-        fused = not grad and not interpolate_image
+        fused = not grad and not interpolate_image and _C.get_tuning("amr_variant") == 4
     elif fused and (grad or interpolate_image):
         raise RuntimeError("render_steps(fused=True) is forward-only without interpolation: run it under "
                            "torch.no_grad() with interpolate_image=False")

@@ -424,6 +424,9 @@ void gs_profile_set_mask(unsigned mask);
  * (1 = matrix-core convolutions, the default; 0 = SGPR-weight FMA kernel).
  * Returns 0, or -1 for an unknown key. */
 int gs_set_tuning(const char* key, int value);
+/* The current value of a gs_set_tuning key into *value (0 = the fallback
+ * variant); -1 for an unknown key. */
+int gs_get_tuning(const char* key, int* value);
 /* Per-call options of the calling thread's forwards (thread-local): "fwd_zero"
  * (1 = the forward render zeroes the backward's accumulator rows, default),
  * "sh_drgb" (1 = the preprocess stores d(rgb)/d(view dir) for the SH

@@ -494,6 +494,210 @@ void orc_render_forward(int W, int H, int block_x, int block_y, const uint32_t* 
         }
 }
 
+/* ---- Conditioning of the blend's discrete decisions (TEST SUPPORT, not the
+ * reference's algorithm).  A pixel's blend takes three discrete decisions
+ * per list entry (base/cr/forward.cu:337-350): the `power > 0` skip, the
+ * `alpha < 1/255` skip and the `test_T < 1e-4` stop.  Where one is taken
+ * within the rounding error any float32 evaluation of the same formulas
+ * carries, a last-bit difference in an operand (another exp implementation,
+ * another operation order) switches it, and the gradient of every Gaussian
+ * on that pixel's chain jumps: the gradient is discontinuous there.  The
+ * margins:
+ *   power:  |power| <= kTieRel * S, S = |cx dx^2| / 2 + |cz dy^2| / 2 + |cy dx dy|
+ *           (the terms it is summed from);
+ *   alpha:  |ln(255 alpha)| <= kTieRel * (1 + S) (exp of an argument known to
+ *           kTieRel * S; alpha clamped at 0.99 is exact);
+ *   T:      |test_T - 1e-4| <= 1e-4 * eT, eT the running relative error bound of
+ *           T (kTieRel per blend plus the alpha error times alpha / (1 - alpha)),
+ * with kTieRel = 32 * 2^-24 (a few ulps of each operand).
+ * orc_render_tie_allowance replays every such decision the other way, one
+ * at a time, and adds |terms(flipped) - terms(as taken)| of every chain entry
+ * to allowance[gid][0..8] (the nine blend-backward terms of bwd_pixel): the
+ * exact jump each near-tie decision can make.  The element-wise gradient
+ * tests (tests/gs_helpers.py) add it to their bound. */
+#define kTieRel (32.0f / 16777216.0f)
+#define TIE_POWER 1
+#define TIE_ALPHA 2
+#define TIE_T 4
+
+/* Forward replay of one pixel (blend_pixel's decisions) with the decision of
+ * kind `fkind` at entry `fp` inverted (fkind 0: none).  Returns the final T
+ * and last contributor; with ties != NULL records up to max_ties near-tie
+ * decisions (entry, kind) of the unforced replay. */
+static void tie_forward(uint32_t rx, uint32_t ry, const uint32_t* point_list, float pixx, float pixy,
+                        const float* points_xy, const float* conic_opacity, uint32_t fp, int fkind,
+                        float* T_out, uint32_t* nc_out, uint32_t* ties, int* nties, int max_ties) {
+    float T = 1.0f, eT = 0.0f;
+    uint32_t contributor = 0, last_contributor = 0;
+    for (uint32_t p = rx; p < ry; p++) {
+        contributor++;
+        const uint32_t id = point_list[p];
+        const float dx = points_xy[2 * id] - pixx, dy = points_xy[2 * id + 1] - pixy;
+        const float* co = conic_opacity + 4 * id;
+        const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+        const float S = 0.5f * fabsf(co[0] * dx * dx) + 0.5f * fabsf(co[2] * dy * dy) + fabsf(co[1] * dx * dy);
+        int near = 0;
+        if (S > 0.0f && fabsf(power) <= kTieRel * S) near |= TIE_POWER;
+        int skip = power > 0.0f;
+        if (p == fp && fkind == TIE_POWER) skip = !skip;
+        float alpha = 0.0f, ea = 0.0f;
+        if (!skip) {
+            alpha = fminf(0.99f, co[3] * expf(power));
+            ea = alpha < 0.99f ? kTieRel * (1.0f + S) : 0.0f;
+            if (fabsf(logf(255.0f * alpha)) <= ea) near |= TIE_ALPHA;
+            int askip = alpha < 1.0f / 255.0f;
+            if (p == fp && fkind == TIE_ALPHA) askip = !askip;
+            skip = askip;
+        }
+        if (!skip) {
+            const float test_T = T * (1 - alpha);
+            eT += kTieRel + ea * alpha / (1.0f - alpha);
+            if (fabsf(test_T - 0.0001f) <= 0.0001f * eT) near |= TIE_T;
+            int stop = test_T < 0.0001f;
+            if (p == fp && fkind == TIE_T) stop = !stop;
+            if (ties)
+                for (int k = 1; k <= 4; k <<= 1)
+                    if ((near & k) && *nties < max_ties) { ties[2 * *nties] = p; ties[2 * *nties + 1] = (uint32_t)k; (*nties)++; }
+            if (stop) break;
+            T = test_T;
+            last_contributor = contributor;
+        } else if (ties) {
+            for (int k = 1; k <= 2; k <<= 1)
+                if ((near & k) && *nties < max_ties) { ties[2 * *nties] = p; ties[2 * *nties + 1] = (uint32_t)k; (*nties)++; }
+        }
+    }
+    *T_out = T;
+    *nc_out = last_contributor;
+}
+
+/* bwd_pixel's nine terms of every chain entry into terms[(p - rx) * 9 + q]
+ * (zeroed first), with the forced decision as in tie_forward. */
+static void tie_terms(int W, int H, int px, int py, uint32_t rx, uint32_t ry, const uint32_t* point_list,
+                      const float* bg_color, const float* points_xy, const float* conic_opacity,
+                      const float* colors, float T_final, uint32_t last_contributor, const float* dL_dpixel,
+                      uint32_t fp, int fkind, float* terms) {
+    const float ddelx_dx = (float)(0.5 * W);
+    const float ddely_dy = (float)(0.5 * H);
+    memset(terms, 0, sizeof(float) * 9 * (size_t)(ry - rx));
+    float T = T_final;
+    uint32_t contributor = ry - rx;
+    float accum_rec[3] = {0, 0, 0}, last_color[3] = {0, 0, 0};
+    float last_alpha = 0;
+    const float pixx = (float)px, pixy = (float)py;
+    for (uint32_t q = ry; q > rx; q--) {
+        const uint32_t p = q - 1;
+        contributor--;
+        if (contributor >= last_contributor) continue;
+        const uint32_t gid = point_list[p];
+        const float dx = points_xy[2 * gid] - pixx, dy = points_xy[2 * gid + 1] - pixy;
+        const float* co = conic_opacity + 4 * gid;
+        const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+        int skip = power > 0.0f;
+        if (p == fp && fkind == TIE_POWER) skip = !skip;
+        if (skip) continue;
+        const float G = expf(power);
+        const float alpha = fminf(0.99f, co[3] * G);
+        int askip = alpha < 1.0f / 255.0f;
+        if (p == fp && fkind == TIE_ALPHA) askip = !askip;
+        if (askip) continue;
+        float* a = terms + 9 * (size_t)(p - rx);
+        T = T / (1.f - alpha);
+        const float dchannel_dcolor = alpha * T;
+        float dL_dalpha = 0.0f;
+        for (int ch = 0; ch < 3; ch++) {
+            const float c = colors[gid * 3 + ch];
+            accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
+            last_color[ch] = c;
+            dL_dalpha += (c - accum_rec[ch]) * dL_dpixel[ch];
+            a[ch] = dchannel_dcolor * dL_dpixel[ch];
+        }
+        dL_dalpha *= T;
+        last_alpha = alpha;
+        float bg_dot_dpixel = 0;
+        for (int i = 0; i < 3; i++) bg_dot_dpixel += bg_color[i] * dL_dpixel[i];
+        dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot_dpixel;
+        const float dL_dG = co[3] * dL_dalpha;
+        const float gdx = G * dx, gdy = G * dy;
+        const float dG_ddelx = -gdx * co[0] - gdy * co[1];
+        const float dG_ddely = -gdy * co[2] - gdx * co[1];
+        a[3] = dL_dG * dG_ddelx * ddelx_dx;
+        a[4] = dL_dG * dG_ddely * ddely_dy;
+        a[5] = -0.5f * gdx * dx * dL_dG;
+        a[6] = -0.5f * gdx * dy * dL_dG;
+        a[7] = -0.5f * gdy * dy * dL_dG;
+        a[8] = G * dL_dalpha;
+    }
+}
+
+/* allowance [P, 9] (double, accumulated); counts[0] = pixels with a
+ * near-tie decision, counts[1..3] = decisions of kind power / alpha / T. */
+void orc_render_tie_allowance(int W, int H, int block_x, int block_y, const uint32_t* ranges,
+                              const uint32_t* point_list, const float* bg_color, const float* points_xy,
+                              const float* conic_opacity, const float* colors, const float* dL_dpixels, int P,
+                              double* allowance, long* counts) {
+    const int gx = (W + block_x - 1) / block_x;
+    long npix = 0, nk[3] = {0, 0, 0};
+    enum { kMaxTies = 64 };
+#pragma omp parallel num_threads(g_threads) if (g_threads > 1) reduction(+ : npix, nk[:3])
+    {
+        float* t0 = NULL;
+        float* t1 = NULL;
+        size_t cap = 0;
+        uint32_t ties[2 * kMaxTies];
+#pragma omp for schedule(dynamic, 1)
+        for (int py = 0; py < H; py++)
+            for (int px = 0; px < W; px++) {
+                const int tile = (py / block_y) * gx + (px / block_x);
+                const uint32_t rx = ranges[2 * tile], ry = ranges[2 * tile + 1];
+                float T;
+                uint32_t nc;
+                int nt = 0;
+                tie_forward(rx, ry, point_list, (float)px, (float)py, points_xy, conic_opacity, 0xffffffffu, 0, &T,
+                            &nc, ties, &nt, kMaxTies);
+                if (nt == 0) continue;
+                npix++;
+                if (cap < (size_t)(ry - rx)) {
+                    cap = (size_t)(ry - rx);
+                    t0 = (float*)realloc(t0, sizeof(float) * 9 * cap);
+                    t1 = (float*)realloc(t1, sizeof(float) * 9 * cap);
+                }
+                const size_t pid = (size_t)W * py + px;
+                const float dpx[3] = {dL_dpixels[pid], dL_dpixels[(size_t)H * W + pid], dL_dpixels[2 * (size_t)H * W + pid]};
+                tie_terms(W, H, px, py, rx, ry, point_list, bg_color, points_xy, conic_opacity, colors, T, nc, dpx,
+                          0xffffffffu, 0, t0);
+                for (int k = 0; k < nt; k++) {
+                    const uint32_t fp = ties[2 * k];
+                    const int kind = (int)ties[2 * k + 1];
+                    nk[kind == TIE_POWER ? 0 : kind == TIE_ALPHA ? 1 : 2]++;
+                    float Tf;
+                    uint32_t ncf;
+                    tie_forward(rx, ry, point_list, (float)px, (float)py, points_xy, conic_opacity, fp, kind, &Tf, &ncf,
+                                NULL, NULL, 0);
+                    tie_terms(W, H, px, py, rx, ry, point_list, bg_color, points_xy, conic_opacity, colors, Tf, ncf,
+                              dpx, fp, kind, t1);
+                    for (uint32_t p = rx; p < ry; p++) {
+                        const float* u = t0 + 9 * (size_t)(p - rx);
+                        const float* v = t1 + 9 * (size_t)(p - rx);
+                        double* al = allowance + 9 * (size_t)point_list[p];
+                        for (int q = 0; q < 9; q++) {
+                            const double d = fabs((double)v[q] - (double)u[q]);
+                            if (d != 0.0) {
+#pragma omp atomic
+                                al[q] += d;
+                            }
+                        }
+                    }
+                }
+            }
+        free(t0);
+        free(t1);
+    }
+    counts[0] = npix;
+    counts[1] = nk[0];
+    counts[2] = nk[1];
+    counts[3] = nk[2];
+}
+
 /* base/cr/backward.cu:399-557 (renderCUDA<3> backward), one pixel: adds its
  * nine per-Gaussian terms to acc[gid * stride + 0..8] in double (the exact
  * sum of the reference's float atomics). */

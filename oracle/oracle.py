@@ -208,35 +208,24 @@ def forward(s: Settings, means3D, opacities, shs=None, colors_precomp=None, scal
     return r
 
 
-def backward(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors_precomp=None, scales=None,
-             rotations=None, cov3D_precomp=None, block: int = 16) -> dict:
-    """Base backward (rasterize_points.cu:117-196 + rasterizer_impl.cu:340-434).
-    Returns the 8 gradients of _C.rasterize_gaussians_backward plus dL_dconic."""
+def _bwd_inputs(means3D, shs, colors_precomp, scales, rotations, cov3D_precomp):
+    none_if_empty = lambda a: None if a is None or np.asarray(a).size == 0 else _f32(a)  # noqa: E731
+    return (_f32(means3D), none_if_empty(shs), none_if_empty(colors_precomp), none_if_empty(scales),
+            none_if_empty(rotations), none_if_empty(cov3D_precomp))
+
+
+def _per_gaussian_backward(s: Settings, fwd: ForwardResult, means3D, shs, scales, rotations, cov3D_precomp,
+                           g_mean2D, g_conic, g_col) -> dict:
+    """computeCov2DCUDA + preprocessCUDA backward (base/cr/backward.cu:144-396)
+    of the blend-level gradients given: a linear map of them."""
     L = lib()
-    means3D = _f32(means3D)
     P = means3D.shape[0]
-    W, H = int(s.image_width), int(s.image_height)
-    shs = None if shs is None or np.asarray(shs).size == 0 else _f32(shs)
     M = 0 if shs is None else shs.shape[1]
-    colors_precomp = None if colors_precomp is None or np.asarray(colors_precomp).size == 0 else _f32(colors_precomp)
-    scales = None if scales is None or np.asarray(scales).size == 0 else _f32(scales)
-    rotations = None if rotations is None or np.asarray(rotations).size == 0 else _f32(rotations)
-    cov3D_precomp = None if cov3D_precomp is None or np.asarray(cov3D_precomp).size == 0 else _f32(cov3D_precomp)
-    dL_dpix = _f32(dL_dpix)
-    g_mean2D = np.zeros((P, 3), np.float32)
-    g_conic = np.zeros((P, 2, 2), np.float32)
-    g_opac = np.zeros((P, 1), np.float32)
-    g_col = np.zeros((P, 3), np.float32)
     g_mean3D = np.zeros((P, 3), np.float32)
     g_cov = np.zeros((P, 6), np.float32)
     g_sh = np.zeros((P, M, 3), np.float32)
     g_scale = np.zeros((P, 3), np.float32)
     g_rot = np.zeros((P, 4), np.float32)
-    colors = colors_precomp if colors_precomp is not None else fwd.rgb
-    L.orc_render_backward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(block), ctypes.c_int(block), _p(fwd.ranges),
-                          _p(fwd.point_list), _p(_f32(s.bg)), _p(fwd.means2D), _p(fwd.conic_opacity),
-                          _p(np.ascontiguousarray(colors)), _p(fwd.final_T), _p(fwd.n_contrib), _p(dL_dpix),
-                          ctypes.c_int(P), _p(g_mean2D), _p(g_conic), _p(g_opac), _p(g_col))
     cov_ptr = cov3D_precomp if cov3D_precomp is not None else fwd.cov3D
     fx, fy = fwd.extra["focal_x"], fwd.extra["focal_y"]
     L.orc_cov2d_backward(ctypes.c_int(P), _p(means3D), _p(fwd.radii), _p(np.ascontiguousarray(cov_ptr)),
@@ -248,9 +237,84 @@ def backward(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors
                               _c_float(s.scale_modifier), _p(_f32(s.projmatrix)), _p(_f32(s.campos)),
                               _p(g_mean2D), _p(g_mean3D), _p(g_col), _p(g_cov), _p(g_sh), _p(g_scale),
                               _p(g_rot))
-    return {"dL_dmeans2D": g_mean2D, "dL_dcolors": g_col, "dL_dopacity": g_opac, "dL_dmeans3D": g_mean3D,
-            "dL_dcov3D": g_cov, "dL_dsh": g_sh, "dL_dscales": g_scale, "dL_drotations": g_rot,
-            "dL_dconic": g_conic}
+    return {"dL_dmeans3D": g_mean3D, "dL_dcov3D": g_cov, "dL_dsh": g_sh, "dL_dscales": g_scale,
+            "dL_drotations": g_rot}
+
+
+def backward(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors_precomp=None, scales=None,
+             rotations=None, cov3D_precomp=None, block: int = 16) -> dict:
+    """Base backward (rasterize_points.cu:117-196 + rasterizer_impl.cu:340-434).
+    Returns the 8 gradients of _C.rasterize_gaussians_backward plus dL_dconic."""
+    means3D, shs, colors_precomp, scales, rotations, cov3D_precomp = _bwd_inputs(
+        means3D, shs, colors_precomp, scales, rotations, cov3D_precomp)
+    P = means3D.shape[0]
+    W, H = int(s.image_width), int(s.image_height)
+    g_mean2D = np.zeros((P, 3), np.float32)
+    g_conic = np.zeros((P, 2, 2), np.float32)
+    g_opac = np.zeros((P, 1), np.float32)
+    g_col = np.zeros((P, 3), np.float32)
+    colors = colors_precomp if colors_precomp is not None else fwd.rgb
+    lib().orc_render_backward(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(block), ctypes.c_int(block),
+                              _p(fwd.ranges), _p(fwd.point_list), _p(_f32(s.bg)), _p(fwd.means2D),
+                              _p(fwd.conic_opacity), _p(np.ascontiguousarray(colors)), _p(fwd.final_T),
+                              _p(fwd.n_contrib), _p(_f32(dL_dpix)), ctypes.c_int(P), _p(g_mean2D), _p(g_conic),
+                              _p(g_opac), _p(g_col))
+    out = _per_gaussian_backward(s, fwd, means3D, shs, scales, rotations, cov3D_precomp, g_mean2D, g_conic, g_col)
+    out.update({"dL_dmeans2D": g_mean2D, "dL_dcolors": g_col, "dL_dopacity": g_opac, "dL_dconic": g_conic})
+    return out
+
+
+def tie_allowance(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors_precomp=None, scales=None,
+                  rotations=None, cov3D_precomp=None) -> tuple:
+    """Test support (gs_oracle.c orc_render_tie_allowance): per gradient
+    element, the total jump the near-tie blend decisions can make -- each
+    decision taken within float32 rounding of its threshold replayed the
+    other way, one at a time, |gradient(flipped) - gradient(as taken)| summed.
+    The nine blend-level terms come from the replays directly; the
+    per-Gaussian gradients after them are a linear map J of those terms, so
+    their allowance is sum_k |J (A_k e_k)| over the nine terms k.  Returns
+    ({tensor name: allowance array shaped like the gradient}, {counts})."""
+    means3D, shs, colors_precomp, scales, rotations, cov3D_precomp = _bwd_inputs(
+        means3D, shs, colors_precomp, scales, rotations, cov3D_precomp)
+    P = means3D.shape[0]
+    W, H = int(s.image_width), int(s.image_height)
+    A = np.zeros((P, 9), np.float64)
+    counts = np.zeros(4, np.int64)
+    colors = colors_precomp if colors_precomp is not None else fwd.rgb
+    lib().orc_render_tie_allowance(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(fwd.block),
+                                   ctypes.c_int(fwd.block), _p(fwd.ranges), _p(fwd.point_list), _p(_f32(s.bg)),
+                                   _p(fwd.means2D), _p(fwd.conic_opacity), _p(np.ascontiguousarray(colors)),
+                                   _p(_f32(dL_dpix)), ctypes.c_int(P), _p(A), _p(counts))
+    Af = A.astype(np.float32)
+    out = {"dL_dcolors": A[:, 0:3].copy(), "dL_dopacity": A[:, 8:9].copy(),
+           "dL_dmeans2D": np.concatenate([A[:, 3:5], np.zeros((P, 1))], 1),
+           "dL_dconic": np.stack([A[:, 5:7], np.stack([np.zeros(P), A[:, 7]], 1)], 1)}
+    touched = np.nonzero(A.any(1))[0]
+    down = None
+    for k in range(9):
+        if not Af[:, k].any():
+            continue
+        g_mean2D = np.zeros((P, 3), np.float32)
+        g_conic = np.zeros((P, 2, 2), np.float32)
+        g_col = np.zeros((P, 3), np.float32)
+        if k < 3:
+            g_col[:, k] = Af[:, k]
+        elif k < 5:
+            g_mean2D[:, k - 3] = Af[:, k]
+        elif k < 8:
+            g_conic.reshape(P, 4)[:, (0, 1, 3)[k - 5]] = Af[:, k]
+        else:
+            continue  # the opacity term feeds no per-Gaussian gradient after the blend
+        r = _per_gaussian_backward(s, fwd, means3D, shs, scales, rotations, cov3D_precomp, g_mean2D, g_conic, g_col)
+        r = {n: np.abs(v.astype(np.float64)) for n, v in r.items()}
+        down = r if down is None else {n: down[n] + r[n] for n in down}
+    if down is None:
+        M = 0 if shs is None else shs.shape[1]
+        down = {"dL_dmeans3D": np.zeros((P, 3)), "dL_dcov3D": np.zeros((P, 6)), "dL_dsh": np.zeros((P, M, 3)),
+                "dL_dscales": np.zeros((P, 3)), "dL_drotations": np.zeros((P, 4))}
+    out.update(down)
+    return out, {"tie_pixels": int(counts[0]), "power": int(counts[1]), "alpha": int(counts[2]), "T": int(counts[3]),
+                 "gaussians": int(touched.size)}
 
 
 def mark_visible(means3D, viewmatrix, projmatrix) -> np.ndarray:

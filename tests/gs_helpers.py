@@ -50,3 +50,113 @@ def rel_err(a, b) -> float:
     if den == 0:
         return float(np.linalg.norm(a))
     return float(np.linalg.norm(a - b) / den)
+
+
+# Element-wise gradient bar, beside the L2-norm bar above:
+#     |g - r| <= GRAD_ELEM_RTOL * |r| + atol,   atol = GRAD_ELEM_ATOL_FRAC * max|r|
+# per tensor.  The absolute floor is one millionth of the tensor's largest
+# element: a gradient element is a sum of per-pixel float terms, and the GPU's
+# float atomics (and the hardware exp, v_exp_f32 against libm expf) round
+# differently from the oracle's double accumulation, so elements that are
+# cancellations of large terms carry an absolute, not a relative, error.
+GRAD_ELEM_RTOL = 1e-4
+GRAD_ELEM_ATOL_FRAC = 1e-6
+
+
+def elementwise_check(got, ref, rtol: float = GRAD_ELEM_RTOL, atol_frac: float = GRAD_ELEM_ATOL_FRAC,
+                      allow=None) -> dict:
+    """Element-wise comparison of one gradient tensor:
+        |g - r| <= rtol |r| + atol + allow
+    where `allow` (optional, shaped like the gradient) is the oracle's jump
+    allowance of the near-tie blend decisions (oracle.tie_allowance; zero for
+    every Gaussian no near-tie pixel's chain reaches).  Returns the violation
+    count, the stated atol, the worst element (largest err / bound) with its
+    leading (per-Gaussian) index, the largest element-wise relative error over
+    the elements above the absolute floor and without allowance, and how many
+    elements needed the allowance."""
+    g = np.asarray(got, np.float64)
+    r = np.asarray(ref, np.float64)
+    assert g.shape == r.shape, (g.shape, r.shape)
+    out = {"n": int(r.size), "violations": 0, "atol": 0.0, "max_abs_ref": 0.0, "worst": None,
+           "max_rel_above_floor": 0.0, "max_excess": 0.0, "allowance_used": 0, "allowance_elements": 0}
+    if r.size == 0:
+        return out
+    maxr = float(np.max(np.abs(r)))
+    atol = atol_frac * maxr
+    err = np.abs(g - r)
+    base = rtol * np.abs(r) + atol
+    al = np.zeros_like(r) if allow is None else np.asarray(allow, np.float64).reshape(r.shape)
+    bound = base + al
+    bad = err > bound
+    out.update(violations=int(bad.sum()), atol=atol, max_abs_ref=maxr,
+               allowance_used=int(((err > base) & ~bad).sum()), allowance_elements=int((al > 0).sum()))
+    ratio = err / np.where(bound > 0, bound, np.inf)
+    ratio[(bound == 0) & (err > 0)] = np.inf
+    w = int(np.argmax(ratio))
+    lead = int(np.unravel_index(w, r.shape)[0]) if r.ndim else 0
+    out["worst"] = {"flat": w, "gaussian": lead, "got": float(g.flat[w]), "ref": float(r.flat[w]),
+                    "err": float(err.flat[w]), "bound": float(bound.flat[w]), "allow": float(al.flat[w]),
+                    "ratio": float(ratio.flat[w])}
+    above = (np.abs(r) > atol) & (al == 0)
+    if above.any():
+        out["max_rel_above_floor"] = float(np.max(err[above] / np.abs(r[above])))
+    out["max_excess"] = float(np.max((err - rtol * np.abs(r)) / maxr)) if maxr > 0 else 0.0
+    return out
+
+
+def gaussian_context(idx: int, sc, cam, ref=None) -> dict:
+    """What makes one Gaussian's backward ill-conditioned
+    (base/cr/backward.cu:144-274): its screen radius, the 2-D covariance's
+    determinant `denom` (the conic is its inverse), the view-space depth t.z
+    and whether the +-1.3 tan(fov) clamp of t.x/t.z, t.y/t.z is active."""
+    m = np.asarray(sc.means3D[idx], np.float64)
+    V = np.asarray(cam.world_view_transform, np.float64)  # row-vector convention: p_view = [m, 1] @ V
+    t = np.append(m, 1.0) @ V
+    lx, ly = 1.3 * cam.tanfovx, 1.3 * cam.tanfovy
+    c = {"index": int(idx), "t_z": float(t[2]),
+         "clamp_x": bool(abs(t[0] / t[2]) > lx) if t[2] != 0 else None,
+         "clamp_y": bool(abs(t[1] / t[2]) > ly) if t[2] != 0 else None}
+    if ref is not None:
+        c["radius"] = int(ref.radii[idx])
+        c["tiles_touched"] = int(ref.tiles_touched[idx])
+        co = np.asarray(ref.conic_opacity[idx], np.float64)
+        dc = co[0] * co[2] - co[1] * co[1]
+        c["denom"] = float(1.0 / dc) if dc != 0 else float("inf")
+        c["opacity"] = float(co[3])
+    return c
+
+
+def _report(record: dict) -> None:
+    """Append one element-wise record to $GS_ELEM_REPORT (JSON lines) when set."""
+    import json
+    import os
+    path = os.environ.get("GS_ELEM_REPORT")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps(record) + "\n")
+
+
+def assert_grads_elementwise(case: str, names, grads, refs, sc=None, cam=None, ref_fwd=None,
+                             atol_frac: dict | None = None, allow: dict | None = None, ties: dict | None = None) -> None:
+    """The element-wise bar over every named gradient: zero violations, with
+    the worst element and its Gaussian's context in the message.  `allow`:
+    oracle.tie_allowance's per-tensor jump allowances (`ties` its counts,
+    recorded with the report)."""
+    fails = []
+    for n, g in zip(names, grads):
+        if n not in refs:
+            continue
+        gg = g.detach().cpu().numpy() if hasattr(g, "detach") else np.asarray(g)
+        af = (atol_frac or {}).get(n, GRAD_ELEM_ATOL_FRAC)
+        rep = elementwise_check(gg, refs[n], atol_frac=af, allow=None if allow is None else allow.get(n))
+        if rep["worst"] is not None and sc is not None and cam is not None:
+            rep["context"] = gaussian_context(rep["worst"]["gaussian"], sc, cam, ref_fwd)
+        _report({"case": case, "tensor": n, "ties": ties, **rep})
+        if rep["violations"]:
+            fails.append((n, rep))
+    import os
+    if os.environ.get("GS_ELEM_SOFT"):  # measurement runs: record only
+        return
+    assert not fails,"element-wise gradient violations: " + "; ".join(
+        f"{n}: {r['violations']} of {r['n']} (atol {r['atol']:.3e}), worst {r['worst']}, "
+        f"context {r.get('context')}" for n, r in fails)

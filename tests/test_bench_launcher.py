@@ -18,13 +18,21 @@ def _env(**kw):
 
 
 @pytest.mark.timeout(300)
-def test_bench_starts_its_own_ranks():
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launcher-dry-run"],
-                       capture_output=True, text=True, env=_env(), timeout=240)
+@pytest.mark.parametrize("n", [2, 4, 8])
+def test_bench_starts_its_own_ranks(n):
+    """`bench.py --gpus N` (the driver's N = 2, 4, 8 scaling runs) starts N
+    ranks, and each rehearses config 5's exchange schedule over gloo: 8 / N
+    views per rank, the pipelined view-record gather (at N = 8 one view per
+    rank: only the chunked last-view path) and the flat gradient all-reduce,
+    bit-identical on every rank."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--launcher-dry-run"],
+                       capture_output=True, text=True, env=_env(), timeout=280)
     assert r.returncode == 0, r.stderr
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1  # rank 0 only
-    assert lines[0]["n_gpus"] == 2 and lines[0]["allreduce_ok"]
+    L = lines[0]
+    assert L["n_gpus"] == n and L["allreduce_ok"] and L["views_per_rank"] == 8 // n
+    assert L["view_exchange_ok"] and L["grad_allreduce_ok"] and L["ranks_identical"]
 
 
 @pytest.mark.timeout(120)

@@ -1,4 +1,5 @@
-"""World-size-2 gloo test of the multi-view data-parallel exchange (CPU).
+"""gloo tests (CPU) of the multi-view data-parallel exchange at world sizes 2,
+3, 4 and 8 -- the driver's N = 2, 4, 8 scaling runs rehearsed rank for rank.
 
 Each rank renders + back-propagates its own view (the CPU oracle stands in
 for the GPU backward here), writes its gradients into the flat buffer, and
@@ -26,7 +27,7 @@ def _free_port():
     return p
 
 
-def _view_grads(rank):
+def _view_grads(rank, world=2):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -35,7 +36,7 @@ def _view_grads(rank):
     W, H = 64, 48
     cam0 = S.make_camera(W, H)
     sc = S.make_scene(800, cam0, seed=0)
-    cam = S.make_orbit_camera(W, H, yaw_deg=(rank - 0.5) * 5.0)
+    cam = S.make_orbit_camera(W, H, yaw_deg=(rank - (world - 1) / 2.0) * 5.0)
     s = O.settings_from_camera(cam)
     kw = dict(shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
     r = O.forward(s, sc.means3D, sc.opacities, **kw)
@@ -50,7 +51,7 @@ def _worker(rank, world, port, q):
         import sys
         sys.path.insert(0, ROOT)
         from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
-        sc, g, r = _view_grads(rank)
+        sc, g, r = _view_grads(rank, world)
         params = {"means3D": torch.from_numpy(sc.means3D), "shs": torch.from_numpy(sc.shs),
                   "opacities": torch.from_numpy(sc.opacities), "scales": torch.from_numpy(sc.scales),
                   "rotations": torch.from_numpy(sc.rotations)}
@@ -70,8 +71,11 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gradient_allreduce():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gradient_allreduce(world):
+    """The north_star exchange: one flat all-reduce of every rank's view
+    gradients (59 floats per Gaussian) and the densification statistics --
+    every rank ends bit-identical, equal to the sum over the views."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -86,22 +90,23 @@ def test_two_rank_gradient_allreduce():
         p.join(timeout=60)
         assert p.exitcode == 0
     # replicas bit-identical
-    for i in range(4):
-        np.testing.assert_array_equal(outs[0][i], outs[1][i])
+    for r in range(1, world):
+        for i in range(4):
+            np.testing.assert_array_equal(outs[0][i], outs[r][i])
     # == sum over views computed locally
     exp = []
     accs, dens, rads = [], [], []
     for rank in range(world):
-        sc, g, r = _view_grads(rank)
+        sc, g, r = _view_grads(rank, world)
         exp.append(np.concatenate([g["dL_dmeans3D"].ravel(), g["dL_dsh"].ravel(), g["dL_dopacity"].ravel(),
                                    g["dL_dscales"].ravel(), g["dL_drotations"].ravel()]))
         accs.append(np.linalg.norm(g["dL_dmeans2D"][:, :2], axis=1).astype(np.float32))
         dens.append((r.radii > 0).astype(np.float32))
         rads.append(r.radii.astype(np.float32))
-    np.testing.assert_allclose(outs[0][0], exp[0] + exp[1], rtol=1e-6, atol=1e-6)
-    np.testing.assert_allclose(outs[0][1], accs[0] + accs[1], rtol=1e-6)
-    np.testing.assert_array_equal(outs[0][2], dens[0] + dens[1])
-    np.testing.assert_array_equal(outs[0][3], np.maximum(rads[0], rads[1]))
+    np.testing.assert_allclose(outs[0][0], np.sum(exp, 0), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(outs[0][1], np.sum(accs, 0), rtol=1e-5)
+    np.testing.assert_array_equal(outs[0][2], np.sum(dens, 0))
+    np.testing.assert_array_equal(outs[0][3], np.max(rads, 0))
 
 
 def _gather_worker(rank, world, port, q):
@@ -202,14 +207,14 @@ def test_view_record_gather_several_views_per_rank_and_empty_model():
         assert outs[r][1] == [(0, 3), (0, 16, 3), (0, 1), (0, 3), (0, 4)]
 
 
-def _pipelined_worker(rank, world, port, q, order=(0, 1, 2)):
+def _pipelined_worker(rank, world, port, q, order=(0, 1, 2), v=3):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import sys
         sys.path.insert(0, ROOT)
         from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
-        P, v = 37, 3
+        P = 37
         n = DP.view_record_numel(P)
         ex = DP.ViewExchange(P, v, "cpu", chunks=4)
         for j in order:  # record of (rank, view j): its values say whose it is
@@ -225,18 +230,20 @@ def _pipelined_worker(rank, world, port, q, order=(0, 1, 2)):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("order", [(0, 1, 2), (1, 2, 0)])
-def test_pipelined_view_gather_order(order):
+@pytest.mark.parametrize("world,order", [(2, (0, 1, 2)), (2, (1, 2, 0)), (4, (0, 1)), (4, (1, 0)), (8, (0,))])
+def test_pipelined_view_gather_order(world, order):
     """data_parallel.ViewExchange (per-view asynchronous gathers, the last view
     in Gaussian chunks) lands every record in rank-then-view order, the order
-    exchange_view_records sums in, on every rank (world size 2, 3 views each),
-    whatever order the views are added in (every rank adding in the same
-    order: the gathers are collectives); a view added twice is refused."""
-    world = 2
+    exchange_view_records sums in, on every rank, whatever order the views are
+    added in (every rank adding in the same order: the gathers are
+    collectives); a view added twice is refused.  Config 5's schedules: world
+    2 with 3 views each, world 4 with 2 (8 / 4), world 8 with one view per
+    rank -- the chunked last-view path alone."""
+    v = len(order)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, q, order)) for r in range(world)]
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, q, order, v)) for r in range(world)]
     for p in procs:
         p.start()
     got = [q.get(timeout=240) for _ in range(world)]
@@ -247,6 +254,6 @@ def test_pipelined_view_gather_order(order):
     assert all(dup for _r, _rec, dup in got)
     from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
     n = DP.view_record_numel(37)
-    want = np.stack([np.arange(n, dtype=np.float32) + 1000.0 * k for k in range(world * 3)])
+    want = np.stack([np.arange(n, dtype=np.float32) + 1000.0 * k for k in range(world * v)])
     for r in range(world):
         np.testing.assert_array_equal(outs[r], want)

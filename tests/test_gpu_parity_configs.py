@@ -78,7 +78,9 @@ def _check_binning(C, out, ref, P, W, H, tile=16):
     return d
 
 
-def _check_grads(grads, rg, skip=()):
+def _check_grads(grads, rg, skip=(), case=None, sc=None, cam=None, ref=None, allow=None):
+    """The norm bar on every gradient, and (with `case`) the element-wise bar
+    (allow: (oracle.tie_allowance's allowances, its counts))."""
     for n, g in zip(GRAD_NAMES, grads):
         if n in skip:
             continue
@@ -86,6 +88,11 @@ def _check_grads(grads, rg, skip=()):
         assert gg.shape == rg[n].shape, n
         assert np.all(np.isfinite(gg)), n
         assert G.rel_err(gg, rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(gg, rg[n]))
+    if case is not None:
+        names = [n for n in GRAD_NAMES if n not in skip]
+        G.assert_grads_elementwise(case, names, [g for n, g in zip(GRAD_NAMES, grads) if n not in skip], rg,
+                                   sc, cam, ref, allow=None if allow is None else allow[0],
+                                   ties=None if allow is None else allow[1])
 
 
 # ------------------------------------------------------------ edge cases ---
@@ -131,7 +138,8 @@ def test_edge_case_parity(name, D, M, mod, bg):
     dpix = S.make_cotangent(H, W, seed + 1)
     grads = _c_backward(s, t, out, dpix)
     assert tuple(grads[5].shape) == (P, M, 3)
-    _check_grads(grads, O.backward(os_, ref, sc.means3D, dpix, **kw))
+    _check_grads(grads, O.backward(os_, ref, sc.means3D, dpix, **kw), case=f"edge_{name}", sc=sc, cam=cam, ref=ref,
+                 allow=O.tie_allowance(os_, ref, sc.means3D, dpix, **kw))
 
 
 def test_active_sh_degree_zero_through_autograd():
@@ -183,7 +191,8 @@ def test_config4_full_size(oracle_threads):
     dpix = S.make_cotangent(H, W, 1)
     grads = _c_backward(s, t, out, dpix)
     del out
-    _check_grads(grads, O.backward(os_, ref, sc.means3D, dpix, **kw))
+    _check_grads(grads, O.backward(os_, ref, sc.means3D, dpix, **kw), case="config4", sc=sc, cam=cam, ref=ref,
+                 allow=O.tie_allowance(os_, ref, sc.means3D, dpix, **kw))
 
 
 # -------------------------------------------------------------- config 3 ---
@@ -291,7 +300,10 @@ def test_config5_eight_views_one_gpu(oracle_threads):
     yaws = S.config5_yaws(8)
     recs = []
     summed = None
-    first = None
+    osum = None  # the oracle's 8 per-view backwards, summed in double
+    asum = tsum = None  # their near-tie allowances and counts, summed
+    pnames = ["dL_dmeans3D", "dL_dsh", "dL_dopacity", "dL_dscales", "dL_drotations"]
+    kw = dict(shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
     for v, yaw in enumerate(yaws):
         cam = S.make_orbit_camera(W, H, yaw)
         s = G.torch_settings(cam)
@@ -304,15 +316,26 @@ def test_config5_eight_views_one_gpu(oracle_threads):
         g = _c_backward(s, t, out, dpix)
         per = [g[3], g[5], g[2], g[6], g[7]]  # means3D, sh, opacity, scales, rotations
         summed = [x.double().clone() for x in per] if summed is None else [a + b.double() for a, b in zip(summed, per)]
-        if v == 0:
-            first = (cam, g, dpix)
         del out
+        os_ = O.settings_from_camera(cam)
+        ref = O.forward(os_, sc.means3D, sc.opacities, **kw)
+        rg = O.backward(os_, ref, sc.means3D, dpix, **kw)
+        al, ties = O.tie_allowance(os_, ref, sc.means3D, dpix, **kw)
+        if v == 0:  # one view alone: every gradient, both bars
+            _check_grads(g, rg, case="config5_view0", sc=sc, cam=cam, ref=ref, allow=(al, ties))
+        osum = ({n: rg[n].astype(np.float64) for n in pnames} if osum is None
+                else {n: osum[n] + rg[n] for n in pnames})
+        asum = ({n: al[n] for n in pnames} if asum is None else {n: asum[n] + al[n] for n in pnames})
+        tsum = ties if tsum is None else {k: tsum[k] + ties[k] for k in ties}
+        del ref, rg, g, al
     mv = DP.multiview_param_grads(torch.stack(recs), t["means3D"], t["shs"], 3, t["scales"], t["rotations"])
     torch.cuda.synchronize()
     for i, (a, b) in enumerate(zip(mv, summed)):
         assert G.rel_err(a.cpu().numpy(), b.cpu().numpy()) < 1e-5, i
-    cam, g, dpix = first
-    os_ = O.settings_from_camera(cam)
-    kw = dict(shs=sc.shs, scales=sc.scales, rotations=sc.rotations)
-    ref = O.forward(os_, sc.means3D, sc.opacities, **kw)
-    _check_grads(g, O.backward(os_, ref, sc.means3D, dpix, **kw))
+    # the multi-view kernel's parameter gradients against the oracle's 8-view
+    # sum: the norm bar and the element-wise bar (the kernel builds with FMA
+    # contraction and reciprocal math, build.py SOURCE_FLAGS)
+    for n, a in zip(pnames, mv):
+        assert G.rel_err(a.cpu().numpy(), osum[n]) < G.GRAD_REL_TOL, n
+    G.assert_grads_elementwise("config5_multiview_sum", pnames, list(mv), osum, sc, S.make_orbit_camera(W, H, yaws[0]),
+                               allow=asum, ties=tsum)

@@ -186,3 +186,48 @@ def test_fovea_levels_rule():
     # min_level 0 leaves tiles outside the first fovea blank
     far = O.fovea_levels(lv, W, H, [(500.0, 500.0)] * 4, radii, min_level=0)
     assert (far == 0).all()
+
+
+def _tie_case(c):
+    """One Gaussian at (8, 8) of a 16x16 tile, isotropic conic c, opacity 1,
+    colour (0.2, 0.5, 0.7), black background: the hand-made screen-space
+    operands of orc_render_tie_allowance."""
+    means2D = np.array([[8.0, 8.0]], np.float32)
+    conic = np.array([[c, 0.0, c, 1.0]], np.float32)
+    cols = np.array([[0.2, 0.5, 0.7]], np.float32)
+    ranges = np.array([[0, 1]], np.uint32)
+    plist = np.array([0], np.uint32)
+    dpix = np.random.default_rng(2).normal(0, 1, (3, 16, 16)).astype(np.float32)
+    A = np.zeros((1, 9), np.float64)
+    counts = np.zeros(4, np.int64)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    O.lib().orc_render_tie_allowance(16, 16, 16, 16, p(ranges), p(plist), p(np.zeros(3, np.float32)), p(means2D),
+                                     p(conic), p(cols), p(dpix), 1, p(A), p(counts))
+    return A, counts, cols, dpix
+
+
+def test_tie_allowance_alpha_threshold():
+    """The near-tie allowance (oracle.tie_allowance, test support for the
+    element-wise gradient bar): a conic chosen so that alpha lands on 1/255
+    (to the float) at the four pixels 3 px from the centre; each such pixel's
+    alpha < 1/255 skip is replayed the other way, and the opacity allowance
+    is the term that pixel adds or drops, |G (c . dL/dpix)| (first and only
+    Gaussian: T = 1, nothing behind it, black background).  A conic away
+    from the threshold has no near-tie decision and zero allowance."""
+    target = np.float32(1.0 / 255.0)
+    c = np.float32(2.0 * math.log(255.0) / 9.0)
+    # walk c by ulps to the float whose alpha at dx = 3 is closest to 1/255
+    best = None
+    for _ in range(64):
+        a = np.float32(math.exp(np.float32(np.float32(-0.5) * np.float32(np.float32(c * np.float32(3.0)) * np.float32(3.0)))))
+        if best is None or abs(a - target) < abs(best[1] - target):
+            best = (c, a)
+        c = np.nextafter(c, np.float32(0) if a < target else np.float32(10))
+    c = best[0]
+    A, counts, cols, dpix = _tie_case(c)
+    assert counts[0] == 4 and counts[2] == 4  # four pixels, each one alpha decision
+    G = np.exp(-0.5 * float(c) * 9.0)
+    want = sum(abs(G * float(np.dot(cols[0], dpix[:, y, x]))) for x, y in ((5, 8), (11, 8), (8, 5), (8, 11)))
+    assert A[0, 8] == pytest.approx(want, rel=1e-4)
+    A2, counts2, _, _ = _tie_case(np.float32(c * 0.83))
+    assert counts2[0] == 0 and not A2.any()

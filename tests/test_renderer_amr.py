@@ -34,6 +34,16 @@ def test_eval_sh_matches_reference(deg):
     np.testing.assert_array_equal(got, p[f"eval_sh_deg{deg}"])
 
 
+@pytest.mark.parametrize("deg", [0, 1, 2, 3, 4])
+def test_eval_sh_degree4_matches_reference(deg):
+    """Up to the reference's C4 branch (utils/sh_utils.py:70-111), 25
+    coefficients per channel, bit for bit (tests/golden/sh4_pins.npz)."""
+    from gaussian_splatting_with_eye_tracking_amd.sh_utils import eval_sh
+    p = np.load(os.path.join(GOLD, "sh4_pins.npz"))
+    got = eval_sh(deg, torch.from_numpy(p["sh_coeffs"]), torch.from_numpy(p["sh_dirs"])).numpy()
+    np.testing.assert_array_equal(got, p[f"eval_sh_deg{deg}"])
+
+
 def test_fused_driver_refuses_autograd():
     from gaussian_splatting_with_eye_tracking_amd.rasterization_amr import render_steps
     x = torch.zeros(4, 3, requires_grad=True)
@@ -294,3 +304,28 @@ def test_unfilled_step0_option_does_not_leak():
             torch.cuda.synchronize()
             assert torch.equal(got, ref)
             assert int(torch.count_nonzero(img0)) == 0
+
+
+@pytest.mark.gpu
+def test_renderer_render_under_fallback_amr_variant():
+    """set_tuning('amr_variant', 0) (the full-list fallback) is safe to flip
+    between calls: renderer_amr.render under no_grad then takes the literal
+    per-step sequence (the fused steps exist for the default variant only)
+    and gives the frame of the default variant's sequence."""
+    import gaussian_splatting_with_eye_tracking_amd._C as C
+    from gaussian_splatting_with_eye_tracking_amd import renderer_amr as R
+    P, W, H = 20_000, 400, 300
+    sc, cam = G.scene_and_camera(P, W, H, 4)
+    t, pc, camera, pipe = _duck(sc, cam)
+    bg = torch.tensor([0.0, 0.0, 0.0], dtype=torch.float32, device="cuda")
+    with torch.no_grad():
+        ref = R.render(camera, pc, pipe, bg)["render"]
+        assert C.get_tuning("amr_variant") == 4
+        C.set_tuning("amr_variant", 0)
+        try:
+            assert C.get_tuning("amr_variant") == 0
+            got = R.render(camera, pc, pipe, bg)["render"]
+        finally:
+            C.set_tuning("amr_variant", 4)
+        torch.cuda.synchronize()
+    assert G.image_l1(got.cpu().numpy(), ref.cpu().numpy()) < G.IMAGE_L1_TOL

@@ -1,4 +1,7 @@
-"""Diagnostic: 5-step frame wall time, fused vs literal sequence (config 3)."""
+"""Diagnostic: 5-step frame wall time, fused vs literal sequence (config 3).
+
+usage: python tools/amr_chain_timing.py [mode ...]   modes: fused chain inline once (default: all)
+(under rocprofv3 --kernel-trace with one mode, tools/frame_gaps.py splits the frame)"""
 import sys
 import time
 
@@ -31,10 +34,15 @@ def inline():
 
 
 fns = {"fused": lambda: RA.render_steps(*a, st, fused=True), "chain": lambda: RA.render_steps(*a, st, fused=False),
-       "inline": inline}
+       "inline": inline,
+       "once": lambda: RA.GaussianRasterizer(st)(means3D=a[0], means2D=a[1], opacities=a[4], shs=a[2], scales=a[5],
+                                                 rotations=a[6], foveaStep=-2, interpolate_image=True)}
+want = sys.argv[1:] or list(fns)
+fns = {k: v for k, v in fns.items() if k in want}
 with torch.no_grad():
     for _ in range(300):
-        inline()
+        for f in fns.values():
+            f()
     for rep in range(3):
         for name, f in fns.items():
             torch.cuda.synchronize()

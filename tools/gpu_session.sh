@@ -72,6 +72,17 @@ for step in "$@"; do
         *) cnt="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_ANY SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT" ;;
       esac
       run "${step}_$c" 300 rocprofv3 --pmc $cnt --kernel-trace -d "gpurun_out/${step}_$c" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
+    sqc2|sqc3|sqc4|sqc5|sqd2|sqd3|sqd4|sqd5)  # wave-cycle breakdown (c) and LDS / L2 behaviour (d)
+      c=$(cfg_of "$step")
+      case "$step" in
+        sqc*) cnt="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY" ;;
+        *) cnt="SQ_WAVES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_BUSY_CYCLES TCC_HIT_sum TCC_MISS_sum" ;;
+      esac
+      run "${step}_$c" 300 rocprofv3 --pmc $cnt --kernel-trace -d "gpurun_out/${step}_$c" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
+    elem) GS_ELEM_SOFT=1 GS_ELEM_REPORT="$O/elem.jsonl" run pytest_elem 900 python -u -m pytest tests/test_gpu_parity_configs.py tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf -k "config2 or config4 or config5 or backward_parity or edge_case" ;;
+    chaintime) run chain_timing 300 python tools/amr_chain_timing.py ;;
+    chaintrace) run chain_trace 300 rocprofv3 --kernel-trace -d "$O/chain_trace" -o run --output-format csv -- python3 tools/amr_chain_timing.py inline &&
+                python tools/frame_gaps.py "$O/chain_trace/run_kernel_trace.csv" > "$O/chain_gaps.txt" 2>&1; cat "$O/chain_gaps.txt" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
