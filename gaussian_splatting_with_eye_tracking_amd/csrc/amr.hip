@@ -259,6 +259,20 @@ __global__ void __launch_bounds__(256) fovea_levels_kernel(int step, int T, uint
             current[t] = (L >= (uint32_t)step) ? (uint32_t)step : prev;
             break;
         }
+        case kAmrStateAfter + 1:
+        case kAmrStateAfter + 2:
+        case kAmrStateAfter + 3:
+        case kAmrStateAfter + 4: {
+            // from the state steps 1..4 leave (current = min(L0, 4), L0 the
+            // levels those steps saw) back to the one steps 1..j leave:
+            // current = min(L0, j), last = min(L0, j - 1) (by induction over
+            // the cases above) -- from current, not from `levels`, which a
+            // fovea-level change may have rewritten since
+            const uint32_t j = (uint32_t)(step - kAmrStateAfter), c4 = current[t];
+            last[t] = min(c4, j - 1);
+            current[t] = min(c4, j);
+            break;
+        }
         default:
             last[t] = 0;
             current[t] = L;

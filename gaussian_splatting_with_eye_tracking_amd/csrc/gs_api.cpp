@@ -1113,12 +1113,15 @@ int gs_amr_accumulate_step(int P, const float* background, int width, int height
                            void* stream) {
     return guarded([&]() -> int {
         if (P <= 0) return 0;
-        if ((foveaStep < 1 || foveaStep > 4) && foveaStep != kAmrStepsAll && foveaStep != kAmrStepsAllFill)
-            throw GsError("gs_amr_accumulate_step: foveaStep in 1..4 or GSPLAT_AMD_AMR_STEPS_1_TO_4(_FILL)");
+        if ((foveaStep < 1 || foveaStep > 4) && foveaStep != kAmrStepsAll && foveaStep != kAmrStepsAllFill &&
+            foveaStep != kAmrStepsAllSplit)
+            throw GsError("gs_amr_accumulate_step: foveaStep in 1..4 or GSPLAT_AMD_AMR_STEPS_1_TO_4(_FILL, _SPLIT)");
         // _FILL: the same launch storing every pixel (0 + value, zeros where
-        // nothing renders) instead of adding: accum holds an unfilled step-0 image
-        const bool fill = foveaStep == kAmrStepsAllFill;
-        if (fill) foveaStep = kAmrStepsAll;
+        // nothing renders) instead of adding: accum holds an unfilled step-0 image.
+        // _SPLIT: storing into the four steps' own images (accum [4][3][H][W],
+        // radii [4][P])
+        const bool fill = foveaStep == kAmrStepsAllFill, split = foveaStep == kAmrStepsAllSplit;
+        if (fill || split) foveaStep = kAmrStepsAll;
         if (g_amr_variant != 4) throw GsError("gs_amr_accumulate_step needs the default amr_variant (4)");
         if (!geom_buffer_precomp || !image_buffer_precomp || !accum)
             throw GsError("gs_amr_accumulate_step needs the buffers returned by foveaStep 0 and the running image");
@@ -1143,9 +1146,27 @@ int gs_amr_accumulate_step(int P, const float* background, int width, int height
         const float* feats = colors_precomp ? colors_precomp : g.rgb;
         { StageTimer _t(kAmrRender, s);
           launch_amr_render(W, H, img, img.levels, img.levels_last, b, ab, g, feats, background, accum, foveaStep, s,
-                            true, P, radii, !fill); }
+                            true, split ? 4 * P : P, radii, split ? 2 : fill ? 0 : 1); }
         stage_check(debug != 0, s, "amr_render (accumulate)");
         return K;
+    });
+}
+
+int gs_amr_set_step_state(char* image_buffer, size_t image_buffer_bytes, int width, int height, int step,
+                          void* stream) {
+    return guarded([&]() -> int {
+        if (step < 1 || step > 4) throw GsError("gs_amr_set_step_state: step in 1..4");
+        if (width <= 0 || height <= 0) return 0;
+        if (!image_buffer) throw GsError("gs_amr_set_step_state: needs the image buffer of foveaStep 0");
+        const size_t T = (size_t)((width + 31) / 32) * ((height + 31) / 32);
+        if (image_buffer_bytes < carve_image(nullptr, (size_t)width * height, T, nullptr, 32))
+            throw GsError("gs_amr_set_step_state: image buffer too small for width x height");
+        ImageView img;
+        carve_image(image_buffer, (size_t)width * height, T, &img, 32);
+        hipStream_t s = static_cast<hipStream_t>(stream);
+        launch_fovea_levels(kAmrStateAfter + step, (int)T, img, s);
+        stage_check(false, s, "amr_set_step_state");
+        return 0;
     });
 }
 

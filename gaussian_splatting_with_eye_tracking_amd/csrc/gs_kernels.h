@@ -91,6 +91,8 @@ void launch_sort_tiles(int T, const ImageView& img, const BinningView& b, int ma
 constexpr int kAmrFusedSortMax = 2048;
 constexpr int kAmrStepsAll = GSPLAT_AMD_AMR_STEPS_1_TO_4;  // foveaStep: steps 1..4 in one launch (gs_amr_accumulate_step)
 constexpr int kAmrStepsAllFill = GSPLAT_AMD_AMR_STEPS_1_TO_4_FILL;  // ... storing every pixel instead of adding
+constexpr int kAmrStepsAllSplit = GSPLAT_AMD_AMR_STEPS_1_TO_4_SPLIT;  // ... into the four steps' own images
+constexpr int kAmrStateAfter = 100;  // launch_fovea_levels step kAmrStateAfter + j: the level state foveaStep j leaves
 bool fused_sort_on();  // the AMR region-list pass sorts its tiles of <= kAmrFusedSortMax instances itself
 // (tile << 32 | depth) reconstruction of the reference's point_list_keys.
 void launch_reconstruct_keys(int T, const ImageView& img, const BinningView& b, const GeomView& g, uint64_t* keys,
@@ -214,7 +216,7 @@ void launch_fovea_levels(int step, int T, const ImageView& img, hipStream_t s, i
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,
                        const float* bg, float* out_color, int foveaStep, hipStream_t s, bool fused = false, int P = 0,
-                       int* zero_radii = nullptr, bool accumulate = false);
+                       int* zero_radii = nullptr, int accumulate = 0);  // 1 add, 2 split (render.hip)
 void launch_amr_interpolate(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                             float* out_color, int foveaStep, const float* out_color_precomp, hipStream_t s);
 

@@ -447,10 +447,40 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     __shared__ float s_out[3][16][16];
     const uint32_t qx0 = (uint32_t)(tile % tgx) * 32 + 16 * (q & 1), qy0 = (uint32_t)(tile / tgx) * 32 + 16 * (q >> 1);
     const uint32_t orow = lane >> 2, ocol = 4 * (lane & 3);
+    // accumulate 2 (GSPLAT_AMD_AMR_STEPS_1_TO_4_SPLIT, the speculative step
+    // images): out_color is four [3, H, W] images, image k - 1 the one
+    // foveaStep k returns; each pixel's value goes to the image of its round
+    // (amr/cr/forward.cu:313-339: (0,0) 1, (1,1) 2, (1,0) 3, (0,1) 4) and the
+    // other three get its zeros -- every image fully written, as four calls
+    // of one round each would write them.
     auto store_quadrant = [&](bool zero) {
         const uint32_t y = qy0 + orow, x = qx0 + ocol;
         if (y >= (uint32_t)H) return;
         const size_t pp = (size_t)W * y + x;
+        if (accumulate == 2) {
+            // the lane's 4 pixels start at an even x: rounds (re, ro, re, ro)
+            const uint32_t re = (y & 1u) ? 4u : 1u, ro = (y & 1u) ? 2u : 3u;
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) {
+                const float4 v = zero ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                      : *reinterpret_cast<const float4*>(&s_out[ch][orow][ocol]);
+#pragma unroll
+                for (uint32_t r = 1; r <= 4; r++) {
+                    const bool ke = r == re, ko = r == ro;
+                    const float4 w = make_float4(ke ? v.x : 0.f, ko ? v.y : 0.f, ke ? v.z : 0.f, ko ? v.w : 0.f);
+                    float* dst = out_color + (size_t)(r - 1) * 3 * plane + ch * plane + pp;
+                    if ((W & 3) == 0 && x + 3 < (uint32_t)W) {
+                        *reinterpret_cast<float4*>(dst) = w;
+                    } else {
+                        const float ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                        for (int j = 0; j < 4; j++)
+                            if (x + j < (uint32_t)W) dst[j] = ww[j];
+                    }
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) {
             const float4 v = zero ? make_float4(0.f, 0.f, 0.f, 0.f)
@@ -515,7 +545,7 @@ __global__ void __launch_bounds__(64) amr_region_render_kernel(
     };
     // Block-uniform early exits (amr/cr/forward.cu:287-367).
     if (L <= L_last) {
-        if (!accumulate) store_quadrant(true);
+        if (accumulate != 1) store_quadrant(true);
         finish_unit();
         return;
     }
@@ -749,7 +779,7 @@ void set_amr_variant(int v) { g_amr_variant = v == 0 ? 0 : 4; }
 void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* levels, const uint32_t* levels_last,
                        const BinningView& b, const AmrBinningView& ab, const GeomView& g, const float* features,
                        const float* bg, float* out_color, int foveaStep, hipStream_t s, bool fused, int P,
-                       int* zero_radii, bool accumulate) {
+                       int* zero_radii, int accumulate) {
     const int tgx = (W + 31) / 32, tgy = (H + 31) / 32;
     if (tgx == 0 || tgy == 0) return;
     if (g_amr_variant == 4) {
@@ -763,7 +793,7 @@ void launch_amr_render(int W, int H, const ImageView& img, const uint32_t* level
                            img.ranges, ab.region_lists, img.region_count, levels, levels_last, ab.rec_a, ab.rec_b, \
                            ab.rec_c, b.point_list, ov, img.accum_alpha, img.n_contrib, bg, out_color, foveaStep,   \
                            fused ? img.levels_current : nullptr, img.levels_last, img.tile_done, P,               \
-                           fused ? zero_radii : nullptr, accumulate ? 1 : 0)
+                           fused ? zero_radii : nullptr, accumulate)
         if (foveaStep > 0) GS_AMR_REGION(1);
         else GS_AMR_REGION(4);
 #undef GS_AMR_REGION

@@ -87,6 +87,47 @@ void check_operands(const Tensor& means3D, int P, const Tensor& bg, const Tensor
 const float* fptr(const Tensor& t) { return t.numel() ? t.data_ptr<float>() : nullptr; }
 float* fptr_mut(Tensor& t) { return t.numel() ? t.data_ptr<float>() : nullptr; }
 
+// Speculative AMR steps.  The reference's foveated caller
+// (gaussian_renderer_amr/__init__.py:183-594) calls foveaStep 1, 2, 3, 4 one
+// after another on step 0's buffers, each call returning its own full image
+// that the caller adds up in torch.  Step k's image depends only on those
+// buffers (levels, lists, records), the background and colors_precomp -- not
+// on anything the caller does in between -- so step 1 renders the rounds of
+// all four steps in ONE launch (GSPLAT_AMD_AMR_STEPS_1_TO_4_SPLIT) into four
+// images and returns the first; steps 2..4 return the others without a
+// launch.  Four launches' tails become one.  A step is served from the
+// speculation only if it is the next step on the same buffers, none of
+// whose torch version counters moved (apply_fovea_levels bumps the image
+// buffer's), with the same background / colours tensors and versions, size,
+// stream and no interpolation or debug; anything else is a miss: the image
+// buffer's level state (left as after step 4 by the one launch) is set back
+// to the state after the last step served (gs_amr_set_step_state) and the
+// step runs as usual.  Final T and n_contrib are those of every round from
+// step 1 on (each pixel belongs to one round; the rounds' values are the
+// same either way).  _C.set_amr_speculation(False) turns it off.
+struct SpecSteps {
+    const void* g = nullptr;
+    const void* b = nullptr;
+    const void* im = nullptr;
+    int64_t vg = 0, vb = 0, vim = 0, vbg = 0, vcol = 0;
+    const void* bg = nullptr;
+    const void* col = nullptr;
+    int W = 0, H = 0, P = 0, K = 0, next = 0;  // next: the step served next (2..4); 0 = nothing cached
+    size_t im_bytes = 0;
+    void* stream = nullptr;
+    Tensor images, radii;  // [4, 3, H, W], [4, P]
+    void clear() {
+        next = 0;
+        images = Tensor();
+        radii = Tensor();
+        g = b = im = bg = col = nullptr;
+    }
+};
+thread_local SpecSteps t_spec;
+thread_local bool t_spec_on = true;
+
+int64_t version_of(const Tensor& t) { return t.defined() && t.numel() ? (int64_t)t._version() : -1; }
+
 std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> rasterize_impl(
     bool amr, const Tensor& background, const Tensor& means3D_in, const Tensor& colors_in, const Tensor& opacity_in,
     const Tensor& scales_in, const Tensor& rotations_in, float scale_modifier, const Tensor& cov3D_precomp_in,
@@ -138,6 +179,60 @@ std::tuple<int, Tensor, Tensor, Tensor, Tensor, Tensor> rasterize_impl(
             Tensor g = geom_pre, b = bin_pre, im = img_pre;
             // K of the precomputed buffers from the binning buffer's size (no sync)
             const int hint = foveaStep >= 1 ? gs_amr_binning_count_of_bytes((size_t)b.numel()) : -1;
+            SpecSteps& sp = t_spec;
+            const bool same_bufs = sp.next != 0 && g.numel() && im.numel() && sp.g == g.data_ptr() &&
+                                   sp.im == im.data_ptr() && sp.b == (b.numel() ? b.data_ptr() : nullptr);
+            if (foveaStep >= 2 && foveaStep <= 4 && same_bufs) {
+                if (sp.next == foveaStep && !interpolate_image && !debug && sp.vg == version_of(g) &&
+                    sp.vb == version_of(b) && sp.vim == version_of(im) && sp.bg == bg.data_ptr() &&
+                    sp.vbg == version_of(background) && sp.col == (colors.numel() ? colors.data_ptr() : nullptr) &&
+                    sp.vcol == version_of(colors_in) && sp.W == W && sp.H == H && sp.P == P && sp.stream == stream) {
+                    Tensor img_k = sp.images[foveaStep - 1], rad_k = sp.radii[foveaStep - 1];
+                    const int K = sp.K;
+                    if (foveaStep == 4) sp.clear();
+                    else sp.next = foveaStep + 1;
+                    return std::make_tuple(K, img_k, rad_k, geom_pre, bin_pre, img_pre);
+                }
+                // a miss on the speculated buffers: back to the state after the last step served
+                check(gs_amr_set_step_state(reinterpret_cast<char*>(im.data_ptr()), (size_t)im.numel(), W, H,
+                                            sp.next - 1, stream),
+                      "amr speculation (level state)");
+                sp.clear();
+            } else if (foveaStep <= 1) {
+                sp.clear();  // a new frame (or a new step 1): nothing cached survives it
+            }
+            int amr_variant = 0;
+            check(gs_get_tuning("amr_variant", &amr_variant), "get_tuning");
+            if (foveaStep == 1 && t_spec_on && !interpolate_image && !debug && amr_variant == 4 && g.numel() &&
+                im.numel()) {
+                Tensor imgs = torch::empty({4, 3, H, W}, float_opts);
+                Tensor rads = torch::empty({4, P}, means3D_in.options().dtype(torch::kInt32));
+                rendered = gs_amr_accumulate_step(P, fptr(bg), W, H, fptr(colors), GSPLAT_AMD_AMR_STEPS_1_TO_4_SPLIT,
+                                                  reinterpret_cast<char*>(g.data_ptr()),
+                                                  b.numel() ? reinterpret_cast<char*>(b.data_ptr()) : nullptr,
+                                                  reinterpret_cast<char*>(im.data_ptr()), imgs.data_ptr<float>(),
+                                                  rads.data_ptr<int>(), 0, hint, stream);
+                check(rendered, "rasterize_gaussians (AMR, speculative steps 1..4)");
+                sp.g = g.data_ptr();
+                sp.b = b.numel() ? b.data_ptr() : nullptr;
+                sp.im = im.data_ptr();
+                sp.vg = version_of(g);
+                sp.vb = version_of(b);
+                sp.vim = version_of(im);
+                sp.bg = bg.data_ptr();
+                sp.vbg = version_of(background);
+                sp.col = colors.numel() ? colors.data_ptr() : nullptr;
+                sp.vcol = version_of(colors_in);
+                sp.W = W;
+                sp.H = H;
+                sp.P = P;
+                sp.K = rendered;
+                sp.stream = stream;
+                sp.images = imgs;
+                sp.radii = rads;
+                sp.next = 2;
+                return std::make_tuple(rendered, imgs[0], rads[0], geom_pre, bin_pre, img_pre);
+            }
             rendered = gs_amr_rasterizer_forward_ex(
                 buf_of(geomBuffer), buf_of(binningBuffer), buf_of(imgBuffer), P, degree, M, fptr(bg), W, H,
                 fptr(means3D), fptr(sh), fptr(colors), fptr(opacity), fptr(scales), scale_modifier, fptr(rotations),
@@ -884,6 +979,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     });
     m.def("profile_read", &ProfileRead, py::arg("reset") = true);
     m.def("set_tuning", [](const std::string& k, int v) { check(gs_set_tuning(k.c_str(), v), "set_tuning"); });
+    m.def("set_amr_speculation", [](bool on) {
+        t_spec_on = on;
+        if (!on) t_spec.clear();
+    }, "speculative AMR steps (this thread): step 1 renders steps 1..4 at once, steps 2..4 return its images");
     m.def("get_tuning", [](const std::string& k) {
         int v = 0;
         check(gs_get_tuning(k.c_str(), &v), "get_tuning");

@@ -241,10 +241,27 @@ int gs_amr_rasterizer_forward_ex(gs_buffer geometry, gs_buffer binning, gs_buffe
  * four steps' images -- instead of added to. */
 #define GSPLAT_AMD_AMR_STEPS_1_TO_4 14
 #define GSPLAT_AMD_AMR_STEPS_1_TO_4_FILL 15
+/* foveaStep = GSPLAT_AMD_AMR_STEPS_1_TO_4_SPLIT: the same one launch writing
+ * the four steps' OWN images -- accum is 4 x 3 x height x width floats, image
+ * k - 1 the one foveaStep k alone returns (its round's pixels, zeros
+ * elsewhere), every element written -- and radii 4 x P zeros (each step's
+ * zero radii).  Final T, n_contrib and the level state are left as after
+ * step 4.  The torch binding uses it to serve the reference's literal
+ * step-by-step sequence (torch_ext.cpp, speculative steps). */
+#define GSPLAT_AMD_AMR_STEPS_1_TO_4_SPLIT 16
 int gs_amr_accumulate_step(int P, const float* background, int width, int height, const float* colors_precomp,
                            int foveaStep, char* geom_buffer_precomp, char* binning_buffer_precomp,
                            char* image_buffer_precomp, float* accum, int* radii, int debug, int num_rendered_hint,
                            void* stream);
+
+/* Takes the level state (tile_AMR_levels_last / _current,
+ * amr/cr/rasterizer_impl.cu:208-243) of an AMR image buffer from the one
+ * foveaStep 1..4 leave (as GSPLAT_AMD_AMR_STEPS_1_TO_4* leave it) back to the
+ * one foveaStep 1..`step` leave (step in 1..4): with c = current, last =
+ * min(c, step - 1), current = min(c, step).  Lets a caller that ran steps
+ * 1..4 at once go back to the literal sequence at step + 1. */
+int gs_amr_set_step_state(char* image_buffer, size_t image_buffer_bytes, int width, int height, int step,
+                          void* stream);
 
 /* Replaces SimpleKNN::knn (knn/simple_knn.h:16-19, knn/simple_knn.cu:185-221)
  * behind simple_knn._C.distCUDA2.  `scratch` is resized to the workspace

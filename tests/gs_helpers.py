@@ -100,6 +100,9 @@ def elementwise_check(got, ref, rtol: float = GRAD_ELEM_RTOL, atol_frac: float =
     above = (np.abs(r) > atol) & (al == 0)
     if above.any():
         out["max_rel_above_floor"] = float(np.max(err[above] / np.abs(r[above])))
+    large = (np.abs(r) >= 100.0 * atol) & (al == 0)  # elements >= 1e-4 of the tensor's largest
+    if large.any():
+        out["max_rel_large"] = float(np.max(err[large] / np.abs(r[large])))
     out["max_excess"] = float(np.max((err - rtol * np.abs(r)) / maxr)) if maxr > 0 else 0.0
     return out
 

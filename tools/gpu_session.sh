@@ -81,6 +81,7 @@ for step in "$@"; do
       run "${step}_$c" 300 rocprofv3 --pmc $cnt --kernel-trace -d "gpurun_out/${step}_$c" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
     elem) GS_ELEM_SOFT=1 GS_ELEM_REPORT="$O/elem.jsonl" run pytest_elem 900 python -u -m pytest tests/test_gpu_parity_configs.py tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf -k "config2 or config4 or config5 or backward_parity or edge_case" ;;
     chaintime) run chain_timing 300 python tools/amr_chain_timing.py ;;
+    spec) run pytest_spec 600 python -u -m pytest tests/test_gpu_amr_speculation.py tests/test_gpu_capi_ctypes.py tests/test_renderer_amr.py -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf ;;
     chaintrace) run chain_trace 300 rocprofv3 --kernel-trace -d "$O/chain_trace" -o run --output-format csv -- python3 tools/amr_chain_timing.py inline &&
                 python tools/frame_gaps.py "$O/chain_trace/run_kernel_trace.csv" > "$O/chain_gaps.txt" 2>&1; cat "$O/chain_gaps.txt" ;;
     *) echo "unknown step $step"; exit 2 ;;
