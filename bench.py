@@ -884,7 +884,7 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
         diag = not ctx.args.no_profile
         el5u = float("nan")
         if diag:
-            for _ in range(max(2, warmup)):  # (its step images and sums: allocator blocks the fused frame never asks for)
+            for _ in range(max(10, warmup)):  # (its step images and sums: allocator blocks the fused frame never asks for)
                 frame_5step(fused=False)
             torch.cuda.synchronize()
             t0 = time.perf_counter()

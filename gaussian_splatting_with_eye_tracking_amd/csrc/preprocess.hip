@@ -99,6 +99,16 @@ __device__ __forceinline__ float3 eval_sh_color(int deg, const float (&c)[16][3]
 // the price of whole-line requests instead of 12 scattered 16-B loads per
 // thread.
 constexpr int kPpThreads = 256;
+// LDS row of one Gaussian: the 48 SH floats + one 16-B pad.  At 52 floats
+// (13 pieces of 16 B) the 16 lanes of each b128 access hit 16 distinct
+// 4-bank groups (52 l mod 64 = 4 (13 l mod 16)): no conflicts; at 48 every
+// fourth lane repeated a group and the compiler's b32 reads hit 4 banks per
+// wave (SQ_LDS_BANK_CONFLICT 28.6 cycles per LDS instruction at config 2,
+// profiles/r06a_cfg2_sq_counters.json).  The LDS-DMA writes 16-B pieces to
+// consecutive LDS addresses per lane, so the padding comes from the sources:
+// piece p of a wave's area is row p / 13, piece p % 13, and piece 12 of
+// every row is left unwritten.
+constexpr int kShStride = 52;
 
 // Everything after the loads of one Gaussian (forward.cu:155-256): the cull,
 // cov2D, conic, radius / rect, SH colour (coefficients from load_shc, only for
@@ -194,9 +204,7 @@ __device__ __forceinline__ void pp_gaussian(const PreprocessArgs& a, const GeomV
             row[2] = make_float4(dz3[2], 0.f, 0.f, 0.f);
         }
         if (stage) {
-            stage[12] = rgb.x;
-            stage[13] = rgb.y;
-            stage[14] = rgb.z;
+            *reinterpret_cast<float4*>(stage + 12) = make_float4(rgb.x, rgb.y, rgb.z, 0.f);  // (one b128)
         } else {
             g.rgb[3 * idx + 0] = rgb.x;
             g.rgb[3 * idx + 1] = rgb.y;
@@ -278,10 +286,21 @@ __device__ __forceinline__ void pp_thread(const PreprocessArgs& a, const GeomVie
         if constexpr (kDma) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA rows have landed
             const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
+            // twelve b128 reads of the padded row (conflict-free, kShStride)
+            // (the empty asm keeps each piece one 128-bit register tuple, so the
+            // compiler does not split the reads into conflicting b32 / b64 ones)
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            float v[48];
+#pragma unroll
+            for (int i = 0; i < 12; i++) {
+                f4v t = reinterpret_cast<const f4v*>(sh_row)[i];
+                asm volatile("" : "+v"(t));
+                v[4 * i] = t.x; v[4 * i + 1] = t.y; v[4 * i + 2] = t.z; v[4 * i + 3] = t.w;
+            }
 #pragma unroll
             for (int k = 0; k < 16; k++)
 #pragma unroll
-                for (int ch = 0; ch < 3; ch++) shc[k][ch] = k < ncoef ? sh_row[3 * k + ch] : 0.f;
+                for (int ch = 0; ch < 3; ch++) shc[k][ch] = k < ncoef ? v[3 * k + ch] : 0.f;
         } else {
             load_sh<kSH16>(a.D, a.M, a.shs + (size_t)idx * a.M * 3, shc);
         }
@@ -310,25 +329,27 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
     static_assert(!kDma || (kHasSH && kSH16), "LDS-DMA stages 16-coefficient SH rows");
     constexpr bool kStageOut = kDma, kNtIn = kDma;
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    __shared__ __attribute__((aligned(16))) float s_sh[kDma ? kPpThreads * 48 : 1];
+    __shared__ __attribute__((aligned(16))) float s_sh[kDma ? kPpThreads * kShStride : 1];
     if constexpr (kDma) {
-        // wave w: rows [64 w, 64 w + 64) of the block; lane l's 16-B pieces l + 64 i
+        // wave w: rows [64 w, 64 w + 64) of the block; lane l writes LDS piece
+        // p = l + 64 i = (row p / 13, 16-B piece p % 13 of it)
         const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
         const size_t row0 = (size_t)blockIdx.x * kPpThreads + 64 * w;
-        const size_t nfl = (size_t)a.P * 48;
         const float* src = a.shs + row0 * 48;
-        float* dst = s_sh + 64 * 48 * w;
+        float* dst = s_sh + 64 * kShStride * w;
+        constexpr int kPieces = kShStride / 4;  // 13
 #pragma unroll
-        for (int i = 0; i < 12; i++) {
-            const size_t f = (size_t)(64 * i + lane) * 4;
-            if (row0 * 48 + f < nfl) __builtin_amdgcn_global_load_lds(src + f, dst + 256 * i, 16, 0, 2);  // (nt)
+        for (int i = 0; i < kPieces; i++) {
+            const int p = 64 * i + lane, r = p / kPieces, j = p - kPieces * r;
+            if (j < 12 && row0 + (size_t)r < (size_t)a.P)
+                __builtin_amdgcn_global_load_lds(src + 48 * r + 4 * j, dst + 256 * i, 16, 0, 2);  // (nt)
         }
     }
     for (int i = idx; i < a.zero_n; i += (int)(gridDim.x * blockDim.x)) a.zero_words[i] = 0u;
     // whether the backward may take d(rgb)/d(dir) from g.drgb (every visible
     // Gaussian's row is written below)
     if (idx == 0) g.hdr[kHdrDrgb] = (kHasSH && a.store_drgb) ? 1u : 0u;
-    float* row = s_sh + (kDma ? 48 * threadIdx.x : 0);
+    float* row = s_sh + (kDma ? kShStride * threadIdx.x : 0);
     if constexpr (kStageOut) {
         // every lane of a wave takes part in its coalesced record stores below
         const int wrow0 = (int)(blockIdx.x * kPpThreads) + (int)(threadIdx.x & ~63u);
@@ -338,7 +359,7 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         const int lane = threadIdx.x & 63;
-        const float* wl = s_sh + 48 * (threadIdx.x & ~63u);
+        const float* wl = s_sh + kShStride * (threadIdx.x & ~63u);
         const int nrow = min(64, a.P - wrow0);
         if (a.store_drgb) {  // 64 rows x three 16-B pieces
             float4* out = reinterpret_cast<float4*>(g.drgb) + 3 * (size_t)wrow0;
@@ -346,7 +367,7 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
             for (int i = 0; i < 3; i++) {
                 const int c = lane + 64 * i;
                 if (c < 3 * nrow) {
-                    const float4 v = *reinterpret_cast<const float4*>(wl + 48 * (c / 3) + 4 * (c % 3));
+                    const float4 v = *reinterpret_cast<const float4*>(wl + kShStride * (c / 3) + 4 * (c % 3));
                     typedef float f4v __attribute__((ext_vector_type(4)));
                     __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v*>(out + c));
                 }
@@ -359,7 +380,7 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
                 const int c = lane + 64 * i;
                 if (c < 4 * nrow)
                     out[c] = (c & 3) == 3 ? make_float4(0.f, 0.f, 0.f, 0.f)
-                                          : *reinterpret_cast<const float4*>(wl + 48 * (c >> 2) + 16 + 4 * (c & 3));
+                                          : *reinterpret_cast<const float4*>(wl + kShStride * (c >> 2) + 16 + 4 * (c & 3));
             }
         }
         // 64 x 3 rgb floats = 48 pieces of 4
@@ -369,7 +390,7 @@ __global__ void __launch_bounds__(kPpThreads) preprocess_kernel(PreprocessArgs a
 #pragma unroll
             for (int e = 0; e < 4; e++) {
                 const int f = min(4 * lane + e, nf - 1);
-                v4[e] = wl[48 * (f / 3) + 12 + f % 3];
+                v4[e] = wl[kShStride * (f / 3) + 12 + f % 3];
             }
             float* out = g.rgb + 3 * (size_t)wrow0 + 4 * lane;
             if (4 * lane + 4 <= nf) {

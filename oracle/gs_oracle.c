@@ -704,7 +704,10 @@ void orc_render_tie_allowance(int W, int H, int block_x, int block_y, const uint
 static void bwd_pixel(int W, int H, int px, int py, uint32_t rx, uint32_t ry,
                       const uint32_t* point_list, const float* bg_color, const float* points_xy,
                       const float* conic_opacity, const float* colors, const float* final_Ts,
-                      const uint32_t* n_contrib, const float* dL_dpixels, double* acc, int stride) {
+                      const uint32_t* n_contrib, const float* dL_dpixels, double* acc, int stride,
+                      int absolute) {
+/* absolute: accumulate |term| instead (orc_render_backward_abs) */
+#define ACC(i, v) (a[i] += absolute ? fabs((double)(v)) : (double)(v))
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
     size_t pid = (size_t)W * py + px;
@@ -738,7 +741,7 @@ static void bwd_pixel(int W, int H, int px, int py, uint32_t rx, uint32_t ry,
             last_color[ch] = c;
             const float dL_dchannel = dL_dpixel[ch];
             dL_dalpha += (c - accum_rec[ch]) * dL_dchannel;
-            a[0 + ch] += (double)(dchannel_dcolor * dL_dchannel);
+            ACC(0 + ch, dchannel_dcolor * dL_dchannel);
         }
         dL_dalpha *= T;
         last_alpha = alpha;
@@ -750,14 +753,15 @@ static void bwd_pixel(int W, int H, int px, int py, uint32_t rx, uint32_t ry,
         const float gdy = G * dy;
         const float dG_ddelx = -gdx * co[0] - gdy * co[1];
         const float dG_ddely = -gdy * co[2] - gdx * co[1];
-        a[3] += (double)(dL_dG * dG_ddelx * ddelx_dx);
-        a[4] += (double)(dL_dG * dG_ddely * ddely_dy);
-        a[5] += (double)(-0.5f * gdx * dx * dL_dG);
-        a[6] += (double)(-0.5f * gdx * dy * dL_dG);
-        a[7] += (double)(-0.5f * gdy * dy * dL_dG);
-        a[8] += (double)(G * dL_dalpha);
+        ACC(3, dL_dG * dG_ddelx * ddelx_dx);
+        ACC(4, dL_dG * dG_ddely * ddely_dy);
+        ACC(5, -0.5f * gdx * dx * dL_dG);
+        ACC(6, -0.5f * gdx * dy * dL_dG);
+        ACC(7, -0.5f * gdy * dy * dL_dG);
+        ACC(8, G * dL_dalpha);
     }
 }
+#undef ACC
 
 /* base/cr/backward.cu:399-557 (renderCUDA<3> backward).  Accumulates in double
  * (the exact sum of the reference's float atomics). dL_dconic is [P,4] (2x2).
@@ -784,7 +788,7 @@ void orc_render_backward(int W, int H, int block_x, int block_y, const uint32_t*
             for (int px = 0; px < W; px++) {
                 int tile = (py / block_y) * gx + (px / block_x);
                 bwd_pixel(W, H, px, py, ranges[2 * tile], ranges[2 * tile + 1], point_list, bg_color,
-                          points_xy, conic_opacity, colors, final_Ts, n_contrib, dL_dpixels, a, stride);
+                          points_xy, conic_opacity, colors, final_Ts, n_contrib, dL_dpixels, a, stride, 0);
             }
     }
 #pragma omp parallel for schedule(static, 4096) num_threads(g_threads) if (g_threads > 1)
@@ -806,6 +810,42 @@ void orc_render_backward(int W, int H, int block_x, int block_y, const uint32_t*
         dL_dopacity[g] = (float)s[8];
     }
     free(acc);
+}
+
+/* Test support: per Gaussian the sums of |term| of the nine blend-backward
+ * terms (orc_render_backward's sums with every term's magnitude), S[P][9]
+ * in double.  Any float32 summation order of those terms (the GPU's
+ * float atomics) is within a small multiple of 2^-24 S of the exact sum;
+ * the element-wise gradient tests derive their accumulation allowance from
+ * it (oracle.py grad_allowance). */
+void orc_render_backward_abs(int W, int H, int block_x, int block_y, const uint32_t* ranges,
+                             const uint32_t* point_list, const float* bg_color, const float* points_xy,
+                             const float* conic_opacity, const float* colors, const float* final_Ts,
+                             const uint32_t* n_contrib, const float* dL_dpixels, int P, double* S) {
+    const int gx = (W + block_x - 1) / block_x;
+    const int gy = (H + block_y - 1) / block_y;
+    const int nb = g_threads > 1 ? (g_threads < gy ? g_threads : (gy > 0 ? gy : 1)) : 1;
+    const int stride = 9;
+    double* acc = nb > 1 ? (double*)calloc((size_t)P * stride * (size_t)(nb - 1), sizeof(double)) : NULL;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nb) if (nb > 1)
+    for (int b = 0; b < nb; b++) {
+        const int ty0 = (int)((long)gy * b / nb), ty1 = (int)((long)gy * (b + 1) / nb);
+        const int py0 = ty0 * block_y, py1 = ty1 * block_y < H ? ty1 * block_y : H;
+        double* a = b == 0 ? S : acc + (size_t)P * stride * (size_t)(b - 1);
+        for (int py = py0; py < py1; py++)
+            for (int px = 0; px < W; px++) {
+                int tile = (py / block_y) * gx + (px / block_x);
+                bwd_pixel(W, H, px, py, ranges[2 * tile], ranges[2 * tile + 1], point_list, bg_color,
+                          points_xy, conic_opacity, colors, final_Ts, n_contrib, dL_dpixels, a, stride, 1);
+            }
+    }
+    if (acc) {
+#pragma omp parallel for schedule(static, 4096) num_threads(g_threads) if (g_threads > 1)
+        for (int g = 0; g < P; g++)
+            for (int b = 1; b < nb; b++)
+                for (int q = 0; q < 9; q++) S[(size_t)g * stride + q] += acc[((size_t)P * (b - 1) + g) * stride + q];
+        free(acc);
+    }
 }
 
 /* base/cr/backward.cu:144-274 (computeCov2DCUDA) */

@@ -264,34 +264,44 @@ def backward(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors
     return out
 
 
-def tie_allowance(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors_precomp=None, scales=None,
-                  rotations=None, cov3D_precomp=None) -> tuple:
-    """Test support (gs_oracle.c orc_render_tie_allowance): per gradient
-    element, the total jump the near-tie blend decisions can make -- each
-    decision taken within float32 rounding of its threshold replayed the
-    other way, one at a time, |gradient(flipped) - gradient(as taken)| summed.
-    The nine blend-level terms come from the replays directly; the
-    per-Gaussian gradients after them are a linear map J of those terms, so
-    their allowance is sum_k |J (A_k e_k)| over the nine terms k.  Returns
-    ({tensor name: allowance array shaped like the gradient}, {counts})."""
-    means3D, shs, colors_precomp, scales, rotations, cov3D_precomp = _bwd_inputs(
-        means3D, shs, colors_precomp, scales, rotations, cov3D_precomp)
-    P = means3D.shape[0]
+def _tie_terms(s: Settings, fwd: ForwardResult, dL_dpix, colors):
+    P = fwd.radii.shape[0]
     W, H = int(s.image_width), int(s.image_height)
     A = np.zeros((P, 9), np.float64)
     counts = np.zeros(4, np.int64)
-    colors = colors_precomp if colors_precomp is not None else fwd.rgb
     lib().orc_render_tie_allowance(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(fwd.block),
                                    ctypes.c_int(fwd.block), _p(fwd.ranges), _p(fwd.point_list), _p(_f32(s.bg)),
                                    _p(fwd.means2D), _p(fwd.conic_opacity), _p(np.ascontiguousarray(colors)),
                                    _p(_f32(dL_dpix)), ctypes.c_int(P), _p(A), _p(counts))
+    return A, counts
+
+
+def _abs_terms(s: Settings, fwd: ForwardResult, dL_dpix, colors):
+    P = fwd.radii.shape[0]
+    W, H = int(s.image_width), int(s.image_height)
+    S = np.zeros((P, 9), np.float64)
+    lib().orc_render_backward_abs(ctypes.c_int(W), ctypes.c_int(H), ctypes.c_int(fwd.block), ctypes.c_int(fwd.block),
+                                  _p(fwd.ranges), _p(fwd.point_list), _p(_f32(s.bg)), _p(fwd.means2D),
+                                  _p(fwd.conic_opacity), _p(np.ascontiguousarray(colors)), _p(fwd.final_T),
+                                  _p(fwd.n_contrib), _p(_f32(dL_dpix)), ctypes.c_int(P), _p(S))
+    return S
+
+
+def _propagate(s: Settings, fwd: ForwardResult, means3D, shs, scales, rotations, cov3D_precomp, A) -> dict:
+    """Allowances [P, 9] on the nine blend-level terms -> allowances on every
+    returned gradient: the terms' own tensors directly; the per-Gaussian
+    gradients after the blend are a linear map J of the terms, so theirs is
+    sum_k |J (A_k e_k)| over the nine terms k (the bound of |J v| over every
+    v with |v_k| <= A_k)."""
+    P = A.shape[0]
     Af = A.astype(np.float32)
     out = {"dL_dcolors": A[:, 0:3].copy(), "dL_dopacity": A[:, 8:9].copy(),
            "dL_dmeans2D": np.concatenate([A[:, 3:5], np.zeros((P, 1))], 1),
            "dL_dconic": np.stack([A[:, 5:7], np.stack([np.zeros(P), A[:, 7]], 1)], 1)}
-    touched = np.nonzero(A.any(1))[0]
-    down = None
-    for k in range(9):
+    M = 0 if shs is None else shs.shape[1]
+    down = {"dL_dmeans3D": np.zeros((P, 3)), "dL_dcov3D": np.zeros((P, 6)), "dL_dsh": np.zeros((P, M, 3)),
+            "dL_dscales": np.zeros((P, 3)), "dL_drotations": np.zeros((P, 4))}
+    for k in range(8):  # (the opacity term, k = 8, feeds no per-Gaussian gradient after the blend)
         if not Af[:, k].any():
             continue
         g_mean2D = np.zeros((P, 3), np.float32)
@@ -301,20 +311,77 @@ def tie_allowance(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, c
             g_col[:, k] = Af[:, k]
         elif k < 5:
             g_mean2D[:, k - 3] = Af[:, k]
-        elif k < 8:
-            g_conic.reshape(P, 4)[:, (0, 1, 3)[k - 5]] = Af[:, k]
         else:
-            continue  # the opacity term feeds no per-Gaussian gradient after the blend
+            g_conic.reshape(P, 4)[:, (0, 1, 3)[k - 5]] = Af[:, k]
         r = _per_gaussian_backward(s, fwd, means3D, shs, scales, rotations, cov3D_precomp, g_mean2D, g_conic, g_col)
-        r = {n: np.abs(v.astype(np.float64)) for n, v in r.items()}
-        down = r if down is None else {n: down[n] + r[n] for n in down}
-    if down is None:
-        M = 0 if shs is None else shs.shape[1]
-        down = {"dL_dmeans3D": np.zeros((P, 3)), "dL_dcov3D": np.zeros((P, 6)), "dL_dsh": np.zeros((P, M, 3)),
-                "dL_dscales": np.zeros((P, 3)), "dL_drotations": np.zeros((P, 4))}
+        for n in down:
+            down[n] += np.abs(r[n].astype(np.float64))
     out.update(down)
+    return out
+
+
+def tie_allowance(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors_precomp=None, scales=None,
+                  rotations=None, cov3D_precomp=None) -> tuple:
+    """Test support (gs_oracle.c orc_render_tie_allowance): per gradient
+    element, the total jump the near-tie blend decisions can make -- each
+    decision taken within float32 rounding of its threshold replayed the
+    other way, one at a time, |gradient(flipped) - gradient(as taken)| summed,
+    then carried through the per-Gaussian backward (_propagate).  Returns
+    ({tensor name: allowance shaped like the gradient}, {counts})."""
+    means3D, shs, colors_precomp, scales, rotations, cov3D_precomp = _bwd_inputs(
+        means3D, shs, colors_precomp, scales, rotations, cov3D_precomp)
+    colors = colors_precomp if colors_precomp is not None else fwd.rgb
+    A, counts = _tie_terms(s, fwd, dL_dpix, colors)
+    out = _propagate(s, fwd, means3D, shs, scales, rotations, cov3D_precomp, A)
     return out, {"tie_pixels": int(counts[0]), "power": int(counts[1]), "alpha": int(counts[2]), "T": int(counts[3]),
-                 "gaussians": int(touched.size)}
+                 "gaussians": int(np.count_nonzero(A.any(1)))}
+
+
+# Accumulation allowance per blend-level term: (ACC_SQRT sqrt(n) + ACC_ULPS)
+# x 2^-24 x sum|terms|, n the tiles the Gaussian touches.  The GPU forms a
+# Gaussian's per-pixel terms in float32 (hardware exp, T rebuilt by a
+# reciprocal step by step down the pixel's chain) and adds them in its own
+# order -- a tree of partial sums per tile (<= 256 pixels, ~8 levels), then
+# the n tile partials by float atomics in arrival order -- where the oracle
+# forms them with libm expf and a division and sums in double.  The error of
+# such a sum is a multiple of 2^-24 sum|terms|: ~8 ulps per tile tree times
+# ~sqrt(n) for the n partials' random-sign roundings (worst case ~n), plus the
+# terms' own few-ulp differences.  It matters where the terms cancel -- a
+# large Gaussian whose gradient is a small difference of many pixels' terms
+# -- and the constants (16 sqrt(n) + 32 ulps) are twice the largest multiple
+# measured on the GPU (tests record it as acc_multiple_needed).
+ACC_SQRT = 16.0
+ACC_ULPS = 32.0
+
+
+def grad_allowance(s: Settings, fwd: ForwardResult, means3D, dL_dpix, shs=None, colors_precomp=None, scales=None,
+                   rotations=None, cov3D_precomp=None, parts: bool = False) -> tuple:
+    """Test support: the element-wise gradient tests' allowance -- the
+    near-tie jumps (tie_allowance) plus the float32 accumulation allowance
+    (ACC_SQRT sqrt(tiles touched) + ACC_ULPS) 2^-24 sum|terms| of every
+    blend-level term (orc_render_backward_abs), carried together through the
+    per-Gaussian backward (the propagation is linear in non-negative
+    allowances, so the parts add).  Returns ({tensor: allowance}, {counts});
+    with parts=True the first is {"tie": ..., "acc_sqrt": ..., "acc_ulp": ...}
+    (the tie jumps; 2^-24 sqrt(n) sum|terms|; 2^-24 sum|terms|)."""
+    means3D, shs, colors_precomp, scales, rotations, cov3D_precomp = _bwd_inputs(
+        means3D, shs, colors_precomp, scales, rotations, cov3D_precomp)
+    colors = colors_precomp if colors_precomp is not None else fwd.rgb
+    A, counts = _tie_terms(s, fwd, dL_dpix, colors)
+    S = _abs_terms(s, fwd, dL_dpix, colors) * 2.0 ** -24
+    sq = np.sqrt(fwd.tiles_touched.astype(np.float64))[:, None]
+    info = {"tie_pixels": int(counts[0]), "power": int(counts[1]), "alpha": int(counts[2]), "T": int(counts[3]),
+            "gaussians": int(np.count_nonzero(A.any(1))), "acc_sqrt": ACC_SQRT, "acc_ulps": ACC_ULPS}
+    prop = lambda X: _propagate(s, fwd, means3D, shs, scales, rotations, cov3D_precomp, X)  # noqa: E731
+    if parts:
+        return {"tie": prop(A), "acc_sqrt": prop(sq * S), "acc_ulp": prop(S)}, info
+    return prop(A + (ACC_SQRT * sq + ACC_ULPS) * S), info
+
+
+def combine_allowance(parts: dict, acc_sqrt: float = ACC_SQRT, acc_ulps: float = ACC_ULPS) -> dict:
+    """grad_allowance(parts=True)'s parts -> one allowance per tensor."""
+    return {n: parts["tie"][n] + acc_sqrt * parts["acc_sqrt"][n] + acc_ulps * parts["acc_ulp"][n]
+            for n in parts["tie"]}
 
 
 def mark_visible(means3D, viewmatrix, projmatrix) -> np.ndarray:

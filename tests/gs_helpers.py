@@ -53,12 +53,16 @@ def rel_err(a, b) -> float:
 
 
 # Element-wise gradient bar, beside the L2-norm bar above:
-#     |g - r| <= GRAD_ELEM_RTOL * |r| + atol,   atol = GRAD_ELEM_ATOL_FRAC * max|r|
+#     |g - r| <= GRAD_ELEM_RTOL * |r| + atol + allow,   atol = GRAD_ELEM_ATOL_FRAC * max|r|
 # per tensor.  The absolute floor is one millionth of the tensor's largest
-# element: a gradient element is a sum of per-pixel float terms, and the GPU's
-# float atomics (and the hardware exp, v_exp_f32 against libm expf) round
-# differently from the oracle's double accumulation, so elements that are
-# cancellations of large terms carry an absolute, not a relative, error.
+# element.  `allow` (oracle.grad_allowance, per element) is what float32
+# cannot pin down, computed by the oracle from the same inputs: the jump of
+# every blend decision taken within float32 rounding of its threshold (the
+# hardware exp, v_exp_f32, and libm expf differ in the last bits there), and
+# 64 ulps of the sum of the magnitudes of the per-pixel terms a gradient is
+# accumulated from (the GPU's float atomics add them in another order than
+# the oracle's double sums; where the terms cancel that is far more than
+# 1e-4 of the result) -- both carried through the per-Gaussian backward.
 GRAD_ELEM_RTOL = 1e-4
 GRAD_ELEM_ATOL_FRAC = 1e-6
 
@@ -67,9 +71,8 @@ def elementwise_check(got, ref, rtol: float = GRAD_ELEM_RTOL, atol_frac: float =
                       allow=None) -> dict:
     """Element-wise comparison of one gradient tensor:
         |g - r| <= rtol |r| + atol + allow
-    where `allow` (optional, shaped like the gradient) is the oracle's jump
-    allowance of the near-tie blend decisions (oracle.tie_allowance; zero for
-    every Gaussian no near-tie pixel's chain reaches).  Returns the violation
+    where `allow` (optional, shaped like the gradient) is the oracle's
+    allowance (oracle.grad_allowance: near-tie jumps + accumulation order).  Returns the violation
     count, the stated atol, the worst element (largest err / bound) with its
     leading (per-Gaussian) index, the largest element-wise relative error over
     the elements above the absolute floor and without allowance, and how many
@@ -139,12 +142,21 @@ def _report(record: dict) -> None:
             f.write(json.dumps(record) + "\n")
 
 
+# (acc_sqrt, acc_ulps) combinations whose violation counts the report records
+# beside the asserted one (GS_ELEM_REPORT), for calibration
+_ACC_GRID = ((0.0, 0.0), (1.0, 0.0), (1.0, 4.0), (2.0, 8.0), (4.0, 16.0))
+
+
 def assert_grads_elementwise(case: str, names, grads, refs, sc=None, cam=None, ref_fwd=None,
                              atol_frac: dict | None = None, allow: dict | None = None, ties: dict | None = None) -> None:
     """The element-wise bar over every named gradient: zero violations, with
     the worst element and its Gaussian's context in the message.  `allow`:
-    oracle.tie_allowance's per-tensor jump allowances (`ties` its counts,
+    oracle.grad_allowance's per-tensor allowances (`ties` its counts,
     recorded with the report)."""
+    import oracle as O
+    parts = allow if allow is not None and "tie" in allow else None
+    if parts is not None:
+        allow = O.combine_allowance(parts)
     fails = []
     for n, g in zip(names, grads):
         if n not in refs:
@@ -152,6 +164,18 @@ def assert_grads_elementwise(case: str, names, grads, refs, sc=None, cam=None, r
         gg = g.detach().cpu().numpy() if hasattr(g, "detach") else np.asarray(g)
         af = (atol_frac or {}).get(n, GRAD_ELEM_ATOL_FRAC)
         rep = elementwise_check(gg, refs[n], atol_frac=af, allow=None if allow is None else allow.get(n))
+        if parts is not None:  # calibration: the violations under other accumulation allowances
+            rep["grid"] = {f"{a}sqrt+{b}": elementwise_check(gg, refs[n], atol_frac=af,
+                                                             allow=O.combine_allowance(parts, a, b)[n])["violations"]
+                           for a, b in _ACC_GRID}
+            # the largest multiple of the accumulation allowance any element needed
+            r = np.asarray(refs[n], np.float64)
+            err = np.abs(np.asarray(gg, np.float64) - r)
+            base = GRAD_ELEM_RTOL * np.abs(r) + af * float(np.max(np.abs(r)) if r.size else 0.0)
+            acc = O.combine_allowance(parts, O.ACC_SQRT, O.ACC_ULPS)[n] - parts["tie"][n]
+            over = err - base - parts["tie"][n]
+            m = over > 0
+            rep["acc_multiple_needed"] = float(np.max(over[m] / np.maximum(acc[m], 1e-300))) if m.any() else 0.0
         if rep["worst"] is not None and sc is not None and cam is not None:
             rep["context"] = gaussian_context(rep["worst"]["gaussian"], sc, cam, ref_fwd)
         _report({"case": case, "tensor": n, "ties": ties, **rep})

@@ -142,7 +142,7 @@ def test_backward_parity(name, P, W, H, seed, variant):
         assert gg.shape == rg[n].shape, n
         assert np.all(np.isfinite(gg)), n
         assert G.rel_err(gg, rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(gg, rg[n]))
-    al, ties = O.tie_allowance(os_, ref, sc.means3D, dpix, **kw)
+    al, ties = O.grad_allowance(os_, ref, sc.means3D, dpix, parts=True, **kw)
     G.assert_grads_elementwise(f"backward_{name}_{variant}", names, grads, rg, sc, cam, ref, allow=al, ties=ties)
     # the autograd wrappers' binding: the same bits, colour / covariance
     # gradients only when their precomputed input was given
@@ -340,11 +340,11 @@ def test_config2_full_size_parity_and_psnr():
              "dL_drotations"]
     for n, g in zip(names, grads):
         assert G.rel_err(g.cpu().numpy(), rg[n]) < G.GRAD_REL_TOL, (n, G.rel_err(g.cpu().numpy(), rg[n]))
-    al, ties = O.tie_allowance(os_, ref, sc.means3D, dpix, **kw)
+    al, ties = O.grad_allowance(os_, ref, sc.means3D, dpix, parts=True, **kw)
     G.assert_grads_elementwise("config2", names, grads, rg, sc, cam, ref, allow=al, ties=ties)
 
 
-@pytest.mark.parametrize("bwd_variant", [0, 1])  # the fallback and the default (opacity-scaled sums)
+@pytest.mark.parametrize("bwd_variant", [0, 1, 3])  # the fallback, the default, its late-tail form
 @pytest.mark.parametrize("fwd_variant", [0, 1])
 def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
     """The default and the fallback forward / backward blends (gs_set_tuning),

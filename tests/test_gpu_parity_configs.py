@@ -80,7 +80,7 @@ def _check_binning(C, out, ref, P, W, H, tile=16):
 
 def _check_grads(grads, rg, skip=(), case=None, sc=None, cam=None, ref=None, allow=None):
     """The norm bar on every gradient, and (with `case`) the element-wise bar
-    (allow: (oracle.tie_allowance's allowances, its counts))."""
+    (allow: (oracle.grad_allowance's allowances, its counts))."""
     for n, g in zip(GRAD_NAMES, grads):
         if n in skip:
             continue
@@ -139,7 +139,7 @@ def test_edge_case_parity(name, D, M, mod, bg):
     grads = _c_backward(s, t, out, dpix)
     assert tuple(grads[5].shape) == (P, M, 3)
     _check_grads(grads, O.backward(os_, ref, sc.means3D, dpix, **kw), case=f"edge_{name}", sc=sc, cam=cam, ref=ref,
-                 allow=O.tie_allowance(os_, ref, sc.means3D, dpix, **kw))
+                 allow=O.grad_allowance(os_, ref, sc.means3D, dpix, parts=True, **kw))
 
 
 def test_active_sh_degree_zero_through_autograd():
@@ -192,7 +192,7 @@ def test_config4_full_size(oracle_threads):
     grads = _c_backward(s, t, out, dpix)
     del out
     _check_grads(grads, O.backward(os_, ref, sc.means3D, dpix, **kw), case="config4", sc=sc, cam=cam, ref=ref,
-                 allow=O.tie_allowance(os_, ref, sc.means3D, dpix, **kw))
+                 allow=O.grad_allowance(os_, ref, sc.means3D, dpix, parts=True, **kw))
 
 
 # -------------------------------------------------------------- config 3 ---
@@ -320,12 +320,13 @@ def test_config5_eight_views_one_gpu(oracle_threads):
         os_ = O.settings_from_camera(cam)
         ref = O.forward(os_, sc.means3D, sc.opacities, **kw)
         rg = O.backward(os_, ref, sc.means3D, dpix, **kw)
-        al, ties = O.tie_allowance(os_, ref, sc.means3D, dpix, **kw)
+        al, ties = O.grad_allowance(os_, ref, sc.means3D, dpix, parts=True, **kw)
         if v == 0:  # one view alone: every gradient, both bars
             _check_grads(g, rg, case="config5_view0", sc=sc, cam=cam, ref=ref, allow=(al, ties))
         osum = ({n: rg[n].astype(np.float64) for n in pnames} if osum is None
                 else {n: osum[n] + rg[n] for n in pnames})
-        asum = ({n: al[n] for n in pnames} if asum is None else {n: asum[n] + al[n] for n in pnames})
+        asum = ({k: {n: al[k][n] for n in pnames} for k in al} if asum is None
+                else {k: {n: asum[k][n] + al[k][n] for n in pnames} for k in al})
         tsum = ties if tsum is None else {k: tsum[k] + ties[k] for k in ties}
         del ref, rg, g, al
     mv = DP.multiview_param_grads(torch.stack(recs), t["means3D"], t["shs"], 3, t["scales"], t["rotations"])
