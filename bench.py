@@ -884,9 +884,12 @@ def run_amr(ctx: Ctx, steps: int, warmup: int, extensions: bool = True) -> dict:
         diag = not ctx.args.no_profile
         el5u = float("nan")
         if diag:
-            for _ in range(max(10, warmup)):  # (its step images and sums: allocator blocks the fused frame never asks for)
-                frame_5step(fused=False)
-            torch.cuda.synchronize()
+            # (its step images and sums: allocator blocks the fused frame never
+            # asks for; a chain timed after only 10 untimed frames ran 0.4625 ms
+            # per frame over 20 frames, 0.4431 over the next 50, 0.437 from then
+            # on -- profiles/r06i_chain_frames.log: the same settling as the
+            # fused frame's)
+            settle(lambda: frame_5step(fused=False), max(10, warmup), ctx)
             t0 = time.perf_counter()
             for _ in range(steps):
                 frame_5step(fused=False)

@@ -48,13 +48,7 @@ constexpr int kPPL = 4;      // pixels per lane: one wave64 covers the 16x16 til
 // and the flush fused into the staging reduce (below).  !kSel (the fallback,
 // and the AMR backward): the predicate form, full sums by transposition into
 // LDS rows, one 64-B atomic row per (tile, Gaussian) at the end of each batch.
-// kProbe (bwd_variant 12 / 13: variant 2 / 3 instrumented): s_memtime
-// brackets around the memory waits -- the record wait at the batch head and
-// the id wait ahead of the next batch's gathers, each forced as an explicit
-// s_waitcnt with the count the compiler uses there -- and around the staging
-// reduces; per-wave sums added into g_bwd_probe (gs_debug_bwd_probe).
-__device__ unsigned long long g_bwd_probe[8];
-template <bool kSel, bool kAMR = false, bool kOpT = false, bool kLateTail = false, bool kProbe = false>
+template <bool kSel, bool kAMR = false, bool kOpT = false>
 __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
     int W, int H, const uint32_t* __restrict__ ranges, const uint32_t* __restrict__ max_contrib,
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
@@ -90,10 +84,6 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    // kProbe: cycles of the whole wave, the batch-head record waits, the id
-    // waits, the staging reduces, batches
-    long long pr_t0 = 0, pr_top = 0, pr_nid = 0, pr_red = 0, pr_nb = 0;
-    if constexpr (kProbe) pr_t0 = clock64();
     // AMR mode (kAMR, amr_mode != 0; the foveated backward, an extension beyond
     // parity): block b = (32-px tile b / 4, sub-lattice (b & 1, (b >> 1) & 1)),
     // its 16 x 16 pixels at stride 2 -- the pixels amr_render_kernel blended
@@ -247,10 +237,6 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
         nrgb[0] = colors[3 * nid]; nrgb[1] = colors[3 * nid + 1]; nrgb[2] = colors[3 * nid + 2];
         s_id[0][tid] = nid;
     }
-    // kLateTail: every batch ends with exactly one atomic behind its gathers
-    // (tail_reduce); one +0 add here gives the first batch the same, so the
-    // record waits at the loop head are exact on every path into it
-    if constexpr (kSel && kLateTail) atomicAdd(&grad_accum[(size_t)nid * kGradRow], 0.0f);
     // kSel staging reduce: lane (slot = lane / 9, value q = lane % 9) sums the
     // 16 column partials of value q parked by slot's Gaussian (za rows hold
     // values swap_sum_slot(r), zb rows 4 + swap_sum_slot(r); swap_sum_slot is
@@ -278,12 +264,6 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
     for (int top = m; top > 0; top -= kB, par ^= 1) {  // entries [top-cnt, top), back to front
         const int cnt = min(kB, top);
         __syncthreads();
-        if constexpr (kProbe) {  // vmcnt(1) behind kLateTail's tail atomic, else vmcnt(0)
-            const long long t = clock64();
-            __builtin_amdgcn_s_waitcnt(kLateTail ? 0xF71 : 0xF70);
-            pr_top += clock64() - t;
-            pr_nb++;
-        }
         uint32_t gm = 0;
         bool fastg = false;  // kSel: p2 <= 0 at every pixel of the tile, provably (below)
         if (tid < cnt) {
@@ -318,7 +298,6 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
         uint64_t written = 0;  // !kSel: batch slots whose sum rows were stored
         int nst = 0;           // kSel: staging slots in use (wave-uniform)
         uint64_t js = 0;       // kSel: batch slot j of staging slot s in bits [6 s, 6 s + 6)
-        bool tail_ot = false;  // kLateTail: the batch's run was opacity-scaled
         // kSel: the staging reduce finishes the reference's nine terms itself
         // (lane 9 s + q holds accumulator entry q of slot s's Gaussian; entries
         // 4 and 5 -- sum t dx, sum t dy -- fetched by two lane shuffles) and
@@ -327,11 +306,8 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
         // kOpT runs of fast entries sum t' = alpha T dL_dalpha / G = o t (below):
         // the flush takes o out of the mean / conic factors and divides the
         // opacity sum by it
-        auto stage_reduce = [&](const int nslot, auto kOT, const bool ot_rt = false) {
-            // (kOT: the batch's run is opacity-scaled; ot_rt: the same chosen at
-            // run time, for the late tail reduce below)
+        auto stage_reduce = [&](const int nslot, auto kOT) {
             constexpr bool kOT_ = decltype(kOT)::value;
-            const long long pr_s = kProbe ? clock64() : 0;
             if (nslot == kStageSlots || lane < 9 * nslot) {
                 const float* src = &s_stage[4 * lane];
                 const float4 a = *reinterpret_cast<const float4*>(src);
@@ -351,58 +327,18 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
                     const int fq = st_q < 3 ? st_q : st_q == 3 ? 8 : st_q - 1;
                     const float qa = (fq == 3 || fq == 4) ? g4 : tot;
                     const float4 pc = s_co[jj];
-                    const bool ot = kOT_ || ot_rt;
-                    const float o = ot ? 1.0f : pc.w;
+                    const float o = kOT_ ? 1.0f : pc.w;
                     const float cx = pc.x * (-1.0f / kHalfLog2e), cy = pc.y * (-1.0f / kLog2e),
                                 cz = pc.z * (-1.0f / kHalfLog2e);
                     const float ka = fq == 3 ? -o * cx * ddelx_dx
                                    : fq == 4 ? -o * cy * ddely_dy
                                    : (fq >= 5 && fq <= 7) ? -0.5f * o
-                                   : (ot && fq == 8) ? 1.0f / pc.w : 1.0f;
+                                   : (kOT_ && fq == 8) ? 1.0f / pc.w : 1.0f;
                     const float kb = fq == 3 ? -o * cy * ddelx_dx : fq == 4 ? -o * cz * ddely_dy : 0.0f;
                     const float v = ka * qa + kb * sy;
                     if (v != 0.f) atomicAdd(&grad_accum[(size_t)s_id[par][jj] * kGradRow + fq], v);
                 }
             }
-            if constexpr (kProbe) pr_red += clock64() - pr_s;
-        };
-        // kLateTail: the batch's last staged group (nslot 0..7), reduced by all
-        // 64 lanes into exactly one atomic instruction with the whole wave
-        // active -- the idle lanes add +0 to their slot-0 neighbour's word (a
-        // no-op: grad_accum never holds -0) -- so every path to the next
-        // batch's record wait has the same one memory operation behind the
-        // gathers and the compiler's wait for them is exact (vmcnt(1)), not
-        // vmcnt(0) behind this atomic.
-        auto tail_reduce = [&](const int nslot, const bool ot) {
-            const long long pr_s = kProbe ? clock64() : 0;
-            const bool valid = lane < 9 * nslot && lane < 63;
-            const int slot = valid ? st_slot : 0;
-            const float* src = &s_stage[4 * lane];
-            const float4 a = *reinterpret_cast<const float4*>(src);
-            const float4 b = *reinterpret_cast<const float4*>(src + kStagePitch);
-            const float4 c = *reinterpret_cast<const float4*>(src + 2 * kStagePitch);
-            const float4 d = *reinterpret_cast<const float4*>(src + 3 * kStagePitch);
-            const gs_f2 x0 = gs_f2{a.x, a.y} + gs_f2{b.x, b.y}, x1 = gs_f2{a.z, a.w} + gs_f2{b.z, b.w};
-            const gs_f2 x2 = gs_f2{c.x, c.y} + gs_f2{d.x, d.y}, x3 = gs_f2{c.z, c.w} + gs_f2{d.z, d.w};
-            const gs_f2 y = (x0 + x1) + (x2 + x3);
-            const uint32_t jj = (uint32_t)(js >> (6 * slot)) & 63u;
-            const float tot = y.x + y.y;
-            const float g4 = __shfl(tot, 9 * st_slot + 4, 64), sy = __shfl(tot, 9 * st_slot + 5, 64);
-            const int q = valid ? st_q : st_q % 9;
-            const int fq = q < 3 ? q : q == 3 ? 8 : q - 1;
-            const float qa = (fq == 3 || fq == 4) ? g4 : tot;
-            const float4 pc = s_co[jj];
-            const float o = ot ? 1.0f : pc.w;
-            const float cx = pc.x * (-1.0f / kHalfLog2e), cy = pc.y * (-1.0f / kLog2e),
-                        cz = pc.z * (-1.0f / kHalfLog2e);
-            const float ka = fq == 3 ? -o * cx * ddelx_dx
-                           : fq == 4 ? -o * cy * ddely_dy
-                           : (fq >= 5 && fq <= 7) ? -0.5f * o
-                           : (ot && fq == 8) ? 1.0f / pc.w : 1.0f;
-            const float kb = fq == 3 ? -o * cy * ddelx_dx : fq == 4 ? -o * cz * ddely_dy : 0.0f;
-            const float v = valid ? ka * qa + kb * sy : 0.0f;
-            atomicAdd(&grad_accum[(size_t)s_id[par][jj] * kGradRow + fq], v);
-            if constexpr (kProbe) pr_red += clock64() - pr_s;
         };
         __syncthreads();
         // first batch slot this wave needs: contributor = top-1-j < wave_last
@@ -592,22 +528,17 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
                     one(std::integral_constant<int, 4>{});
                     one(std::integral_constant<int, 5>{});
                     one(std::integral_constant<int, 6>{});
-                    // (kLateTail: the batch's last group is reduced after the
-                    // next batch's gathers are issued, below)
-                    if (nst == kStageSlots && (!kLateTail || todo)) {
+                    if (nst == kStageSlots) {
                         stage_reduce(kStageSlots, std::integral_constant<bool, kOpT && decltype(kFastT)::value>{});
                         nst = 0;
                         js = 0ull;
                     }
                 }
-                if constexpr (!kLateTail) {
-                    if (nst) stage_reduce(nst, std::integral_constant<bool, kOpT && decltype(kFastT)::value>{});
-                    nst = 0;
-                }
+                if (nst) stage_reduce(nst, std::integral_constant<bool, kOpT && decltype(kFastT)::value>{});
+                nst = 0;
             };
             // every entry this wave visits has a provably negative-definite form
             const bool bsafe = (todo & ~fast_mask) == 0ull;
-            tail_ot = kOpT && bsafe;
             if (bsafe && bstarted) run(T1{}, T1{});
             else if (bsafe) run(T1{}, T0{});
             else run(T0{}, T0{});
@@ -622,24 +553,11 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
             }
         }
         __syncthreads();
-        if constexpr (kProbe) {
-            const long long t = clock64();
-            __builtin_amdgcn_s_waitcnt(0xF70);
-            pr_nid += clock64() - t;
-        }
         if (has_next) {  // gathers for the next batch, ahead of the flush atomics
             s_id[par ^ 1][tid] = nid;
             nxy = means2D[nid];
             nco = conic_opacity[nid];
             nrgb[0] = colors[3 * nid]; nrgb[1] = colors[3 * nid + 1]; nrgb[2] = colors[3 * nid + 2];
-        }
-        if constexpr (kSel && kLateTail) {
-            // The batch's last staged group, reduced behind the gathers: the
-            // wait for the next ids above (issued at the top of this batch, so
-            // vmcnt(0) behind every atomic issued since) then covers no atomic
-            // issued in the batch's last group, and the group's atomics are
-            // outstanding during the next batch's record wait instead.
-            tail_reduce(nst, tail_ot);
         }
         if constexpr (!kSel) {
             // Flush: 16 lanes per Gaussian row, 4 rows per wave instruction
@@ -669,26 +587,6 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
             }
         }
     }
-    if constexpr (kProbe) {
-        const long long pr_all = clock64() - pr_t0;
-        if (lane == 0) {
-            atomicAdd(&g_bwd_probe[0], (unsigned long long)pr_all);
-            atomicAdd(&g_bwd_probe[1], (unsigned long long)pr_top);
-            atomicAdd(&g_bwd_probe[2], (unsigned long long)pr_nid);
-            atomicAdd(&g_bwd_probe[3], (unsigned long long)pr_red);
-            atomicAdd(&g_bwd_probe[4], (unsigned long long)pr_nb);
-            atomicAdd(&g_bwd_probe[5], 1ull);
-        }
-    }
-}
-
-int debug_bwd_probe(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_probe), sizeof(g_bwd_probe)) != hipSuccess) return -1;
-    if (reset) {
-        static const unsigned long long zero[8] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_probe), zero, sizeof(zero)) != hipSuccess) return -1;
-    }
-    return 0;
 }
 
 extern int g_cull;  // render.hip
@@ -713,9 +611,7 @@ extern int g_cull;  // render.hip
 // diagnostics.
 constexpr int kDefaultBwdVariant = 2;
 int g_bwd_variant = kDefaultBwdVariant;
-void set_backward_variant(int v) {
-    g_bwd_variant = v == 0 || v == 3 || v == 12 || v == 13 ? v : kDefaultBwdVariant;
-}
+void set_backward_variant(int v) { g_bwd_variant = v == 0 ? 0 : kDefaultBwdVariant; }
 
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s, int K) {
@@ -734,9 +630,6 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
                        dL_dpix, bg, g.grad_accum, g_cull, gx, 0, nullptr, img.bucket_count, img.bucket_list,       \
                        g.hdr)
     if (g_bwd_variant == 0) GS_BWD_LAUNCH(false);
-    else if (g_bwd_variant == 3) GS_BWD_LAUNCH(true, false, true, true);
-    else if (g_bwd_variant == 12) GS_BWD_LAUNCH(true, false, true, false, true);
-    else if (g_bwd_variant == 13) GS_BWD_LAUNCH(true, false, true, true, true);
     else GS_BWD_LAUNCH(true, false, true);
 #undef GS_BWD_LAUNCH
 }

@@ -1286,10 +1286,6 @@ int gs_set_tuning(const char* key, int value) {
         set_backward_variant(value);
         return 0;
     }
-    if (std::strcmp(key, "mv_variant") == 0) {  // 1: one-pass multi-view backward; else two phases (2 / 3 waves)
-        set_multiview_variant(value);
-        return 0;
-    }
     if (std::strcmp(key, "amr_variant") == 0) {  // 0: full-list AMR blocks; else region sub-lists (default)
         set_amr_variant(value);
         return 0;
@@ -1326,7 +1322,7 @@ int gs_get_tuning(const char* key, int* value) {
     const struct { const char* k; const int* v; } table[] = {
         {"fwd_variant", &g_fwd_variant}, {"bwd_variant", &g_bwd_variant}, {"amr_variant", &g_amr_variant},
         {"sort_algo", &g_sort_algo},     {"cull", &g_cull},               {"hdr_mirror", &g_hdr_mirror},
-        {"spec_dup", &g_spec_dup},       {"ritnet_mfma", &g_ritnet_mfma}, {"mv_variant", &g_mv_variant}};
+        {"spec_dup", &g_spec_dup},       {"ritnet_mfma", &g_ritnet_mfma}};
     for (const auto& e : table)
         if (std::strcmp(key, e.k) == 0) {
             *value = *e.v;
@@ -1334,15 +1330,6 @@ int gs_get_tuning(const char* key, int* value) {
         }
     g_err = std::string("unknown tuning key ") + key;
     return -1;
-}
-
-int gs_debug_bwd_probe(unsigned long long* out, int reset) {
-    if (!out) return -1;
-    if (debug_bwd_probe(out, reset) != 0) {
-        g_err = "gs_debug_bwd_probe: HIP error";
-        return -1;
-    }
-    return 0;
 }
 
 int gs_set_thread_option(const char* key, int value) {

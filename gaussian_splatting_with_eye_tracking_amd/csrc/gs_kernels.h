@@ -108,7 +108,6 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
 // Tuning knobs (gs_set_tuning): the default or one fallback each.
 void set_forward_variant(int v);
 void set_backward_variant(int v);
-int debug_bwd_probe(unsigned long long* out, int reset);  // backward.hip (gs_debug_bwd_probe)
 void set_amr_variant(int v);
 void set_cull(int v);  // row-group cull in the blend kernels (default on)
 void set_ritnet_mfma(int v);
@@ -180,8 +179,6 @@ void launch_pack_view_grads(int P, const GeomView& g, const int* radii, bool has
                             const float* projmatrix, const float* campos, int width, int height, float tan_fovx,
                             float tan_fovy, float* out, hipStream_t s);
 void launch_multiview_backward(const MultiViewArgs& a, hipStream_t s);
-extern int g_mv_variant;  // multiview.hip
-void set_multiview_variant(int v);
 
 // Eye-tracking front end (ritnet.hip): RITnet DenseNet2D building blocks.
 void launch_ritnet_conv(int k, const float* const* in_ptr, const int* in_c, const int* in_up, int nseg, int H, int W,

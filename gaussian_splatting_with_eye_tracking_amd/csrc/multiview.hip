@@ -350,180 +350,6 @@ __global__ void __launch_bounds__(kMvT) multiview_backward1_kernel(MultiViewArgs
     }
 }
 
-// Two phases per Gaussian (degree-3 SH, V <= kMvStash views): the geometry
-// terms over the views first (cov2D / projection / opacity / statistics, the
-// rows staged through LDS as above), each visible view's masked dL/drgb
-// parked in LDS; then the SH terms over the same views with the Gaussian's
-// 48 coefficients in registers.  The one-pass form keeps the geometry state,
-// the SH accumulators and the staged SH rows live at once (202 VGPRs and
-// 15 KB of LDS: 2 waves per SIMD); here the phases' live sets do not overlap
-// (VGPRs: the larger of the two; LDS: rows 2.5 KB + parked dL/drgb 6 KB).
-// Same sums in the same view order as multiview_backward1_kernel.
-// (kWaves: the occupancy asked of the register allocator -- 3 fits without
-// spills, 4 spills part of phase 2's live set)
-constexpr int kMvStash = 8;
-template <int kWaves>
-__global__ void __launch_bounds__(kMvT) __attribute__((amdgpu_waves_per_eu(kWaves)))
-multiview_backward2_kernel(MultiViewArgs a) {
-    __shared__ __attribute__((aligned(16))) float s_rows[kMvT * kViewRow];
-    __shared__ float s_drgb[kMvStash * 3 * kMvT];  // [view][channel][thread]
-    const int tid = threadIdx.x;
-    const int local0 = blockIdx.x * kMvT;
-    const int nblk = min(kMvT, a.count - local0);
-    const int local = local0 + tid;
-    const bool live = local < a.count;
-    const int idx = a.g0 + local;
-    const int nf2 = nblk * (kViewRow / 2);
-    auto load_rows = [&](int v, float2 (&r)[kMvRowPer]) {
-        const float2* src = reinterpret_cast<const float2*>(mv_row(a, v) + (size_t)local0 * kViewRow);
-#pragma unroll
-        for (int i = 0; i < kMvRowPer; i++) {
-            const int f = tid + kMvT * i;
-            if (f < nf2) {
-                typedef float f2v __attribute__((ext_vector_type(2)));
-                const f2v t = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(src + f));
-                r[i] = make_float2(t.x, t.y);
-            } else {
-                r[i] = make_float2(0.f, 0.f);
-            }
-        }
-    };
-    float mx = 0.f, my = 0.f, mz = 0.f;
-    float4 qrot = make_float4(0.f, 0.f, 0.f, 0.f);
-    float scl[3] = {0.f, 0.f, 0.f}, cov3D[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float st_acc = 0.f, st_den = 0.f, st_max = 0.f;
-    const bool stats = a.grad_norm_accum != nullptr;
-    if (live) {
-        mx = a.means3D[3 * idx];
-        my = a.means3D[3 * idx + 1];
-        mz = a.means3D[3 * idx + 2];
-        qrot = reinterpret_cast<const float4*>(a.rotations)[idx];
-        scl[0] = a.scales[3 * idx + 0];
-        scl[1] = a.scales[3 * idx + 1];
-        scl[2] = a.scales[3 * idx + 2];
-        if (stats) {
-            st_acc = a.grad_norm_accum[idx];
-            st_den = a.denom[idx];
-            st_max = a.max_radii[idx];
-        }
-    }
-    compute_cov3d(scl, qrot, a.scale_modifier, cov3D);
-    float dmean_t[3] = {0.f, 0.f, 0.f};
-    float dcov_t[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, dop = 0.f;
-    uint32_t vis = 0;  // views that see this Gaussian
-    // ---- phase 1: geometry terms
-    float2 nxt[kMvRowPer];
-    load_rows(0, nxt);
-    for (int v = 0; v < a.V; v++) {
-        __syncthreads();  // the previous view's rows are read
-        float2* srow = reinterpret_cast<float2*>(s_rows);
-#pragma unroll
-        for (int i = 0; i < kMvRowPer; i++) {
-            const int f = tid + kMvT * i;
-            if (f < kMvRowF2) srow[f] = nxt[i];
-        }
-        __syncthreads();
-        if (v + 1 < a.V) load_rows(v + 1, nxt);
-        const float* row = s_rows + tid * kViewRow;
-        const uint32_t w9 = __float_as_uint(row[9]);
-        if (!live || w9 == 0u) continue;
-        vis |= 1u << v;
-        const uint8_t cb = (uint8_t)(w9 >> 24);
-#pragma unroll
-        for (int c = 0; c < 3; c++) s_drgb[(3 * v + c) * kMvT + tid] = row[c] * (((cb >> c) & 1) ? 0.0f : 1.0f);
-        const float gx = row[3], gy = row[4], dcx = row[5], dcy = row[6], dcw = row[7], dop_v = row[8];
-        const ConstF cam = uniform_const(mv_cam(a, v));
-        Mat4 V, Pm;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-            V.m[i] = cam[i];
-            Pm.m[i] = cam[16 + i];
-        }
-        const float tan_fovx = cam[37], tan_fovy = cam[38];
-        const float focal_x = cam[35] / (2.0f * tan_fovx);
-        const float focal_y = cam[36] / (2.0f * tan_fovy);
-        float dmean[3], dcov[6];
-        cov2d_backward(mx, my, mz, cov3D, dcx, dcy, dcw, V, focal_x, focal_y, tan_fovx, tan_fovy, dmean, dcov);
-        proj_backward(mx, my, mz, Pm, gx, gy, dmean);
-#pragma unroll
-        for (int i = 0; i < 3; i++) dmean_t[i] += dmean[i];
-#pragma unroll
-        for (int i = 0; i < 6; i++) dcov_t[i] += dcov[i];
-        dop += dop_v;
-        if (stats) {
-            st_acc = st_acc + sqrtf(gx * gx + gy * gy);
-            st_den = st_den + 1.f;
-            st_max = fmaxf(st_max, (float)(w9 & 0xFFFFFFu));
-        }
-    }
-    const bool any = vis != 0u;
-    if (live) {
-        a.dL_dopacity[idx] = any ? dop : 0.f;
-        float dscale[3] = {0.f, 0.f, 0.f};
-        float4 dq = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (any) cov3d_backward(qrot, scl, a.scale_modifier, dcov_t, dscale, dq);
-#pragma unroll
-        for (int i = 0; i < 3; i++) a.dL_dscale[3 * idx + i] = dscale[i];
-        reinterpret_cast<float4*>(a.dL_drot)[idx] = dq;
-        if (stats && any) {
-            a.grad_norm_accum[idx] = st_acc;
-            a.denom[idx] = st_den;
-            a.max_radii[idx] = st_max;
-        }
-    }
-    // ---- phase 2: SH terms, coefficients in registers
-    const int ncoef = min((a.D + 1) * (a.D + 1), a.M);
-    float s_reg[16][3];
-    {
-        const float4* in = reinterpret_cast<const float4*>(a.shs) + (size_t)(live ? idx : a.g0) * 12;
-        float f[48];
-#pragma unroll
-        for (int k = 0; k < 12; k++) {
-            const float4 t = any ? ldg4<true>(in + k) : make_float4(0.f, 0.f, 0.f, 0.f);
-            f[4 * k] = t.x; f[4 * k + 1] = t.y; f[4 * k + 2] = t.z; f[4 * k + 3] = t.w;
-        }
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) s_reg[k][c] = k < ncoef ? f[3 * k + c] : 0.f;
-    }
-    float dsh_t[48];
-#pragma unroll
-    for (int i = 0; i < 48; i++) dsh_t[i] = 0.f;
-    float ddir[3] = {0.f, 0.f, 0.f};
-    for (int v = 0; v < a.V; v++) {
-        if (!((vis >> v) & 1u)) continue;
-        const ConstF cam = uniform_const(mv_cam(a, v));
-        const float campos[3] = {cam[32], cam[33], cam[34]};
-        const float acc[3] = {s_drgb[(3 * v) * kMvT + tid], s_drgb[(3 * v + 1) * kMvT + tid],
-                              s_drgb[(3 * v + 2) * kMvT + tid]};
-        float dsh_c[16], dRGB[3];
-        mv_sh_terms(a.D, campos, mx, my, mz, s_reg, 0, acc, dsh_c, dRGB, ddir);
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) dsh_t[3 * k + c] += dsh_c[k] * dRGB[c];
-    }
-    if (live) {
-#pragma unroll
-        for (int i = 0; i < 3; i++) a.dL_dmean3D[3 * idx + i] = any ? dmean_t[i] + ddir[i] : 0.f;
-        float4* out = reinterpret_cast<float4*>(a.dL_dsh) + (size_t)idx * 12;
-#pragma unroll
-        for (int k = 0; k < 12; k++) {
-            float o[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) o[j] = (any && 4 * k + j < 3 * ncoef) ? dsh_t[4 * k + j] : 0.f;
-            store_out4(&out[k], make_float4(o[0], o[1], o[2], o[3]), a.nt != 0);
-        }
-    }
-}
-
-// set_tuning("mv_variant"): 1 = the one-pass kernel; 2 / 3 = two phases
-// (where they apply: degree-3 SH, V <= kMvStash) at 3 / 4 waves per SIMD
-constexpr int kDefaultMvVariant = 1;
-int g_mv_variant = kDefaultMvVariant;
-void set_multiview_variant(int v) { g_mv_variant = v >= 1 && v <= 3 ? v : kDefaultMvVariant; }
-
 void launch_multiview_backward(const MultiViewArgs& args, hipStream_t s) {
     if (args.count <= 0) return;
     MultiViewArgs a = args;
@@ -536,11 +362,7 @@ void launch_multiview_backward(const MultiViewArgs& args, hipStream_t s) {
     // 8-view step at config 5, profiles/r05d_bench_cfg5_roles.log: the
     // per-view barrier waits on the geometry wave and the channel waves redo
     // the direction and basis; removed.)
-    if (sh && a.M == 16 && a.V <= kMvStash && g_mv_variant == 2)
-        hipLaunchKernelGGL(multiview_backward2_kernel<3>, grid, dim3(kMvT), 0, s, a);
-    else if (sh && a.M == 16 && a.V <= kMvStash && g_mv_variant == 3)
-        hipLaunchKernelGGL(multiview_backward2_kernel<4>, grid, dim3(kMvT), 0, s, a);
-    else if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward1_kernel<true, true>), grid, dim3(kMvT), 0, s, a);
+    if (sh && a.M == 16) hipLaunchKernelGGL((multiview_backward1_kernel<true, true>), grid, dim3(kMvT), 0, s, a);
     else if (sh) hipLaunchKernelGGL((multiview_backward1_kernel<true, false>), grid, dim3(kMvT), 0, s, a);
     else hipLaunchKernelGGL((multiview_backward1_kernel<false, false>), grid, dim3(kMvT), 0, s, a);
 }

@@ -430,33 +430,20 @@ void gs_profile_set_mask(unsigned mask);
 /* Process-wide performance choices for A/B measurements, each the default
  * or one fallback (every pair gives the same results): "fwd_variant" (0 = one
  * wave x 4 px/lane predicate form; else the default 4 waves x 1 px/lane select
- * form), "bwd_variant" (0 = predicate form with LDS-row sums; 3 = the
- * default with each batch's last staged group reduced behind the next
- * batch's gathers; 12 / 13 = the default / 3 instrumented, see
- * gs_debug_bwd_probe; else the default select form with staged sums),
- * "amr_variant" (0 = full-list AMR
+ * form), "bwd_variant" (0 = predicate form with LDS-row sums; else the
+ * default select form with staged sums), "amr_variant" (0 = full-list AMR
  * blocks; else the default 8x8 region sub-lists), "sort_algo" (0 = bitonic
  * networks only; 1 = per-tile bucket sort, the default), "cull" (1 = skip
  * Gaussians whose alpha >= 1/255 ellipse misses a 16x4 row group, the
  * default; 0 only to verify that the cull is exact), "hdr_mirror" (2 = the
  * polled K read-back, the default; 0 = copy + event), "spec_dup" (1 = the
  * speculative duplicate before the K read-back, the default), "ritnet_mfma"
- * (1 = matrix-core convolutions, the default; 0 = SGPR-weight FMA kernel),
- * "mv_variant" (1 = the one-pass multi-view backward, the default; 2 / 3 =
- * two phases, geometry then SH, at 3 / 4 waves per SIMD).
+ * (1 = matrix-core convolutions, the default; 0 = SGPR-weight FMA kernel).
  * Returns 0, or -1 for an unknown key. */
 int gs_set_tuning(const char* key, int value);
 /* The current value of a gs_set_tuning key into *value (0 = the fallback
  * variant); -1 for an unknown key. */
 int gs_get_tuning(const char* key, int* value);
-/* Diagnostics of the blend backward's instrumented forms ("bwd_variant" 12
- * and 13: the default and its late-tail form, 3, with s_memtime brackets):
- * copies the 8 device-side sums into out -- [0] cycles of every wave, [1] in
- * the record waits at the batch heads, [2] in the id waits ahead of the next
- * batch's gathers, [3] in the staging reduces, [4] batches, [5] waves -- and
- * zeroes them when reset != 0.  Synchronous.  Returns 0, or -1 on a HIP
- * error.  (Not part of the reference's interface.) */
-int gs_debug_bwd_probe(unsigned long long* out, int reset);
 /* Per-call options of the calling thread's forwards (thread-local): "fwd_zero"
  * (1 = the forward render zeroes the backward's accumulator rows, default),
  * "sh_drgb" (1 = the preprocess stores d(rgb)/d(view dir) for the SH

@@ -81,48 +81,6 @@ def test_multiview_equals_sum_of_view_backwards(yaws, deg):
     np.testing.assert_array_equal(stats[2].cpu().numpy(), stats_ref[2].cpu().numpy())
 
 
-@pytest.mark.parametrize("nviews", [5, 8, 9])
-def test_multiview_variants_agree(nviews):
-    """The two-phase multi-view backward (geometry over the views, then SH
-    with the coefficients in registers; mv_variant 2 = 3 waves per SIMD, the
-    default, 3 = 4 waves) against the one-pass kernel (1): the same sums in
-    the same view order -- equal to the float-contraction noise of two
-    compilations, the view counts and radii bit for bit.  (9 views: beyond the two-phase
-    stash, every variant takes the one-pass kernel.)"""
-    import gaussian_splatting_with_eye_tracking_amd._C as C
-    from gaussian_splatting_with_eye_tracking_amd import data_parallel as DP
-    from gaussian_splatting_with_eye_tracking_amd import synthetic as S
-    P, W, H = 20000, 256, 192
-    yaws = tuple(-12.0 + 3.0 * v for v in range(nviews))
-    sc, cams = _views(P, W, H, yaws)
-    t = G.scene_tensors(sc)
-    records = []
-    for v, cam in enumerate(cams):
-        s = G.torch_settings(cam)
-        dpix = torch.from_numpy(S.make_cotangent(H, W, 10 + v)).cuda()
-        fwd = _forward(C, s, t, 3)
-        records.append(DP.view_record(s, fwd[2], fwd[3], fwd[0], fwd[4], fwd[5], dpix))
-    views = torch.stack(records)
-    res = {}
-    try:
-        for mv in (1, 2, 3):
-            C.set_tuning("mv_variant", mv)
-            stats = tuple(torch.zeros(P, device="cuda") for _ in range(3))
-            got = DP.multiview_param_grads(views, t["means3D"], t["shs"], 3, t["scales"], t["rotations"], 1.0,
-                                           stats=stats)
-            torch.cuda.synchronize()
-            res[mv] = ([g.cpu().numpy() for g in got], [x.cpu().numpy() for x in stats])
-    finally:
-        C.set_tuning("mv_variant", -1)
-    for mv in (2, 3):
-        for i, (a, b) in enumerate(zip(res[mv][0], res[1][0])):
-            assert np.isfinite(a).all(), (mv, i)
-            assert G.rel_err(a, b) < 1e-6, (mv, i)
-        assert G.rel_err(res[mv][1][0], res[1][1][0]) < 1e-6, mv  # sum of |dL/dmean2D| (contractions may differ)
-        np.testing.assert_array_equal(res[mv][1][1], res[1][1][1])
-        np.testing.assert_array_equal(res[mv][1][2], res[1][1][2])
-
-
 def test_view_record_layout():
     """Word 9 = radius | clamped << 24, zero rows for invisible Gaussians, and
     the 40 camera words closing the record."""

@@ -37,6 +37,22 @@ fns = {"fused": lambda: RA.render_steps(*a, st, fused=True), "chain": lambda: RA
        "inline": inline,
        "once": lambda: RA.GaussianRasterizer(st)(means3D=a[0], means2D=a[1], opacities=a[4], shs=a[2], scales=a[5],
                                                  rotations=a[6], foveaStep=-2, interpolate_image=True)}
+if sys.argv[1:2] == ["frames"]:
+    # the bench's order (fused frames, then 10 chain frames, then timed chains
+    # of growing length): the fixed per-measurement overhead is the intercept
+    with torch.no_grad():
+        for _ in range(100):
+            fns["fused"]()
+        for _ in range(10):
+            fns["chain"]()
+        for n in (20, 50, 100, 20, 50, 100):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                fns["chain"]()
+            torch.cuda.synchronize()
+            print("chain", n, "%.4f ms/frame" % ((time.perf_counter() - t0) / n * 1e3), flush=True)
+    sys.exit(0)
 want = sys.argv[1:] or list(fns)
 fns = {k: v for k, v in fns.items() if k in want}
 with torch.no_grad():

@@ -82,13 +82,7 @@ for step in "$@"; do
       run "${step}_$c" 300 rocprofv3 --pmc $cnt --kernel-trace -d "gpurun_out/${step}_$c" -o run --output-format csv -- python3 bench.py --config "$c" --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-sub --no-ext ;;
     elem) GS_ELEM_SOFT=1 GS_ELEM_REPORT="$O/elem.jsonl" run pytest_elem 900 python -u -m pytest tests/test_gpu_parity_configs.py tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf -k "config2 or config4 or config5 or backward_parity or edge_case" ;;
     chaintime) run chain_timing 300 python tools/amr_chain_timing.py ;;
-    bwdprobe) run bwd_probe 300 python tools/bwd_probe.py --out "$O/bwd_probe_cfg2.json" &&
-      run bwd_probe4 400 python tools/bwd_probe.py --P 6100000 --W 1600 --H 1063 --iters 10 --out "$O/bwd_probe_cfg4.json" ;;
-    abbwd) run ab_bwd3_cfg2 400 python tools/ab_tuning.py --key bwd_variant --values 2 3 --stage render_bwd --backward --rounds 10 &&
-      run ab_bwd3_cfg4 500 python tools/ab_tuning.py --key bwd_variant --values 2 3 --stage render_bwd --backward --rounds 6 --P 6100000 --W 1600 --H 1063 ;;
-    abmv) GSAMD_TUNING=mv_variant=1 run bench_cfg5_mv1 400 python bench.py --config cfg5_8view_1080p_1M --steps 20 --warmup 5 --no-cpu-baseline &&
-      GSAMD_TUNING=mv_variant=2 run bench_cfg5_mv2 400 python bench.py --config cfg5_8view_1080p_1M --steps 20 --warmup 5 --no-cpu-baseline &&
-      GSAMD_TUNING=mv_variant=3 run bench_cfg5_mv3 400 python bench.py --config cfg5_8view_1080p_1M --steps 20 --warmup 5 --no-cpu-baseline ;;
+    chainframes) run chain_frames 300 python tools/amr_chain_timing.py frames ;;
     mvtests) run pytest_mv2 600 python -u -m pytest tests/test_gpu_multiview.py tests/test_gpu_parity_configs.py -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf -k "multiview or config5" ;;
     bwdtests) run pytest_bwd3 600 python -u -m pytest tests/test_gpu_cull.py tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf -k "default_backward_matches_fallback or blend_geometries" ;;
     spec) run pytest_spec 600 python -u -m pytest tests/test_gpu_amr_speculation.py tests/test_gpu_capi_ctypes.py tests/test_renderer_amr.py -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf ;;
