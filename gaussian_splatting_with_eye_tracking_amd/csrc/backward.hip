@@ -48,7 +48,7 @@ constexpr int kPPL = 4;      // pixels per lane: one wave64 covers the 16x16 til
 // and the flush fused into the staging reduce (below).  !kSel (the fallback,
 // and the AMR backward): the predicate form, full sums by transposition into
 // LDS rows, one 64-B atomic row per (tile, Gaussian) at the end of each batch.
-template <bool kSel, bool kAMR = false, bool kOpT = false, bool kPk = false>
+template <bool kSel, bool kAMR = false, bool kOpT = false>
 __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
     int W, int H, const uint32_t* __restrict__ ranges, const uint32_t* __restrict__ max_contrib,
     const uint32_t* __restrict__ point_list, const float2* __restrict__ means2D,
@@ -251,25 +251,15 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
     // q = v except s2 (v = 6) -> q = 8; g6 (q = 6) = dx x (g4's column
     // partial), formed after the transposition by lanes 0-15 (zb row 0 = g4),
     // the other lanes' product into their dummy word: no ninth-value DPP tree.
-    // kPk: the visit hands the transposition (c0, s0, c2, dx s0, c1, s1, s2,
-    // dx s1) instead -- the register pairs its packed adds take, values (i, i +
-    // 4), are then the visit's packed accumulators (c0, c1), (s0, s1) and the
-    // packed product dx (s0, s1), no moves -- so za row r holds q = 0, 2, 3, 4
-    // and zb row r q = 1, 8, 5, 7, and the dx s0 row is za's row 3.
-    const int st_r = lane >> 4;
-    const int st_dst = ((lane & 15) >> 2) * kStagePitch +
-                       4 * (kPk ? (st_r == 0 ? 0 : st_r + 1) : swap_sum_slot(st_r)) + (lane & 3);
+    const int st_dst = ((lane & 15) >> 2) * kStagePitch + 4 * swap_sum_slot(lane >> 4) + (lane & 3);
     const int st_dst_b = [&] {
-        const int v = 4 + swap_sum_slot(st_r);
-        const int q = kPk ? (st_r == 0 ? 1 : st_r == 1 ? 8 : st_r == 2 ? 5 : 7) : (v == 6 ? 8 : v);
-        return ((lane & 15) >> 2) * kStagePitch + 4 * q + (lane & 3);
+        const int v = 4 + swap_sum_slot(lane >> 4);
+        return ((lane & 15) >> 2) * kStagePitch + 4 * (v == 6 ? 8 : v) + (lane & 3);
     }();
-    // (the idle lanes -- 16-63, kPk 0-47 -- store into the 16-word pads of
-    // pitch rows 0-2, which the reduce never reads)
-    const int st_g6_lane = kPk ? 48 : 0;  // first lane of the dx s0 row
-    const int st_g6 = (lane >= st_g6_lane && lane < st_g6_lane + 16)
-                          ? ((lane & 15) >> 2) * kStagePitch + 4 * 6 + (lane & 3)
-                          : ((kPk ? lane : lane - 16) >> 4) * kStagePitch + 256 + (lane & 15);
+    // (the idle lanes 16-63 store into the 16-word pads of pitch rows 0-2,
+    // which the reduce never reads)
+    const int st_g6 = lane < 16 ? ((lane & 15) >> 2) * kStagePitch + 4 * 6 + (lane & 3)
+                                : ((lane - 16) >> 4) * kStagePitch + 256 + (lane & 15);
     int par = 0;
     for (int top = m; top > 0; top -= kB, par ^= 1) {  // entries [top-cnt, top), back to front
         const int cnt = min(kB, top);
@@ -388,8 +378,6 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
             // fma(a, b, -0) / -0 + t fold to a plain v_mul / move instead of a
             // 3-operand fma with an inline 0)
             float c0 = -0.f, c1 = -0.f, c2 = -0.f, s0 = -0.f, s1 = -0.f, s2 = -0.f;
-            // kPk: (c0, c1) and (s0, s1) as packed pairs, one v_pk_fma_f32 each
-            gs_f2 c01 = gs_f2{-0.f, -0.f}, s01 = gs_f2{-0.f, -0.f};
             bool any = false;
             if constexpr (kSel) {
                 // The select form: a rejected pixel takes alpha = G = 0, i.e.
@@ -429,19 +417,13 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
                                                       __builtin_fmaf(cf.y, dpx[k][1],
                                                                      __builtin_fmaf(cf.x, dpx[k][0], -acc_dot[k])));
                     acc_dot[k] = __builtin_fmaf(alpha, diff, acc_dot[k]);
+                    c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
+                    c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
+                    c2 = __builtin_fmaf(dchannel_dcolor, dpx[k][2], c2);
                     const float t = kOT ? dchannel_dcolor * diff : G * (diff * T[k]);
                     const float tdy = t * dy;
-                    if constexpr (kPk) {
-                        c01 = __builtin_elementwise_fma(gs_f2{dchannel_dcolor, dchannel_dcolor},
-                                                        gs_f2{dpx[k][0], dpx[k][1]}, c01);
-                        s01 = __builtin_elementwise_fma(gs_f2{t, t}, gs_f2{1.0f, dy}, s01);
-                    } else {
-                        c0 = __builtin_fmaf(dchannel_dcolor, dpx[k][0], c0);
-                        c1 = __builtin_fmaf(dchannel_dcolor, dpx[k][1], c1);
-                        s0 += t;
-                        s1 += tdy;
-                    }
-                    c2 = __builtin_fmaf(dchannel_dcolor, dpx[k][2], c2);
+                    s0 += t;
+                    s1 += tdy;
                     s2 = __builtin_fmaf(tdy, dy, s2);
                 }
                 any = true;
@@ -483,30 +465,24 @@ __global__ void __launch_bounds__(64, 4) render_bwd_kernel(
                 }
             }
             float g[kNG];
-            if constexpr (kPk) {  // (the pair order, st_dst above)
-                const gs_f2 dxs = gs_f2{dx, dx} * s01;
-                g[0] = c01.x; g[1] = s01.x; g[2] = c2; g[3] = dxs.x;
-                g[4] = c01.y; g[5] = s01.y; g[6] = s2; g[7] = dxs.y;
-            } else {
-                g[0] = c0;
-                g[1] = c1;
-                g[2] = c2;
-                g[3] = s0;
-                g[4] = dx * s0;
-                g[5] = s1;
-                g[6] = kSel ? s2 : dx * g[4];
-                g[7] = dx * s1;
-            }
+            g[0] = c0;
+            g[1] = c1;
+            g[2] = c2;
+            g[3] = s0;
+            g[4] = dx * s0;
+            g[5] = s1;
+            g[6] = kSel ? s2 : dx * g[4];
+            g[7] = dx * s1;
             g[8] = s2;
             if constexpr (kSel) {
-                // s2 rides in the 8-value transposition (dx^2 s0 leaves it; its
-                // column partials are dx x dx s0's, formed after it)
+                // s2 rides in the 8-value transposition (g6 = dx^2 s0 leaves it;
+                // g6's column partials are dx x g4's, formed after it)
                 float za, zb;
                 swap_rows8_pk_t<false>(g, za, zb);
-                const float w6 = dx * (kPk ? za : zb);
+                const float w6 = dx * zb;
                 s_stage[st_dst + 36 * kSlot] = za;
                 s_stage[st_dst_b + 36 * kSlot] = zb;
-                s_stage[st_g6 + ((lane >= st_g6_lane && lane < st_g6_lane + 16) ? 36 * kSlot : 0)] = w6;
+                s_stage[st_g6 + (lane < 16 ? 36 * kSlot : 0)] = w6;
                 js |= (uint64_t)j << (6 * kSlot);
             } else if (__ballot(any) != 0ull) {  // wave-uniform
                 // full sums by transposition: 2 values per row leader + g8 in lane 63
@@ -635,7 +611,7 @@ extern int g_cull;  // render.hip
 // diagnostics.
 constexpr int kDefaultBwdVariant = 2;
 int g_bwd_variant = kDefaultBwdVariant;
-void set_backward_variant(int v) { g_bwd_variant = v == 0 || v == 3 ? v : kDefaultBwdVariant; }
+void set_backward_variant(int v) { g_bwd_variant = v == 0 ? 0 : kDefaultBwdVariant; }
 
 void launch_render_backward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                             const float* colors, const float* bg, const float* dL_dpix, hipStream_t s, int K) {
@@ -654,7 +630,6 @@ void launch_render_backward(int W, int H, const ImageView& img, const BinningVie
                        dL_dpix, bg, g.grad_accum, g_cull, gx, 0, nullptr, img.bucket_count, img.bucket_list,       \
                        g.hdr)
     if (g_bwd_variant == 0) GS_BWD_LAUNCH(false);
-    else if (g_bwd_variant == 3) GS_BWD_LAUNCH(true, false, true, true);
     else GS_BWD_LAUNCH(true, false, true);
 #undef GS_BWD_LAUNCH
 }

@@ -297,22 +297,10 @@ struct BlendStateT {
 // modifiers.  The last contributor is tracked as the entry's LDS byte offset
 // (lo, the VGPR the record reads already use) and converted once per 64
 // entries.  No exec masks, no SALU bookkeeping.
-typedef float gs_f2 __attribute__((ext_vector_type(2)));
-// kPk: the offsets as one v_pk_add_f32 of the (x, y) pair and the negated
-// pixel pair, C0 and C1 as one v_pk_fma_f32 (the same fp32 results, each
-// half rounded as the scalar form)
-template <bool kSafe = false, bool kPk = false>
-__device__ __forceinline__ bool blend_one_sel2(float2 xy, float4 co, float4 f, gs_f2 npx, uint32_t lo,
-                                               float& T, gs_f2& C01, float& C2, uint32_t& last_lo) {
-    float dx, dy;
-    if constexpr (kPk) {
-        const gs_f2 d = gs_f2{xy.x, xy.y} + npx;
-        dx = d.x;
-        dy = d.y;
-    } else {
-        dx = xy.x + npx.x;
-        dy = xy.y + npx.y;
-    }
+template <bool kSafe = false>
+__device__ __forceinline__ bool blend_one_sel2(float2 xy, float4 co, float4 f, float pxx, float pxy, uint32_t lo,
+                                               float& T, float (&C)[3], uint32_t& last_lo) {
+    const float dx = xy.x - pxx, dy = xy.y - pxy;
     const float p = splat_p2(dx, dy, co);
     float a = fminf(0.99f, co.w * splat_exp(p));
     // power > 0: skipped (kSafe: splat_form_safe -- the computed power is
@@ -323,13 +311,9 @@ __device__ __forceinline__ bool blend_one_sel2(float2 xy, float4 co, float4 f, g
     const bool stop = test_T < 0.0001f;  // false whenever a == 0 and T >= 1e-4; true for every finished pixel
     a = stop ? 0.0f : a;
     const float w = a * T;
-    if constexpr (kPk) {
-        C01 = __builtin_elementwise_fma(gs_f2{f.x, f.y}, gs_f2{w, w}, C01);
-    } else {
-        C01.x = __builtin_fmaf(f.x, w, C01.x);
-        C01.y = __builtin_fmaf(f.y, w, C01.y);
-    }
-    C2 = __builtin_fmaf(f.z, w, C2);
+    C[0] = __builtin_fmaf(f.x, w, C[0]);
+    C[1] = __builtin_fmaf(f.y, w, C[1]);
+    C[2] = __builtin_fmaf(f.z, w, C[2]);
     T = stop ? -fabsf(T) : test_T;
     const bool blended = a != 0.0f;
     last_lo = blended ? lo : last_lo;
@@ -346,7 +330,7 @@ __device__ __forceinline__ bool blend_one_sel2(float2 xy, float4 co, float4 f, g
 // wave's exit tested after every pair of entries, and the exact row-group
 // hit codes recorded for the backward.  !kSel: the predicate form for any
 // kPPL (the fallback geometry and the AMR full-list blocks).
-template <int kPPL, int kWaves, bool kSel = false, bool kPk = false>
+template <int kPPL, int kWaves, bool kSel = false>
 __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const PixelSetT<kPPL>& px, float ox, float oy,
                                                           float st, const uint32_t* __restrict__ point_list,
                                                           const float2* __restrict__ means2D,
@@ -440,11 +424,6 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 const char* sa = reinterpret_cast<const char*>(s_a);
                 const char* sco = reinterpret_cast<const char*>(s_co);
                 const char* sb = reinterpret_cast<const char*>(s_b);
-                // (x - px = x + (-px): the same result; the negated pixel pair
-                // feeds the packed add)
-                const gs_f2 npx = gs_f2{-px.x, -px.y[0]};
-                gs_f2 c01 = gs_f2{st_.C[0][0], st_.C[0][1]};
-                float c2 = st_.C[0][2];
                 auto loop = [&](auto kSafeT) {
                     constexpr bool kSafe = decltype(kSafeT)::value;
                     while (todo) {
@@ -460,14 +439,14 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                         const float4 coB = *reinterpret_cast<const float4*>(sco + loB);
                         const float bAc = *reinterpret_cast<const float*>(sb + loA);
                         const float bBc = *reinterpret_cast<const float*>(sb + loB);
-                        const bool hA = blend_one_sel2<kSafe, kPk>(make_float2(sA.x, sA.y), coA,
-                                                                   make_float4(sA.z, sA.w, bAc, 0.f), npx, loA,
-                                                                   st_.T[0], c01, c2, last_lo);
+                        const bool hA = blend_one_sel2<kSafe>(make_float2(sA.x, sA.y), coA,
+                                                              make_float4(sA.z, sA.w, bAc, 0.f), px.x, px.y[0], loA,
+                                                              st_.T[0], st_.C[0], last_lo);
                         hits |= __ballot(hA) != 0ull ? 1ull << bA : 0ull;
                         if (two) {
-                            const bool hB = blend_one_sel2<kSafe, kPk>(make_float2(sB.x, sB.y), coB,
-                                                                       make_float4(sB.z, sB.w, bBc, 0.f), npx, loB,
-                                                                       st_.T[0], c01, c2, last_lo);
+                            const bool hB = blend_one_sel2<kSafe>(make_float2(sB.x, sB.y), coB,
+                                                                  make_float4(sB.z, sB.w, bBc, 0.f), px.x, px.y[0],
+                                                                  loB, st_.T[0], st_.C[0], last_lo);
                             hits |= __ballot(hB) != 0ull ? 1ull << bB : 0ull;
                         }
                         // every pixel of the wave finished: the rest of the chunk
@@ -477,9 +456,6 @@ __device__ __forceinline__ BlendStateT<kPPL> blend_tile_t(uint2 range, const Pix
                 };
                 if ((todo & ~safe_m) == 0ull) loop(std::integral_constant<bool, true>{});
                 else loop(std::integral_constant<bool, false>{});
-                st_.C[0][0] = c01.x;
-                st_.C[0][1] = c01.y;
-                st_.C[0][2] = c2;
                 // lo = 16 j, contributor = b0 + j + 1
                 if (last_lo != ~0u) st_.last[0] = b0 + (last_lo >> 4) + 1;
                 if (rec && (tid & 63) == 0) s_hit[c * kWaves + wave] = hits;
@@ -568,6 +544,7 @@ __device__ __forceinline__ float pl_add16(float a, float b) {
 }
 
 // Swaps returning both halves (for packed adds of the pairs).
+typedef float gs_f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ gs_f2 pl_swap32(float a, float b) {
     const auto r = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b),
                                                     false, false);

@@ -52,7 +52,7 @@ __device__ __forceinline__ void write_pixels(const PixelSetT<kPPL>& px, const Bl
 // other workgroups' blending, but its LDS and registers cost the blend
 // occupancy; profiles/r05g_ab_fuse*.log.  The AMR region-list pass keeps it,
 // amr_region_lists_kernel.)
-template <int kPPL, int kWaves, int kMinWaves = 1, bool kSel = false, bool kPk = false>
+template <int kPPL, int kWaves, int kMinWaves = 1, bool kSel = false>
 __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int W, int H, const uint32_t* __restrict__ ranges,
                                                                  const uint32_t* __restrict__ point_list,
                                                                  const float2* __restrict__ means2D,
@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(64 * kWaves, kMinWaves) render_fwd_kernel(int 
     const PixelSetT<kPPL> px = make_pixels_t<kPPL, kWaves>(W, H, ox, oy, 1);
     const uint2 range = reinterpret_cast<const uint2*>(ranges)[tile];
     const BlendStateT<kPPL> st =
-        blend_tile_t<kPPL, kWaves, kSel, kPk>(range, px, (float)ox, (float)oy, 1.0f, point_list,
+        blend_tile_t<kPPL, kWaves, kSel>(range, px, (float)ox, (float)oy, 1.0f, point_list,
                                          means2D, features, conic_opacity, s_a, s_co, s_b, s_bal, cull != 0,
                                          kSel ? hit_codes : nullptr, s_hit);
     write_pixels(px, st, W, H, final_T, n_contrib, bg, out_color);
@@ -136,7 +136,7 @@ void set_cull(int v) { g_cull = v; }
 constexpr int kDefaultFwdVariant = 1;
 int g_fwd_variant = kDefaultFwdVariant;
 
-void set_forward_variant(int v) { g_fwd_variant = (v == 0 || v == 3) ? v : kDefaultFwdVariant; }
+void set_forward_variant(int v) { g_fwd_variant = (v == 0) ? 0 : kDefaultFwdVariant; }
 
 bool launch_render_forward(int W, int H, const ImageView& img, const BinningView& b, const GeomView& g,
                            const float* features, const float* bg, float* out_color, hipStream_t s,
@@ -158,7 +158,6 @@ bool launch_render_forward(int W, int H, const ImageView& img, const BinningView
                        img.max_contrib, bg, out_color, g_cull, gx, zero4, zero_n4,                               \
                        img.bucket_count, img.bucket_list, hit_codes, g.hdr, hit_codes_word(b.point_list, hit_codes))
     if (g_fwd_variant == 0) GS_FWD_LAUNCH(4, 1);
-    else if (g_fwd_variant == 3) GS_FWD_LAUNCH(1, 4, 8, true, true);
     else GS_FWD_LAUNCH(1, 4, 8, true);  // <= 64 VGPRs: 8 waves per SIMD
 #undef GS_FWD_LAUNCH
     return zero_n4 > 0;

@@ -344,8 +344,8 @@ def test_config2_full_size_parity_and_psnr():
     G.assert_grads_elementwise("config2", names, grads, rg, sc, cam, ref, allow=al, ties=ties)
 
 
-@pytest.mark.parametrize("bwd_variant", [0, 1, 3])  # the fallback, the default, its packed-pair form
-@pytest.mark.parametrize("fwd_variant", [0, 1, 3])
+@pytest.mark.parametrize("bwd_variant", [0, 1])  # the fallback and the default (opacity-scaled sums)
+@pytest.mark.parametrize("fwd_variant", [0, 1])
 def test_blend_geometries_match_oracle(fwd_variant, bwd_variant):
     """The default and the fallback forward / backward blends (gs_set_tuning),
     every pairing, against the oracle (the fallback forward leaves no hit

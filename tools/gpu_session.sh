@@ -83,11 +83,6 @@ for step in "$@"; do
     elem) GS_ELEM_SOFT=1 GS_ELEM_REPORT="$O/elem.jsonl" run pytest_elem 900 python -u -m pytest tests/test_gpu_parity_configs.py tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread -rf -k "config2 or config4 or config5 or backward_parity or edge_case" ;;
     chaintime) run chain_timing 300 python tools/amr_chain_timing.py ;;
     chainframes) run chain_frames 300 python tools/amr_chain_timing.py frames ;;
-    abbwd) run ab_bwd_pk_cfg2 400 python tools/ab_tuning.py --key bwd_variant --values 2 3 --stage render_bwd --backward --rounds 10 &&
-      run ab_bwd_pk_cfg4 500 python tools/ab_tuning.py --key bwd_variant --values 2 3 --stage render_bwd --backward --rounds 6 --P 6100000 --W 1600 --H 1063 ;;
-    abfwd) run ab_fwd_pk_cfg2 400 python tools/ab_tuning.py --key fwd_variant --values 1 3 --stage render --rounds 10 &&
-      run ab_fwd_pk_cfg4 500 python tools/ab_tuning.py --key fwd_variant --values 1 3 --stage render --rounds 6 --P 6100000 --W 1600 --H 1063 ;;
-    bwdtests) run pytest_bwdpk 600 python -u -m pytest tests/test_gpu_cull.py tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf -k "default_backward_matches_fallback or blend_geometries" ;;
     mvtests) run pytest_mv2 600 python -u -m pytest tests/test_gpu_multiview.py tests/test_gpu_parity_configs.py -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf -k "multiview or config5" ;;
     spec) run pytest_spec 600 python -u -m pytest tests/test_gpu_amr_speculation.py tests/test_gpu_capi_ctypes.py tests/test_renderer_amr.py -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -rf ;;
     chaintrace) run chain_trace 300 rocprofv3 --kernel-trace -d "$O/chain_trace" -o run --output-format csv -- python3 tools/amr_chain_timing.py inline &&
