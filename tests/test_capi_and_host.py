@@ -54,6 +54,39 @@ def test_library_carries_the_tree_digest():
     assert d == b.source_digest() == b.check_loaded_digest()
 
 
+def test_tuning_keys_round_trip():
+    """gs_set_tuning / gs_get_tuning (pure host state): every documented key
+    reports its default, a fallback value sticks, a negative value restores
+    the default, and an unknown key is refused with a message."""
+    lib = ctypes.CDLL(LIB)
+    lib.gs_set_tuning.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.gs_get_tuning.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+    lib.gs_last_error.restype = ctypes.c_char_p
+
+    def get(k):
+        v = ctypes.c_int(-99)
+        assert lib.gs_get_tuning(k.encode(), ctypes.byref(v)) == 0, k
+        return v.value
+
+    defaults = {k: get(k) for k in ("fwd_variant", "bwd_variant", "amr_variant", "sort_algo", "cull", "hdr_mirror",
+                                    "spec_dup", "ritnet_mfma")}
+    assert defaults["fwd_variant"] != 0 and defaults["bwd_variant"] != 0 and defaults["amr_variant"] != 0
+    assert defaults["cull"] == 1 and defaults["sort_algo"] == 1 and defaults["ritnet_mfma"] == 1
+    try:
+        for k in ("fwd_variant", "bwd_variant", "amr_variant"):
+            assert lib.gs_set_tuning(k.encode(), 0) == 0
+            assert get(k) == 0, k
+            assert lib.gs_set_tuning(k.encode(), -1) == 0
+            assert get(k) == defaults[k], k
+    finally:
+        for k, v in defaults.items():
+            lib.gs_set_tuning(k.encode(), v)
+    v = ctypes.c_int(0)
+    assert lib.gs_get_tuning(b"no_such_key", ctypes.byref(v)) == -1
+    assert b"no_such_key" in lib.gs_last_error()
+    assert lib.gs_set_tuning(b"no_such_key", 1) == -1
+
+
 def test_host_layout_helpers():
     lib = ctypes.CDLL(LIB)
     lib.gs_geom_bytes.restype = ctypes.c_size_t
