@@ -38,6 +38,7 @@ for step in "$@"; do
     parity) run pytest_parity 600 python -m pytest tests/test_gpu_parity.py tests/test_gpu_cull.py -q -m gpu -p no:cacheprovider --timeout 300 -rf ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 20 --warmup 5 ;;
+    benchdef) run bench_default 600 python bench.py ;;  # the driver's exact command
     bench3) run bench_cfg3 600 python bench.py --config cfg3_amr_1080p_1M --steps 20 --warmup 3 ;;
     bench4) run bench_cfg4 600 python bench.py --config cfg4_bicycle_6M --steps 10 --warmup 3 --no-cpu-baseline ;;
     dist2) GS_BENCH_SHARE_DEVICE=1 GS_BENCH_BACKEND=gloo run bench_dist2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 2 ;;
